@@ -1,0 +1,224 @@
+"""
+Distributed runtime helpers (L1), API-compatible with the reference
+`basic_utils/dist_util.py` (reference: basic_utils/dist_util.py:19-167).
+
+Everything here is safe to call in a plain single-process run: rank 0, world 1,
+no-op barrier/broadcast.  Under `torchrun` (or our `dist_run` launcher) the
+process group is created over RCCL (torch backend name ``"nccl"`` on ROCm) when
+a HIP device is visible, otherwise gloo.
+
+MI355X-specific differences from the reference:
+
+* ``setup_dist`` binds the device *before* creating the process group and passes
+  ``device_id=`` so RCCL communicators are created eagerly on the right GCD, and
+  sets a finite collective timeout so a hung xGMI collective aborts instead of
+  hanging the node.
+* ``sync_params`` coalesces all tensors of one dtype/device into a single flat
+  buffer and issues ONE broadcast per dtype instead of one per tensor
+  (SURVEY X-3: 209 calls -> 1-2 calls).
+* ``load_state_dict`` only uses ``blobfile`` when it is importable (remote
+  paths); local paths go through ``open`` and ``torch.load(weights_only=...)``.
+"""
+
+import datetime
+import functools
+import io
+import os
+import socket
+
+import torch
+import torch.distributed as dist
+
+USE_DIST_IN_WINDOWS = False  # kept for API parity; Linux-only framework.
+
+# Collective timeout for the RCCL/gloo process group (seconds).  Overridable.
+DIST_TIMEOUT_S = int(os.environ.get("DPA_DIST_TIMEOUT_S", "1800"))
+
+
+def _cuda_available():
+    # ``torch.cuda`` is HIP on ROCm builds.
+    return torch.cuda.is_available()
+
+
+# --------------------------------------------------------------------------- #
+#                                 Setup Tools                                 #
+# --------------------------------------------------------------------------- #
+
+def is_available():
+    """Return whether torch was built with the c10d runtime (cached).
+
+    Reference: basic_utils/dist_util.py:26-45 (function-attribute cache).
+    """
+    if hasattr(is_available, "cache"):
+        return is_available.cache
+    if os.name == "nt" and not USE_DIST_IN_WINDOWS:
+        if os.environ.get("LOCAL_RANK", "0") != "0":
+            raise RuntimeError("torch.distributed is disabled on Windows by default "
+                               "(set basic_utils.dist_util.USE_DIST_IN_WINDOWS=True).")
+    elif dist.is_available():
+        is_available.cache = True
+        return True
+    os.environ.setdefault("LOCAL_RANK", "0")
+    is_available.cache = False
+    return False
+
+
+def is_initialized():
+    """Guarded ``dist.is_initialized()`` (reference dist_util.py:48-54)."""
+    return is_available() and getattr(dist, "is_initialized", lambda: False)()
+
+
+@functools.lru_cache(maxsize=None)
+def setup_dist(backend=None, silent=False):
+    """Create the process group once; returns True when running distributed.
+
+    Reference: basic_utils/dist_util.py:57-85.  Same fallback semantics (an init
+    failure prints and continues single-process), but RCCL-specific setup:
+    device bound first, eager communicator init, finite timeout.
+    """
+    if is_initialized():
+        return True
+
+    if is_available() and os.environ.get("LOCAL_RANK") is not None:
+        try:
+            use_gpu = _cuda_available()
+            if backend is None:
+                backend = "nccl" if use_gpu else "gloo"
+            # Fail fast on hung collectives rather than wedging the node.
+            os.environ.setdefault("TORCH_NCCL_ASYNC_ERROR_HANDLING", "1")
+            kwargs = dict(backend=backend, init_method="env://",
+                          timeout=datetime.timedelta(seconds=DIST_TIMEOUT_S))
+            if use_gpu:
+                torch.cuda.set_device(dev())
+                if backend == "nccl":
+                    kwargs["device_id"] = dev()
+            dist.init_process_group(**kwargs)
+            if use_gpu:
+                torch.cuda.empty_cache()
+            if os.environ["LOCAL_RANK"] == "0" and not silent:
+                print("<INFO> torch.distributed setup success, using distributed setting..")
+            return True
+        except Exception as exc:  # same fallback policy as the reference
+            if not silent:
+                print(f"<INFO> {exc.__class__.__qualname__}: {exc}")
+            is_available.cache = False
+
+    os.environ.setdefault("LOCAL_RANK", "0")
+    if int(os.getenv("LOCAL_RANK")) == 0 and not silent:
+        print("<INFO> torch.distributed is not available, skipping distributed setting..")
+    return False
+
+
+# --------------------------------------------------------------------------- #
+#                                General Tools                                #
+# --------------------------------------------------------------------------- #
+
+def get_rank(group=None):
+    if is_initialized():
+        return dist.get_rank(group=group)
+    return 0
+
+
+def get_world_size(group=None):
+    if is_initialized():
+        return dist.get_world_size(group=group)
+    return 1
+
+
+def get_local_rank():
+    return int(os.environ.get("LOCAL_RANK", "0"))
+
+
+def barrier(*args, **kwargs):
+    if is_initialized():
+        if (dist.get_backend() == "nccl" and _cuda_available()
+                and "device_ids" not in kwargs):
+            kwargs["device_ids"] = [get_local_rank()]
+        return dist.barrier(*args, **kwargs)
+
+
+def dev():
+    """Device of this rank: ``cuda:{LOCAL_RANK}`` (a HIP device) or cpu."""
+    if _cuda_available():
+        return torch.device(f"cuda:{os.environ.get('LOCAL_RANK', '0')}")
+    return torch.device("cpu")
+
+
+def _open_for_read(path):
+    if "://" in path:
+        try:
+            import blobfile as bf  # optional; only needed for remote paths
+        except ImportError as exc:
+            raise RuntimeError(f"remote path {path!r} requires blobfile") from exc
+        return bf.BlobFile(path, "rb")
+    return open(path, "rb")
+
+
+def load_state_dict(local_or_remote_path, **kwargs):
+    """Load a torch checkpoint from a local (or, with blobfile, remote) path.
+
+    Reference: basic_utils/dist_util.py:118-124.  ``weights_only`` defaults to
+    True: checkpoints are plain tensor dicts / AdamW state dicts.
+    """
+    kwargs.setdefault("weights_only", True)
+    with _open_for_read(local_or_remote_path) as f:
+        data = f.read()
+    return torch.load(io.BytesIO(data), **kwargs)
+
+
+def broadcast(tensor, src=0, group=None, async_op=False):
+    """Broadcast one tensor from ``src`` (reference dist_util.py:127-138)."""
+    if not is_initialized():
+        return
+    with torch.no_grad():
+        return dist.broadcast(tensor, src, group=group, async_op=async_op)
+
+
+def sync_params(params, src=0, group=None, async_op=False):
+    """Broadcast a sequence of tensors from ``src`` with coalesced collectives.
+
+    Reference: basic_utils/dist_util.py:141-152 issues one broadcast per tensor;
+    here tensors are grouped by (device, dtype), packed into one flat buffer,
+    broadcast once and unpacked.  ``async_op`` is accepted for API parity; the
+    unpack needs the data so the call is always synchronous.
+    """
+    if not is_initialized():
+        return
+    params = [p for p in params if p is not None]
+    groups = {}
+    for p in params:
+        groups.setdefault((p.device, p.dtype), []).append(p)
+    with torch.no_grad():
+        for (_device, _dtype), ts in groups.items():
+            flat = torch.cat([t.detach().reshape(-1) for t in ts])
+            dist.broadcast(flat, src, group=group)
+            off = 0
+            for t in ts:
+                n = t.numel()
+                t.detach().copy_(flat[off:off + n].view_as(t))
+                off += n
+
+
+def all_reduce_mean_scalars(values, group=None):
+    """Average a list of python floats across ranks with one collective."""
+    if not is_initialized():
+        return list(values)
+    device = dev() if dist.get_backend() == "nccl" else torch.device("cpu")
+    t = torch.tensor(list(values), dtype=torch.float64, device=device)
+    dist.all_reduce(t, group=group)
+    t /= get_world_size(group)
+    return t.tolist()
+
+
+def find_free_port():
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        s.setsockopt(socket.SOL_SOCKET, socket.SO_REUSEADDR, 1)
+        return s.getsockname()[1]
+
+
+__all__ = [
+    "is_available", "is_initialized", "setup_dist", "get_rank", "get_world_size",
+    "get_local_rank", "barrier", "dev", "load_state_dict", "broadcast",
+    "sync_params", "all_reduce_mean_scalars", "find_free_port",
+]

@@ -1,0 +1,92 @@
+// Shared device helpers for the gfx950 (MI355X / CDNA4) kernels.
+//
+// All kernels in this directory are written for wave64 CDNA4 only: block
+// sizes are multiples of 64, cross-lane reductions go across 64 lanes, bf16 is
+// moved in 8/16-byte vectors (hipcc does not vectorise scalar bf16 loads).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#define DPA_WAVE 64
+
+namespace dpa {
+
+typedef uint16_t bf16_t;  // raw bf16 bits in memory
+typedef __attribute__((ext_vector_type(2))) float f32x2;
+typedef __attribute__((ext_vector_type(4))) float f32x4;
+typedef __attribute__((ext_vector_type(16))) float f32x16;
+typedef __attribute__((ext_vector_type(8))) short bf16x8;   // MFMA A/B fragment
+typedef __attribute__((ext_vector_type(4))) short bf16x4;
+
+__device__ __forceinline__ float bf2f(bf16_t h) {
+  return __uint_as_float(((uint32_t)h) << 16);
+}
+
+// Round-to-nearest-even f32 -> bf16 (NaN-preserving).
+__device__ __forceinline__ bf16_t f2bf(float f) {
+  uint32_t u = __float_as_uint(f);
+  if ((u & 0x7fffffffu) > 0x7f800000u) return (bf16_t)((u >> 16) | 0x40u);
+  u += 0x7fffu + ((u >> 16) & 1u);
+  return (bf16_t)(u >> 16);
+}
+
+__device__ __forceinline__ uint32_t pack_bf2(float lo, float hi) {
+  return (uint32_t)f2bf(lo) | ((uint32_t)f2bf(hi) << 16);
+}
+
+// ---- wave64 reductions ----------------------------------------------------
+__device__ __forceinline__ float wave_sum(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+__device__ __forceinline__ float wave_max(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
+  return v;
+}
+__device__ __forceinline__ double wave_sum_d(double v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+
+// Block-wide sum for blockDim.x <= 1024; `red` needs blockDim.x/64 floats.
+__device__ __forceinline__ float block_sum(float v, float* red) {
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const int nw = (blockDim.x + 63) >> 6;
+  v = wave_sum(v);
+  if (lane == 0) red[wid] = v;
+  __syncthreads();
+  float r = (threadIdx.x < (unsigned)nw) ? red[threadIdx.x] : 0.f;
+  if (wid == 0) r = wave_sum(r);
+  if (threadIdx.x == 0) red[0] = r;
+  __syncthreads();
+  r = red[0];
+  __syncthreads();
+  return r;
+}
+
+// ---- counter-based RNG (Philox-4x32-7-ish) for dropout / noise -------------
+// Stateless: (seed, offset, subsequence) -> 4 uniform u32.  Replays inside a
+// HIP graph read seed/offset from device memory so every replay advances.
+__device__ __forceinline__ void philox4(uint32_t k0, uint32_t k1, uint32_t c0, uint32_t c1,
+                                        uint32_t c2, uint32_t c3, uint32_t out[4]) {
+  const uint32_t M0 = 0xD2511F53u, M1 = 0xCD9E8D57u;
+  const uint32_t W0 = 0x9E3779B9u, W1 = 0xBB67AE85u;
+#pragma unroll
+  for (int r = 0; r < 7; ++r) {
+    uint32_t hi0 = __umulhi(M0, c0), lo0 = M0 * c0;
+    uint32_t hi1 = __umulhi(M1, c2), lo1 = M1 * c2;
+    uint32_t n0 = hi1 ^ c1 ^ k0, n1 = lo1, n2 = hi0 ^ c3 ^ k1, n3 = lo0;
+    c0 = n0; c1 = n1; c2 = n2; c3 = n3;
+    k0 += W0; k1 += W1;
+  }
+  out[0] = c0; out[1] = c1; out[2] = c2; out[3] = c3;
+}
+
+__device__ __forceinline__ float u32_to_unit(uint32_t x) {  // [0,1)
+  return (float)(x >> 8) * (1.0f / 16777216.0f);
+}
+
+}  // namespace dpa
