@@ -1,0 +1,97 @@
+"""
+DiffuSeq ``TransformerNetModel`` (the workload the reference
+template's trainer was adapted for, reference utils/trainer.py:1-4).
+
+    word_embedding: Embedding(V, E)           lm_head: Linear(E, V), weight tied
+    time_embed:     Linear(E_t, 4E_t) -> SiLU -> Linear(4E_t, H)
+    input_up_proj:  Linear(E, H) -> Tanh -> Linear(H, H)
+    h = Dropout(LN(pos_emb + up(x_t) + time_emb[:, None]))
+    h = BertEncoder(h)                        (post-LN, 12 x 768 for DiffuSeq-base)
+    out = output_down_proj(h):  Linear(H, H) -> Tanh -> Linear(H, E)
+
+Parameter names follow DiffuSeq where the structure is the same
+(``word_embedding``, ``lm_head``, ``time_embed.{0,2}``, ``input_up_proj.{0,2}``,
+``position_embeddings``, ``LayerNorm``, ``output_down_proj.{0,2}``); the
+encoder packs Q/K/V into ``input_transformers.layer.N.attn.qkv``.
+"""
+import torch
+import torch.nn.functional as F
+from torch import nn
+
+from ..ops import nn as ops
+from . import presets
+from .layers import BertEncoder, Embedding, LayerNorm, Linear
+
+
+class _Seq(nn.Sequential):
+    """Sequential whose index names match DiffuSeq (0 = first Linear, 2 = second)."""
+
+
+class TransformerNetModel(nn.Module):
+    def __init__(self, *, vocab_size=30522, input_dims=128, hidden_t_dim=128, seq_len=128,
+                 config_name="bert-base-uncased", hidden_size=0, num_layers=0, num_heads=0,
+                 intermediate_size=0, dropout=0.1, compute_dtype=torch.bfloat16, **_):
+        super().__init__()
+        cfg = presets.resolve(config_name, hidden_size=hidden_size, num_layers=num_layers,
+                              num_heads=num_heads, intermediate_size=intermediate_size,
+                              vocab_size=vocab_size)
+        H = cfg["hidden_size"]
+        self.cfg = cfg
+        self.input_dims, self.hidden_t_dim, self.hidden_size = input_dims, hidden_t_dim, H
+        self.dropout = dropout
+        self.compute_dtype = compute_dtype
+        self.seq_len = seq_len
+        assert seq_len <= cfg["max_position_embeddings"]
+
+        self.word_embedding = Embedding(cfg["vocab_size"], input_dims)
+        self.lm_head = Linear(input_dims, cfg["vocab_size"])
+        with torch.no_grad():
+            self.lm_head.weight = self.word_embedding.weight  # tied rounding head
+
+        t4 = hidden_t_dim * 4
+        self.time_embed = nn.Sequential(Linear(hidden_t_dim, t4, act="silu"), nn.Identity(),
+                                        Linear(t4, H))
+        self.input_up_proj = nn.Sequential(Linear(input_dims, H, act="tanh"), nn.Identity(),
+                                           Linear(H, H))
+        self.input_transformers = BertEncoder(H, cfg["num_layers"], cfg["num_heads"],
+                                              cfg["intermediate_size"], dropout,
+                                              eps=cfg["layer_norm_eps"], init_std=0.02)
+        self.register_buffer("position_ids", torch.arange(cfg["max_position_embeddings"]).unsqueeze(0),
+                             persistent=False)
+        self.position_embeddings = Embedding(cfg["max_position_embeddings"], H, init_std=0.02)
+        self.LayerNorm = LayerNorm(H, eps=cfg["layer_norm_eps"])
+        self.output_down_proj = nn.Sequential(Linear(H, H, act="tanh"), nn.Identity(),
+                                              Linear(H, input_dims))
+
+    # -- DiffuSeq API -------------------------------------------------------
+    def get_embeds(self, input_ids):
+        """Word embeddings in fp32 (diffusion space stays fp32)."""
+        return ops.embedding(input_ids, self.word_embedding.weight, torch.float32)
+
+    def get_logits(self, hidden_repr):
+        """Materialised rounding logits (API parity; training uses :meth:`token_nll`)."""
+        return ops.linear(hidden_repr.float(), self.lm_head.weight, self.lm_head.bias)
+
+    def token_nll(self, x, ids):
+        """Per-token CE of the tied rounding head, fused (x: [N, E], ids: [N])."""
+        dt = self.compute_dtype
+        return ops.linear_cross_entropy(x.to(dt), self.lm_head.weight, self.lm_head.bias, ids)
+
+    # -- forward ------------------------------------------------------------
+    def forward(self, x, timesteps):
+        dt = self.compute_dtype
+        B, L, _ = x.shape
+        temb = ops.timestep_embedding(timesteps, self.hidden_t_dim).to(dt)
+        emb_t = self.time_embed(temb)                                        # [B, H]
+        emb_x = self.input_up_proj(x.to(dt))                                 # [B, L, H]
+        pos = self.position_embeddings(self.position_ids[:, :L], dt)         # [1, L, H]
+        h = emb_x + pos + emb_t.unsqueeze(1)
+        h = self.LayerNorm(h)
+        if self.training and self.dropout > 0:
+            h = F.dropout(h, self.dropout, True)
+        h = self.input_transformers(h)
+        return self.output_down_proj(h)
+
+
+def count_params(model):
+    return sum(p.numel() for p in model.parameters())

@@ -1,0 +1,153 @@
+"""
+Gaussian diffusion for continuous text embeddings (DiffuSeq, ICLR 2023 -
+the workload the reference template is written for; SURVEY Appendix B,
+call stack CS-5).
+
+Implements the training objective of DiffuSeq's ``training_losses_seq2seq``:
+
+    x0_mean = Emb(ids);  x0 = x0_mean + sqrt(1 - abar_0) * eps0
+    x_t     = sqrt(abar_t) x0 + sqrt(1 - abar_t) eps      (target positions only;
+                                                          source positions keep x0)
+    x0_hat  = model(x_t, t * 1000 / T)                    (predict_xstart)
+    mse     = mean_flat((x0 - x0_hat)^2)   [t == 0: mean_flat((x0_mean - x0_hat)^2)]
+    tT      = mean_flat((sqrt(abar_{T-1}) x0)^2)
+    decoder_nll = mean_L CE(lm_head(x0), ids)
+    loss    = mse + decoder_nll + tT ;   nll = masked CE(lm_head(x0_hat), ids)  (logged)
+
+The CE terms go through the fused linear-cross-entropy op (no [N, V] logits
+in memory); ``nll`` is computed without autograd since it is only logged.
+"""
+import math
+
+import numpy as np
+import torch
+
+from ..ops import nn as ops
+
+
+def betas_for_alpha_bar(num_steps, alpha_bar, max_beta=0.999):
+    betas = []
+    for i in range(num_steps):
+        t1, t2 = i / num_steps, (i + 1) / num_steps
+        betas.append(min(1 - alpha_bar(t2) / alpha_bar(t1), max_beta))
+    return np.array(betas, dtype=np.float64)
+
+
+def get_named_beta_schedule(name, num_steps):
+    if name == "linear":
+        scale = 1000 / num_steps
+        return np.linspace(scale * 0.0001, scale * 0.02, num_steps, dtype=np.float64)
+    if name == "cosine":
+        return betas_for_alpha_bar(num_steps, lambda t: math.cos((t + 0.008) / 1.008 * math.pi / 2) ** 2)
+    if name == "sqrt":
+        return betas_for_alpha_bar(num_steps, lambda t: 1 - np.sqrt(t + 0.0001))
+    if name == "trunc_cos":
+        return betas_for_alpha_bar(num_steps, lambda t: np.cos((t + 0.1) / 1.1 * np.pi / 2) ** 2)
+    if name == "trunc_lin":
+        scale = 1000 / num_steps
+        return np.linspace(scale * 0.0001 + 0.01, scale * 0.02 + 0.01, num_steps, dtype=np.float64)
+    if name == "pw_lin":
+        scale = 1000 / num_steps
+        b0 = np.linspace(scale * 0.0001 + 0.01, 0.1, 10, dtype=np.float64)
+        b1 = np.linspace(0.1, scale * 0.02, num_steps - 10, dtype=np.float64)
+        return np.concatenate([b0, b1])
+    raise NotImplementedError(f"unknown beta schedule: {name}")
+
+
+def mean_flat(x):
+    return x.mean(dim=list(range(1, x.dim())))
+
+
+class GaussianDiffusion:
+    """Noise schedule tables (kept on device) + the seq2seq training loss."""
+
+    def __init__(self, betas, predict_xstart=True, rescale_timesteps=True, learn_sigma=False):
+        if learn_sigma:
+            raise NotImplementedError("learn_sigma=True is not supported (DiffuSeq default is False)")
+        self.predict_xstart = predict_xstart
+        self.rescale_timesteps = rescale_timesteps
+        betas = np.asarray(betas, dtype=np.float64)
+        self.num_timesteps = int(betas.shape[0])
+        alphas = 1.0 - betas
+        self.betas = betas
+        self.alphas_cumprod = np.cumprod(alphas, axis=0)
+        self.alphas_cumprod_prev = np.append(1.0, self.alphas_cumprod[:-1])
+        self.sqrt_alphas_cumprod = np.sqrt(self.alphas_cumprod)
+        self.sqrt_one_minus_alphas_cumprod = np.sqrt(1.0 - self.alphas_cumprod)
+        self.posterior_variance = betas * (1.0 - self.alphas_cumprod_prev) / (1.0 - self.alphas_cumprod)
+        self._dev_tables = {}
+
+    # -- device tables ------------------------------------------------------
+    def _table(self, name, device):
+        key = (name, str(device))
+        t = self._dev_tables.get(key)
+        if t is None:
+            t = torch.as_tensor(getattr(self, name), dtype=torch.float32, device=device)
+            self._dev_tables[key] = t
+        return t
+
+    def _extract(self, name, t, ndim):
+        v = self._table(name, t.device)[t]
+        return v.view(-1, *([1] * (ndim - 1)))
+
+    def scale_timesteps(self, t):
+        if self.rescale_timesteps:
+            return t.float() * (1000.0 / self.num_timesteps)
+        return t
+
+    # -- forward process ----------------------------------------------------
+    def q_sample(self, x_start, t, noise, mask=None):
+        x_t = (self._extract("sqrt_alphas_cumprod", t, x_start.dim()) * x_start
+               + self._extract("sqrt_one_minus_alphas_cumprod", t, x_start.dim()) * noise)
+        if mask is None:
+            return x_t
+        return torch.where(mask.unsqueeze(-1) == 0, x_start, x_t)
+
+    # -- loss ---------------------------------------------------------------
+    def training_losses(self, model, *args, **kwargs):
+        return self.training_losses_seq2seq(model, *args, **kwargs)
+
+    def training_losses_seq2seq(self, model, x_start_unused, t, model_kwargs, noise=None,
+                                compute_nll=True):
+        """DiffuSeq loss terms, each [B] fp32.  ``model`` may be wrapped (DDP engine)."""
+        net = getattr(model, "module", model)
+        input_ids = model_kwargs["input_ids"]
+        input_mask = model_kwargs["input_mask"]
+        x0_mean = net.get_embeds(input_ids)                                  # [B, L, E] fp32
+        std0 = float(self.sqrt_one_minus_alphas_cumprod[0])
+        x_start = x0_mean + std0 * torch.randn_like(x0_mean)
+        if noise is None:
+            noise = torch.randn_like(x_start)
+        x_t = self.q_sample(x_start, t, noise, mask=input_mask)
+        model_out = model(x_t, self.scale_timesteps(t)).float()             # x0_hat
+        terms = {}
+        mse = mean_flat((x_start - model_out) ** 2)
+        t0_loss = mean_flat((x0_mean - model_out) ** 2)
+        terms["mse"] = torch.where(t == 0, t0_loss, mse)
+        sa_last = float(self.sqrt_alphas_cumprod[self.num_timesteps - 1])
+        tT_loss = mean_flat((sa_last * x_start) ** 2)
+        decoder_nll = self.token_discrete_loss(x_start, net, input_ids)
+        if compute_nll:
+            with torch.no_grad():
+                terms["nll"] = self.token_discrete_loss(model_out.detach(), net, input_ids,
+                                                        mask=input_mask)
+        terms["decoder_nll"] = decoder_nll
+        terms["loss"] = terms["mse"] + decoder_nll + tT_loss
+        return terms
+
+    @staticmethod
+    def token_discrete_loss(x, net, input_ids, mask=None):
+        """Per-sample CE of the rounding head (DiffuSeq ``_token_discrete_loss``)."""
+        B, L = input_ids.shape
+        per_tok = net.token_nll(x.reshape(B * L, -1), input_ids.reshape(-1)).view(B, L)
+        if mask is not None:
+            m = mask.to(per_tok.dtype)
+            return (per_tok * m).sum(-1) / m.sum(-1).clamp_min(1.0)
+        return per_tok.mean(-1)
+
+
+def create_gaussian_diffusion(steps=2000, noise_schedule="sqrt", predict_xstart=True,
+                              rescale_timesteps=True, learn_sigma=False, **_):
+    betas = get_named_beta_schedule(noise_schedule, steps)
+    return GaussianDiffusion(betas, predict_xstart=predict_xstart,
+                             rescale_timesteps=rescale_timesteps, learn_sigma=learn_sigma)

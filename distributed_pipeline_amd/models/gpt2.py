@@ -1,0 +1,51 @@
+"""GPT-2 small causal LM (BASELINE config #4: the generic-model path).
+
+Trained through the *generic* ``TrainLoop`` hooks (``compute_losses`` /
+``backward_from_losses``) rather than the diffusion loop.  Weight tying
+``lm_head.weight is wte.weight``; the LM loss uses the fused
+linear-cross-entropy op so the [tokens, 50257] logits never exist in memory.
+"""
+import torch
+from torch import nn
+
+from ..ops import nn as ops
+from . import presets
+from .layers import Embedding, GPT2Block, LayerNorm
+
+
+class GPT2LMModel(nn.Module):
+    def __init__(self, *, config_name="gpt2", vocab_size=0, seq_len=1024, hidden_size=0,
+                 num_layers=0, num_heads=0, dropout=0.1, compute_dtype=torch.bfloat16, **_):
+        super().__init__()
+        cfg = presets.resolve(config_name, hidden_size=hidden_size, num_layers=num_layers,
+                              num_heads=num_heads, vocab_size=vocab_size)
+        H = cfg["hidden_size"]
+        self.cfg, self.compute_dtype, self.dropout = cfg, compute_dtype, dropout
+        assert seq_len <= cfg["max_position_embeddings"]
+        self.wte = Embedding(cfg["vocab_size"], H, init_std=0.02)
+        self.wpe = Embedding(cfg["max_position_embeddings"], H, init_std=0.01)
+        self.h = nn.ModuleList(GPT2Block(H, cfg["num_heads"], dropout, eps=cfg["layer_norm_eps"],
+                                         n_layers=cfg["num_layers"]) for _ in range(cfg["num_layers"]))
+        self.ln_f = LayerNorm(H, eps=cfg["layer_norm_eps"])
+        self.register_buffer("position_ids", torch.arange(cfg["max_position_embeddings"]).unsqueeze(0),
+                             persistent=False)
+
+    def hidden_states(self, input_ids):
+        dt = self.compute_dtype
+        B, L = input_ids.shape
+        h = self.wte(input_ids, dt) + self.wpe(self.position_ids[:, :L], dt)
+        if self.training and self.dropout > 0:
+            h = torch.nn.functional.dropout(h, self.dropout, True)
+        for blk in self.h:
+            h = blk(h)
+        return self.ln_f(h)
+
+    def forward(self, input_ids, labels=None):
+        """Returns per-token CE [B, L-1] when ``labels`` (shifted internally) are given."""
+        h = self.hidden_states(input_ids)
+        if labels is None:
+            return ops.linear(h, self.wte.weight)
+        B, L, H = h.shape
+        x = h[:, :-1].reshape(-1, H)
+        tgt = labels[:, 1:].reshape(-1)
+        return ops.linear_cross_entropy(x, self.wte.weight, None, tgt).view(B, L - 1)

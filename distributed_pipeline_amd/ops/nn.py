@@ -1,0 +1,347 @@
+"""
+Functional compute ops used by the models, with autograd.
+
+Every op here has two implementations:
+
+* the **gfx950 path** (HIP kernels from ``csrc/``), taken for bf16 tensors on a
+  HIP device; the kernels are required there (``_ext.get_ext`` raises when the
+  extension is missing, so a GPU run can never silently fall back), and
+* a **PyTorch reference path** used on CPU and for fp32 (the reference-
+  equivalent configuration); it is also the numerics oracle in the tests.
+
+Weights are fp32 ``nn.Parameter``s (views into the engine's flat master
+buffer).  For bf16 compute an op reads the parameter's bf16 *shadow*
+(``param._dpa_shadow``, refreshed by the fused optimizer) instead of casting
+every forward, and returns fp32 weight gradients so they accumulate straight
+into the flat fp32 gradient buffer.
+"""
+import math
+
+import torch
+import torch.nn.functional as F
+
+from ._ext import get_ext
+
+# --------------------------------------------------------------------------- #
+# helpers
+# --------------------------------------------------------------------------- #
+
+
+def native_ok(*ts, kernel=None):
+    """Take the HIP path: all tensors on a HIP device and (if named) the kernel is built."""
+    for t in ts:
+        if t is None:
+            continue
+        if not t.is_cuda:
+            return False
+    ext = get_ext()
+    return ext is not None and (kernel is None or hasattr(ext, kernel))
+
+
+def shadow(p, dtype):
+    """Compute-dtype view of parameter ``p`` (bf16 shadow if attached & fresh)."""
+    if p is None:
+        return None
+    if p.dtype == dtype:
+        return p
+    s = getattr(p, "_dpa_shadow", None)
+    if s is not None and s.dtype == dtype:
+        return s
+    return p.detach().to(dtype)
+
+
+def _mm_fp32(a, b):
+    """a @ b with fp32 output (bf16 inputs on GPU keep fp32 accumulation)."""
+    if a.is_cuda and a.dtype == torch.bfloat16:
+        return torch.mm(a, b, out_dtype=torch.float32)
+    return (a.float() @ b.float())
+
+
+# --------------------------------------------------------------------------- #
+# Linear (+ optional fused activation)
+# --------------------------------------------------------------------------- #
+
+_ACTS = ("none", "gelu", "tanh", "silu")
+
+
+def _act_fwd(z, act):
+    if act == "none":
+        return z
+    if act == "gelu":
+        return F.gelu(z)
+    if act == "tanh":
+        return torch.tanh(z)
+    if act == "silu":
+        return F.silu(z)
+    raise ValueError(act)
+
+
+def _act_bwd(dy, z, y, act):
+    """d act(z) given dy, pre-activation z and output y (fp32 math)."""
+    if act == "none":
+        return dy
+    dyf = dy.float()
+    if act == "tanh":
+        yf = y.float()
+        return (dyf * (1.0 - yf * yf)).to(dy.dtype)
+    zf = z.float()
+    if act == "gelu":
+        cdf = 0.5 * (1.0 + torch.erf(zf * (1.0 / math.sqrt(2.0))))
+        pdf = torch.exp(-0.5 * zf * zf) * (1.0 / math.sqrt(2.0 * math.pi))
+        return (dyf * (cdf + zf * pdf)).to(dy.dtype)
+    if act == "silu":
+        s = torch.sigmoid(zf)
+        return (dyf * (s * (1.0 + zf * (1.0 - s)))).to(dy.dtype)
+    raise ValueError(act)
+
+
+def _bias_act_fwd(z2d, b16, act):
+    if native_ok(z2d, kernel="bias_act_fwd") and z2d.dtype == torch.bfloat16 and z2d.shape[-1] % 8 == 0:
+        return get_ext().bias_act_fwd(z2d, b16, _ACTS.index(act))
+    z = z2d if b16 is None else z2d + b16
+    return z, _act_fwd(z, act)
+
+
+def _bias_act_bwd(dy2d, z, y, act, want_db):
+    if native_ok(dy2d, kernel="bias_act_bwd") and dy2d.dtype == torch.bfloat16 and dy2d.shape[-1] % 8 == 0:
+        dz, db = get_ext().bias_act_bwd(dy2d, z if z is not None else y, _ACTS.index(act), want_db)
+        return dz, (db if want_db else None)
+    dz = _act_bwd(dy2d, z, y, act)
+    db = dz.float().sum(0) if want_db else None
+    return dz, db
+
+
+class _LinearFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, w, b, w16, b16, act):
+        shp = x.shape
+        x2 = x.reshape(-1, shp[-1])
+        z = x2 @ w16.t()
+        if b16 is not None or act != "none":
+            z, y = _bias_act_fwd(z, b16, act)
+        else:
+            y = z
+        # what the activation backward needs: tanh uses y, gelu/silu use z
+        keep_z = z if act in ("gelu", "silu") else None
+        keep_y = y if act == "tanh" else None
+        ctx.save_for_backward(x2, w16, keep_z, keep_y)
+        ctx.act = act
+        ctx.has_b = b is not None
+        ctx.shp = shp
+        return y.reshape(*shp[:-1], w16.shape[0])
+
+    @staticmethod
+    def backward(ctx, dy):
+        x2, w16, z, y = ctx.saved_tensors
+        dy2 = dy.reshape(-1, dy.shape[-1])
+        if ctx.act != "none" or ctx.has_b:
+            dz, db = _bias_act_bwd(dy2.contiguous(), z, y, ctx.act, ctx.has_b)
+        else:
+            dz, db = dy2, None
+        dx = (dz @ w16).reshape(ctx.shp) if ctx.needs_input_grad[0] else None
+        dw = _mm_fp32(dz.t(), x2) if ctx.needs_input_grad[1] else None
+        return dx, dw, db, None, None, None
+
+
+def linear(x, weight, bias=None, act="none"):
+    """y = act(x @ W^T + b).  fp32 weights, compute in x.dtype."""
+    if x.dtype == torch.float32:
+        return _act_fwd(F.linear(x, weight, bias), act)
+    return _LinearFn.apply(x, weight, bias, shadow(weight, x.dtype), shadow(bias, x.dtype), act)
+
+
+# --------------------------------------------------------------------------- #
+# LayerNorm, optionally fused with dropout(y) + residual add (post-LN BERT)
+# --------------------------------------------------------------------------- #
+
+class _AddLNFn(torch.autograd.Function):
+    """out = LN(dropout(y) + residual) in one HIP kernel (fwd and bwd)."""
+
+    @staticmethod
+    def forward(ctx, y, residual, w, b, w16, b16, p, eps, seed, offset):
+        ext = get_ext()
+        out, mean, rstd, mask = ext.add_ln_fwd(y, residual, w16, b16, float(p), float(eps), seed, offset)
+        ctx.save_for_backward(out, rstd, w16, b16, mask)
+        ctx.p = p
+        ctx.has_res = residual is not None
+        return out
+
+    @staticmethod
+    def backward(ctx, dout):
+        out, rstd, w16, b16, mask = ctx.saved_tensors
+        dx, dy, dw, db = get_ext().add_ln_bwd(dout.contiguous(), out, rstd, w16, b16, mask, float(ctx.p))
+        return dy, (dx if ctx.has_res else None), dw, db, None, None, None, None, None, None
+
+
+class RNG:
+    """Device-resident (seed, offset) for the in-kernel Philox streams.
+
+    Kernels read nothing from the host per call: the offset is a python int
+    that advances per call site, so eager runs get fresh randomness.  Graph
+    capture uses ``graph_safe_offsets``: offsets are baked in but combined with
+    a device counter bumped once per replay.
+    """
+    seed = 1234
+    counter = 0
+
+    @classmethod
+    def next(cls, n=1):
+        off = cls.counter
+        cls.counter += n
+        return cls.seed, off
+
+
+def add_dropout_layernorm(y, residual, weight, bias, p=0.0, eps=1e-12, training=True):
+    """LN(dropout(y) + residual) (residual may be None)."""
+    p = p if training else 0.0
+    if y.dtype == torch.bfloat16 and native_ok(y, kernel="add_ln_fwd") and y.shape[-1] % 64 == 0 and y.shape[-1] <= 2048:
+        seed, off = RNG.next()
+        shp = y.shape
+        out = _AddLNFn.apply(y.reshape(-1, shp[-1]).contiguous(),
+                             None if residual is None else residual.reshape(-1, shp[-1]).contiguous(),
+                             weight, bias, shadow(weight, y.dtype), shadow(bias, y.dtype),
+                             p, eps, seed, off)
+        return out.reshape(shp)
+    h = F.dropout(y, p, True) if p > 0 else y
+    if residual is not None:
+        h = h + residual
+    if h.dtype == torch.float32:
+        return F.layer_norm(h, (h.shape[-1],), weight, bias, eps)
+    return _LNTorchFn.apply(h, weight, bias, eps)
+
+
+class _LNTorchFn(torch.autograd.Function):
+    """Reference LN for bf16 activations with fp32 weight grads (non-native path)."""
+
+    @staticmethod
+    def forward(ctx, x, w, b, eps):
+        xf = x.float()
+        mu = xf.mean(-1, keepdim=True)
+        var = ((xf - mu) ** 2).mean(-1, keepdim=True)
+        rstd = torch.rsqrt(var + eps)
+        xhat = (xf - mu) * rstd
+        out = xhat * w + b
+        ctx.save_for_backward(xhat, rstd, w)
+        return out.to(x.dtype)
+
+    @staticmethod
+    def backward(ctx, dout):
+        xhat, rstd, w = ctx.saved_tensors
+        g = dout.float()
+        d = g.shape[-1]
+        dw = (g * xhat).reshape(-1, d).sum(0)
+        db = g.reshape(-1, d).sum(0)
+        gx = g * w
+        dx = rstd * (gx - gx.mean(-1, keepdim=True) - xhat * (gx * xhat).mean(-1, keepdim=True))
+        return dx.to(dout.dtype), dw, db, None
+
+
+def layer_norm(x, weight, bias, eps=1e-12):
+    return add_dropout_layernorm(x, None, weight, bias, 0.0, eps, training=False)
+
+
+# --------------------------------------------------------------------------- #
+# Attention (bidirectional or causal), qkv packed [B, L, 3, H, D]
+# --------------------------------------------------------------------------- #
+
+class _AttnFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, qkv, n_heads, p, causal, seed, offset):
+        out, lse = get_ext().attn_fwd(qkv, n_heads, float(p), bool(causal), seed, offset)
+        ctx.save_for_backward(qkv, out, lse)
+        ctx.cfg = (n_heads, p, causal, seed, offset)
+        return out
+
+    @staticmethod
+    def backward(ctx, dout):
+        qkv, out, lse = ctx.saved_tensors
+        n_heads, p, causal, seed, offset = ctx.cfg
+        dqkv = get_ext().attn_bwd(dout.contiguous(), qkv, out, lse, n_heads, float(p), bool(causal),
+                                  seed, offset)
+        return dqkv, None, None, None, None, None
+
+
+def attention(qkv, n_heads, p=0.0, causal=False, training=True):
+    """qkv: [B, L, 3*H*D] packed projection output -> [B, L, H*D]."""
+    p = p if training else 0.0
+    B, L, three_hd = qkv.shape
+    hd = three_hd // 3
+    D = hd // n_heads
+    if (qkv.dtype == torch.bfloat16 and native_ok(qkv, kernel="attn_fwd") and D == 64
+            and L % 64 == 0 and L <= 1024):
+        seed, off = RNG.next()
+        return _AttnFn.apply(qkv.contiguous(), n_heads, p, causal, seed, off)
+    q, k, v = qkv.view(B, L, 3, n_heads, D).permute(2, 0, 3, 1, 4).unbind(0)
+    o = F.scaled_dot_product_attention(q, k, v, dropout_p=p, is_causal=causal)
+    return o.transpose(1, 2).reshape(B, L, hd)
+
+
+# --------------------------------------------------------------------------- #
+# Fused linear + cross-entropy (tied lm_head), per-token loss
+# --------------------------------------------------------------------------- #
+
+class _LinearXentFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, w, b, w16, b16, target):
+        loss, lse = get_ext().lxent_fwd(x, w16, b16, target)
+        ctx.save_for_backward(x, w16, b16, target, lse)
+        ctx.has_b = b is not None
+        return loss
+
+    @staticmethod
+    def backward(ctx, dloss):
+        x, w16, b16, target, lse = ctx.saved_tensors
+        dx, dw, db = get_ext().lxent_bwd(dloss.contiguous().float(), x, w16, b16, target, lse,
+                                         ctx.needs_input_grad[0], ctx.needs_input_grad[1],
+                                         ctx.has_b and ctx.needs_input_grad[2])
+        return dx, dw, db, None, None, None
+
+
+def linear_cross_entropy(x, weight, bias, target):
+    """Per-token CE of logits = x @ W^T + b against ``target`` without materialising logits.
+
+    x: [N, E]; weight: [V, E]; target: [N] int64 -> loss [N] fp32.
+    """
+    if (x.dtype == torch.bfloat16 and native_ok(x, kernel="lxent_fwd")
+            and x.shape[-1] % 64 == 0 and x.shape[-1] <= 256):
+        return _LinearXentFn.apply(x.contiguous(), weight, bias, shadow(weight, x.dtype),
+                                   shadow(bias, x.dtype), target.contiguous())
+    logits = linear(x, weight, bias)
+    return F.cross_entropy(logits.float(), target, reduction="none")
+
+
+# --------------------------------------------------------------------------- #
+# Embedding gather with fp32 weight grad
+# --------------------------------------------------------------------------- #
+
+class _EmbFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, ids, w, w16):
+        ctx.save_for_backward(ids)
+        ctx.n = w.shape[0]
+        return F.embedding(ids, w16)
+
+    @staticmethod
+    def backward(ctx, dy):
+        (ids,) = ctx.saved_tensors
+        dw = torch.zeros(ctx.n, dy.shape[-1], dtype=torch.float32, device=dy.device)
+        dw.index_add_(0, ids.reshape(-1), dy.reshape(-1, dy.shape[-1]).float())
+        return None, dw, None
+
+
+def embedding(ids, weight, dtype):
+    if dtype == torch.float32:
+        return F.embedding(ids, weight)
+    return _EmbFn.apply(ids, weight, shadow(weight, dtype))
+
+
+def timestep_embedding(timesteps, dim, max_period=10000):
+    """Sinusoidal embedding [cos | sin] (DiffuSeq / guided-diffusion convention)."""
+    half = dim // 2
+    freqs = torch.exp(-math.log(max_period) *
+                      torch.arange(half, dtype=torch.float32, device=timesteps.device) / half)
+    args = timesteps[:, None].float() * freqs[None]
+    emb = torch.cat([torch.cos(args), torch.sin(args)], dim=-1)
+    if dim % 2:
+        emb = torch.cat([emb, torch.zeros_like(emb[:, :1])], dim=-1)
+    return emb

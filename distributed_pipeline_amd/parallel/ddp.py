@@ -1,0 +1,220 @@
+"""
+Native data-parallel engine (SURVEY N-1/P-DP/P-GA): the MI355X replacement for
+``torch.nn.parallel.DistributedDataParallel`` as used by the reference trainer
+(reference: utils/trainer.py:115-128, 209-221).
+
+Design (xGMI/RCCL-first rather than a translation of the C++ Reducer):
+
+* Gradients live in ONE flat fp32 buffer (:class:`FlatParamSpace`); buckets are
+  contiguous slices of it, so a bucket all-reduce reads/writes the gradients
+  in place - no copy-in/copy-out kernels.
+* Bucket sizes are chosen for point-to-point xGMI rings, not NVSwitch: a small
+  first bucket (default 4 MiB) so RCCL starts while backward is still deep in
+  the network, then ~32 MiB buckets - large enough to saturate a ring's links,
+  small enough to overlap.  (reference: ``bucket_cap_mb=128``.)
+* Readiness: a post-accumulate-grad hook per parameter decrements its bucket's
+  pending counter; the bucket whose counter hits zero is all-reduced
+  asynchronously (RCCL on its own internal stream, ordered after the
+  gradient-producing kernels of the current stream).  Buckets are launched in
+  order so every rank issues collectives in the same sequence.
+* ``no_sync()`` has torch-DDP semantics: the decision is taken at *forward*
+  time, so gradient accumulation over micro-batches issues exactly one
+  reduction per optimizer step (SURVEY P-GA).
+* The 1/world averaging is NOT applied here: the fused AdamW kernel folds it
+  into its gradient scale (one fewer pass over 348 MiB per step).  Call
+  :meth:`average_gradients` if a plain torch optimizer consumes the grads.
+* Startup: one flat broadcast of all parameters from rank 0 plus a shape
+  checksum all-reduce (replaces DDP's per-tensor broadcast, SURVEY X-4).
+* HIP-graph mode: when backward runs inside a captured graph no Python hook
+  fires; :meth:`finalize` then launches every bucket after the replay.
+"""
+import contextlib
+
+import torch
+import torch.distributed as dist
+from torch import nn
+
+from .flat import FlatParamSpace
+
+_MiB = 1024 * 1024
+
+
+def plan_buckets(space, cap_mb, first_mb):
+    """Split the flat layout into contiguous buckets at parameter boundaries."""
+    layout = space.layout
+    starts = [space.offsets[id(p)] for p in layout] + [space.numel]
+    buckets = []
+    cur_start, cur_params = 0, []
+    limit = first_mb * _MiB
+    for i, p in enumerate(layout):
+        cur_params.append(p)
+        end = starts[i + 1]
+        if (end - cur_start) * 4 >= limit or i == len(layout) - 1:
+            buckets.append((cur_start, end if i < len(layout) - 1 else space.numel, cur_params))
+            cur_start, cur_params = end, []
+            limit = cap_mb * _MiB
+    return buckets
+
+
+class _Bucket:
+    __slots__ = ("index", "start", "end", "params", "pending", "work", "launched")
+
+    def __init__(self, index, start, end, params):
+        self.index, self.start, self.end, self.params = index, start, end, params
+        self.pending = len(params)
+        self.work = None
+        self.launched = False
+
+
+class DDPEngine(nn.Module):
+    def __init__(self, module, *, device=None, bucket_cap_mb=32.0, first_bucket_mb=4.0,
+                 shadow_dtype=None, process_group=None, reduce_dtype=torch.float32,
+                 broadcast_from_rank0=True, space=None):
+        super().__init__()
+        self.module = module
+        self.pg = process_group
+        self.space = space or FlatParamSpace(module.parameters(), device=device,
+                                             shadow_dtype=shadow_dtype)
+        self.distributed = dist.is_available() and dist.is_initialized()
+        self.world_size = dist.get_world_size(self.pg) if self.distributed else 1
+        self.reduce_dtype = reduce_dtype
+        self._sync_enabled = True
+        self._armed = False
+        self._next_launch = 0
+        self.bucket_cap_mb, self.first_bucket_mb = bucket_cap_mb, first_bucket_mb
+        self.buckets = [_Bucket(i, s, e, ps) for i, (s, e, ps) in
+                        enumerate(plan_buckets(self.space, bucket_cap_mb, first_bucket_mb))]
+        self._bucket_of = {}
+        for b in self.buckets:
+            for p in b.params:
+                self._bucket_of[id(p)] = b
+        self._hooks = []
+        if self.distributed:
+            self._verify_shapes()
+            if broadcast_from_rank0:
+                self.broadcast_parameters()
+            for p in self.space.layout:
+                self._hooks.append(p.register_post_accumulate_grad_hook(self._make_hook(p)))
+        self._comm_buf = None
+
+    # -- setup ---------------------------------------------------------------
+    def _coll_device(self):
+        return self.space.device
+
+    def _verify_shapes(self):
+        sig = torch.tensor([self.space.numel, len(self.space.layout),
+                            sum((i + 1) * p.numel() for i, p in enumerate(self.space.layout))],
+                           dtype=torch.int64, device=self._coll_device())
+        mx, mn = sig.clone(), sig.clone()
+        dist.all_reduce(mx, op=dist.ReduceOp.MAX, group=self.pg)
+        dist.all_reduce(mn, op=dist.ReduceOp.MIN, group=self.pg)
+        if not torch.equal(mx, mn):
+            raise RuntimeError("DDPEngine: parameter shapes differ across ranks")
+
+    def broadcast_parameters(self, src=0):
+        if self.distributed:
+            dist.broadcast(self.space.param_flat, src, group=self.pg)
+            self.space.refresh_shadow()
+
+    def broadcast_flat(self, flat, src=0):
+        if self.distributed:
+            dist.broadcast(flat, src, group=self.pg)
+
+    # -- forward ---------------------------------------------------------------
+    def forward(self, *args, **kwargs):
+        if self.distributed and torch.is_grad_enabled() and self.training:
+            self._armed = self._sync_enabled
+            if self._armed:
+                for b in self.buckets:
+                    b.pending = len(b.params)
+                    b.work = None
+                    b.launched = False
+                self._next_launch = 0
+        return self.module(*args, **kwargs)
+
+    @contextlib.contextmanager
+    def no_sync(self):
+        prev = self._sync_enabled
+        self._sync_enabled = False
+        try:
+            yield
+        finally:
+            self._sync_enabled = prev
+
+    # -- reduction ----------------------------------------------------------------
+    def _make_hook(self, p):
+        def hook(_param):
+            if not self._armed:
+                return
+            b = self._bucket_of[id(p)]
+            b.pending -= 1
+            if b.pending == 0:
+                self._launch_ready_in_order()
+        return hook
+
+    def _launch_ready_in_order(self):
+        while self._next_launch < len(self.buckets):
+            b = self.buckets[self._next_launch]
+            if b.pending > 0:
+                return
+            self._launch(b)
+            self._next_launch += 1
+
+    def _launch(self, b):
+        if b.launched:
+            return
+        view = self.space.grad_flat[b.start:b.end]
+        if self.reduce_dtype == torch.float32:
+            b.work = dist.all_reduce(view, group=self.pg, async_op=True)
+        else:  # narrow wire format: pack, reduce, unpack (fp32 accumulation of ranks in RCCL)
+            if self._comm_buf is None:
+                self._comm_buf = torch.empty(self.space.numel, dtype=self.reduce_dtype,
+                                             device=self.space.device)
+            buf = self._comm_buf[b.start:b.end]
+            buf.copy_(view)
+            b.work = (dist.all_reduce(buf, group=self.pg, async_op=True), buf, view)
+        b.launched = True
+
+    def finalize(self):
+        """Wait for (and launch any not-yet-launched) bucket reductions."""
+        if not self.distributed or not self._armed:
+            return
+        for b in self.buckets[self._next_launch:]:
+            self._launch(b)
+        self._next_launch = len(self.buckets)
+        for b in self.buckets:
+            w = b.work
+            if isinstance(w, tuple):
+                w[0].wait()
+                w[2].copy_(w[1])
+            elif w is not None:
+                w.wait()
+            b.work = None
+        self._armed = False
+
+    def reduce_all_now(self):
+        """Graph mode: backward ran without hooks; reduce every bucket now."""
+        if not self.distributed:
+            return
+        self._armed = True
+        for b in self.buckets:
+            b.launched = False
+        self._next_launch = 0
+        self.finalize()
+
+    def average_gradients(self):
+        if self.world_size > 1:
+            self.space.grad_flat.mul_(1.0 / self.world_size)
+
+    def zero_grad(self, set_to_none=False):  # noqa: ARG002 - flat grads are never None
+        self.space.zero_grad()
+
+    # -- misc -----------------------------------------------------------------------
+    def bucket_sizes_mb(self):
+        return [round((b.end - b.start) * 4 / _MiB, 3) for b in self.buckets]
+
+    def state_dict(self, *args, **kwargs):
+        return self.module.state_dict(*args, **kwargs)
+
+    def load_state_dict(self, *args, **kwargs):
+        return self.module.load_state_dict(*args, **kwargs)
