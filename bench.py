@@ -1,0 +1,189 @@
+"""
+Headline benchmark (BASELINE.json): DiffuSeq-base, seq 128, DDP training
+throughput on N MI355X of one node, one process per GPU over RCCL/xGMI.
+
+    python bench.py --gpus N --steps K --warmup W
+    (N>1: python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 ... bench.py ...)
+
+A *step* is exactly the reference's optimizer step (reference
+utils/trainer.py:198-201 + config/train.py defaults): 2048 samples per rank
+(global batch 2048*N), gradient accumulation over micro-batches of 64, one
+all-reduce, AdamW, 3 EMA rates, grad-norm logging, linear LR decay, logger
+dump every 20 steps.  Synthetic tokens, random-init weights.
+
+Reported ``value`` is the whole-job aggregate: optimizer steps/s x N
+(= samples/s / 2048), so it scales with N under weak scaling; rank-local
+steps/s, samples/s and tokens/s are reported alongside.
+
+``--reference-equivalent`` runs the reference's configuration instead (fp32,
+torch DistributedDataParallel with bucket_cap_mb=128, torch AdamW, eager
+PyTorch model) - the measured baseline in BASELINE.md.
+"""
+import argparse
+import json
+import os
+import sys
+import tempfile
+import time
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, HERE)
+
+METRIC = "train steps/sec (whole node), DiffuSeq-base seq128 DDP at 1/2/4/8 MI355X"
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--batch-size", type=int, default=2048)
+    ap.add_argument("--microbatch", type=int, default=64)
+    ap.add_argument("--exec-microbatch", type=int, default=-1,
+                    help="samples per executed fwd/bwd (-1: engine default)")
+    ap.add_argument("--seq-len", type=int, default=128)
+    ap.add_argument("--config-name", default="bert-base-uncased")
+    ap.add_argument("--model", default="diffuseq")
+    ap.add_argument("--reference-equivalent", action="store_true")
+    ap.add_argument("--precision", default=None)
+    ap.add_argument("--bucket-cap-mb", type=float, default=32.0)
+    ap.add_argument("--first-bucket-mb", type=float, default=4.0)
+    ap.add_argument("--hip-graphs", type=int, default=0)
+    ap.add_argument("--data-workers", type=int, default=2)
+    ap.add_argument("--log-interval", type=int, default=20)
+    ap.add_argument("--json-out", default=None)
+    return ap.parse_args()
+
+
+DEFAULT_EXEC_MB = 2048
+
+
+def main():
+    a = parse()
+    import torch
+    import torch.distributed as dist
+
+    from basic_utils import dist_util, logger
+    from data import load_data_from_args
+    from utils.initialization import create_diffusion_from_config, create_model_from_config, seed_all
+    from utils.trainer import DiffusionTrainLoop, LMTrainLoop
+
+    if int(os.environ.get("WORLD_SIZE", "1")) > 1:
+        dist_util.setup_dist(silent=True)
+    rank, world = dist_util.get_rank(), dist_util.get_world_size()
+    if a.gpus != world and rank == 0:
+        print(f"<WARN> --gpus {a.gpus} but WORLD_SIZE={world}", file=sys.stderr)
+    dev = dist_util.dev()
+    if dev.type == "cuda":
+        torch.cuda.set_device(dev)
+
+    ref = a.reference_equivalent
+    precision = a.precision or ("fp32" if ref else "bf16")
+    engine = "torch" if ref else "native"
+    exec_mb = a.exec_microbatch
+    if exec_mb < 0:
+        exec_mb = a.microbatch if ref else min(DEFAULT_EXEC_MB, a.batch_size)
+
+    logdir = tempfile.mkdtemp(prefix="dpa_bench_")
+    logger.configure(dir=logdir, format_strs=["log"] if rank == 0 else [])
+    seed_all(102)
+    settings = dict(model=a.model, precision=precision, config_name=a.config_name,
+                    seq_len=a.seq_len, vocab_size=30522 if a.model != "gpt2" else 50257,
+                    hidden_dim=128, hidden_t_dim=128, dropout=0.1)
+    model = create_model_from_config(**settings).to(dev)
+    n_params = sum(p.numel() for p in model.parameters())
+    data = load_data_from_args("train", "synthetic", a.batch_size, deterministic=False, loop=True,
+                               num_loader_proc=a.data_workers, dataset="synthetic",
+                               seq_len=a.seq_len, vocab_size=settings["vocab_size"], seed=102 + rank,
+                               model=a.model)
+    kw = dict(model=model, data=data, batch_size=a.batch_size, microbatch=a.microbatch, lr=1e-4,
+              ema_rate="0.5,0.9,0.99", log_interval=a.log_interval, save_interval=10 ** 9,
+              resume_checkpoint="", weight_decay=0.0, learning_steps=320000,
+              checkpoint_path=logdir, gradient_clipping=0.0, ddp_engine=engine,
+              precision=precision, bucket_cap_mb=a.bucket_cap_mb,
+              first_bucket_mb=a.first_bucket_mb, exec_microbatch=exec_mb,
+              hip_graphs=bool(a.hip_graphs))
+    if a.model == "gpt2":
+        loop = LMTrainLoop(**kw)
+    else:
+        diffusion, sampler = create_diffusion_from_config(diffusion_steps=2000, noise_schedule="sqrt")
+        loop = DiffusionTrainLoop(diffusion=diffusion, schedule_sampler=sampler, **kw)
+
+    def one_step():
+        batch = next(loop.data)
+        loop.run_step(batch)
+        if loop.step % loop.log_interval == 0:
+            logger.dumpkvs()
+        loop.step += 1
+
+    def sync():
+        if dev.type == "cuda":
+            torch.cuda.synchronize()
+        dist_util.barrier()
+
+    t_w = time.time()
+    for _ in range(a.warmup):
+        one_step()
+    sync()
+    warm_s = time.time() - t_w
+    sync()
+    t0 = time.perf_counter()
+    for _ in range(a.steps):
+        one_step()
+    sync()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=dev if dev.type == "cuda" else "cpu")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+
+    ms = elapsed / a.steps * 1e3
+    steps_per_s = a.steps / elapsed
+    value = steps_per_s * world
+    samples_per_s = steps_per_s * a.batch_size * world
+    baseline = None
+    bpath = os.path.join(HERE, "baseline_measured.json")
+    if os.path.exists(bpath) and not ref:
+        with open(bpath) as f:
+            b = json.load(f)
+        per_gpu = b.get("reference_equivalent_steps_per_sec_per_gpu")
+        if per_gpu:
+            baseline = per_gpu * world
+    out = {
+        "metric": METRIC,
+        "value": round(value, 4),
+        "unit": "steps/s summed over GPUs (1 step = 2048 samples x 128 tokens per GPU)",
+        "n_gpus": world,
+        "steps": a.steps,
+        "warmup": a.warmup,
+        "ms_per_step": round(ms, 3),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": round(value / baseline, 3) if baseline else None,
+        "dtype": "bf16" if precision == "bf16" else "fp32",
+        "data": "synthetic (random token ids, random src/trg split; random-init weights)",
+        "config": {"model": "DiffuSeq-base" if a.config_name == "bert-base-uncased" else a.config_name,
+                   "global_batch": a.batch_size * world, "per_gpu_batch": a.batch_size,
+                   "microbatch": a.microbatch, "exec_microbatch": loop.exec_microbatch,
+                   "seq_len": a.seq_len, "parallelism": f"dp{world}",
+                   "engine": engine, "params": n_params},
+        "optimizer_steps_per_sec": round(steps_per_s, 4),
+        "samples_per_sec": round(samples_per_s, 1),
+        "tokens_per_sec": round(samples_per_s * a.seq_len, 1),
+        "warmup_s": round(warm_s, 2),
+    }
+    if engine == "native":
+        out["config"]["bucket_mb"] = loop.ddp_model.bucket_sizes_mb()
+    if rank == 0:
+        line = json.dumps(out)
+        print(line, flush=True)
+        if a.json_out:
+            with open(a.json_out, "w") as f:
+                f.write(line + "\n")
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

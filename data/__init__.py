@@ -20,12 +20,6 @@ def _identity_collate(batch):
     return batch
 
 
-def _pin_collate(batch):
-    if isinstance(batch, dict):
-        return {k: (v.pin_memory() if torch.cuda.is_available() else v) for k, v in batch.items()}
-    return torch.utils.data.default_collate(batch)
-
-
 def make_dataset(split, data_dir, *, dataset="synthetic", seq_len=128, vocab_size=30522, seed=0,
                  model="diffuseq", n_samples=None):
     if dataset in ("synthetic", "dataset") or dataset.startswith("synthetic"):
@@ -67,7 +61,7 @@ def load_data_from_args(
         shuffle = False
     batched = hasattr(data, "__getitems__")
     pin = torch.cuda.is_available() if pin_memory is None else pin_memory
-    collate = (_pin_collate if pin else _identity_collate) if batched else None
+    collate = _identity_collate if batched else None  # pinning happens in the main process
     loader = DataLoader(
         data,
         batch_size=batch_size,
@@ -76,7 +70,7 @@ def load_data_from_args(
         num_workers=num_loader_proc,
         persistent_workers=num_loader_proc > 0,
         collate_fn=collate,
-        pin_memory=pin and not batched,
+        pin_memory=pin,
         drop_last=True,
     )
     if loop:

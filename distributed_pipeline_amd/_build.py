@@ -55,7 +55,7 @@ def _hash_files(paths, extra):
     h = hashlib.sha256()
     for p in sorted(paths):
         with open(p, "rb") as f:
-            h.update(p.encode())
+            h.update(os.path.basename(p).encode())
             h.update(f.read())
     h.update(extra.encode())
     return h.hexdigest()[:16]

@@ -83,10 +83,174 @@ static void cast_bf16(const at::Tensor& src, at::Tensor& dst) {
                         src.numel(), cur_stream());
 }
 
+// ---- fused linear + cross-entropy ---------------------------------------------
+static inline const uint16_t* bf_ptr(const at::Tensor& t) {
+  return reinterpret_cast<const uint16_t*>(t.data_ptr());
+}
+static inline const uint16_t* opt_bf_ptr(const c10::optional<at::Tensor>& t) {
+  return (t.has_value() && t->defined()) ? bf_ptr(*t) : nullptr;
+}
+
+static void check_lxent(const at::Tensor& x, const at::Tensor& W, const c10::optional<at::Tensor>& b,
+                        const at::Tensor& tgt) {
+  CHECK_DEV(x); CHECK_DEV(W); CHECK_DEV(tgt);
+  CHECK_BF16(x); CHECK_BF16(W); CHECK_CONTIG(x); CHECK_CONTIG(W); CHECK_CONTIG(tgt);
+  TORCH_CHECK(x.dim() == 2 && W.dim() == 2 && x.size(1) == W.size(1), "x [N,E], W [V,E]");
+  TORCH_CHECK(x.size(1) == 128 || x.size(1) == 256, "lxent: E must be 128 or 256");
+  TORCH_CHECK(tgt.scalar_type() == at::kLong && tgt.numel() == x.size(0), "target [N] int64");
+  if (b.has_value() && b->defined()) {
+    CHECK_BF16((*b)); CHECK_CONTIG((*b));
+    TORCH_CHECK(b->numel() == W.size(0), "bias [V]");
+  }
+}
+
+static std::vector<at::Tensor> lxent_fwd(const at::Tensor& x, const at::Tensor& W,
+                                         c10::optional<at::Tensor> b, const at::Tensor& tgt) {
+  check_lxent(x, W, b, tgt);
+  const c10::DeviceGuard guard(x.device());
+  const int N = (int)x.size(0), V = (int)W.size(0), E = (int)x.size(1);
+  auto f32 = x.options().dtype(at::kFloat);
+  at::Tensor loss = at::empty({N}, f32), lse = at::empty({N}, f32);
+  at::Tensor ws = at::empty({dpa::lxent_workspace_floats(N, V)}, f32);
+  if (N > 0)
+    dpa::launch_lxent_fwd(bf_ptr(x), bf_ptr(W), opt_bf_ptr(b), tgt.data_ptr<int64_t>(), N, V, E,
+                          loss.data_ptr<float>(), lse.data_ptr<float>(), ws.data_ptr<float>(),
+                          cur_stream());
+  return {loss, lse};
+}
+
+static std::vector<at::Tensor> lxent_bwd(const at::Tensor& dloss, const at::Tensor& x,
+                                         const at::Tensor& W, c10::optional<at::Tensor> b,
+                                         const at::Tensor& tgt, const at::Tensor& lse, bool need_dx,
+                                         bool need_dw, bool need_db) {
+  check_lxent(x, W, b, tgt);
+  CHECK_F32(dloss); CHECK_F32(lse); CHECK_CONTIG(dloss); CHECK_CONTIG(lse);
+  const c10::DeviceGuard guard(x.device());
+  const int N = (int)x.size(0), V = (int)W.size(0), E = (int)x.size(1);
+  auto f32 = x.options().dtype(at::kFloat);
+  at::Tensor dx, dW, db;
+  if (need_dx) {
+    dx = at::empty_like(x);
+    at::Tensor acc;
+    if (dpa::lxent_dx_needs_acc(N)) acc = at::zeros({(int64_t)N * E}, f32);
+    if (N > 0)
+      dpa::launch_lxent_dx(bf_ptr(x), bf_ptr(W), opt_bf_ptr(b), tgt.data_ptr<int64_t>(),
+                           lse.data_ptr<float>(), dloss.data_ptr<float>(), N, V, E,
+                           reinterpret_cast<uint16_t*>(dx.data_ptr()),
+                           acc.defined() ? acc.data_ptr<float>() : nullptr, cur_stream());
+  }
+  if (need_dw || need_db) {
+    dW = at::zeros({V, E}, f32);
+    if (need_db) db = at::zeros({V}, f32);
+    if (N > 0)
+      dpa::launch_lxent_dw(bf_ptr(x), bf_ptr(W), opt_bf_ptr(b), tgt.data_ptr<int64_t>(),
+                           lse.data_ptr<float>(), dloss.data_ptr<float>(), N, V, E,
+                           dW.data_ptr<float>(), need_db ? db.data_ptr<float>() : nullptr,
+                           cur_stream());
+    if (!need_dw) dW = at::Tensor();
+  }
+  return {dx, dW, db};
+}
+
+// ---- fused dropout + residual + LayerNorm ------------------------------------------
+static std::vector<at::Tensor> add_ln_fwd(const at::Tensor& y, c10::optional<at::Tensor> res,
+                                          const at::Tensor& g, const at::Tensor& b, double p,
+                                          double eps, int64_t seed, int64_t offset) {
+  CHECK_DEV(y); CHECK_BF16(y); CHECK_CONTIG(y); CHECK_BF16(g); CHECK_BF16(b);
+  TORCH_CHECK(y.dim() == 2, "y must be [R, D]");
+  const int64_t R = y.size(0);
+  const int D = (int)y.size(1);
+  TORCH_CHECK(g.numel() == D && b.numel() == D, "gamma/beta size");
+  const uint16_t* rp = nullptr;
+  if (res.has_value() && res->defined()) {
+    CHECK_BF16((*res)); CHECK_CONTIG((*res));
+    TORCH_CHECK(res->sizes() == y.sizes(), "residual shape");
+    rp = bf_ptr(*res);
+  }
+  const c10::DeviceGuard guard(y.device());
+  at::Tensor out = at::empty_like(y), hs = at::empty_like(y);
+  auto f32 = y.options().dtype(at::kFloat);
+  at::Tensor mean = at::empty({R}, f32), rstd = at::empty({R}, f32);
+  bool ok = dpa::launch_add_ln_fwd(bf_ptr(y), rp, bf_ptr(g), bf_ptr(b),
+                                   reinterpret_cast<uint16_t*>(out.data_ptr()),
+                                   reinterpret_cast<uint16_t*>(hs.data_ptr()), mean.data_ptr<float>(),
+                                   rstd.data_ptr<float>(), R, D, (float)p, (float)eps,
+                                   (uint32_t)seed, (uint32_t)offset, cur_stream());
+  TORCH_CHECK(ok, "add_ln_fwd: unsupported hidden size ", D);
+  return {out, hs, mean, rstd};
+}
+
+static std::vector<at::Tensor> add_ln_bwd(const at::Tensor& dout, const at::Tensor& hs,
+                                          const at::Tensor& mean, const at::Tensor& rstd,
+                                          const at::Tensor& g, double p, int64_t seed,
+                                          int64_t offset, bool need_dres, bool need_dy) {
+  CHECK_DEV(dout); CHECK_BF16(dout); CHECK_CONTIG(dout); CHECK_BF16(hs); CHECK_CONTIG(hs);
+  const int64_t R = dout.size(0);
+  const int D = (int)dout.size(1);
+  const c10::DeviceGuard guard(dout.device());
+  at::Tensor dres, dy;
+  if (need_dres) dres = at::empty_like(dout);
+  if (need_dy) dy = at::empty_like(dout);
+  auto f32 = dout.options().dtype(at::kFloat);
+  const int nb = dpa::ln_bwd_blocks(R);
+  at::Tensor part = at::empty({2 * (int64_t)nb * D}, f32);
+  at::Tensor dg = at::empty({D}, f32), db = at::empty({D}, f32);
+  bool ok = dpa::launch_add_ln_bwd(
+      bf_ptr(dout), bf_ptr(hs), mean.data_ptr<float>(), rstd.data_ptr<float>(), bf_ptr(g),
+      need_dres ? reinterpret_cast<uint16_t*>(dres.data_ptr()) : nullptr,
+      need_dy ? reinterpret_cast<uint16_t*>(dy.data_ptr()) : nullptr, part.data_ptr<float>(),
+      dg.data_ptr<float>(), db.data_ptr<float>(), R, D, (float)p, (uint32_t)seed, (uint32_t)offset,
+      cur_stream());
+  TORCH_CHECK(ok, "add_ln_bwd: unsupported hidden size ", D);
+  return {dres, dy, dg, db};
+}
+
+// ---- bias + activation epilogues ------------------------------------------------------
+static std::vector<at::Tensor> bias_act_fwd(at::Tensor& z, c10::optional<at::Tensor> b, int64_t act) {
+  CHECK_DEV(z); CHECK_BF16(z); CHECK_CONTIG(z);
+  TORCH_CHECK(z.dim() == 2 && z.size(1) % 8 == 0, "z must be [R, N] with N % 8 == 0");
+  const int64_t R = z.size(0);
+  const int N = (int)z.size(1);
+  const uint16_t* bp = opt_bf_ptr(b);
+  if (bp) TORCH_CHECK(b->numel() == N, "bias size");
+  const c10::DeviceGuard guard(z.device());
+  at::Tensor y = act == 0 ? z : at::empty_like(z);
+  if (bp || act != 0)
+    dpa::launch_bias_act_fwd(reinterpret_cast<uint16_t*>(z.data_ptr()), bp,
+                             act == 0 ? nullptr : reinterpret_cast<uint16_t*>(y.data_ptr()), R, N,
+                             (int)act, cur_stream());
+  return {z, y};
+}
+
+static std::vector<at::Tensor> bias_act_bwd(const at::Tensor& dy, const at::Tensor& zy, int64_t act,
+                                            bool want_db) {
+  CHECK_DEV(dy); CHECK_BF16(dy); CHECK_CONTIG(dy);
+  const int64_t R = dy.size(0);
+  const int N = (int)dy.size(1);
+  TORCH_CHECK(N % 8 == 0, "N % 8");
+  const c10::DeviceGuard guard(dy.device());
+  at::Tensor dz = act == 0 ? dy : at::empty_like(dy);
+  at::Tensor db;
+  if (want_db) db = at::zeros({N}, dy.options().dtype(at::kFloat));
+  if (act != 0 || want_db) {
+    CHECK_CONTIG(zy);
+    dpa::launch_bias_act_bwd(bf_ptr(dy), bf_ptr(zy),
+                             act == 0 ? nullptr : reinterpret_cast<uint16_t*>(dz.data_ptr()),
+                             want_db ? db.data_ptr<float>() : nullptr, R, N, (int)act, cur_stream());
+  }
+  return {dz, db};
+}
+
 PYBIND11_MODULE(_C, m) {
   m.doc() = "distributed_pipeline_amd native gfx950 kernels";
   m.def("sqnorm", &sqnorm, "flat grad L2 norm + clip coefficient (device)");
   m.def("adamw_ema", &adamw_ema, "fused AdamW + EMA + bf16 shadow refresh");
   m.def("ema_update", &ema_update, "flat EMA update");
   m.def("cast_bf16", &cast_bf16, "flat fp32->bf16");
+  m.def("add_ln_fwd", &add_ln_fwd, "LN(dropout(y)+res) -> (out, hsave, mean, rstd)");
+  m.def("add_ln_bwd", &add_ln_bwd, "backward of add_ln_fwd -> (dres, dy, dgamma, dbeta)");
+  m.def("bias_act_fwd", &bias_act_fwd, "z += bias (in place); y = act(z) -> (z, y)");
+  m.def("bias_act_bwd", &bias_act_bwd, "dz = dy*act'(zy); db = colsum(dz) -> (dz, db)");
+  m.def("lxent_fwd", &lxent_fwd, "fused linear + cross-entropy forward -> (loss, lse)");
+  m.def("lxent_bwd", &lxent_bwd, "fused linear + cross-entropy backward -> (dx, dW fp32, db fp32)");
 }

@@ -17,4 +17,32 @@ void launch_adamw_ema(float* p, const void* g, bool g_bf16, float* m, float* v, 
 void launch_ema(float* e, const float* p, int64_t n, float rate, hipStream_t s);
 void launch_cast_bf16(const float* src, uint16_t* dst, int64_t n, hipStream_t s);
 
+// ---- xent.hip (fused linear + cross-entropy) ----------------------------------
+int64_t lxent_workspace_floats(int N, int V);
+bool lxent_dx_needs_acc(int N);
+void launch_lxent_fwd(const uint16_t* x, const uint16_t* W, const uint16_t* b, const int64_t* tgt,
+                      int N, int V, int E, float* loss, float* lse, float* ws, hipStream_t s);
+void launch_lxent_dx(const uint16_t* x, const uint16_t* W, const uint16_t* b, const int64_t* tgt,
+                     const float* lse, const float* dloss, int N, int V, int E, uint16_t* dx,
+                     float* dx_acc, hipStream_t s);
+void launch_lxent_dw(const uint16_t* x, const uint16_t* W, const uint16_t* b, const int64_t* tgt,
+                     const float* lse, const float* dloss, int N, int V, int E, float* dW, float* db,
+                     hipStream_t s);
+
+// ---- norm.hip (fused dropout + residual + LayerNorm) ---------------------------
+bool launch_add_ln_fwd(const uint16_t* y, const uint16_t* res, const uint16_t* g, const uint16_t* b,
+                       uint16_t* out, uint16_t* hsave, float* mean, float* rstd, int64_t R, int D,
+                       float p, float eps, uint32_t seed, uint32_t off, hipStream_t s);
+int ln_bwd_blocks(int64_t R);
+bool launch_add_ln_bwd(const uint16_t* dout, const uint16_t* hsave, const float* mean,
+                       const float* rstd, const uint16_t* g, uint16_t* dres, uint16_t* dy, float* part,
+                       float* dg, float* db, int64_t R, int D, float p, uint32_t seed, uint32_t off,
+                       hipStream_t s);
+
+// ---- elementwise.hip (bias + activation epilogues) -------------------------------
+void launch_bias_act_fwd(uint16_t* z, const uint16_t* bias, uint16_t* y, int64_t R, int N, int act,
+                         hipStream_t s);
+void launch_bias_act_bwd(const uint16_t* dy, const uint16_t* zy, uint16_t* dz, float* db, int64_t R,
+                         int N, int act, hipStream_t s);
+
 }  // namespace dpa

@@ -1,0 +1,65 @@
+// CDNA4 (gfx950) matrix-core helpers: bf16 MFMA 32x32x16 with fp32 accumulate,
+// fragment loaders and the LDS transposed read.
+//
+// v_mfma_f32_32x32x16_bf16 lane maps (lane l, r = l & 31, h = l >> 5):
+//   A (32 x 16):  lane l holds A[row r][k = 8h + j], j = 0..7   (8 bf16, 4 VGPRs)
+//   B (16 x 32):  lane l holds B[k = 8h + j][col r]
+//   C/D (32x32):  reg i (0..15) of lane l is C[row (i&3) + 8*(i>>2) + 4h][col r]
+//
+// "Accumulator as the next operand": a C tile X (rows in registers, column on
+// the lane) converted pairwise to bf16 is directly the A operand of Z = X^T*B
+// (k-step s uses registers 8s..8s+7), with the k order permuted: element j of
+// lane half h is row 16s + 8(j>>2) + 4h + (j&3) of X - the B operand must be
+// loaded in that same k order (see tr_rows_for_acc_operand below).
+#pragma once
+#include "common.h"
+
+namespace dpa {
+
+typedef __attribute__((ext_vector_type(8))) __bf16 bf16x8_t;
+
+__device__ __forceinline__ f32x16 mfma32(const bf16x8& a, const bf16x8& b, const f32x16& c) {
+  return __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8_t, a),
+                                                 __builtin_bit_cast(bf16x8_t, b), c, 0, 0, 0);
+}
+
+__device__ __forceinline__ f32x16 zero16() {
+  f32x16 z;
+#pragma unroll
+  for (int i = 0; i < 16; ++i) z[i] = 0.f;
+  return z;
+}
+
+// Row index (within the 32x32 tile) of accumulator register i for lane half h.
+__device__ __forceinline__ int acc_row(int i, int h) { return (i & 3) + 8 * (i >> 2) + 4 * h; }
+
+// Pack accumulator registers 8s..8s+7 (scaled) to a bf16x8 A/B fragment.
+__device__ __forceinline__ bf16x8 acc_to_frag(const f32x16& c, int s) {
+  bf16x8 f;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) f[j] = (short)f2bf(c[8 * s + j]);
+  return f;
+}
+
+// 16-byte global load as a fragment (8 bf16).
+__device__ __forceinline__ bf16x8 ld_frag(const bf16_t* p) {
+  return *reinterpret_cast<const bf16x8*>(p);
+}
+
+// LDS byte offset of 16-byte chunk `ch` of row `row` for a [rows][ROWBYTES]
+// bf16 tile with XOR swizzle (conflict-free ds_read_b128 row reads and 8-byte
+// transposed reads).  ROWBYTES is a multiple of 256.
+template <int ROWBYTES>
+__device__ __forceinline__ int swz(int row, int ch) {
+  return row * ROWBYTES + ((ch ^ (row & 15)) << 4);
+}
+
+// ds_read_b64_tr_b16: per 16-lane group, lane 4q+p supplies the address of
+// row q (cols 4p..4p+3) of a 4x16 block; lane i of the group receives column
+// i of the 4 rows (row q in element q).
+typedef __attribute__((address_space(3))) bf16x4 lds_bf16x4;
+__device__ __forceinline__ bf16x4 ds_read_tr16(const void* lds_ptr) {
+  return __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_bf16x4*)(lds_ptr));
+}
+
+}  // namespace dpa

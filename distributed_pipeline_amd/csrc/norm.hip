@@ -1,0 +1,251 @@
+// Fused post-LN residual block epilogue (SURVEY K-M6/K-M9/K-M10):
+//
+//   h   = dropout_p(y) + residual          (either term optional)
+//   out = LayerNorm(h) * gamma + beta      -> bf16; saves h (bf16), mean, rstd
+//
+// and its backward (dy, dresidual, dgamma, dbeta) in one pass per row.  One
+// wave64 owns a row: D/64 contiguous elements per lane (D = 768 -> 12), loaded
+// as 8-byte vectors, so a row is one fully coalesced 1.5 KiB transaction and
+// both reductions are a single wave-wide shuffle tree (no LDS, no barriers).
+// The dropout mask is never stored: it is regenerated from the counter-based
+// Philox stream (seed, offset, row, column) in the backward.
+//
+// dgamma/dbeta: each block accumulates its rows' contributions in registers,
+// writes one fp32 partial row; a second kernel sums the partials per column.
+#include "common.h"
+#include "launchers.h"
+
+namespace dpa {
+
+template <int VEC>
+struct RowIO {
+  // load VEC bf16 (VEC % 4 == 0 uses 8-byte vectors)
+  __device__ __forceinline__ static void load(const bf16_t* p, float* v) {
+    if constexpr (VEC % 4 == 0) {
+#pragma unroll
+      for (int c = 0; c < VEC / 4; ++c) {
+        uint2 raw = *reinterpret_cast<const uint2*>(p + 4 * c);
+        v[4 * c + 0] = __uint_as_float(raw.x << 16);
+        v[4 * c + 1] = __uint_as_float(raw.x & 0xffff0000u);
+        v[4 * c + 2] = __uint_as_float(raw.y << 16);
+        v[4 * c + 3] = __uint_as_float(raw.y & 0xffff0000u);
+      }
+    } else {
+#pragma unroll
+      for (int c = 0; c < VEC; ++c) v[c] = bf2f(p[c]);
+    }
+  }
+  __device__ __forceinline__ static void store(bf16_t* p, const float* v) {
+    if constexpr (VEC % 4 == 0) {
+#pragma unroll
+      for (int c = 0; c < VEC / 4; ++c) {
+        uint2 raw;
+        raw.x = pack_bf2(v[4 * c + 0], v[4 * c + 1]);
+        raw.y = pack_bf2(v[4 * c + 2], v[4 * c + 3]);
+        *reinterpret_cast<uint2*>(p + 4 * c) = raw;
+      }
+    } else {
+#pragma unroll
+      for (int c = 0; c < VEC; ++c) p[c] = f2bf(v[c]);
+    }
+  }
+};
+
+// keep-mask bits for this lane's VEC elements of `row`, from one Philox call per 4.
+template <int VEC>
+__device__ __forceinline__ void dropout_keep(uint32_t seed, uint32_t offset, int64_t row, int col0,
+                                             float p, bool* keep) {
+  const uint32_t thr = (uint32_t)(p * 4294967296.0);
+#pragma unroll
+  for (int c = 0; c < (VEC + 3) / 4; ++c) {
+    uint32_t r[4];
+    philox4(seed, 0x5bd1e995u, (uint32_t)row, (uint32_t)(row >> 32) ^ (uint32_t)((col0 >> 2) + c),
+            offset, 0xdeadbeefu, r);
+#pragma unroll
+    for (int k = 0; k < 4; ++k)
+      if (4 * c + k < VEC) keep[4 * c + k] = r[k] >= thr;
+  }
+}
+
+template <int VEC>
+__global__ void __launch_bounds__(256) add_ln_fwd_kernel(
+    const bf16_t* __restrict__ y, const bf16_t* __restrict__ res, const bf16_t* __restrict__ gamma,
+    const bf16_t* __restrict__ beta, bf16_t* __restrict__ out, bf16_t* __restrict__ hsave,
+    float* __restrict__ mean_out, float* __restrict__ rstd_out, int64_t R, float p, float eps,
+    uint32_t seed, uint32_t offset) {
+  constexpr int D = VEC * 64;
+  const int lane = threadIdx.x & 63;
+  const int64_t row = (int64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+  if (row >= R) return;
+  const int col0 = lane * VEC;
+  float h[VEC];
+  RowIO<VEC>::load(y + row * D + col0, h);
+  if (p > 0.f) {
+    bool keep[VEC];
+    dropout_keep<VEC>(seed, offset, row, col0, p, keep);
+    const float sc = 1.f / (1.f - p);
+#pragma unroll
+    for (int i = 0; i < VEC; ++i) h[i] = keep[i] ? h[i] * sc : 0.f;
+  }
+  if (res) {
+    float r[VEC];
+    RowIO<VEC>::load(res + row * D + col0, r);
+#pragma unroll
+    for (int i = 0; i < VEC; ++i) h[i] += r[i];
+  }
+  // round h to bf16 first so the backward (which reloads the bf16 copy) is consistent
+#pragma unroll
+  for (int i = 0; i < VEC; ++i) h[i] = bf2f(f2bf(h[i]));
+  if (hsave) RowIO<VEC>::store(hsave + row * D + col0, h);
+  float s = 0.f;
+#pragma unroll
+  for (int i = 0; i < VEC; ++i) s += h[i];
+  const float mean = wave_sum(s) * (1.f / D);
+  float v = 0.f;
+#pragma unroll
+  for (int i = 0; i < VEC; ++i) { const float d = h[i] - mean; v += d * d; }
+  const float rstd = rsqrtf(wave_sum(v) * (1.f / D) + eps);
+  float g[VEC], b[VEC], o[VEC];
+  RowIO<VEC>::load(gamma + col0, g);
+  RowIO<VEC>::load(beta + col0, b);
+#pragma unroll
+  for (int i = 0; i < VEC; ++i) o[i] = (h[i] - mean) * rstd * g[i] + b[i];
+  RowIO<VEC>::store(out + row * D + col0, o);
+  if (lane == 0) {
+    mean_out[row] = mean;
+    rstd_out[row] = rstd;
+  }
+}
+
+// grid-stride over rows; block = 4 waves; partial dgamma/dbeta per block.
+template <int VEC>
+__global__ void __launch_bounds__(256) add_ln_bwd_kernel(
+    const bf16_t* __restrict__ dout, const bf16_t* __restrict__ hsave,
+    const float* __restrict__ mean_in, const float* __restrict__ rstd_in,
+    const bf16_t* __restrict__ gamma, bf16_t* __restrict__ dres, bf16_t* __restrict__ dy,
+    float* __restrict__ part_dg, float* __restrict__ part_db, int64_t R, float p, uint32_t seed,
+    uint32_t offset) {
+  constexpr int D = VEC * 64;
+  __shared__ float red[2][4][D];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int col0 = lane * VEC;
+  float g[VEC], adg[VEC], adb[VEC];
+  RowIO<VEC>::load(gamma + col0, g);
+#pragma unroll
+  for (int i = 0; i < VEC; ++i) { adg[i] = 0.f; adb[i] = 0.f; }
+  const float sc = p > 0.f ? 1.f / (1.f - p) : 1.f;
+  for (int64_t row = (int64_t)blockIdx.x * 4 + w; row < R; row += (int64_t)gridDim.x * 4) {
+    float h[VEC], d[VEC];
+    RowIO<VEC>::load(hsave + row * D + col0, h);
+    RowIO<VEC>::load(dout + row * D + col0, d);
+    const float mean = mean_in[row], rstd = rstd_in[row];
+    float s1 = 0.f, s2 = 0.f;
+#pragma unroll
+    for (int i = 0; i < VEC; ++i) {
+      const float xh = (h[i] - mean) * rstd;
+      adg[i] += d[i] * xh;
+      adb[i] += d[i];
+      const float gx = d[i] * g[i];
+      h[i] = xh;
+      d[i] = gx;
+      s1 += gx;
+      s2 += gx * xh;
+    }
+    s1 = wave_sum(s1) * (1.f / D);
+    s2 = wave_sum(s2) * (1.f / D);
+#pragma unroll
+    for (int i = 0; i < VEC; ++i) d[i] = rstd * (d[i] - s1 - h[i] * s2);
+    if (dres) RowIO<VEC>::store(dres + row * D + col0, d);
+    if (dy) {
+      if (p > 0.f) {
+        bool keep[VEC];
+        dropout_keep<VEC>(seed, offset, row, col0, p, keep);
+#pragma unroll
+        for (int i = 0; i < VEC; ++i) d[i] = keep[i] ? d[i] * sc : 0.f;
+      }
+      RowIO<VEC>::store(dy + row * D + col0, d);
+    }
+  }
+#pragma unroll
+  for (int i = 0; i < VEC; ++i) {
+    red[0][w][col0 + i] = adg[i];
+    red[1][w][col0 + i] = adb[i];
+  }
+  __syncthreads();
+  for (int c = threadIdx.x; c < D; c += blockDim.x) {
+    part_dg[(int64_t)blockIdx.x * D + c] = red[0][0][c] + red[0][1][c] + red[0][2][c] + red[0][3][c];
+    part_db[(int64_t)blockIdx.x * D + c] = red[1][0][c] + red[1][1][c] + red[1][2][c] + red[1][3][c];
+  }
+}
+
+// out[c] = sum_b part[b][c]  (one thread per column, coalesced over c)
+__global__ void __launch_bounds__(256) colsum_kernel(const float* __restrict__ part, int nb, int D,
+                                                    float* __restrict__ out) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= D) return;
+  float s = 0.f;
+  for (int b = 0; b < nb; ++b) s += part[(int64_t)b * D + c];
+  out[c] = s;
+}
+
+#define DPA_LN_DISPATCH(D, FN, ...)                      \
+  switch (D) {                                           \
+    case 64: FN<1>(__VA_ARGS__); break;                  \
+    case 128: FN<2>(__VA_ARGS__); break;                 \
+    case 256: FN<4>(__VA_ARGS__); break;                 \
+    case 512: FN<8>(__VA_ARGS__); break;                 \
+    case 768: FN<12>(__VA_ARGS__); break;                \
+    case 1024: FN<16>(__VA_ARGS__); break;               \
+    case 1536: FN<24>(__VA_ARGS__); break;               \
+    case 2048: FN<32>(__VA_ARGS__); break;               \
+    default: return false;                               \
+  }
+
+template <int VEC>
+static void ln_fwd_impl(const uint16_t* y, const uint16_t* res, const uint16_t* g, const uint16_t* b,
+                        uint16_t* out, uint16_t* hsave, float* mean, float* rstd, int64_t R, float p,
+                        float eps, uint32_t seed, uint32_t off, hipStream_t s) {
+  const unsigned grid = (unsigned)((R + 3) / 4);
+  hipLaunchKernelGGL(add_ln_fwd_kernel<VEC>, dim3(grid), dim3(256), 0, s, (const bf16_t*)y,
+                     (const bf16_t*)res, (const bf16_t*)g, (const bf16_t*)b, (bf16_t*)out,
+                     (bf16_t*)hsave, mean, rstd, R, p, eps, seed, off);
+}
+
+bool launch_add_ln_fwd(const uint16_t* y, const uint16_t* res, const uint16_t* g, const uint16_t* b,
+                       uint16_t* out, uint16_t* hsave, float* mean, float* rstd, int64_t R, int D,
+                       float p, float eps, uint32_t seed, uint32_t off, hipStream_t s) {
+  DPA_LN_DISPATCH(D, ln_fwd_impl, y, res, g, b, out, hsave, mean, rstd, R, p, eps, seed, off, s)
+  return true;
+}
+
+int ln_bwd_blocks(int64_t R) {
+  int64_t nb = (R + 3) / 4;
+  return (int)(nb < 1024 ? nb : 1024);
+}
+
+template <int VEC>
+static void ln_bwd_impl(const uint16_t* dout, const uint16_t* hsave, const float* mean,
+                        const float* rstd, const uint16_t* g, uint16_t* dres, uint16_t* dy,
+                        float* part, float* dg, float* db, int64_t R, float p, uint32_t seed,
+                        uint32_t off, hipStream_t s) {
+  constexpr int D = VEC * 64;
+  const int nb = ln_bwd_blocks(R);
+  float* pdg = part;
+  float* pdb = part + (int64_t)nb * D;
+  hipLaunchKernelGGL(add_ln_bwd_kernel<VEC>, dim3(nb), dim3(256), 0, s, (const bf16_t*)dout,
+                     (const bf16_t*)hsave, mean, rstd, (const bf16_t*)g, (bf16_t*)dres, (bf16_t*)dy,
+                     pdg, pdb, R, p, seed, off);
+  hipLaunchKernelGGL(colsum_kernel, dim3((D + 255) / 256), dim3(256), 0, s, pdg, nb, D, dg);
+  hipLaunchKernelGGL(colsum_kernel, dim3((D + 255) / 256), dim3(256), 0, s, pdb, nb, D, db);
+}
+
+bool launch_add_ln_bwd(const uint16_t* dout, const uint16_t* hsave, const float* mean,
+                       const float* rstd, const uint16_t* g, uint16_t* dres, uint16_t* dy, float* part,
+                       float* dg, float* db, int64_t R, int D, float p, uint32_t seed, uint32_t off,
+                       hipStream_t s) {
+  DPA_LN_DISPATCH(D, ln_bwd_impl, dout, hsave, mean, rstd, g, dres, dy, part, dg, db, R, p, seed,
+                  off, s)
+  return true;
+}
+
+}  // namespace dpa

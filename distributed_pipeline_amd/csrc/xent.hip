@@ -1,0 +1,486 @@
+// Fused linear + cross-entropy for a tied rounding head (SURVEY K-M12):
+//
+//   logits[t][v] = x[t] . W[v] + b[v]        x: [N, E] bf16, W: [V, E] bf16
+//   loss[t]      = logsumexp_v logits[t] - logits[t][target[t]]
+//
+// The [N, V] logits (1 GB fp32 per 8192x30522 call) are never written: every
+// kernel recomputes 32x32 logit tiles on the matrix cores and consumes them
+// in registers.
+//
+//   fwd : workgroup = 128 tokens, sweeps (a split of) the vocabulary in
+//         64-row W tiles staged through LDS; S = W x^T so the token sits on
+//         the MFMA lane and the vocabulary in the 16 accumulator registers:
+//         the online log-sum-exp is lane-local (one cross-half merge at the end).
+//   dx  : same sweep; dS = g (softmax - onehot) is rebuilt per tile and fed,
+//         still in registers, as the A operand of dx = dS^T W (the W B-operand
+//         comes from the same LDS tile through ds_read_b64_tr_b16).
+//   dW  : workgroup = 256 vocabulary rows (W in registers), sweeps tokens in
+//         64-row x tiles; S' = x W^T, dS' rebuilt, dW += dS'^T x with x read
+//         transposed from LDS; partial dW / db are added with fp32 atomics
+//         (token splits), two 128-B row segments per wave instruction.
+//
+// Out-of-range targets (< 0 or >= V) are ignored (loss 0, no gradient).
+#include "common.h"
+#include "launchers.h"
+#include "mfma.h"
+
+namespace dpa {
+
+static constexpr float LOG2E = 1.4426950408889634f;
+static constexpr float LN2 = 0.6931471805599453f;
+
+// ---------------------------------------------------------------------------
+// W-tile staging (64 rows x E) into a swizzled LDS image, register-staged.
+// ---------------------------------------------------------------------------
+template <int E, int NT>
+struct WTile {
+  static constexpr int CH = E / 8;             // 16-byte chunks per row
+  static constexpr int ROWB = E * 2;
+  static constexpr int PER = 64 * CH / NT;     // chunks per thread
+  uint4 r[PER];
+
+  __device__ __forceinline__ void load(const bf16_t* __restrict__ W, int v0, int V, int tid) {
+#pragma unroll
+    for (int i = 0; i < PER; ++i) {
+      const int c = tid + i * NT;
+      const int row = c / CH, ch = c % CH;
+      const int v = v0 + row;
+      if (v < V)
+        r[i] = *reinterpret_cast<const uint4*>(W + (int64_t)v * E + ch * 8);
+      else
+        r[i] = make_uint4(0, 0, 0, 0);
+    }
+  }
+  __device__ __forceinline__ void store(char* lds, int tid) const {
+#pragma unroll
+    for (int i = 0; i < PER; ++i) {
+      const int c = tid + i * NT;
+      const int row = c / CH, ch = c % CH;
+      *reinterpret_cast<uint4*>(lds + swz<ROWB>(row, ch)) = r[i];
+    }
+  }
+};
+
+// A/B fragment (8 bf16 of row `row`, 16-byte chunk `ch`) from a swizzled tile.
+template <int ROWB>
+__device__ __forceinline__ bf16x8 lds_frag(const char* lds, int row, int ch) {
+  return *reinterpret_cast<const bf16x8*>(lds + swz<ROWB>(row, ch));
+}
+
+// B fragment for "acc as A operand" products: 8 rows in the permuted k order
+// (rows r0 + 4h + q and r0 + 8 + 4h + q, q = 0..3) of column block col0..col0+31
+// (this lane receives column col0 + (lane & 31)), read transposed from LDS.
+template <int ROWB>
+__device__ __forceinline__ bf16x8 lds_tr_frag(const char* lds, int r0, int col0, int lane) {
+  const int g = lane >> 4, li = lane & 15, q = li >> 2, p = li & 3, h = lane >> 5;
+  const int col = col0 + 16 * (g & 1) + 4 * p;
+  const int ra = r0 + 4 * h + q;
+  const char* pa = lds + swz<ROWB>(ra, col >> 3) + (col & 7) * 2;
+  const char* pb = lds + swz<ROWB>(ra + 8, col >> 3) + (col & 7) * 2;
+  bf16x4 a = ds_read_tr16(pa);
+  bf16x4 b = ds_read_tr16(pb);
+  bf16x8 f;
+  f[0] = a[0]; f[1] = a[1]; f[2] = a[2]; f[3] = a[3];
+  f[4] = b[0]; f[5] = b[1]; f[6] = b[2]; f[7] = b[3];
+  return f;
+}
+
+__device__ __forceinline__ float sel16(const f32x16& a, int i) {
+  float v = 0.f;
+#pragma unroll
+  for (int k = 0; k < 16; ++k) v = (k == i) ? a[k] : v;
+  return v;
+}
+
+// ---------------------------------------------------------------------------
+// Forward
+// ---------------------------------------------------------------------------
+template <int E>
+__global__ void __launch_bounds__(256) lxent_fwd_kernel(
+    const bf16_t* __restrict__ x, const bf16_t* __restrict__ W, const bf16_t* __restrict__ bias,
+    const int64_t* __restrict__ target, int N, int V, int v_per_split, float* __restrict__ loss,
+    float* __restrict__ lse_out, float* __restrict__ part_m, float* __restrict__ part_s,
+    float* __restrict__ tgt_logit) {
+  constexpr int KS = E / 16, ROWB = E * 2;
+  __shared__ __attribute__((aligned(16))) char smem[64 * ROWB + 64 * 4];
+  char* wt = smem;
+  float* bt = reinterpret_cast<float*>(smem + 64 * ROWB);
+
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, h = lane >> 5;
+  const int t = blockIdx.x * 128 + w * 32 + (lane & 31);
+  const bool tok_ok = t < N;
+  bf16x8 xf[KS];
+#pragma unroll
+  for (int s = 0; s < KS; ++s) {
+    if (tok_ok) xf[s] = ld_frag(x + (int64_t)t * E + 16 * s + 8 * h);
+    else for (int j = 0; j < 8; ++j) xf[s][j] = 0;
+  }
+  const int64_t tg = tok_ok ? target[t] : -1;
+
+  const int vbeg = blockIdx.y * v_per_split;
+  const int vend = min(V, vbeg + v_per_split);
+  float m = -1e30f, ssum = 0.f, tl = -INFINITY;
+
+  WTile<E, 256> stage;
+  if (vbeg < vend) stage.load(W, vbeg, V, tid);
+  for (int v0 = vbeg; v0 < vend; v0 += 64) {
+    stage.store(wt, tid);
+    if (tid < 64) {
+      const int v = v0 + tid;
+      bt[tid] = (v < V) ? (bias ? bf2f(bias[v]) : 0.f) : 0.f;
+    }
+    __syncthreads();
+    if (v0 + 64 < vend) stage.load(W, v0 + 64, V, tid);  // prefetch next tile behind the MFMAs
+
+    f32x16 acc[2];
+#pragma unroll
+    for (int vt = 0; vt < 2; ++vt) {
+      acc[vt] = zero16();
+#pragma unroll
+      for (int s = 0; s < KS; ++s)
+        acc[vt] = mfma32(lds_frag<ROWB>(wt, vt * 32 + (lane & 31), 2 * s + h), xf[s], acc[vt]);
+    }
+    const bool tail = (v0 + 64 > V);
+    float tmax = -INFINITY;
+#pragma unroll
+    for (int vt = 0; vt < 2; ++vt) {
+#pragma unroll
+      for (int i = 0; i < 16; ++i) {
+        const int r = vt * 32 + acc_row(i, h);
+        float y = (acc[vt][i] + bt[r]) * LOG2E;
+        if (tail && v0 + r >= V) y = -INFINITY;
+        acc[vt][i] = y;
+        tmax = fmaxf(tmax, y);
+      }
+    }
+    const float mn = fmaxf(m, tmax);
+    float add = 0.f;
+#pragma unroll
+    for (int vt = 0; vt < 2; ++vt)
+#pragma unroll
+      for (int i = 0; i < 16; ++i) add += exp2f(acc[vt][i] - mn);
+    ssum = ssum * exp2f(m - mn) + add;
+    m = mn;
+    const int64_t r = tg - v0;
+    if (r >= 0 && r < 64 && v0 + r < vend) {
+      const int rr = (int)r & 31, vt = (int)r >> 5;
+      if (((rr >> 2) & 1) == h) {
+        const int i = (rr & 3) + 4 * (rr >> 3);
+        tl = (vt ? sel16(acc[1], i) : sel16(acc[0], i)) * LN2;
+      }
+    }
+    __syncthreads();
+  }
+  // merge the two lane halves that share a token
+  const float m2 = __shfl_xor(m, 32, 64), s2 = __shfl_xor(ssum, 32, 64);
+  const float tl2 = __shfl_xor(tl, 32, 64);
+  const float M = fmaxf(m, m2);
+  const float S = ssum * exp2f(m - M) + s2 * exp2f(m2 - M);
+  tl = fmaxf(tl, tl2);
+  if (h == 0 && tok_ok) {
+    if (gridDim.y == 1) {
+      const bool valid = tg >= 0 && tg < V;
+      const float lse = (M + log2f(S)) * LN2;
+      loss[t] = valid ? lse - tl : 0.f;
+      lse_out[t] = lse;
+    } else {
+      part_m[(int64_t)blockIdx.y * N + t] = M;
+      part_s[(int64_t)blockIdx.y * N + t] = S;
+      if (tl > -INFINITY) tgt_logit[t] = tl;
+    }
+  }
+}
+
+__global__ void __launch_bounds__(256) lxent_combine_kernel(
+    const float* __restrict__ part_m, const float* __restrict__ part_s,
+    const float* __restrict__ tgt_logit, const int64_t* __restrict__ target, int N, int V, int S,
+    float* __restrict__ loss, float* __restrict__ lse_out) {
+  const int t = blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= N) return;
+  float M = -1e30f;
+  for (int s = 0; s < S; ++s) M = fmaxf(M, part_m[(int64_t)s * N + t]);
+  float sum = 0.f;
+  for (int s = 0; s < S; ++s) sum += part_s[(int64_t)s * N + t] * exp2f(part_m[(int64_t)s * N + t] - M);
+  const float lse = (M + log2f(sum)) * LN2;
+  const int64_t tg = target[t];
+  const bool valid = tg >= 0 && tg < V;
+  loss[t] = valid ? lse - tgt_logit[t] : 0.f;
+  lse_out[t] = lse;
+}
+
+// ---------------------------------------------------------------------------
+// Backward: dx
+// ---------------------------------------------------------------------------
+template <int E>
+__global__ void __launch_bounds__(256) lxent_dx_kernel(
+    const bf16_t* __restrict__ x, const bf16_t* __restrict__ W, const bf16_t* __restrict__ bias,
+    const int64_t* __restrict__ target, const float* __restrict__ lse, const float* __restrict__ dloss,
+    int N, int V, int v_per_split, bf16_t* __restrict__ dx, float* __restrict__ dx_acc) {
+  constexpr int KS = E / 16, ROWB = E * 2, KT = E / 32;
+  __shared__ __attribute__((aligned(16))) char smem[64 * ROWB + 64 * 4];
+  char* wt = smem;
+  float* bt = reinterpret_cast<float*>(smem + 64 * ROWB);
+
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, h = lane >> 5;
+  const int t = blockIdx.x * 128 + w * 32 + (lane & 31);
+  const bool tok_ok = t < N;
+  bf16x8 xf[KS];
+#pragma unroll
+  for (int s = 0; s < KS; ++s) {
+    if (tok_ok) xf[s] = ld_frag(x + (int64_t)t * E + 16 * s + 8 * h);
+    else for (int j = 0; j < 8; ++j) xf[s][j] = 0;
+  }
+  const int64_t tg = tok_ok ? target[t] : -1;
+  const bool valid = tok_ok && tg >= 0 && tg < V;
+  const float g = valid ? dloss[t] : 0.f;
+  const float lse2 = tok_ok ? lse[t] * LOG2E : 0.f;
+
+  const int vbeg = blockIdx.y * v_per_split;
+  const int vend = min(V, vbeg + v_per_split);
+  f32x16 dacc[KT];
+#pragma unroll
+  for (int k = 0; k < KT; ++k) dacc[k] = zero16();
+
+  WTile<E, 256> stage;
+  if (vbeg < vend) stage.load(W, vbeg, V, tid);
+  for (int v0 = vbeg; v0 < vend; v0 += 64) {
+    stage.store(wt, tid);
+    if (tid < 64) {
+      const int v = v0 + tid;
+      bt[tid] = (v < V) ? (bias ? bf2f(bias[v]) : 0.f) : 0.f;
+    }
+    __syncthreads();
+    if (v0 + 64 < vend) stage.load(W, v0 + 64, V, tid);
+
+#pragma unroll
+    for (int vt = 0; vt < 2; ++vt) {
+      f32x16 acc = zero16();
+#pragma unroll
+      for (int s = 0; s < KS; ++s)
+        acc = mfma32(lds_frag<ROWB>(wt, vt * 32 + (lane & 31), 2 * s + h), xf[s], acc);
+#pragma unroll
+      for (int i = 0; i < 16; ++i) {
+        const int r = vt * 32 + acc_row(i, h);
+        const int v = v0 + r;
+        float p = exp2f((acc[i] + bt[r]) * LOG2E - lse2);
+        p = (v < vend) ? p : 0.f;
+        acc[i] = g * (p - ((int64_t)v == tg ? 1.f : 0.f));
+      }
+      // dx[t][k] += sum_v dS[v][t] W[v][k]   (dS as A operand, W read transposed)
+#pragma unroll
+      for (int s = 0; s < 2; ++s) {
+        const bf16x8 af = acc_to_frag(acc, s);
+#pragma unroll
+        for (int kt = 0; kt < KT; ++kt)
+          dacc[kt] = mfma32(af, lds_tr_frag<ROWB>(wt, vt * 32 + 16 * s, kt * 32, lane), dacc[kt]);
+      }
+    }
+    __syncthreads();
+  }
+  // dacc[kt] reg i: row = token (w*32 + acc_row(i,h)), col = k (kt*32 + lane&31)
+  const int tb = blockIdx.x * 128 + w * 32;
+#pragma unroll
+  for (int kt = 0; kt < KT; ++kt) {
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+      const int tt = tb + acc_row(i, h);
+      if (tt < N) {
+        const int64_t o = (int64_t)tt * E + kt * 32 + (lane & 31);
+        if (dx_acc) atomicAdd(dx_acc + o, dacc[kt][i]);
+        else dx[o] = f2bf(dacc[kt][i]);
+      }
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
+// Backward: dW (+ db)
+// ---------------------------------------------------------------------------
+template <int E>
+__global__ void __launch_bounds__(512) lxent_dw_kernel(
+    const bf16_t* __restrict__ x, const bf16_t* __restrict__ W, const bf16_t* __restrict__ bias,
+    const int64_t* __restrict__ target, const float* __restrict__ lse, const float* __restrict__ dloss,
+    int N, int V, int t_per_split, float* __restrict__ dW, float* __restrict__ db) {
+  constexpr int KS = E / 16, ROWB = E * 2, KT = E / 32, CH = E / 8;
+  __shared__ __attribute__((aligned(16))) char smem[64 * ROWB + 3 * 64 * 4];
+  char* xt = smem;
+  float* s_lse = reinterpret_cast<float*>(smem + 64 * ROWB);
+  float* s_g = s_lse + 64;
+  int* s_tg = reinterpret_cast<int*>(s_g + 64);
+
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, h = lane >> 5;
+  const int vw = blockIdx.x * 256 + w * 32;       // this wave's 32 vocabulary rows
+  const int v = vw + (lane & 31);                 // this lane's column (vocab)
+  const bool v_ok = v < V;
+  bf16x8 wf[KS];
+#pragma unroll
+  for (int s = 0; s < KS; ++s) {
+    if (v_ok) wf[s] = ld_frag(W + (int64_t)v * E + 16 * s + 8 * h);
+    else for (int j = 0; j < 8; ++j) wf[s][j] = 0;
+  }
+  const float bv = (v_ok && bias) ? bf2f(bias[v]) : 0.f;
+
+  f32x16 dacc[KT];
+#pragma unroll
+  for (int k = 0; k < KT; ++k) dacc[k] = zero16();
+  float dbs = 0.f;
+
+  const int tbeg = blockIdx.y * t_per_split;
+  const int tend = min(N, tbeg + t_per_split);
+  for (int t0 = tbeg; t0 < tend; t0 += 64) {
+    // stage x tile [64 tokens][E] + per-token scalars
+    for (int c = tid; c < 64 * CH; c += 512) {
+      const int row = c / CH, ch = c % CH;
+      const int t = t0 + row;
+      uint4 val = make_uint4(0, 0, 0, 0);
+      if (t < tend) val = *reinterpret_cast<const uint4*>(x + (int64_t)t * E + ch * 8);
+      *reinterpret_cast<uint4*>(xt + swz<ROWB>(row, ch)) = val;
+    }
+    if (tid < 64) {
+      const int t = t0 + tid;
+      const bool ok = t < tend;
+      const int64_t tg = ok ? target[t] : -1;
+      const bool valid = ok && tg >= 0 && tg < V;
+      s_lse[tid] = ok ? lse[t] * LOG2E : 0.f;
+      s_g[tid] = valid ? dloss[t] : 0.f;
+      s_tg[tid] = valid ? (int)tg : -1;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int tt = 0; tt < 2; ++tt) {
+      f32x16 acc = zero16();  // S'[t][v]: rows = tokens, cols = vocab (lane)
+#pragma unroll
+      for (int s = 0; s < KS; ++s)
+        acc = mfma32(lds_frag<ROWB>(xt, tt * 32 + (lane & 31), 2 * s + h), wf[s], acc);
+#pragma unroll
+      for (int i = 0; i < 16; ++i) {
+        const int r = tt * 32 + acc_row(i, h);
+        const float p = exp2f((acc[i] + bv) * LOG2E - s_lse[r]);
+        const float d = v_ok ? s_g[r] * (p - (s_tg[r] == v ? 1.f : 0.f)) : 0.f;
+        acc[i] = d;
+        dbs += d;
+      }
+#pragma unroll
+      for (int s = 0; s < 2; ++s) {
+        const bf16x8 af = acc_to_frag(acc, s);
+#pragma unroll
+        for (int kt = 0; kt < KT; ++kt)
+          dacc[kt] = mfma32(af, lds_tr_frag<ROWB>(xt, tt * 32 + 16 * s, kt * 32, lane), dacc[kt]);
+      }
+    }
+    __syncthreads();
+  }
+  dbs += __shfl_xor(dbs, 32, 64);
+  if (h == 0 && v_ok && db) atomicAdd(db + v, dbs);
+  // dacc[kt] reg i: row = vocab vw + acc_row(i,h), col = k
+#pragma unroll
+  for (int kt = 0; kt < KT; ++kt) {
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+      const int vv = vw + acc_row(i, h);
+      if (vv < V) atomicAdd(dW + (int64_t)vv * E + kt * 32 + (lane & 31), dacc[kt][i]);
+    }
+  }
+}
+
+__global__ void __launch_bounds__(256) f32_to_bf16_kernel(const float* __restrict__ a,
+                                                         bf16_t* __restrict__ b, int64_t n) {
+  const int64_t i = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) * 4;
+  if (i + 3 < n) {
+    f32x4 v = *reinterpret_cast<const f32x4*>(a + i);
+    uint2 p;
+    p.x = pack_bf2(v[0], v[1]);
+    p.y = pack_bf2(v[2], v[3]);
+    *reinterpret_cast<uint2*>(b + i) = p;
+  } else {
+    for (int64_t k = i; k < n; ++k) b[k] = f2bf(a[k]);
+  }
+}
+
+// ---------------------------------------------------------------------------
+// Launchers
+// ---------------------------------------------------------------------------
+static int pick_splits(int blocks, int chunks, int target_wgs) {
+  int s = (target_wgs + blocks - 1) / blocks;
+  if (s < 1) s = 1;
+  if (s > chunks) s = chunks;
+  return s;
+}
+
+template <int E>
+static void fwd_impl(const bf16_t* x, const bf16_t* W, const bf16_t* b, const int64_t* tgt, int N,
+                     int V, float* loss, float* lse, float* ws, hipStream_t st) {
+  const int tb = (N + 127) / 128;
+  const int vchunks = (V + 63) / 64;
+  const int S = pick_splits(tb, vchunks, 1024);
+  const int vps = ((vchunks + S - 1) / S) * 64;
+  const int Sx = (V + vps - 1) / vps;
+  float* pm = ws;
+  float* ps = ws + (int64_t)Sx * N;
+  float* tl = ws + 2 * (int64_t)Sx * N;
+  hipLaunchKernelGGL(lxent_fwd_kernel<E>, dim3(tb, Sx), dim3(256), 0, st, x, W, b, tgt, N, V, vps,
+                     loss, lse, pm, ps, tl);
+  if (Sx > 1)
+    hipLaunchKernelGGL(lxent_combine_kernel, dim3((N + 255) / 256), dim3(256), 0, st, pm, ps, tl,
+                       tgt, N, V, Sx, loss, lse);
+}
+
+int64_t lxent_workspace_floats(int N, int V) {
+  const int tb = (N + 127) / 128;
+  const int vchunks = (V + 63) / 64;
+  const int S = pick_splits(tb, vchunks, 1024);
+  const int vps = ((vchunks + S - 1) / S) * 64;
+  const int Sx = (V + vps - 1) / vps;
+  return (2 * (int64_t)Sx + 1) * N + 64;
+}
+
+void launch_lxent_fwd(const uint16_t* x, const uint16_t* W, const uint16_t* b, const int64_t* tgt,
+                      int N, int V, int E, float* loss, float* lse, float* ws, hipStream_t s) {
+  if (E == 128) fwd_impl<128>(x, W, b, tgt, N, V, loss, lse, ws, s);
+  else fwd_impl<256>(x, W, b, tgt, N, V, loss, lse, ws, s);
+}
+
+template <int E>
+static void dx_impl(const bf16_t* x, const bf16_t* W, const bf16_t* b, const int64_t* tgt,
+                    const float* lse, const float* dl, int N, int V, uint16_t* dx, float* dx_acc,
+                    hipStream_t st) {
+  const int tb = (N + 127) / 128;
+  const int vchunks = (V + 63) / 64;
+  const int S = dx_acc ? pick_splits(tb, vchunks, 1024) : 1;
+  const int vps = ((vchunks + S - 1) / S) * 64;
+  const int Sx = (V + vps - 1) / vps;
+  hipLaunchKernelGGL(lxent_dx_kernel<E>, dim3(tb, Sx), dim3(256), 0, st, x, W, b, tgt, lse, dl, N,
+                     V, vps, (bf16_t*)dx, Sx > 1 ? dx_acc : nullptr);
+  if (Sx > 1) {
+    const int64_t n = (int64_t)N * E;
+    hipLaunchKernelGGL(f32_to_bf16_kernel, dim3((unsigned)((n / 4 + 255) / 256 + 1)), dim3(256), 0,
+                       st, dx_acc, (bf16_t*)dx, n);
+  }
+}
+
+bool lxent_dx_needs_acc(int N) { return (N + 127) / 128 < 512; }
+
+void launch_lxent_dx(const uint16_t* x, const uint16_t* W, const uint16_t* b, const int64_t* tgt,
+                     const float* lse, const float* dloss, int N, int V, int E, uint16_t* dx,
+                     float* dx_acc, hipStream_t s) {
+  if (E == 128) dx_impl<128>(x, W, b, tgt, lse, dloss, N, V, dx, dx_acc, s);
+  else dx_impl<256>(x, W, b, tgt, lse, dloss, N, V, dx, dx_acc, s);
+}
+
+void launch_lxent_dw(const uint16_t* x, const uint16_t* W, const uint16_t* b, const int64_t* tgt,
+                     const float* lse, const float* dloss, int N, int V, int E, float* dW, float* db,
+                     hipStream_t s) {
+  const int vb = (V + 255) / 256;
+  const int tchunks = (N + 63) / 64;
+  const int TS = pick_splits(vb, tchunks, 960);
+  const int tps = ((tchunks + TS - 1) / TS) * 64;
+  const int TSx = (N + tps - 1) / tps;
+  if (E == 128)
+    hipLaunchKernelGGL(lxent_dw_kernel<128>, dim3(vb, TSx), dim3(512), 0, s, (const bf16_t*)x,
+                       (const bf16_t*)W, (const bf16_t*)b, tgt, lse, dloss, N, V, tps, dW, db);
+  else
+    hipLaunchKernelGGL(lxent_dw_kernel<256>, dim3(vb, TSx), dim3(512), 0, s, (const bf16_t*)x,
+                       (const bf16_t*)W, (const bf16_t*)b, tgt, lse, dloss, N, V, tps, dW, db);
+}
+
+}  // namespace dpa

@@ -104,7 +104,8 @@ def _bias_act_fwd(z2d, b16, act):
 
 def _bias_act_bwd(dy2d, z, y, act, want_db):
     if native_ok(dy2d, kernel="bias_act_bwd") and dy2d.dtype == torch.bfloat16 and dy2d.shape[-1] % 8 == 0:
-        dz, db = get_ext().bias_act_bwd(dy2d, z if z is not None else y, _ACTS.index(act), want_db)
+        zy = z if z is not None else (y if y is not None else dy2d)
+        dz, db = get_ext().bias_act_bwd(dy2d, zy, _ACTS.index(act), want_db)
         return dz, (db if want_db else None)
     dz = _act_bwd(dy2d, z, y, act)
     db = dz.float().sum(0) if want_db else None
@@ -159,18 +160,19 @@ class _AddLNFn(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, y, residual, w, b, w16, b16, p, eps, seed, offset):
-        ext = get_ext()
-        out, mean, rstd, mask = ext.add_ln_fwd(y, residual, w16, b16, float(p), float(eps), seed, offset)
-        ctx.save_for_backward(out, rstd, w16, b16, mask)
-        ctx.p = p
-        ctx.has_res = residual is not None
+        out, hsave, mean, rstd = get_ext().add_ln_fwd(y, residual, w16, b16, float(p), float(eps),
+                                                      seed, offset)
+        ctx.save_for_backward(hsave, mean, rstd, w16)
+        ctx.cfg = (p, seed, offset, residual is not None)
         return out
 
     @staticmethod
     def backward(ctx, dout):
-        out, rstd, w16, b16, mask = ctx.saved_tensors
-        dx, dy, dw, db = get_ext().add_ln_bwd(dout.contiguous(), out, rstd, w16, b16, mask, float(ctx.p))
-        return dy, (dx if ctx.has_res else None), dw, db, None, None, None, None, None, None
+        hsave, mean, rstd, w16 = ctx.saved_tensors
+        p, seed, offset, has_res = ctx.cfg
+        dres, dy, dw, db = get_ext().add_ln_bwd(dout.contiguous(), hsave, mean, rstd, w16, float(p),
+                                                seed, offset, has_res, ctx.needs_input_grad[0])
+        return dy, (dres if has_res else None), dw, db, None, None, None, None, None, None
 
 
 class RNG:
@@ -303,7 +305,7 @@ def linear_cross_entropy(x, weight, bias, target):
     x: [N, E]; weight: [V, E]; target: [N] int64 -> loss [N] fp32.
     """
     if (x.dtype == torch.bfloat16 and native_ok(x, kernel="lxent_fwd")
-            and x.shape[-1] % 64 == 0 and x.shape[-1] <= 256):
+            and x.shape[-1] in (128, 256)):
         return _LinearXentFn.apply(x.contiguous(), weight, bias, shadow(weight, x.dtype),
                                    shadow(bias, x.dtype), target.contiguous())
     logits = linear(x, weight, bias)
