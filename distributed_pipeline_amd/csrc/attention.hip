@@ -1,0 +1,404 @@
+// Fused multi-head attention for head_dim 64 on CDNA4 matrix cores
+// (SURVEY K-M8): softmax(Q K^T / 8) with attention dropout, bidirectional
+// (DiffuSeq/BERT) or causal (GPT-2).  Inputs are the packed QKV projection
+// [B, L, 3, H, 64] so no head split/transposes are materialised.
+//
+// Forward: one workgroup = 128 queries of one (batch, head), 4 waves x 32.
+//   S^T = K Q^T is computed key-major (keys in the accumulator registers, the
+//   query on the MFMA lane) so softmax statistics are lane-local.  Pass 1
+//   streams K tiles and builds (max, sum) per query -> LSE; pass 2 recomputes
+//   S^T, forms the exact probabilities (no online rescale of O needed),
+//   applies dropout and feeds them - still in registers - as the A operand of
+//   O = P^T V, with V read transposed from LDS (ds_read_b64_tr_b16).
+// Backward: one workgroup = 128 keys of one (batch, head), 4 waves x 32 keys,
+//   K and V of the wave's keys in registers; sweeps query tiles of 64:
+//   S = Q K^T and dP = dO V^T (query-major), P rebuilt from the saved LSE,
+//   dS = P (dP - delta); dV += P^T dO and dK += dS^T Q straight from the
+//   accumulators; dS crosses LDS once for dQ = dS K, which the 4 waves reduce
+//   with LDS float atomics.  With one key block per (batch, head) (L <= 128)
+//   dQ is final and stored directly; longer sequences add fp32 global atomics.
+// Dropout: keep/drop bits come from a per-(query, key-pair) hash of
+//   (seed, offset, batch*head), so forward and backward agree without storing
+//   a mask.
+#include "common.h"
+#include "launchers.h"
+#include "mfma.h"
+
+namespace dpa {
+
+static constexpr int HD = 64;                        // head dim
+static constexpr float ATT_C = 1.4426950408889634f / 8.0f;  // log2(e) / sqrt(64)
+static constexpr float LN2f = 0.6931471805599453f;
+
+struct DropCfg {
+  uint32_t seedmix;
+  uint32_t thr16;  // drop if (16 random bits) < thr16
+  float scale;     // 1 / (1 - p)
+  bool on;
+};
+
+__device__ __forceinline__ DropCfg make_drop(float p, uint32_t seed, uint32_t offset, uint32_t bh) {
+  DropCfg d;
+  d.on = p > 0.f;
+  d.thr16 = (uint32_t)(p * 65536.f + 0.5f);
+  d.scale = d.on ? 1.f / (1.f - p) : 1.f;
+  d.seedmix = lowbias32(seed ^ lowbias32(offset * 0xC2B2AE3Du ^ (bh * 0x27D4EB2Fu)));
+  return d;
+}
+
+__device__ __forceinline__ bool keep_bit(const DropCfg& d, int q, int key) {
+  const uint32_t h = lowbias32(d.seedmix ^ ((uint32_t)q * 0x9E3779B1u) ^ ((uint32_t)(key >> 1) * 0x85EBCA77u));
+  const uint32_t r = (key & 1) ? (h >> 16) : (h & 0xffffu);
+  return r >= d.thr16;
+}
+
+// stage a [64 rows][64 d] bf16 tile (rows r0.., stride `ld` elements) -> swizzled LDS
+__device__ __forceinline__ void stage64(char* lds, const bf16_t* __restrict__ src, int64_t ld,
+                                        int r0, int nrows, int tid) {
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const int c = tid + i * 256;  // 512 chunks of 16 B
+    const int row = c >> 3, ch = c & 7;
+    uint4 v = make_uint4(0, 0, 0, 0);
+    if (r0 + row < nrows) v = *reinterpret_cast<const uint4*>(src + (int64_t)(r0 + row) * ld + ch * 8);
+    *reinterpret_cast<uint4*>(lds + swz<128>(row, ch)) = v;
+  }
+}
+
+// ---------------------------------------------------------------------------
+// forward
+// ---------------------------------------------------------------------------
+template <bool CAUSAL>
+__global__ void __launch_bounds__(256) attn_fwd_kernel(const bf16_t* __restrict__ qkv,
+                                                      bf16_t* __restrict__ out, float* __restrict__ lse,
+                                                      int L, int H, float p, uint32_t seed,
+                                                      uint32_t offset) {
+  __shared__ __attribute__((aligned(16))) char smem[2 * 64 * 128];
+  char* kt_lds = smem;
+  char* vt_lds = smem + 64 * 128;
+  const int b = blockIdx.z, hd = blockIdx.y;
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, hf = lane >> 5;
+  const int64_t ld = 3LL * H * HD;  // token stride
+  const bf16_t* qb = qkv + (int64_t)b * L * ld + (int64_t)hd * HD;
+  const bf16_t* kb = qb + (int64_t)H * HD;
+  const bf16_t* vb = qb + 2LL * H * HD;
+  const int qbase = blockIdx.x * 128 + w * 32;
+  const int q = qbase + (lane & 31);
+  const bool q_ok = q < L;
+  bf16x8 qf[4];
+#pragma unroll
+  for (int s = 0; s < 4; ++s) {
+    if (q_ok) qf[s] = ld_frag(qb + (int64_t)q * ld + 16 * s + 8 * hf);
+    else for (int j = 0; j < 8; ++j) qf[s][j] = 0;
+  }
+  const DropCfg dc = make_drop(p, seed, offset, (uint32_t)(b * H + hd));
+  const int kv_end = CAUSAL ? min(L, (int)blockIdx.x * 128 + 128) : L;
+
+  // ---- pass 1: row statistics -------------------------------------------------
+  float m = -1e30f, l = 0.f;
+  for (int kv0 = 0; kv0 < kv_end; kv0 += 64) {
+    stage64(kt_lds, kb, ld, kv0, L, tid);
+    __syncthreads();
+    f32x16 acc[2];
+#pragma unroll
+    for (int t = 0; t < 2; ++t) {
+      acc[t] = zero16();
+#pragma unroll
+      for (int s = 0; s < 4; ++s) acc[t] = mfma32(lds_frag<128>(kt_lds, t * 32 + (lane & 31), 2 * s + hf), qf[s], acc[t]);
+    }
+    float tmax = -INFINITY;
+#pragma unroll
+    for (int t = 0; t < 2; ++t)
+#pragma unroll
+      for (int i = 0; i < 16; ++i) {
+        const int key = kv0 + t * 32 + acc_row(i, hf);
+        float y = acc[t][i] * ATT_C;
+        if (CAUSAL && key > q) y = -INFINITY;
+        acc[t][i] = y;
+        tmax = fmaxf(tmax, y);
+      }
+    const float mn = fmaxf(m, tmax);
+    float add = 0.f;
+#pragma unroll
+    for (int t = 0; t < 2; ++t)
+#pragma unroll
+      for (int i = 0; i < 16; ++i) add += exp2f(acc[t][i] - mn);
+    l = l * exp2f(m - mn) + add;
+    m = mn;
+    __syncthreads();
+  }
+  {
+    const float m2 = __shfl_xor(m, 32, 64), l2 = __shfl_xor(l, 32, 64);
+    const float M = fmaxf(m, m2);
+    l = l * exp2f(m - M) + l2 * exp2f(m2 - M);
+    m = M;
+  }
+  const float lse2 = m + log2f(l);
+  if (hf == 0 && q_ok) lse[((int64_t)b * H + hd) * L + q] = lse2 * LN2f;
+
+  // ---- pass 2: O = dropout(P) V --------------------------------------------------
+  f32x16 o[2];
+  o[0] = zero16();
+  o[1] = zero16();
+  for (int kv0 = 0; kv0 < kv_end; kv0 += 64) {
+    stage64(kt_lds, kb, ld, kv0, L, tid);
+    stage64(vt_lds, vb, ld, kv0, L, tid);
+    __syncthreads();
+#pragma unroll
+    for (int t = 0; t < 2; ++t) {
+      f32x16 acc = zero16();
+#pragma unroll
+      for (int s = 0; s < 4; ++s) acc = mfma32(lds_frag<128>(kt_lds, t * 32 + (lane & 31), 2 * s + hf), qf[s], acc);
+#pragma unroll
+      for (int i = 0; i < 16; ++i) {
+        const int key = kv0 + t * 32 + acc_row(i, hf);
+        float pr = exp2f(acc[i] * ATT_C - lse2);
+        if (CAUSAL && key > q) pr = 0.f;
+        if (dc.on) pr = keep_bit(dc, q, key) ? pr * dc.scale : 0.f;
+        acc[i] = pr;
+      }
+#pragma unroll
+      for (int s = 0; s < 2; ++s) {
+        const bf16x8 af = acc_to_frag(acc, s);
+#pragma unroll
+        for (int dt = 0; dt < 2; ++dt)
+          o[dt] = mfma32(af, lds_tr_frag<128>(vt_lds, t * 32 + 16 * s, dt * 32, lane), o[dt]);
+      }
+    }
+    __syncthreads();
+  }
+  // o[dt] reg i: row = query qbase + acc_row(i,hf), col = d (dt*32 + lane&31)
+  bf16_t* ob = out + (int64_t)b * L * H * HD + (int64_t)hd * HD;
+#pragma unroll
+  for (int dt = 0; dt < 2; ++dt)
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+      const int qq = qbase + acc_row(i, hf);
+      if (qq < L) ob[(int64_t)qq * H * HD + dt * 32 + (lane & 31)] = f2bf(o[dt][i]);
+    }
+}
+
+// delta[b,h,q] = sum_d dO * O
+__global__ void __launch_bounds__(256) attn_delta_kernel(const bf16_t* __restrict__ dout,
+                                                        const bf16_t* __restrict__ out,
+                                                        float* __restrict__ delta, int B, int L, int H) {
+  const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;  // (b, q, h)
+  if (idx >= (int64_t)B * L * H) return;
+  const int hd = (int)(idx % H);
+  const int64_t bq = idx / H;
+  const int q = (int)(bq % L), b = (int)(bq / L);
+  const bf16_t* d = dout + idx * HD;
+  const bf16_t* o = out + idx * HD;
+  float s = 0.f;
+#pragma unroll
+  for (int c = 0; c < 8; ++c) {
+    uint4 a = *reinterpret_cast<const uint4*>(d + c * 8);
+    uint4 bb = *reinterpret_cast<const uint4*>(o + c * 8);
+    const uint32_t aw[4] = {a.x, a.y, a.z, a.w}, bw[4] = {bb.x, bb.y, bb.z, bb.w};
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      s += __uint_as_float(aw[k] << 16) * __uint_as_float(bw[k] << 16);
+      s += __uint_as_float(aw[k] & 0xffff0000u) * __uint_as_float(bw[k] & 0xffff0000u);
+    }
+  }
+  delta[((int64_t)b * H + hd) * L + q] = s;
+}
+
+// ---------------------------------------------------------------------------
+// backward
+// ---------------------------------------------------------------------------
+template <bool CAUSAL>
+__global__ void __launch_bounds__(256) attn_bwd_kernel(
+    const bf16_t* __restrict__ qkv, const bf16_t* __restrict__ dout, const float* __restrict__ lse,
+    const float* __restrict__ delta, bf16_t* __restrict__ dqkv, float* __restrict__ dq_acc, int L,
+    int H, float p, uint32_t seed, uint32_t offset) {
+  constexpr int QT_B = 64 * 128;    // Q or dO tile bytes
+  constexpr int KC_B = 32 * 128;    // per-wave K copy
+  constexpr int DS_B = 64 * 64;     // per-wave dS tile [64 q][32 keys] bf16
+  __shared__ __attribute__((aligned(16))) char smem[2 * QT_B + 4 * KC_B + 4 * DS_B + 64 * 64 * 4 + 2 * 64 * 4];
+  char* qt_lds = smem;
+  char* dot_lds = smem + QT_B;
+  char* kc_lds = smem + 2 * QT_B;
+  char* ds_lds = kc_lds + 4 * KC_B;
+  float* dq_red = reinterpret_cast<float*>(ds_lds + 4 * DS_B);
+  float* s_lse = dq_red + 64 * 64;
+  float* s_del = s_lse + 64;
+
+  const int b = blockIdx.z, hd = blockIdx.y;
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, hf = lane >> 5;
+  const int64_t ld = 3LL * H * HD;
+  const bf16_t* qb = qkv + (int64_t)b * L * ld + (int64_t)hd * HD;
+  const bf16_t* kb = qb + (int64_t)H * HD;
+  const bf16_t* vb = qb + 2LL * H * HD;
+  const bf16_t* dob = dout + (int64_t)b * L * H * HD + (int64_t)hd * HD;
+  const int64_t ldo = (int64_t)H * HD;
+  const int kbase = blockIdx.x * 128 + w * 32;
+  const int key = kbase + (lane & 31);
+  const bool k_ok = key < L;
+  char* kc = kc_lds + w * KC_B;
+  char* dsw = ds_lds + w * DS_B;
+
+  bf16x8 kf[4], vf[4];
+#pragma unroll
+  for (int s = 0; s < 4; ++s) {
+    if (k_ok) {
+      kf[s] = ld_frag(kb + (int64_t)key * ld + 16 * s + 8 * hf);
+      vf[s] = ld_frag(vb + (int64_t)key * ld + 16 * s + 8 * hf);
+    } else {
+      for (int j = 0; j < 8; ++j) { kf[s][j] = 0; vf[s][j] = 0; }
+    }
+    // K copy for the dQ product: row = key (local), chunk = 2s + hf
+    *reinterpret_cast<bf16x8*>(kc + swz<128>(lane & 31, 2 * s + hf)) = kf[s];
+  }
+  const DropCfg dc = make_drop(p, seed, offset, (uint32_t)(b * H + hd));
+  const int64_t lrow = ((int64_t)b * H + hd) * L;
+  f32x16 dk[2], dv[2];
+  dk[0] = zero16(); dk[1] = zero16(); dv[0] = zero16(); dv[1] = zero16();
+
+  const int qbeg = CAUSAL ? (int)blockIdx.x * 128 : 0;
+  for (int q0 = qbeg; q0 < L; q0 += 64) {
+    stage64(qt_lds, qb, ld, q0, L, tid);
+    stage64(dot_lds, dob, ldo, q0, L, tid);
+    if (tid < 64) {
+      const bool ok = q0 + tid < L;
+      s_lse[tid] = ok ? lse[lrow + q0 + tid] * 1.4426950408889634f : 0.f;
+      s_del[tid] = ok ? delta[lrow + q0 + tid] : 0.f;
+    }
+    for (int i = tid; i < 64 * 64; i += 256) dq_red[i] = 0.f;
+    __syncthreads();
+#pragma unroll
+    for (int qt = 0; qt < 2; ++qt) {
+      f32x16 sacc = zero16(), dpacc = zero16();
+#pragma unroll
+      for (int s = 0; s < 4; ++s) {
+        sacc = mfma32(lds_frag<128>(qt_lds, qt * 32 + (lane & 31), 2 * s + hf), kf[s], sacc);
+        dpacc = mfma32(lds_frag<128>(dot_lds, qt * 32 + (lane & 31), 2 * s + hf), vf[s], dpacc);
+      }
+      // rows = queries (regs), cols = keys (lanes)
+#pragma unroll
+      for (int i = 0; i < 16; ++i) {
+        const int r = qt * 32 + acc_row(i, hf);
+        const int qq = q0 + r;
+        float pr = exp2f(sacc[i] * ATT_C - s_lse[r]);
+        if ((CAUSAL && key > qq) || !k_ok || qq >= L) pr = 0.f;
+        float pd = pr, dpd = dpacc[i];
+        if (dc.on) {
+          const bool kp = keep_bit(dc, qq, key);
+          pd = kp ? pr * dc.scale : 0.f;
+          dpd = kp ? dpd * dc.scale : 0.f;
+        }
+        sacc[i] = pd;                       // dropout(P)   -> dV
+        dpacc[i] = pr * (dpd - s_del[r]);   // dS           -> dK, dQ
+      }
+#pragma unroll
+      for (int s = 0; s < 2; ++s) {
+        const bf16x8 pf = acc_to_frag(sacc, s);
+        const bf16x8 sf = acc_to_frag(dpacc, s);
+#pragma unroll
+        for (int dt = 0; dt < 2; ++dt) {
+          dv[dt] = mfma32(pf, lds_tr_frag<128>(dot_lds, qt * 32 + 16 * s, dt * 32, lane), dv[dt]);
+          dk[dt] = mfma32(sf, lds_tr_frag<128>(qt_lds, qt * 32 + 16 * s, dt * 32, lane), dk[dt]);
+        }
+      }
+      // dS -> LDS as [query][key] bf16 for dQ = dS K
+#pragma unroll
+      for (int i = 0; i < 16; ++i) {
+        const int r = qt * 32 + acc_row(i, hf);
+        const int c = lane & 31;
+        *reinterpret_cast<bf16_t*>(dsw + swz<64>(r, c >> 3) + (c & 7) * 2) = f2bf(dpacc[i]);
+      }
+    }
+    __syncthreads();
+    // dQ partial of this wave: [64 q][64 d] = dS[64 q][32 keys] K[32 keys][64 d]
+#pragma unroll
+    for (int qt = 0; qt < 2; ++qt) {
+#pragma unroll
+      for (int dt = 0; dt < 2; ++dt) {
+        f32x16 acc = zero16();
+#pragma unroll
+        for (int s = 0; s < 2; ++s)
+          acc = mfma32(lds_frag<64>(dsw, qt * 32 + (lane & 31), 2 * s + hf),
+                       lds_tr_frag_nat<128>(kc, 16 * s, dt * 32, lane), acc);
+#pragma unroll
+        for (int i = 0; i < 16; ++i)
+          atomicAdd(dq_red + (qt * 32 + acc_row(i, hf)) * 64 + dt * 32 + (lane & 31), acc[i]);
+      }
+    }
+    __syncthreads();
+    // write / accumulate dQ for these 64 queries
+    for (int i = tid; i < 64 * 64; i += 256) {
+      const int r = i >> 6, d = i & 63;
+      const int qq = q0 + r;
+      if (qq < L) {
+        const float v = dq_red[i] * 0.125f;
+        if (dq_acc) atomicAdd(dq_acc + (((int64_t)b * L + qq) * H + hd) * HD + d, v);
+        else dqkv[((int64_t)b * L + qq) * ld + (int64_t)hd * HD + d] = f2bf(v);
+      }
+    }
+    __syncthreads();
+  }
+  // dK (scaled by 1/sqrt(64)), dV: reg i -> row key kbase + acc_row(i,hf), col d
+#pragma unroll
+  for (int dt = 0; dt < 2; ++dt)
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+      const int kk = kbase + acc_row(i, hf);
+      if (kk < L) {
+        bf16_t* base = dqkv + ((int64_t)b * L + kk) * ld + (int64_t)hd * HD + dt * 32 + (lane & 31);
+        base[(int64_t)H * HD] = f2bf(dk[dt][i] * 0.125f);
+        base[2LL * H * HD] = f2bf(dv[dt][i]);
+      }
+    }
+}
+
+// dq fp32 [B, L, H, 64] -> dqkv[:, :, 0] bf16
+__global__ void __launch_bounds__(256) attn_dq_cast_kernel(const float* __restrict__ dq,
+                                                          bf16_t* __restrict__ dqkv, int64_t rows,
+                                                          int H) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;  // over rows*64/4
+  if (i * 4 >= rows * HD) return;
+  const int64_t e = i * 4;
+  const int64_t row = e / HD;  // (b*L + q)*H + h
+  const int d = (int)(e % HD);
+  const int64_t bq = row / H;
+  const int hd = (int)(row % H);
+  f32x4 v = *reinterpret_cast<const f32x4*>(dq + e);
+  uint2 pk;
+  pk.x = pack_bf2(v[0], v[1]);
+  pk.y = pack_bf2(v[2], v[3]);
+  *reinterpret_cast<uint2*>(dqkv + bq * 3LL * H * HD + (int64_t)hd * HD + d) = pk;
+}
+
+void launch_attn_fwd(const uint16_t* qkv, uint16_t* out, float* lse, int B, int L, int H, float p,
+                     bool causal, uint32_t seed, uint32_t offset, hipStream_t s) {
+  dim3 grid((L + 127) / 128, H, B);
+  if (causal)
+    hipLaunchKernelGGL(attn_fwd_kernel<true>, grid, dim3(256), 0, s, (const bf16_t*)qkv,
+                       (bf16_t*)out, lse, L, H, p, seed, offset);
+  else
+    hipLaunchKernelGGL(attn_fwd_kernel<false>, grid, dim3(256), 0, s, (const bf16_t*)qkv,
+                       (bf16_t*)out, lse, L, H, p, seed, offset);
+}
+
+bool attn_bwd_needs_dq_acc(int L) { return L > 128; }
+
+void launch_attn_bwd(const uint16_t* qkv, const uint16_t* out, const uint16_t* dout, const float* lse,
+                     float* delta, uint16_t* dqkv, float* dq_acc, int B, int L, int H, float p,
+                     bool causal, uint32_t seed, uint32_t offset, hipStream_t s) {
+  const int64_t rows = (int64_t)B * L * H;
+  hipLaunchKernelGGL(attn_delta_kernel, dim3((unsigned)((rows + 255) / 256)), dim3(256), 0, s,
+                     (const bf16_t*)dout, (const bf16_t*)out, delta, B, L, H);
+  dim3 grid((L + 127) / 128, H, B);
+  float* acc = attn_bwd_needs_dq_acc(L) ? dq_acc : nullptr;
+  if (causal)
+    hipLaunchKernelGGL(attn_bwd_kernel<true>, grid, dim3(256), 0, s, (const bf16_t*)qkv,
+                       (const bf16_t*)dout, lse, delta, (bf16_t*)dqkv, acc, L, H, p, seed, offset);
+  else
+    hipLaunchKernelGGL(attn_bwd_kernel<false>, grid, dim3(256), 0, s, (const bf16_t*)qkv,
+                       (const bf16_t*)dout, lse, delta, (bf16_t*)dqkv, acc, L, H, p, seed, offset);
+  if (acc)
+    hipLaunchKernelGGL(attn_dq_cast_kernel, dim3((unsigned)((rows * HD / 4 + 255) / 256)), dim3(256),
+                       0, s, acc, (bf16_t*)dqkv, rows, H);
+}
+
+}  // namespace dpa

@@ -193,12 +193,13 @@ static std::vector<at::Tensor> add_ln_bwd(const at::Tensor& dout, const at::Tens
   if (need_dy) dy = at::empty_like(dout);
   auto f32 = dout.options().dtype(at::kFloat);
   const int nb = dpa::ln_bwd_blocks(R);
-  at::Tensor part = at::empty({2 * (int64_t)nb * D}, f32);
+  (void)nb;
+  at::Tensor part;
   at::Tensor dg = at::empty({D}, f32), db = at::empty({D}, f32);
   bool ok = dpa::launch_add_ln_bwd(
       bf_ptr(dout), bf_ptr(hs), mean.data_ptr<float>(), rstd.data_ptr<float>(), bf_ptr(g),
       need_dres ? reinterpret_cast<uint16_t*>(dres.data_ptr()) : nullptr,
-      need_dy ? reinterpret_cast<uint16_t*>(dy.data_ptr()) : nullptr, part.data_ptr<float>(),
+      need_dy ? reinterpret_cast<uint16_t*>(dy.data_ptr()) : nullptr, nullptr,
       dg.data_ptr<float>(), db.data_ptr<float>(), R, D, (float)p, (uint32_t)seed, (uint32_t)offset,
       cur_stream());
   TORCH_CHECK(ok, "add_ln_bwd: unsupported hidden size ", D);
@@ -241,6 +242,41 @@ static std::vector<at::Tensor> bias_act_bwd(const at::Tensor& dy, const at::Tens
   return {dz, db};
 }
 
+// ---- attention ---------------------------------------------------------------------
+static std::vector<at::Tensor> attn_fwd(const at::Tensor& qkv, int64_t heads, double p, bool causal,
+                                        int64_t seed, int64_t offset) {
+  CHECK_DEV(qkv); CHECK_BF16(qkv); CHECK_CONTIG(qkv);
+  TORCH_CHECK(qkv.dim() == 3, "qkv must be [B, L, 3*H*64]");
+  const int B = (int)qkv.size(0), L = (int)qkv.size(1), H = (int)heads;
+  TORCH_CHECK(qkv.size(2) == 3LL * H * 64, "attn: head_dim must be 64");
+  TORCH_CHECK(L % 64 == 0, "attn: L must be a multiple of 64");
+  const c10::DeviceGuard guard(qkv.device());
+  at::Tensor out = at::empty({B, L, (int64_t)H * 64}, qkv.options());
+  at::Tensor lse = at::empty({B, H, L}, qkv.options().dtype(at::kFloat));
+  dpa::launch_attn_fwd(bf_ptr(qkv), reinterpret_cast<uint16_t*>(out.data_ptr()),
+                       lse.data_ptr<float>(), B, L, H, (float)p, causal, (uint32_t)seed,
+                       (uint32_t)offset, cur_stream());
+  return {out, lse};
+}
+
+static at::Tensor attn_bwd(const at::Tensor& dout, const at::Tensor& qkv, const at::Tensor& out,
+                           const at::Tensor& lse, int64_t heads, double p, bool causal, int64_t seed,
+                           int64_t offset) {
+  CHECK_DEV(dout); CHECK_BF16(dout); CHECK_CONTIG(dout); CHECK_CONTIG(out); CHECK_CONTIG(qkv);
+  const int B = (int)qkv.size(0), L = (int)qkv.size(1), H = (int)heads;
+  TORCH_CHECK(dout.sizes() == out.sizes(), "dout shape");
+  const c10::DeviceGuard guard(qkv.device());
+  at::Tensor dqkv = at::empty_like(qkv);
+  at::Tensor delta = at::empty({B, H, L}, qkv.options().dtype(at::kFloat));
+  at::Tensor dq;
+  if (dpa::attn_bwd_needs_dq_acc(L)) dq = at::zeros({B, L, H, 64}, qkv.options().dtype(at::kFloat));
+  dpa::launch_attn_bwd(bf_ptr(qkv), bf_ptr(out), bf_ptr(dout), lse.data_ptr<float>(),
+                       delta.data_ptr<float>(), reinterpret_cast<uint16_t*>(dqkv.data_ptr()),
+                       dq.defined() ? dq.data_ptr<float>() : nullptr, B, L, H, (float)p, causal,
+                       (uint32_t)seed, (uint32_t)offset, cur_stream());
+  return dqkv;
+}
+
 PYBIND11_MODULE(_C, m) {
   m.doc() = "distributed_pipeline_amd native gfx950 kernels";
   m.def("sqnorm", &sqnorm, "flat grad L2 norm + clip coefficient (device)");
@@ -251,6 +287,8 @@ PYBIND11_MODULE(_C, m) {
   m.def("add_ln_bwd", &add_ln_bwd, "backward of add_ln_fwd -> (dres, dy, dgamma, dbeta)");
   m.def("bias_act_fwd", &bias_act_fwd, "z += bias (in place); y = act(z) -> (z, y)");
   m.def("bias_act_bwd", &bias_act_bwd, "dz = dy*act'(zy); db = colsum(dz) -> (dz, db)");
+  m.def("attn_fwd", &attn_fwd, "fused attention forward (head_dim 64) -> (out, lse)");
+  m.def("attn_bwd", &attn_bwd, "fused attention backward -> dqkv");
   m.def("lxent_fwd", &lxent_fwd, "fused linear + cross-entropy forward -> (loss, lse)");
   m.def("lxent_bwd", &lxent_bwd, "fused linear + cross-entropy backward -> (dx, dW fp32, db fp32)");
 }

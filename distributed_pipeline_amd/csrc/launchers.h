@@ -45,4 +45,12 @@ void launch_bias_act_fwd(uint16_t* z, const uint16_t* bias, uint16_t* y, int64_t
 void launch_bias_act_bwd(const uint16_t* dy, const uint16_t* zy, uint16_t* dz, float* db, int64_t R,
                          int N, int act, hipStream_t s);
 
+// ---- attention.hip (head_dim 64, dropout, causal) ---------------------------------
+void launch_attn_fwd(const uint16_t* qkv, uint16_t* out, float* lse, int B, int L, int H, float p,
+                     bool causal, uint32_t seed, uint32_t offset, hipStream_t s);
+bool attn_bwd_needs_dq_acc(int L);
+void launch_attn_bwd(const uint16_t* qkv, const uint16_t* out, const uint16_t* dout, const float* lse,
+                     float* delta, uint16_t* dqkv, float* dq_acc, int B, int L, int H, float p,
+                     bool causal, uint32_t seed, uint32_t offset, hipStream_t s);
+
 }  // namespace dpa

@@ -51,7 +51,14 @@ __device__ __forceinline__ bf16x8 ld_frag(const bf16_t* p) {
 // transposed reads).  ROWBYTES is a multiple of 256.
 template <int ROWBYTES>
 __device__ __forceinline__ int swz(int row, int ch) {
-  return row * ROWBYTES + ((ch ^ (row & 15)) << 4);
+  if constexpr (ROWBYTES == 64) {
+    return row * 64 + ((ch ^ ((row >> 2) & 3)) << 4);
+  } else if constexpr (ROWBYTES == 128) {
+    return row * 128 + ((ch ^ ((row >> 1) & 7)) << 4);
+  } else {
+    static_assert(ROWBYTES % 256 == 0, "row must be 64, 128 or a multiple of 256 bytes");
+    return row * ROWBYTES + ((ch ^ (row & 15)) << 4);
+  }
 }
 
 // ds_read_b64_tr_b16: per 16-lane group, lane 4q+p supplies the address of
@@ -60,6 +67,50 @@ __device__ __forceinline__ int swz(int row, int ch) {
 typedef __attribute__((address_space(3))) bf16x4 lds_bf16x4;
 __device__ __forceinline__ bf16x4 ds_read_tr16(const void* lds_ptr) {
   return __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_bf16x4*)(lds_ptr));
+}
+
+// A/B fragment (8 bf16 of row `row`, 16-byte chunk `ch`) from a swizzled tile.
+template <int ROWB>
+__device__ __forceinline__ bf16x8 lds_frag(const char* lds, int row, int ch) {
+  return *reinterpret_cast<const bf16x8*>(lds + swz<ROWB>(row, ch));
+}
+
+__device__ __forceinline__ bf16x8 cat44(const bf16x4& a, const bf16x4& b) {
+  bf16x8 f;
+  f[0] = a[0]; f[1] = a[1]; f[2] = a[2]; f[3] = a[3];
+  f[4] = b[0]; f[5] = b[1]; f[6] = b[2]; f[7] = b[3];
+  return f;
+}
+
+// B fragment for "accumulator as A operand" products (k order permuted as in
+// the header comment): rows r0 + 4h + q and r0 + 8 + 4h + q (q = 0..3) of the
+// column block col0..col0+31 (this lane receives column col0 + (lane & 31)),
+// read transposed from a swizzled LDS tile.  EXEC must be all ones.
+template <int ROWB>
+__device__ __forceinline__ bf16x8 lds_tr_frag(const char* lds, int r0, int col0, int lane) {
+  const int g = lane >> 4, li = lane & 15, q = li >> 2, p = li & 3, h = lane >> 5;
+  const int col = col0 + 16 * (g & 1) + 4 * p;
+  const int ra = r0 + 4 * h + q;
+  const char* pa = lds + swz<ROWB>(ra, col >> 3) + (col & 7) * 2;
+  const char* pb = lds + swz<ROWB>(ra + 8, col >> 3) + (col & 7) * 2;
+  return cat44(ds_read_tr16(pa), ds_read_tr16(pb));
+}
+
+// Same, natural k order (B[k = 8h + j][col]): rows r0 + 8h + q and r0 + 8h + 4 + q.
+template <int ROWB>
+__device__ __forceinline__ bf16x8 lds_tr_frag_nat(const char* lds, int r0, int col0, int lane) {
+  const int g = lane >> 4, li = lane & 15, q = li >> 2, p = li & 3, h = lane >> 5;
+  const int col = col0 + 16 * (g & 1) + 4 * p;
+  const int ra = r0 + 8 * h + q;
+  const char* pa = lds + swz<ROWB>(ra, col >> 3) + (col & 7) * 2;
+  const char* pb = lds + swz<ROWB>(ra + 4, col >> 3) + (col & 7) * 2;
+  return cat44(ds_read_tr16(pa), ds_read_tr16(pb));
+}
+
+// Cheap 32-bit hash (lowbias32) for dropout masks inside matrix-core loops.
+__device__ __forceinline__ uint32_t lowbias32(uint32_t x) {
+  x ^= x >> 16; x *= 0x7feb352du; x ^= x >> 15; x *= 0x846ca68bu; x ^= x >> 16;
+  return x;
 }
 
 }  // namespace dpa

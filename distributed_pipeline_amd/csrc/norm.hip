@@ -11,7 +11,7 @@
 // Philox stream (seed, offset, row, column) in the backward.
 //
 // dgamma/dbeta: each block accumulates its rows' contributions in registers,
-// writes one fp32 partial row; a second kernel sums the partials per column.
+// reduces its 4 waves through LDS and adds one fp32 atomic per column.
 #include "common.h"
 #include "launchers.h"
 
@@ -172,20 +172,11 @@ __global__ void __launch_bounds__(256) add_ln_bwd_kernel(
     red[1][w][col0 + i] = adb[i];
   }
   __syncthreads();
+  // one fp32 atomic per column per block (dg/db zeroed by the launcher)
   for (int c = threadIdx.x; c < D; c += blockDim.x) {
-    part_dg[(int64_t)blockIdx.x * D + c] = red[0][0][c] + red[0][1][c] + red[0][2][c] + red[0][3][c];
-    part_db[(int64_t)blockIdx.x * D + c] = red[1][0][c] + red[1][1][c] + red[1][2][c] + red[1][3][c];
+    atomicAdd(part_dg + c, red[0][0][c] + red[0][1][c] + red[0][2][c] + red[0][3][c]);
+    atomicAdd(part_db + c, red[1][0][c] + red[1][1][c] + red[1][2][c] + red[1][3][c]);
   }
-}
-
-// out[c] = sum_b part[b][c]  (one thread per column, coalesced over c)
-__global__ void __launch_bounds__(256) colsum_kernel(const float* __restrict__ part, int nb, int D,
-                                                    float* __restrict__ out) {
-  const int c = blockIdx.x * blockDim.x + threadIdx.x;
-  if (c >= D) return;
-  float s = 0.f;
-  for (int b = 0; b < nb; ++b) s += part[(int64_t)b * D + c];
-  out[c] = s;
 }
 
 #define DPA_LN_DISPATCH(D, FN, ...)                      \
@@ -220,7 +211,7 @@ bool launch_add_ln_fwd(const uint16_t* y, const uint16_t* res, const uint16_t* g
 
 int ln_bwd_blocks(int64_t R) {
   int64_t nb = (R + 3) / 4;
-  return (int)(nb < 1024 ? nb : 1024);
+  return (int)(nb < 512 ? nb : 512);
 }
 
 template <int VEC>
@@ -230,13 +221,12 @@ static void ln_bwd_impl(const uint16_t* dout, const uint16_t* hsave, const float
                         uint32_t off, hipStream_t s) {
   constexpr int D = VEC * 64;
   const int nb = ln_bwd_blocks(R);
-  float* pdg = part;
-  float* pdb = part + (int64_t)nb * D;
+  (void)part;
+  hipMemsetAsync(dg, 0, sizeof(float) * D, s);
+  hipMemsetAsync(db, 0, sizeof(float) * D, s);
   hipLaunchKernelGGL(add_ln_bwd_kernel<VEC>, dim3(nb), dim3(256), 0, s, (const bf16_t*)dout,
                      (const bf16_t*)hsave, mean, rstd, (const bf16_t*)g, (bf16_t*)dres, (bf16_t*)dy,
-                     pdg, pdb, R, p, seed, off);
-  hipLaunchKernelGGL(colsum_kernel, dim3((D + 255) / 256), dim3(256), 0, s, pdg, nb, D, dg);
-  hipLaunchKernelGGL(colsum_kernel, dim3((D + 255) / 256), dim3(256), 0, s, pdb, nb, D, db);
+                     dg, db, R, p, seed, off);
 }
 
 bool launch_add_ln_bwd(const uint16_t* dout, const uint16_t* hsave, const float* mean,

@@ -61,30 +61,6 @@ struct WTile {
   }
 };
 
-// A/B fragment (8 bf16 of row `row`, 16-byte chunk `ch`) from a swizzled tile.
-template <int ROWB>
-__device__ __forceinline__ bf16x8 lds_frag(const char* lds, int row, int ch) {
-  return *reinterpret_cast<const bf16x8*>(lds + swz<ROWB>(row, ch));
-}
-
-// B fragment for "acc as A operand" products: 8 rows in the permuted k order
-// (rows r0 + 4h + q and r0 + 8 + 4h + q, q = 0..3) of column block col0..col0+31
-// (this lane receives column col0 + (lane & 31)), read transposed from LDS.
-template <int ROWB>
-__device__ __forceinline__ bf16x8 lds_tr_frag(const char* lds, int r0, int col0, int lane) {
-  const int g = lane >> 4, li = lane & 15, q = li >> 2, p = li & 3, h = lane >> 5;
-  const int col = col0 + 16 * (g & 1) + 4 * p;
-  const int ra = r0 + 4 * h + q;
-  const char* pa = lds + swz<ROWB>(ra, col >> 3) + (col & 7) * 2;
-  const char* pb = lds + swz<ROWB>(ra + 8, col >> 3) + (col & 7) * 2;
-  bf16x4 a = ds_read_tr16(pa);
-  bf16x4 b = ds_read_tr16(pb);
-  bf16x8 f;
-  f[0] = a[0]; f[1] = a[1]; f[2] = a[2]; f[3] = a[3];
-  f[4] = b[0]; f[5] = b[1]; f[6] = b[2]; f[7] = b[3];
-  return f;
-}
-
 __device__ __forceinline__ float sel16(const f32x16& a, int i) {
   float v = 0.f;
 #pragma unroll

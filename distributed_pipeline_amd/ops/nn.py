@@ -117,9 +117,14 @@ class _LinearFn(torch.autograd.Function):
     def forward(ctx, x, w, b, w16, b16, act):
         shp = x.shape
         x2 = x.reshape(-1, shp[-1])
-        z = x2 @ w16.t()
-        if b16 is not None or act != "none":
-            z, y = _bias_act_fwd(z, b16, act)
+        if act == "none" and b16 is not None and x2.is_cuda:
+            z = torch.addmm(b16, x2, w16.t())  # hipBLASLt bias epilogue
+            b16_epi = None
+        else:
+            z = x2 @ w16.t()
+            b16_epi = b16
+        if b16_epi is not None or act != "none":
+            z, y = _bias_act_fwd(z, b16_epi, act)
         else:
             y = z
         # what the activation backward needs: tanh uses y, gelu/silu use z
