@@ -10,13 +10,12 @@
 //   S^T, forms the exact probabilities (no online rescale of O needed),
 //   applies dropout and feeds them - still in registers - as the A operand of
 //   O = P^T V, with V read transposed from LDS (ds_read_b64_tr_b16).
-// Backward: one workgroup = 128 keys of one (batch, head), 4 waves x 32 keys,
-//   K and V of the wave's keys in registers; sweeps query tiles of 64:
-//   S = Q K^T and dP = dO V^T (query-major), P rebuilt from the saved LSE,
-//   dS = P (dP - delta); dV += P^T dO and dK += dS^T Q straight from the
-//   accumulators; dS crosses LDS once for dQ = dS K, which the 4 waves reduce
-//   with LDS float atomics.  With one key block per (batch, head) (L <= 128)
-//   dQ is final and stored directly; longer sequences add fp32 global atomics.
+//   For L <= 128 a single pass holds the whole S^T column in registers.
+// Backward: two lean kernels, neither with atomics.  kv-kernel: 128 keys per
+//   workgroup (keys on the lane, K/V in registers), sweeps query tiles:
+//   dV += dropout(P)^T dO and dK += dS^T Q straight from the accumulators.
+//   q-kernel: 128 queries per workgroup (like the forward), sweeps key tiles:
+//   dQ += dS K with dS^T as the A operand.  P and dP are recomputed in each.
 // Dropout: keep/drop bits come from a per-(query, key-pair) hash of
 //   (seed, offset, batch*head), so forward and backward agree without storing
 //   a mask.
@@ -178,6 +177,103 @@ __global__ void __launch_bounds__(256) attn_fwd_kernel(const bf16_t* __restrict_
     }
 }
 
+
+// L <= 128: every key of the (batch, head) fits one LDS image and the whole
+// S^T column of a query fits in registers -> exact softmax in one pass.
+template <bool CAUSAL>
+__global__ void __launch_bounds__(256) attn_fwd_small_kernel(const bf16_t* __restrict__ qkv,
+                                                            bf16_t* __restrict__ out,
+                                                            float* __restrict__ lse, int L, int H,
+                                                            float p, uint32_t seed, uint32_t offset) {
+  __shared__ __attribute__((aligned(16))) char smem[2 * 128 * 128];
+  char* kt_lds = smem;
+  char* vt_lds = smem + 128 * 128;
+  const int b = blockIdx.z, hd = blockIdx.y;
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, hf = lane >> 5;
+  const int64_t ld = 3LL * H * HD;
+  const bf16_t* qb = qkv + (int64_t)b * L * ld + (int64_t)hd * HD;
+  const bf16_t* kb = qb + (int64_t)H * HD;
+  const bf16_t* vb = qb + 2LL * H * HD;
+  const int nt = L >> 5;  // 32-key tiles (<= 4)
+  for (int r0 = 0; r0 < L; r0 += 64) {
+    stage64(kt_lds + r0 * 128, kb, ld, r0, L, tid);
+    stage64(vt_lds + r0 * 128, vb, ld, r0, L, tid);
+  }
+  const int qbase = w * 32;
+  const int q = qbase + (lane & 31);
+  const bool q_ok = q < L;
+  bf16x8 qf[4];
+#pragma unroll
+  for (int s = 0; s < 4; ++s) {
+    if (q_ok) qf[s] = ld_frag(qb + (int64_t)q * ld + 16 * s + 8 * hf);
+    else for (int j = 0; j < 8; ++j) qf[s][j] = 0;
+  }
+  const DropCfg dc = make_drop(p, seed, offset, (uint32_t)(b * H + hd));
+  __syncthreads();
+  if (qbase >= L) return;  // whole wave idle (L < 128); no barrier follows
+  f32x16 acc[4];
+  float m = -INFINITY;
+#pragma unroll
+  for (int t = 0; t < 4; ++t) {
+    acc[t] = zero16();
+    if (t < nt) {
+#pragma unroll
+      for (int s = 0; s < 4; ++s) acc[t] = mfma32(lds_frag<128>(kt_lds, t * 32 + (lane & 31), 2 * s + hf), qf[s], acc[t]);
+#pragma unroll
+      for (int i = 0; i < 16; ++i) {
+        const int key = t * 32 + acc_row(i, hf);
+        float y = acc[t][i] * ATT_C;
+        if (CAUSAL && key > q) y = -INFINITY;
+        acc[t][i] = y;
+        m = fmaxf(m, y);
+      }
+    }
+  }
+  m = fmaxf(m, __shfl_xor(m, 32, 64));
+  float l = 0.f;
+#pragma unroll
+  for (int t = 0; t < 4; ++t)
+    if (t < nt)
+#pragma unroll
+      for (int i = 0; i < 16; ++i) {
+        const float e = exp2f(acc[t][i] - m);
+        acc[t][i] = e;
+        l += e;
+      }
+  l += __shfl_xor(l, 32, 64);
+  const float inv_l = 1.f / l;
+  if (hf == 0 && q_ok) lse[((int64_t)b * H + hd) * L + q] = (m + log2f(l)) * LN2f;
+  f32x16 o[2];
+  o[0] = zero16();
+  o[1] = zero16();
+#pragma unroll
+  for (int t = 0; t < 4; ++t) {
+    if (t < nt) {
+#pragma unroll
+      for (int i = 0; i < 16; ++i) {
+        float pr = acc[t][i] * inv_l;
+        if (dc.on) pr = keep_bit(dc, q, t * 32 + acc_row(i, hf)) ? pr * dc.scale : 0.f;
+        acc[t][i] = pr;
+      }
+#pragma unroll
+      for (int s = 0; s < 2; ++s) {
+        const bf16x8 af = acc_to_frag(acc[t], s);
+#pragma unroll
+        for (int dt = 0; dt < 2; ++dt)
+          o[dt] = mfma32(af, lds_tr_frag<128>(vt_lds, t * 32 + 16 * s, dt * 32, lane), o[dt]);
+      }
+    }
+  }
+  bf16_t* ob = out + (int64_t)b * L * H * HD + (int64_t)hd * HD;
+#pragma unroll
+  for (int dt = 0; dt < 2; ++dt)
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+      const int qq = qbase + acc_row(i, hf);
+      if (qq < L) ob[(int64_t)qq * H * HD + dt * 32 + (lane & 31)] = f2bf(o[dt][i]);
+    }
+}
+
 // delta[b,h,q] = sum_d dO * O
 __global__ void __launch_bounds__(256) attn_delta_kernel(const bf16_t* __restrict__ dout,
                                                         const bf16_t* __restrict__ out,
@@ -205,39 +301,32 @@ __global__ void __launch_bounds__(256) attn_delta_kernel(const bf16_t* __restric
 }
 
 // ---------------------------------------------------------------------------
-// backward
+// backward, part 1: dK, dV.  Workgroup = 128 keys (4 waves x 32, keys on the
+// MFMA lane, K/V fragments in registers); sweeps query tiles of 64 staged in LDS.
+//   S = Q K^T, dP = dO V^T (queries in registers);  P from the saved LSE;
+//   dV += dropout(P)^T dO,  dK += dS^T Q   with dS = P (dropout'(dP) - delta),
+// both straight from the accumulators (dO / Q read transposed from LDS).
 // ---------------------------------------------------------------------------
 template <bool CAUSAL>
-__global__ void __launch_bounds__(256) attn_bwd_kernel(
+__global__ void __launch_bounds__(256) attn_bwd_kv_kernel(
     const bf16_t* __restrict__ qkv, const bf16_t* __restrict__ dout, const float* __restrict__ lse,
-    const float* __restrict__ delta, bf16_t* __restrict__ dqkv, float* __restrict__ dq_acc, int L,
-    int H, float p, uint32_t seed, uint32_t offset) {
-  constexpr int QT_B = 64 * 128;    // Q or dO tile bytes
-  constexpr int KC_B = 32 * 128;    // per-wave K copy
-  constexpr int DS_B = 64 * 64;     // per-wave dS tile [64 q][32 keys] bf16
-  __shared__ __attribute__((aligned(16))) char smem[2 * QT_B + 4 * KC_B + 4 * DS_B + 64 * 64 * 4 + 2 * 64 * 4];
+    const float* __restrict__ delta, bf16_t* __restrict__ dqkv, int L, int H, float p,
+    uint32_t seed, uint32_t offset) {
+  __shared__ __attribute__((aligned(16))) char smem[2 * 64 * 128 + 2 * 64 * 4];
   char* qt_lds = smem;
-  char* dot_lds = smem + QT_B;
-  char* kc_lds = smem + 2 * QT_B;
-  char* ds_lds = kc_lds + 4 * KC_B;
-  float* dq_red = reinterpret_cast<float*>(ds_lds + 4 * DS_B);
-  float* s_lse = dq_red + 64 * 64;
+  char* dot_lds = smem + 64 * 128;
+  float* s_lse = reinterpret_cast<float*>(smem + 2 * 64 * 128);
   float* s_del = s_lse + 64;
-
   const int b = blockIdx.z, hd = blockIdx.y;
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, hf = lane >> 5;
-  const int64_t ld = 3LL * H * HD;
+  const int64_t ld = 3LL * H * HD, ldo = (int64_t)H * HD;
   const bf16_t* qb = qkv + (int64_t)b * L * ld + (int64_t)hd * HD;
   const bf16_t* kb = qb + (int64_t)H * HD;
   const bf16_t* vb = qb + 2LL * H * HD;
-  const bf16_t* dob = dout + (int64_t)b * L * H * HD + (int64_t)hd * HD;
-  const int64_t ldo = (int64_t)H * HD;
+  const bf16_t* dob = dout + (int64_t)b * L * ldo + (int64_t)hd * HD;
   const int kbase = blockIdx.x * 128 + w * 32;
   const int key = kbase + (lane & 31);
   const bool k_ok = key < L;
-  char* kc = kc_lds + w * KC_B;
-  char* dsw = ds_lds + w * DS_B;
-
   bf16x8 kf[4], vf[4];
 #pragma unroll
   for (int s = 0; s < 4; ++s) {
@@ -247,14 +336,11 @@ __global__ void __launch_bounds__(256) attn_bwd_kernel(
     } else {
       for (int j = 0; j < 8; ++j) { kf[s][j] = 0; vf[s][j] = 0; }
     }
-    // K copy for the dQ product: row = key (local), chunk = 2s + hf
-    *reinterpret_cast<bf16x8*>(kc + swz<128>(lane & 31, 2 * s + hf)) = kf[s];
   }
   const DropCfg dc = make_drop(p, seed, offset, (uint32_t)(b * H + hd));
   const int64_t lrow = ((int64_t)b * H + hd) * L;
   f32x16 dk[2], dv[2];
   dk[0] = zero16(); dk[1] = zero16(); dv[0] = zero16(); dv[1] = zero16();
-
   const int qbeg = CAUSAL ? (int)blockIdx.x * 128 : 0;
   for (int q0 = qbeg; q0 < L; q0 += 64) {
     stage64(qt_lds, qb, ld, q0, L, tid);
@@ -264,9 +350,8 @@ __global__ void __launch_bounds__(256) attn_bwd_kernel(
       s_lse[tid] = ok ? lse[lrow + q0 + tid] * 1.4426950408889634f : 0.f;
       s_del[tid] = ok ? delta[lrow + q0 + tid] : 0.f;
     }
-    for (int i = tid; i < 64 * 64; i += 256) dq_red[i] = 0.f;
     __syncthreads();
-#pragma unroll
+#pragma unroll 1
     for (int qt = 0; qt < 2; ++qt) {
       f32x16 sacc = zero16(), dpacc = zero16();
 #pragma unroll
@@ -274,7 +359,6 @@ __global__ void __launch_bounds__(256) attn_bwd_kernel(
         sacc = mfma32(lds_frag<128>(qt_lds, qt * 32 + (lane & 31), 2 * s + hf), kf[s], sacc);
         dpacc = mfma32(lds_frag<128>(dot_lds, qt * 32 + (lane & 31), 2 * s + hf), vf[s], dpacc);
       }
-      // rows = queries (regs), cols = keys (lanes)
 #pragma unroll
       for (int i = 0; i < 16; ++i) {
         const int r = qt * 32 + acc_row(i, hf);
@@ -287,8 +371,8 @@ __global__ void __launch_bounds__(256) attn_bwd_kernel(
           pd = kp ? pr * dc.scale : 0.f;
           dpd = kp ? dpd * dc.scale : 0.f;
         }
-        sacc[i] = pd;                       // dropout(P)   -> dV
-        dpacc[i] = pr * (dpd - s_del[r]);   // dS           -> dK, dQ
+        sacc[i] = pd;
+        dpacc[i] = pr * (dpd - s_del[r]);
       }
 #pragma unroll
       for (int s = 0; s < 2; ++s) {
@@ -300,44 +384,9 @@ __global__ void __launch_bounds__(256) attn_bwd_kernel(
           dk[dt] = mfma32(sf, lds_tr_frag<128>(qt_lds, qt * 32 + 16 * s, dt * 32, lane), dk[dt]);
         }
       }
-      // dS -> LDS as [query][key] bf16 for dQ = dS K
-#pragma unroll
-      for (int i = 0; i < 16; ++i) {
-        const int r = qt * 32 + acc_row(i, hf);
-        const int c = lane & 31;
-        *reinterpret_cast<bf16_t*>(dsw + swz<64>(r, c >> 3) + (c & 7) * 2) = f2bf(dpacc[i]);
-      }
-    }
-    __syncthreads();
-    // dQ partial of this wave: [64 q][64 d] = dS[64 q][32 keys] K[32 keys][64 d]
-#pragma unroll
-    for (int qt = 0; qt < 2; ++qt) {
-#pragma unroll
-      for (int dt = 0; dt < 2; ++dt) {
-        f32x16 acc = zero16();
-#pragma unroll
-        for (int s = 0; s < 2; ++s)
-          acc = mfma32(lds_frag<64>(dsw, qt * 32 + (lane & 31), 2 * s + hf),
-                       lds_tr_frag_nat<128>(kc, 16 * s, dt * 32, lane), acc);
-#pragma unroll
-        for (int i = 0; i < 16; ++i)
-          atomicAdd(dq_red + (qt * 32 + acc_row(i, hf)) * 64 + dt * 32 + (lane & 31), acc[i]);
-      }
-    }
-    __syncthreads();
-    // write / accumulate dQ for these 64 queries
-    for (int i = tid; i < 64 * 64; i += 256) {
-      const int r = i >> 6, d = i & 63;
-      const int qq = q0 + r;
-      if (qq < L) {
-        const float v = dq_red[i] * 0.125f;
-        if (dq_acc) atomicAdd(dq_acc + (((int64_t)b * L + qq) * H + hd) * HD + d, v);
-        else dqkv[((int64_t)b * L + qq) * ld + (int64_t)hd * HD + d] = f2bf(v);
-      }
     }
     __syncthreads();
   }
-  // dK (scaled by 1/sqrt(64)), dV: reg i -> row key kbase + acc_row(i,hf), col d
 #pragma unroll
   for (int dt = 0; dt < 2; ++dt)
 #pragma unroll
@@ -351,27 +400,101 @@ __global__ void __launch_bounds__(256) attn_bwd_kernel(
     }
 }
 
-// dq fp32 [B, L, H, 64] -> dqkv[:, :, 0] bf16
-__global__ void __launch_bounds__(256) attn_dq_cast_kernel(const float* __restrict__ dq,
-                                                          bf16_t* __restrict__ dqkv, int64_t rows,
-                                                          int H) {
-  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;  // over rows*64/4
-  if (i * 4 >= rows * HD) return;
-  const int64_t e = i * 4;
-  const int64_t row = e / HD;  // (b*L + q)*H + h
-  const int d = (int)(e % HD);
-  const int64_t bq = row / H;
-  const int hd = (int)(row % H);
-  f32x4 v = *reinterpret_cast<const f32x4*>(dq + e);
-  uint2 pk;
-  pk.x = pack_bf2(v[0], v[1]);
-  pk.y = pack_bf2(v[2], v[3]);
-  *reinterpret_cast<uint2*>(dqkv + bq * 3LL * H * HD + (int64_t)hd * HD + d) = pk;
+// ---------------------------------------------------------------------------
+// backward, part 2: dQ.  Workgroup = 128 queries (queries on the lane, Q and dO
+// fragments in registers, like the forward); sweeps key tiles of 64 in LDS:
+//   S^T = K Q^T, dP^T = V dO^T (keys in registers), dS^T rebuilt, and
+//   dQ += dS K with dS^T fed as the A operand and K read transposed.
+// No atomics: each workgroup owns its queries' dQ rows completely.
+// ---------------------------------------------------------------------------
+template <bool CAUSAL>
+__global__ void __launch_bounds__(256) attn_bwd_q_kernel(
+    const bf16_t* __restrict__ qkv, const bf16_t* __restrict__ dout, const float* __restrict__ lse,
+    const float* __restrict__ delta, bf16_t* __restrict__ dqkv, int L, int H, float p,
+    uint32_t seed, uint32_t offset) {
+  __shared__ __attribute__((aligned(16))) char smem[2 * 64 * 128];
+  char* kt_lds = smem;
+  char* vt_lds = smem + 64 * 128;
+  const int b = blockIdx.z, hd = blockIdx.y;
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, hf = lane >> 5;
+  const int64_t ld = 3LL * H * HD, ldo = (int64_t)H * HD;
+  const bf16_t* qb = qkv + (int64_t)b * L * ld + (int64_t)hd * HD;
+  const bf16_t* kb = qb + (int64_t)H * HD;
+  const bf16_t* vb = qb + 2LL * H * HD;
+  const bf16_t* dob = dout + (int64_t)b * L * ldo + (int64_t)hd * HD;
+  const int qbase = blockIdx.x * 128 + w * 32;
+  const int q = qbase + (lane & 31);
+  const bool q_ok = q < L;
+  bf16x8 qf[4], df[4];
+#pragma unroll
+  for (int s = 0; s < 4; ++s) {
+    if (q_ok) {
+      qf[s] = ld_frag(qb + (int64_t)q * ld + 16 * s + 8 * hf);
+      df[s] = ld_frag(dob + (int64_t)q * ldo + 16 * s + 8 * hf);
+    } else {
+      for (int j = 0; j < 8; ++j) { qf[s][j] = 0; df[s][j] = 0; }
+    }
+  }
+  const int64_t lrow = ((int64_t)b * H + hd) * L;
+  const float lse2 = q_ok ? lse[lrow + q] * 1.4426950408889634f : 0.f;
+  const float dlt = q_ok ? delta[lrow + q] : 0.f;
+  const DropCfg dc = make_drop(p, seed, offset, (uint32_t)(b * H + hd));
+  f32x16 dq[2];
+  dq[0] = zero16();
+  dq[1] = zero16();
+  const int kv_end = CAUSAL ? min(L, (int)blockIdx.x * 128 + 128) : L;
+  for (int kv0 = 0; kv0 < kv_end; kv0 += 64) {
+    stage64(kt_lds, kb, ld, kv0, L, tid);
+    stage64(vt_lds, vb, ld, kv0, L, tid);
+    __syncthreads();
+#pragma unroll 1
+    for (int t = 0; t < 2; ++t) {
+      f32x16 sacc = zero16(), dpacc = zero16();
+#pragma unroll
+      for (int s = 0; s < 4; ++s) {
+        sacc = mfma32(lds_frag<128>(kt_lds, t * 32 + (lane & 31), 2 * s + hf), qf[s], sacc);
+        dpacc = mfma32(lds_frag<128>(vt_lds, t * 32 + (lane & 31), 2 * s + hf), df[s], dpacc);
+      }
+#pragma unroll
+      for (int i = 0; i < 16; ++i) {
+        const int kk = kv0 + t * 32 + acc_row(i, hf);
+        float pr = exp2f(sacc[i] * ATT_C - lse2);
+        if ((CAUSAL && kk > q) || !q_ok || kk >= L) pr = 0.f;
+        float dpd = dpacc[i];
+        if (dc.on) dpd = keep_bit(dc, q, kk) ? dpd * dc.scale : 0.f;
+        sacc[i] = pr * (dpd - dlt);
+      }
+#pragma unroll
+      for (int s = 0; s < 2; ++s) {
+        const bf16x8 sf = acc_to_frag(sacc, s);
+#pragma unroll
+        for (int dt = 0; dt < 2; ++dt)
+          dq[dt] = mfma32(sf, lds_tr_frag<128>(kt_lds, t * 32 + 16 * s, dt * 32, lane), dq[dt]);
+      }
+    }
+    __syncthreads();
+  }
+#pragma unroll
+  for (int dt = 0; dt < 2; ++dt)
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+      const int qq = qbase + acc_row(i, hf);
+      if (qq < L) dqkv[((int64_t)b * L + qq) * ld + (int64_t)hd * HD + dt * 32 + (lane & 31)] = f2bf(dq[dt][i] * 0.125f);
+    }
 }
 
 void launch_attn_fwd(const uint16_t* qkv, uint16_t* out, float* lse, int B, int L, int H, float p,
                      bool causal, uint32_t seed, uint32_t offset, hipStream_t s) {
   dim3 grid((L + 127) / 128, H, B);
+  if (L <= 128) {
+    if (causal)
+      hipLaunchKernelGGL(attn_fwd_small_kernel<true>, grid, dim3(256), 0, s, (const bf16_t*)qkv,
+                         (bf16_t*)out, lse, L, H, p, seed, offset);
+    else
+      hipLaunchKernelGGL(attn_fwd_small_kernel<false>, grid, dim3(256), 0, s, (const bf16_t*)qkv,
+                         (bf16_t*)out, lse, L, H, p, seed, offset);
+    return;
+  }
   if (causal)
     hipLaunchKernelGGL(attn_fwd_kernel<true>, grid, dim3(256), 0, s, (const bf16_t*)qkv,
                        (bf16_t*)out, lse, L, H, p, seed, offset);
@@ -380,25 +503,27 @@ void launch_attn_fwd(const uint16_t* qkv, uint16_t* out, float* lse, int B, int 
                        (bf16_t*)out, lse, L, H, p, seed, offset);
 }
 
-bool attn_bwd_needs_dq_acc(int L) { return L > 128; }
+bool attn_bwd_needs_dq_acc(int L) { (void)L; return false; }
 
 void launch_attn_bwd(const uint16_t* qkv, const uint16_t* out, const uint16_t* dout, const float* lse,
                      float* delta, uint16_t* dqkv, float* dq_acc, int B, int L, int H, float p,
                      bool causal, uint32_t seed, uint32_t offset, hipStream_t s) {
+  (void)dq_acc;
   const int64_t rows = (int64_t)B * L * H;
   hipLaunchKernelGGL(attn_delta_kernel, dim3((unsigned)((rows + 255) / 256)), dim3(256), 0, s,
                      (const bf16_t*)dout, (const bf16_t*)out, delta, B, L, H);
   dim3 grid((L + 127) / 128, H, B);
-  float* acc = attn_bwd_needs_dq_acc(L) ? dq_acc : nullptr;
-  if (causal)
-    hipLaunchKernelGGL(attn_bwd_kernel<true>, grid, dim3(256), 0, s, (const bf16_t*)qkv,
-                       (const bf16_t*)dout, lse, delta, (bf16_t*)dqkv, acc, L, H, p, seed, offset);
-  else
-    hipLaunchKernelGGL(attn_bwd_kernel<false>, grid, dim3(256), 0, s, (const bf16_t*)qkv,
-                       (const bf16_t*)dout, lse, delta, (bf16_t*)dqkv, acc, L, H, p, seed, offset);
-  if (acc)
-    hipLaunchKernelGGL(attn_dq_cast_kernel, dim3((unsigned)((rows * HD / 4 + 255) / 256)), dim3(256),
-                       0, s, acc, (bf16_t*)dqkv, rows, H);
+  if (causal) {
+    hipLaunchKernelGGL(attn_bwd_kv_kernel<true>, grid, dim3(256), 0, s, (const bf16_t*)qkv,
+                       (const bf16_t*)dout, lse, delta, (bf16_t*)dqkv, L, H, p, seed, offset);
+    hipLaunchKernelGGL(attn_bwd_q_kernel<true>, grid, dim3(256), 0, s, (const bf16_t*)qkv,
+                       (const bf16_t*)dout, lse, delta, (bf16_t*)dqkv, L, H, p, seed, offset);
+  } else {
+    hipLaunchKernelGGL(attn_bwd_kv_kernel<false>, grid, dim3(256), 0, s, (const bf16_t*)qkv,
+                       (const bf16_t*)dout, lse, delta, (bf16_t*)dqkv, L, H, p, seed, offset);
+    hipLaunchKernelGGL(attn_bwd_q_kernel<false>, grid, dim3(256), 0, s, (const bf16_t*)qkv,
+                       (const bf16_t*)dout, lse, delta, (bf16_t*)dqkv, L, H, p, seed, offset);
+  }
 }
 
 }  // namespace dpa

@@ -277,6 +277,57 @@ static at::Tensor attn_bwd(const at::Tensor& dout, const at::Tensor& qkv, const 
   return dqkv;
 }
 
+// ---- GEMMs ---------------------------------------------------------------------------
+static std::vector<at::Tensor> gemm_nt(const at::Tensor& x, const at::Tensor& W,
+                                       c10::optional<at::Tensor> b, int64_t act) {
+  CHECK_DEV(x); CHECK_BF16(x); CHECK_BF16(W); CHECK_CONTIG(x); CHECK_CONTIG(W);
+  const int T = (int)x.size(0), K = (int)x.size(1), N = (int)W.size(0);
+  TORCH_CHECK(W.size(1) == K, "gemm_nt: W [N, K]");
+  const c10::DeviceGuard guard(x.device());
+  at::Tensor y = at::empty({T, N}, x.options());
+  at::Tensor z;
+  if (act == 1 || act == 3) z = at::empty({T, N}, x.options());
+  bool ok = dpa::launch_gemm_nt(bf_ptr(x), bf_ptr(W), opt_bf_ptr(b),
+                                reinterpret_cast<uint16_t*>(y.data_ptr()),
+                                z.defined() ? reinterpret_cast<uint16_t*>(z.data_ptr()) : nullptr, T, N,
+                                K, (int)act, cur_stream());
+  TORCH_CHECK(ok, "gemm_nt: unsupported shape T=", T, " N=", N, " K=", K);
+  return {y, z};
+}
+
+static at::Tensor gemm_nn(const at::Tensor& dy, const at::Tensor& W) {
+  CHECK_DEV(dy); CHECK_BF16(dy); CHECK_BF16(W); CHECK_CONTIG(dy); CHECK_CONTIG(W);
+  const int T = (int)dy.size(0), N = (int)dy.size(1), K = (int)W.size(1);
+  TORCH_CHECK(W.size(0) == N, "gemm_nn: W [N, K]");
+  const c10::DeviceGuard guard(dy.device());
+  at::Tensor dx = at::empty({T, K}, dy.options());
+  bool ok = dpa::launch_gemm_nn(bf_ptr(dy), bf_ptr(W), reinterpret_cast<uint16_t*>(dx.data_ptr()), T,
+                                N, K, cur_stream());
+  TORCH_CHECK(ok, "gemm_nn: unsupported shape");
+  return dx;
+}
+
+static void gemm_wgrad(const at::Tensor& dy, const at::Tensor& x, at::Tensor& dW,
+                       c10::optional<at::Tensor> db) {
+  CHECK_DEV(dy); CHECK_BF16(dy); CHECK_BF16(x); CHECK_CONTIG(dy); CHECK_CONTIG(x);
+  CHECK_F32(dW); CHECK_CONTIG(dW);
+  const int T = (int)dy.size(0), N = (int)dy.size(1), K = (int)x.size(1);
+  TORCH_CHECK(x.size(0) == T && dW.size(0) == N && dW.size(1) == K, "gemm_wgrad shapes");
+  float* dbp = nullptr;
+  if (db.has_value() && db->defined()) {
+    CHECK_F32((*db)); TORCH_CHECK(db->numel() == N, "db size");
+    dbp = db->data_ptr<float>();
+  }
+  const c10::DeviceGuard guard(dy.device());
+  bool ok = dpa::launch_gemm_wgrad(bf_ptr(dy), bf_ptr(x), dW.data_ptr<float>(), dbp, T, N, K,
+                                   cur_stream());
+  TORCH_CHECK(ok, "gemm_wgrad: unsupported shape");
+}
+
+static bool gemm_supported(int64_t M, int64_t N, int64_t K) {
+  return M % 128 == 0 && N % 128 == 0 && K % 128 == 0;
+}
+
 PYBIND11_MODULE(_C, m) {
   m.doc() = "distributed_pipeline_amd native gfx950 kernels";
   m.def("sqnorm", &sqnorm, "flat grad L2 norm + clip coefficient (device)");
@@ -289,6 +340,10 @@ PYBIND11_MODULE(_C, m) {
   m.def("bias_act_bwd", &bias_act_bwd, "dz = dy*act'(zy); db = colsum(dz) -> (dz, db)");
   m.def("attn_fwd", &attn_fwd, "fused attention forward (head_dim 64) -> (out, lse)");
   m.def("attn_bwd", &attn_bwd, "fused attention backward -> dqkv");
+  m.def("gemm_nt", &gemm_nt, "y = act(x W^T + b) (bf16 MFMA) -> (y, z_preact)");
+  m.def("gemm_nn", &gemm_nn, "dx = dy W (bf16 MFMA)");
+  m.def("gemm_wgrad", &gemm_wgrad, "dW += dy^T x, db += colsum(dy) (fp32 atomics, split-K)");
+  m.def("gemm_supported", &gemm_supported, "shape check for the native GEMMs");
   m.def("lxent_fwd", &lxent_fwd, "fused linear + cross-entropy forward -> (loss, lse)");
   m.def("lxent_bwd", &lxent_bwd, "fused linear + cross-entropy backward -> (dx, dW fp32, db fp32)");
 }

@@ -53,4 +53,12 @@ void launch_attn_bwd(const uint16_t* qkv, const uint16_t* out, const uint16_t* d
                      float* delta, uint16_t* dqkv, float* dq_acc, int B, int L, int H, float p,
                      bool causal, uint32_t seed, uint32_t offset, hipStream_t s);
 
+// ---- gemm.hip (bf16 MFMA GEMMs of Linear layers) ----------------------------------
+bool launch_gemm_nt(const uint16_t* x, const uint16_t* W, const uint16_t* bias, uint16_t* y,
+                    uint16_t* z, int T, int N, int K, int act, hipStream_t s);
+bool launch_gemm_nn(const uint16_t* dy, const uint16_t* W, uint16_t* dx, int T, int N, int K,
+                    hipStream_t s);
+bool launch_gemm_wgrad(const uint16_t* dy, const uint16_t* x, float* dW, float* db, int T, int N,
+                       int K, hipStream_t s);
+
 }  // namespace dpa
