@@ -63,7 +63,8 @@ class SyntheticSeq2SeqDataset(_BatchedDataset):
         src_len = (lo + (h[:, L] % np.uint64(max(1, L // 4))).astype(np.int64))
         trg_len = (1 + (h[:, L + 1] % np.uint64(max(1, body - src_len.max()))).astype(np.int64))
         trg_len = np.minimum(trg_len, L - 3 - src_len)
-        tok = (1000 + (h[:, :L] % np.uint64(self.V - 1000))).astype(np.int64)
+        t0 = 1000 if self.V > 2000 else 103  # skip [PAD]/[CLS]/[SEP]-range ids
+        tok = (t0 + (h[:, :L] % np.uint64(self.V - t0))).astype(np.int64)
         j = np.arange(L)[None, :]
         s_end = 1 + src_len[:, None]
         t_end = s_end + 1 + trg_len[:, None]

@@ -112,36 +112,92 @@ def _bias_act_bwd(dy2d, z, y, act, want_db):
     return dz, db
 
 
+def _native_gemm_ok(x2, n_out):
+    return (x2.is_cuda and x2.dtype == torch.bfloat16 and native_ok(x2, kernel="gemm_nt")
+            and x2.shape[0] % 128 == 0 and n_out % 128 == 0 and x2.shape[1] % 128 == 0)
+
+
+def _accumulate_wgrad(p, dz, x2, bias):
+    """dW (+db) straight into the parameters' fp32 .grad buffers via the split-K GEMM.
+
+    Returns (dw, db) tensors only when a parameter has no preallocated gradient.
+    """
+    ext = get_ext()
+    dw_out = db_out = None
+    gw = p.grad
+    if gw is None or gw.dtype != torch.float32 or not gw.is_contiguous():
+        gw = dw_out = torch.zeros(p.shape, dtype=torch.float32, device=dz.device)
+    gb = None
+    if bias is not None and bias.requires_grad:
+        gb = bias.grad
+        if gb is None or gb.dtype != torch.float32:
+            gb = db_out = torch.zeros(bias.shape, dtype=torch.float32, device=dz.device)
+    ext.gemm_wgrad(dz, x2, gw, gb)
+    for t, out in ((p, dw_out), (bias, db_out)):
+        if t is not None and out is None:
+            notify = getattr(t, "_dpa_notify", None)
+            if notify is not None:
+                notify(t)
+    return dw_out, db_out
+
+
 class _LinearFn(torch.autograd.Function):
+    """y = act(x W^T + b) in bf16 with fp32 master weights.
+
+    Native path: one MFMA GEMM with the bias/activation epilogue forward; in
+    backward the activation derivative, one dgrad GEMM and one split-K wgrad
+    GEMM that atomically accumulates dW and db into the fp32 ``.grad`` views of
+    the flat gradient buffer (gradient-accumulation fusion).
+    """
+
     @staticmethod
     def forward(ctx, x, w, b, w16, b16, act):
         shp = x.shape
         x2 = x.reshape(-1, shp[-1])
-        if act == "none" and b16 is not None and x2.is_cuda:
-            z = torch.addmm(b16, x2, w16.t())  # hipBLASLt bias epilogue
-            b16_epi = None
+        native = _native_gemm_ok(x2, w16.shape[0])
+        if native:
+            y, z = get_ext().gemm_nt(x2, w16, b16, _ACTS.index(act))
+            if act == "none":
+                z = None
         else:
-            z = x2 @ w16.t()
-            b16_epi = b16
-        if b16_epi is not None or act != "none":
-            z, y = _bias_act_fwd(z, b16_epi, act)
-        else:
-            y = z
+            if act == "none" and b16 is not None and x2.is_cuda:
+                z = torch.addmm(b16, x2, w16.t())  # hipBLASLt bias epilogue
+                b16_epi = None
+            else:
+                z = x2 @ w16.t()
+                b16_epi = b16
+            if b16_epi is not None or act != "none":
+                z, y = _bias_act_fwd(z, b16_epi, act)
+            else:
+                y = z
         # what the activation backward needs: tanh uses y, gelu/silu use z
         keep_z = z if act in ("gelu", "silu") else None
         keep_y = y if act == "tanh" else None
         ctx.save_for_backward(x2, w16, keep_z, keep_y)
+        ctx.params = (w, b)
         ctx.act = act
         ctx.has_b = b is not None
+        ctx.native = native
         ctx.shp = shp
         return y.reshape(*shp[:-1], w16.shape[0])
 
     @staticmethod
     def backward(ctx, dy):
         x2, w16, z, y = ctx.saved_tensors
-        dy2 = dy.reshape(-1, dy.shape[-1])
+        w, b = ctx.params
+        dy2 = dy.reshape(-1, dy.shape[-1]).contiguous()
+        if ctx.native:
+            dz = dy2
+            if ctx.act != "none":
+                zy = z if z is not None else y
+                dz, _ = get_ext().bias_act_bwd(dy2, zy, _ACTS.index(ctx.act), False)
+            dx = get_ext().gemm_nn(dz, w16).reshape(ctx.shp) if ctx.needs_input_grad[0] else None
+            dw = db = None
+            if ctx.needs_input_grad[1] or (ctx.has_b and ctx.needs_input_grad[2]):
+                dw, db = _accumulate_wgrad(w, dz, x2, b if ctx.has_b else None)
+            return dx, dw, db, None, None, None
         if ctx.act != "none" or ctx.has_b:
-            dz, db = _bias_act_bwd(dy2.contiguous(), z, y, ctx.act, ctx.has_b)
+            dz, db = _bias_act_bwd(dy2, z, y, ctx.act, ctx.has_b)
         else:
             dz, db = dy2, None
         dx = (dz @ w16).reshape(ctx.shp) if ctx.needs_input_grad[0] else None

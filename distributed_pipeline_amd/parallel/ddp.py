@@ -94,7 +94,9 @@ class DDPEngine(nn.Module):
             if broadcast_from_rank0:
                 self.broadcast_parameters()
             for p in self.space.layout:
-                self._hooks.append(p.register_post_accumulate_grad_hook(self._make_hook(p)))
+                hook = self._make_hook(p)
+                self._hooks.append(p.register_post_accumulate_grad_hook(hook))
+                p._dpa_notify = hook  # fused ops that write .grad directly call this
         self._comm_buf = None
 
     # -- setup ---------------------------------------------------------------

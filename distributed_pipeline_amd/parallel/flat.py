@@ -51,6 +51,8 @@ class FlatParamSpace:
                 o, n = self.offsets[id(p)], p.numel()
                 self.param_flat[o:o + n].copy_(p.detach().reshape(-1).to(torch.float32))
                 p.data = self.param_flat[o:o + n].view(p.shape)
+                if p.grad is not None:  # keep already-accumulated gradients
+                    self.grad_flat[o:o + n].copy_(p.grad.detach().reshape(-1))
                 p.grad = self.grad_flat[o:o + n].view(p.shape)
                 if self.shadow_flat is not None:
                     p._dpa_shadow = self.shadow_flat[o:o + n].view(p.shape)

@@ -1,0 +1,51 @@
+"""End-to-end numerics of the native bf16 DiffuSeq path (all HIP kernels) against the
+same model evaluated in fp32 with stock PyTorch ops."""
+import copy
+
+import pytest
+import torch
+
+from distributed_pipeline_amd.models import build_model, create_gaussian_diffusion
+from distributed_pipeline_amd.parallel.ddp import DDPEngine
+
+pytestmark = pytest.mark.gpu
+
+CFG = dict(model="diffuseq", config_name="tiny", hidden_size=256, num_layers=2, num_heads=4,
+           intermediate_size=1024, vocab_size=3000, seq_len=128, hidden_dim=128, hidden_t_dim=128,
+           dropout=0.0)
+
+
+def _grads(model):
+    return {n: p.grad.detach().float().clone() for n, p in model.named_parameters() if p.grad is not None}
+
+
+def test_diffuseq_native_bf16_matches_fp32(monkeypatch):
+    torch.manual_seed(0)
+    ref = build_model(precision="fp32", **CFG).cuda()
+    nat = build_model(precision="bf16", **CFG).cuda()
+    nat.load_state_dict(ref.state_dict())
+    eng = DDPEngine(nat, shadow_dtype=torch.bfloat16)
+    diff = create_gaussian_diffusion(steps=2000)
+    B, L = 4, 128
+    ids = torch.randint(1000, 3000, (B, L), device="cuda")
+    mask = torch.zeros(B, L, dtype=torch.long, device="cuda")
+    mask[:, 40:] = 1
+    t = torch.tensor([0, 10, 900, 1999], device="cuda")
+    gen_state = torch.cuda.get_rng_state()
+
+    def run(model):
+        torch.cuda.set_rng_state(gen_state)
+        terms = diff.training_losses(model, None, t, dict(input_ids=ids, input_mask=mask))
+        terms["loss"].mean().backward()
+        return {k: v.detach().float() for k, v in terms.items()}
+
+    tr = run(ref)
+    tn = run(eng)
+    for k in ("mse", "decoder_nll", "loss", "nll"):
+        torch.testing.assert_close(tn[k], tr[k], rtol=3e-2, atol=3e-2, msg=k)
+    gr, gn = _grads(ref), _grads(nat)
+    assert set(gr) == set(gn)
+    for n in gr:
+        scale = gr[n].abs().max().item() + 1e-6
+        err = (gn[n] - gr[n]).abs().max().item() / scale
+        assert err < 6e-2, (n, err)

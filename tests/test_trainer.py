@@ -1,0 +1,118 @@
+"""TrainLoop semantics (reference utils/trainer.py): engines agree, checkpoint layout,
+cadences, auto-resume, AdamW state compatibility (SURVEY T-3..T-14, Appendix A/C)."""
+import os
+
+import pytest
+import torch
+
+from basic_utils import logger
+from data import load_data_from_args
+from utils.initialization import create_diffusion_from_config, create_model_from_config, seed_all
+from utils.trainer import DiffusionTrainLoop, TrainLoop, update_ema
+
+SETTINGS = dict(model="mlp_diffusion", precision="fp32", vocab_size=512, seq_len=16, hidden_dim=16,
+                hidden_t_dim=16, hidden_size=32)
+
+
+def _loop(tmpdir, engine, steps=4, save_interval=2, resume="", seed=0, **kw):
+    logger.configure(dir=str(tmpdir), format_strs=["log", "csv"])
+    seed_all(seed, deterministic=True)
+    model = create_model_from_config(**SETTINGS)
+    data = load_data_from_args("train", "x", 8, deterministic=True, loop=True, num_loader_proc=0,
+                               dataset="synthetic", seq_len=16, vocab_size=512, seed=0)
+    diffusion, sampler = create_diffusion_from_config(diffusion_steps=50)
+    loop = DiffusionTrainLoop(diffusion=diffusion, schedule_sampler=sampler, model=model, data=data,
+                              batch_size=8, microbatch=4, lr=1e-2, ema_rate="0.5,0.9",
+                              log_interval=1, save_interval=save_interval, resume_checkpoint=resume,
+                              learning_steps=steps, checkpoint_path=str(tmpdir), ddp_engine=engine,
+                              precision="fp32", **kw)
+    return loop
+
+
+def test_native_engine_matches_reference_engine(tmp_path):
+    a = _loop(tmp_path / "a", "native", steps=3, save_interval=100)
+    a.run_loop()
+    b = _loop(tmp_path / "b", "torch", steps=3, save_interval=100)
+    b.run_loop()
+    for pa, pb in zip(a.model.parameters(), b.model.parameters()):
+        torch.testing.assert_close(pa, pb, rtol=1e-4, atol=1e-5)
+    for ea, eb in zip(a.ema_params, b.ema_params):
+        for x, y in zip(ea, eb):
+            torch.testing.assert_close(x, y, rtol=1e-4, atol=1e-5)
+
+
+def test_checkpoint_layout_and_cadence(tmp_path):
+    loop = _loop(tmp_path, "native", steps=5, save_interval=3)
+    loop.run_loop()
+    names = sorted(os.listdir(tmp_path))
+    # save at step 3 (step>0 and step % 3 == 0) and a final save at step 5 ((5-1) % 3 != 0)
+    assert not any(n.startswith("model_000004") for n in names)
+    for n in (3, 5):
+        assert f"model_{n:06d}.pt" in names and f"opt_{n:06d}.pt" in names
+        assert f"ema_0.5_{n:06d}.pt" in names and f"ema_0.9_{n:06d}.pt" in names
+    assert "progress.csv" in names and "log.txt" in names
+    sd = torch.load(tmp_path / "model_000005.pt", weights_only=True)
+    assert set(sd) == set(loop.model.state_dict())
+    opt = torch.load(tmp_path / "opt_000005.pt", weights_only=True)
+    # the optimizer state loads into a stock torch AdamW over the same parameters
+    ref = torch.optim.AdamW(create_model_from_config(**SETTINGS).parameters(), lr=1e-2)
+    ref.load_state_dict(opt)
+    assert float(opt["state"][0]["step"]) == 5.0
+
+
+def test_auto_resume_from_checkpoint_dir(tmp_path):
+    loop = _loop(tmp_path, "native", steps=4, save_interval=2)
+    loop.run_loop()
+    final = {k: v.clone() for k, v in loop.model.state_dict().items()}
+    # a new loop in the same directory resumes from model_000004.pt (Q1: step N re-executed)
+    loop2 = _loop(tmp_path, "native", steps=6, save_interval=100)
+    assert loop2.resume_step == 4
+    for k, v in loop2.model.state_dict().items():
+        torch.testing.assert_close(v, final[k])
+    assert loop2.opt.step_count == 4
+    loop2.run_loop()
+    assert "model_000006.pt" in os.listdir(tmp_path)
+
+
+def test_lr_anneal_linear_to_zero(tmp_path):
+    loop = _loop(tmp_path, "native", steps=10)
+    loop.step, loop.resume_step = 3, 2
+    loop._anneal_lr()
+    assert loop.opt.param_groups[0]["lr"] == pytest.approx(1e-2 * (1 - 5 / 10))
+
+
+def test_update_ema_math():
+    t = [torch.ones(3)]
+    s = [torch.zeros(3)]
+    update_ema(t, s, rate=0.9)
+    torch.testing.assert_close(t[0], torch.full((3,), 0.9))
+
+
+def test_get_batch_length_variants():
+    assert TrainLoop.get_batch_length(torch.zeros(5, 2)) == 5
+    assert TrainLoop.get_batch_length({"a": torch.zeros(7)}) == 7
+    assert TrainLoop.get_batch_length([torch.zeros(3)]) == 3
+    with pytest.raises(TypeError):
+        TrainLoop.get_batch_length(3)
+
+
+def test_parse_resume_step():
+    assert TrainLoop.parse_resume_step_from_filename("/x/model_000123.pt") == 123
+    with pytest.raises(AssertionError):
+        TrainLoop.parse_resume_step_from_filename("/x/ema_0.9_000123.pt")
+
+
+def test_microbatch_fusion_gives_same_gradients(tmp_path, monkeypatch):
+    """exec_microbatch=8 (one fused fwd/bwd) == two semantic micro-batches of 4."""
+    from distributed_pipeline_amd.models.resample import FixSampler
+    monkeypatch.setattr(torch, "randn_like", lambda x: torch.zeros_like(x))  # deterministic noise
+    a = _loop(tmp_path / "a", "native", steps=1, save_interval=100)
+    b = _loop(tmp_path / "b", "native", steps=1, save_interval=100, exec_microbatch=8)
+    assert a.exec_microbatch == 4 and b.exec_microbatch == 8 and b.loss_scale == 2
+    a.schedule_sampler = FixSampler(a.diffusion.num_timesteps)
+    b.schedule_sampler = FixSampler(b.diffusion.num_timesteps)
+    batch = next(a.data)
+    a.forward_backward(batch)
+    b.forward_backward(batch)
+    torch.testing.assert_close(a.ddp_model.space.grad_flat, b.ddp_model.space.grad_flat,
+                               rtol=1e-5, atol=1e-6)

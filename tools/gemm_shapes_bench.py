@@ -3,8 +3,12 @@ fwd (addmm / mm), dgrad (dz @ W), wgrad (mm(dz^T, x, out_dtype=fp32)), per layer
 Optionally also the native MFMA GEMM kernels (--native)."""
 import argparse
 import json
+import os
+import sys
 
 import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
 
 def bench(fn, iters=20, warmup=5):
