@@ -16,6 +16,7 @@ every forward, and returns fp32 weight gradients so they accumulate straight
 into the flat fp32 gradient buffer.
 """
 import math
+import os
 
 import torch
 import torch.nn.functional as F
@@ -112,8 +113,15 @@ def _bias_act_bwd(dy2d, z, y, act, want_db):
     return dz, db
 
 
+# Linear GEMMs: the hand-written MFMA GEMM (fused epilogues, fused wgrad
+# accumulation) is used when DPA_NATIVE_GEMM=1; otherwise the plain GEMMs go
+# to hipBLASLt (bias epilogue) and only the fused ops run hand-written kernels.
+NATIVE_GEMM = os.environ.get("DPA_NATIVE_GEMM", "0") == "1"
+
+
 def _native_gemm_ok(x2, n_out):
-    return (x2.is_cuda and x2.dtype == torch.bfloat16 and native_ok(x2, kernel="gemm_nt")
+    return (NATIVE_GEMM and x2.is_cuda and x2.dtype == torch.bfloat16
+            and native_ok(x2, kernel="gemm_nt")
             and x2.shape[0] % 128 == 0 and n_out % 128 == 0 and x2.shape[1] % 128 == 0)
 
 
