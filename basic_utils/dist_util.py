@@ -83,7 +83,7 @@ def setup_dist(backend=None, silent=False):
         try:
             use_gpu = _cuda_available()
             if backend is None:
-                backend = "nccl" if use_gpu else "gloo"
+                backend = os.environ.get("DPA_DIST_BACKEND") or ("nccl" if use_gpu else "gloo")
             # Fail fast on hung collectives rather than wedging the node.
             os.environ.setdefault("TORCH_NCCL_ASYNC_ERROR_HANDLING", "1")
             kwargs = dict(backend=backend, init_method="env://",

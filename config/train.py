@@ -120,7 +120,7 @@ class PerfSettings(S):
     exec_microbatch: int \
         = _(0, "Samples per executed forward/backward (multiple of microbatch; 0 = microbatch). Gradients are identical.")
     hip_graphs: bool \
-        = _(True, "Capture the micro-batch forward/backward in a HIP graph.")
+        = _(False, "Capture the micro-batch forward/backward in a HIP graph (launch-bound configs).")
     shard_data: bool \
         = _(False, "Give each rank a disjoint shard of the data (DistributedSampler-style).")
     log_cross_rank_mean: bool \

@@ -113,16 +113,30 @@ def _bias_act_bwd(dy2d, z, y, act, want_db):
     return dz, db
 
 
-# Linear GEMMs: the hand-written MFMA GEMM (fused epilogues, fused wgrad
-# accumulation) is used when DPA_NATIVE_GEMM=1; otherwise the plain GEMMs go
-# to hipBLASLt (bias epilogue) and only the fused ops run hand-written kernels.
-NATIVE_GEMM = os.environ.get("DPA_NATIVE_GEMM", "0") == "1"
+# Linear GEMM routing (DPA_GEMM):
+#   "auto"   (default) - per product, the faster of the two measured on MI355X
+#            (tools/gemm_shapes_bench.py, profiles/): hand-written MFMA kernels
+#            for the fused cases - forward with a GELU/SiLU epilogue, and every
+#            weight-gradient GEMM (split-K, dW/db accumulated straight into the
+#            fp32 grad buffer) - and hipBLASLt for the plain bias-epilogue
+#            forward and the data-gradient GEMM;
+#   "native" - every Linear GEMM on the hand-written kernels;
+#   "blas"   - every Linear GEMM on hipBLASLt (plus separate epilogue kernels).
+GEMM_MODE = os.environ.get("DPA_GEMM", "auto")
 
 
-def _native_gemm_ok(x2, n_out):
-    return (NATIVE_GEMM and x2.is_cuda and x2.dtype == torch.bfloat16
-            and native_ok(x2, kernel="gemm_nt")
+def _gemm_shape_ok(x2, n_out):
+    return (x2.is_cuda and x2.dtype == torch.bfloat16 and native_ok(x2, kernel="gemm_nt")
             and x2.shape[0] % 128 == 0 and n_out % 128 == 0 and x2.shape[1] % 128 == 0)
+
+
+def _route(x2, n_out, act):
+    """-> (native_fwd, native_dgrad, native_wgrad)"""
+    if GEMM_MODE == "blas" or not _gemm_shape_ok(x2, n_out):
+        return False, False, False
+    if GEMM_MODE == "native":
+        return True, True, True
+    return act in ("gelu", "silu"), False, True
 
 
 def _accumulate_wgrad(p, dz, x2, bias):
@@ -162,8 +176,8 @@ class _LinearFn(torch.autograd.Function):
     def forward(ctx, x, w, b, w16, b16, act):
         shp = x.shape
         x2 = x.reshape(-1, shp[-1])
-        native = _native_gemm_ok(x2, w16.shape[0])
-        if native:
+        route = _route(x2, w16.shape[0], act)
+        if route[0]:
             y, z = get_ext().gemm_nt(x2, w16, b16, _ACTS.index(act))
             if act == "none":
                 z = None
@@ -185,7 +199,7 @@ class _LinearFn(torch.autograd.Function):
         ctx.params = (w, b)
         ctx.act = act
         ctx.has_b = b is not None
-        ctx.native = native
+        ctx.route = route
         ctx.shp = shp
         return y.reshape(*shp[:-1], w16.shape[0])
 
@@ -194,12 +208,15 @@ class _LinearFn(torch.autograd.Function):
         x2, w16, z, y = ctx.saved_tensors
         w, b = ctx.params
         dy2 = dy.reshape(-1, dy.shape[-1]).contiguous()
-        if ctx.native:
+        _, nat_dgrad, nat_wgrad = ctx.route
+        if nat_wgrad:
             dz = dy2
             if ctx.act != "none":
-                zy = z if z is not None else y
-                dz, _ = get_ext().bias_act_bwd(dy2, zy, _ACTS.index(ctx.act), False)
-            dx = get_ext().gemm_nn(dz, w16).reshape(ctx.shp) if ctx.needs_input_grad[0] else None
+                dz, _ = _bias_act_bwd(dy2, z, y, ctx.act, False)
+            dx = None
+            if ctx.needs_input_grad[0]:
+                dx = get_ext().gemm_nn(dz, w16) if nat_dgrad else dz @ w16
+                dx = dx.reshape(ctx.shp)
             dw = db = None
             if ctx.needs_input_grad[1] or (ctx.has_b and ctx.needs_input_grad[2]):
                 dw, db = _accumulate_wgrad(w, dz, x2, b if ctx.has_b else None)
