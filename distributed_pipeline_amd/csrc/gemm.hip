@@ -173,19 +173,33 @@ __global__ void __launch_bounds__(256) gemm_kernel(
         }
       }
     }
+    // k-steps pipelined through two fragment register sets: the LDS reads of
+    // step kk+1 are in flight while the 4 MFMAs of step kk issue.
+    bf16x8 af[2][2], bfr[2][2];
+#pragma unroll
+    for (int i = 0; i < 2; ++i) af[0][i] = Op<A_TR>::frag(la, wm * 64 + i * 32, 0, lane);
+#pragma unroll
+    for (int j = 0; j < 2; ++j) bfr[0][j] = Op<B_TR>::frag(lb, wn * 64 + j * 32, 0, lane);
+    if constexpr (A_TR || B_TR)
+      asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(af[0][0]), "+v"(af[0][1]), "+v"(bfr[0][0]), "+v"(bfr[0][1]));
 #pragma unroll
     for (int kk = 0; kk < 4; ++kk) {
-      bf16x8 af[2], bfr[2];
+      const int cur = kk & 1, nxt = cur ^ 1;
+      if (kk < 3) {
 #pragma unroll
-      for (int i = 0; i < 2; ++i) af[i] = Op<A_TR>::frag(la, wm * 64 + i * 32, kk, lane);
+        for (int i = 0; i < 2; ++i) af[nxt][i] = Op<A_TR>::frag(la, wm * 64 + i * 32, kk + 1, lane);
 #pragma unroll
-      for (int j = 0; j < 2; ++j) bfr[j] = Op<B_TR>::frag(lb, wn * 64 + j * 32, kk, lane);
-      if constexpr (A_TR || B_TR)  // retire the asm transposed reads (results named as operands)
-        asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(af[0]), "+v"(af[1]), "+v"(bfr[0]), "+v"(bfr[1]));
+        for (int j = 0; j < 2; ++j) bfr[nxt][j] = Op<B_TR>::frag(lb, wn * 64 + j * 32, kk + 1, lane);
+      }
 #pragma unroll
       for (int i = 0; i < 2; ++i)
 #pragma unroll
-        for (int j = 0; j < 2; ++j) acc[i][j] = mfma32(af[i], bfr[j], acc[i][j]);
+        for (int j = 0; j < 2; ++j) acc[i][j] = mfma32(af[cur][i], bfr[cur][j], acc[i][j]);
+      if constexpr (A_TR || B_TR) {
+        if (kk < 3)  // retire the asm transposed reads (results named as operands)
+          asm volatile("s_waitcnt lgkmcnt(0)"
+                       : "+v"(af[nxt][0]), "+v"(af[nxt][1]), "+v"(bfr[nxt][0]), "+v"(bfr[nxt][1]));
+      }
     }
     if (t + 1 < nk) {
       wait_lds_and_barrier();  // every wave is done reading this buffer
@@ -219,27 +233,47 @@ __global__ void __launch_bounds__(256) gemm_kernel(
       for (int q = 0; q < 8; ++q) atomicAdd(colsum + c0 + q, cs[q]);
     }
   } else {
+    // Stage the bf16 tile through LDS and write whole 256-B rows with 16-B stores
+    // (instead of 64 scattered 2-B stores per lane).  Z (pre-activation) second.
+    constexpr int LDC = 136;  // padded row (elements)
+    bf16_t* ct = reinterpret_cast<bf16_t*>(smem);
     float bv[2] = {0.f, 0.f};
     if (EPI == EPI_BIAS_ACT && bias) {
 #pragma unroll
       for (int j = 0; j < 2; ++j) bv[j] = bf2f(bias[n0 + wn * 64 + j * 32 + (lane & 31)]);
     }
+    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");  // operand LDS no longer read
 #pragma unroll
     for (int i = 0; i < 2; ++i)
 #pragma unroll
       for (int j = 0; j < 2; ++j)
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
-          const int row = m0 + wm * 64 + i * 32 + acc_row(r, h);
-          const int col = n0 + wn * 64 + j * 32 + (lane & 31);
-          float v = acc[i][j][r] + bv[j];
-          if (EPI == EPI_BIAS_ACT && act != 0) {
-            v = bf2f(f2bf(v));
-            if (Zout) Zout[(int64_t)row * ldc + col] = f2bf(v);
-            v = gemm_act(v, act);
-          }
-          C[(int64_t)row * ldc + col] = f2bf(v);
+          const int row = wm * 64 + i * 32 + acc_row(r, h);
+          const int col = wn * 64 + j * 32 + (lane & 31);
+          ct[row * LDC + col] = f2bf(acc[i][j][r] + bv[j]);
         }
+    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+    // 128 rows x 16 chunks of 8: pre-activation to Zout, act(z) to C
+#pragma unroll 2
+    for (int c = 0; c < 8; ++c) {
+      const int idx = tid + c * 256;
+      const int row = idx >> 4, ch = idx & 15;
+      uint4 v = *reinterpret_cast<const uint4*>(ct + row * LDC + ch * 8);
+      const int64_t o = (int64_t)(m0 + row) * ldc + n0 + ch * 8;
+      if (EPI == EPI_BIAS_ACT && act != 0) {
+        if (Zout) *reinterpret_cast<uint4*>(Zout + o) = v;
+        uint32_t wv[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const float lo = gemm_act(__uint_as_float(wv[q] << 16), act);
+          const float hi = gemm_act(__uint_as_float(wv[q] & 0xffff0000u), act);
+          wv[q] = pack_bf2(lo, hi);
+        }
+        v = make_uint4(wv[0], wv[1], wv[2], wv[3]);
+      }
+      *reinterpret_cast<uint4*>(C + o) = v;
+    }
   }
 }
 

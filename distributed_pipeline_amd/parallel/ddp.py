@@ -98,6 +98,11 @@ class DDPEngine(nn.Module):
                 self._hooks.append(p.register_post_accumulate_grad_hook(hook))
                 p._dpa_notify = hook  # fused ops that write .grad directly call this
         self._comm_buf = None
+        # gloo on device tensors (test-only transport on one GPU): its staging copy is
+        # not ordered after pending kernels of the calling stream on ROCm, so drain the
+        # stream before handing it a bucket.  RCCL ("nccl") orders via events itself.
+        self._host_sync_before_comm = (self.distributed and self.space.device.type == "cuda"
+                                       and dist.get_backend(self.pg) == "gloo")
 
     # -- setup ---------------------------------------------------------------
     def _coll_device(self):
@@ -166,6 +171,8 @@ class DDPEngine(nn.Module):
         if b.launched:
             return
         view = self.space.grad_flat[b.start:b.end]
+        if self._host_sync_before_comm:
+            torch.cuda.current_stream(self.space.device).synchronize()
         if self.reduce_dtype == torch.float32:
             b.work = dist.all_reduce(view, group=self.pg, async_op=True)
         else:  # narrow wire format: pack, reduce, unpack (fp32 accumulation of ranks in RCCL)
