@@ -172,7 +172,14 @@ class DDPEngine(nn.Module):
             return
         view = self.space.grad_flat[b.start:b.end]
         if self._host_sync_before_comm:
-            torch.cuda.current_stream(self.space.device).synchronize()
+            # test transport: stage through host memory synchronously (gloo's own
+            # device-tensor path is not used)
+            host = view.to("cpu")
+            dist.all_reduce(host, group=self.pg)
+            view.copy_(host)
+            b.work = None
+            b.launched = True
+            return
         if self.reduce_dtype == torch.float32:
             b.work = dist.all_reduce(view, group=self.pg, async_op=True)
         else:  # narrow wire format: pack, reduce, unpack (fp32 accumulation of ranks in RCCL)
