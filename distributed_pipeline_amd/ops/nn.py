@@ -155,11 +155,10 @@ def _accumulate_wgrad(p, dz, x2, bias):
         if gb is None or gb.dtype != torch.float32:
             gb = db_out = torch.zeros(bias.shape, dtype=torch.float32, device=dz.device)
     ext.gemm_wgrad(dz, x2, gw, gb)
-    for t, out in ((p, dw_out), (bias, db_out)):
-        if t is not None and out is None:
-            notify = getattr(t, "_dpa_notify", None)
-            if notify is not None:
-                notify(t)
+    # Readiness needs no explicit signal: autograd still runs the parameter's
+    # AccumulateGrad node (with an undefined grad) after this backward, and its
+    # post-accumulate hook - the DDP engine's bucket counter - fires exactly once
+    # per backward, after every use of the parameter has been processed.
     return dw_out, db_out
 
 

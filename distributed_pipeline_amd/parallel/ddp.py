@@ -13,7 +13,9 @@ Design (xGMI/RCCL-first rather than a translation of the C++ Reducer):
   the network, then ~32 MiB buckets - large enough to saturate a ring's links,
   small enough to overlap.  (reference: ``bucket_cap_mb=128``.)
 * Readiness: a post-accumulate-grad hook per parameter decrements its bucket's
-  pending counter; the bucket whose counter hits zero is all-reduced
+  pending counter (autograd runs it once per backward per leaf, after all uses,
+  even when a fused wgrad GEMM accumulated the gradient in place and returned
+  None); the bucket whose counter hits zero is all-reduced
   asynchronously (RCCL on its own internal stream, ordered after the
   gradient-producing kernels of the current stream).  Buckets are launched in
   order so every rank issues collectives in the same sequence.
@@ -95,12 +97,14 @@ class DDPEngine(nn.Module):
                 self.broadcast_parameters()
             for p in self.space.layout:
                 hook = self._make_hook(p)
+                # Fires once per backward per leaf, also when a fused op wrote the
+                # gradient in place and returned None for it (AccumulateGrad still
+                # runs), so no op-side notification is needed.
                 self._hooks.append(p.register_post_accumulate_grad_hook(hook))
-                p._dpa_notify = hook  # fused ops that write .grad directly call this
         self._comm_buf = None
-        # gloo on device tensors (test-only transport on one GPU): its staging copy is
-        # not ordered after pending kernels of the calling stream on ROCm, so drain the
-        # stream before handing it a bucket.  RCCL ("nccl") orders via events itself.
+        # gloo on device tensors is only a test transport (several ranks sharing one
+        # GPU): stage each bucket through host memory synchronously so its ordering
+        # w.r.t. the producing kernels is explicit.  RCCL ("nccl") orders via events.
         self._host_sync_before_comm = (self.distributed and self.space.device.type == "cuda"
                                        and dist.get_backend(self.pg) == "gloo")
 

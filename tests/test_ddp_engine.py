@@ -15,17 +15,43 @@ from distributed_pipeline_amd.parallel.ddp import DDPEngine, plan_buckets
 from distributed_pipeline_amd.parallel.flat import FlatParamSpace
 
 
-def _model(seed):
+class _InplaceWgrad(torch.autograd.Function):
+    """Mimics the fused wgrad GEMM: dW/db accumulated straight into .grad, None returned."""
+
+    @staticmethod
+    def forward(ctx, x, w, b):
+        ctx.save_for_backward(x, w)
+        ctx.params = (w, b)
+        return x @ w.t() + b
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, w = ctx.saved_tensors
+        pw, pb = ctx.params
+        pw.grad.add_(dy.t() @ x)
+        pb.grad.add_(dy.sum(0))
+        return dy @ w, None, None
+
+
+class _FusedLinear(torch.nn.Linear):
+    def forward(self, x):
+        if self.weight.grad is None:  # reference model: plain autograd
+            return super().forward(x)
+        return _InplaceWgrad.apply(x, self.weight, self.bias)
+
+
+def _model(seed, fused=False):
     torch.manual_seed(seed)
-    return torch.nn.Sequential(torch.nn.Linear(16, 64), torch.nn.Tanh(), torch.nn.Linear(64, 64),
-                               torch.nn.Tanh(), torch.nn.Linear(64, 4))
+    lin = _FusedLinear if fused else torch.nn.Linear
+    return torch.nn.Sequential(lin(16, 64), torch.nn.Tanh(), torch.nn.Linear(64, 64),
+                               torch.nn.Tanh(), lin(64, 4))
 
 
-def _worker(rank, world, port, q):
+def _worker(rank, world, port, q, fused=False):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
-        model = _model(seed=100 + rank)  # different init per rank: engine must broadcast rank 0
+        model = _model(seed=100 + rank, fused=fused)  # different init per rank: engine broadcasts rank 0
         eng = DDPEngine(model, bucket_cap_mb=0.01, first_bucket_mb=0.002)
         torch.manual_seed(0)
         xs = torch.randn(2, world * 8, 16)  # 2 micro-batches, full batch split over ranks
@@ -46,12 +72,14 @@ def _worker(rank, world, port, q):
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world", [2, 4])
-def test_ddp_engine_matches_single_process(world):
+@pytest.mark.parametrize("world,fused", [(2, False), (4, False), (2, True)])
+def test_ddp_engine_matches_single_process(world, fused):
+    """fused=True: some layers accumulate their weight grads in place and return None
+    (like the split-K wgrad GEMM); buckets must still wait for those gradients."""
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = find_free_port()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, q)) for r in range(world)]
+    procs = [ctx.Process(target=_worker, args=(r, world, port, q, fused)) for r in range(world)]
     for p in procs:
         p.start()
     res = sorted([q.get(timeout=240) for _ in range(world)], key=lambda t: t[0])
