@@ -344,6 +344,7 @@ PYBIND11_MODULE(_C, m) {
   m.def("gemm_nn", &gemm_nn, "dx = dy W (bf16 MFMA)");
   m.def("gemm_wgrad", &gemm_wgrad, "dW += dy^T x, db += colsum(dy) (fp32 atomics, split-K)");
   m.def("gemm_supported", &gemm_supported, "shape check for the native GEMMs");
+  m.def("set_gemm256", &dpa::set_gemm256, "enable/disable the 256x256 8-phase GEMM path");
   m.def("lxent_fwd", &lxent_fwd, "fused linear + cross-entropy forward -> (loss, lse)");
   m.def("lxent_bwd", &lxent_bwd, "fused linear + cross-entropy backward -> (dx, dW fp32, db fp32)");
 }

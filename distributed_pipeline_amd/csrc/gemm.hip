@@ -98,14 +98,6 @@ __device__ __forceinline__ void wait_vm0_barrier() {
   asm volatile("s_waitcnt vmcnt(0)\n\ts_barrier" ::: "memory");
 }
 
-// bijective XCD remap: ids with equal (id % 8) run on one XCD; give each XCD a
-// contiguous range of logical tile ids.
-__device__ __forceinline__ int xcd_remap(int id, int total) {
-  const int q = total >> 3, r = total & 7, xcd = id & 7;
-  const int base = xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q;
-  return base + (id >> 3);
-}
-
 template <bool A_TR, bool B_TR, int EPI>
 __global__ void __launch_bounds__(256) gemm_kernel(
     const bf16_t* __restrict__ A, int64_t lda, const bf16_t* __restrict__ B, int64_t ldb,
@@ -281,6 +273,7 @@ static bool gemm_shape_ok(int M, int N, int K) { return M % 128 == 0 && N % 128 
 
 bool launch_gemm_nt(const uint16_t* x, const uint16_t* W, const uint16_t* bias, uint16_t* y,
                     uint16_t* z, int T, int N, int K, int act, hipStream_t s) {
+  if (launch_gemm256_nt(x, W, bias, y, z, T, N, K, act, s)) return true;
   if (!gemm_shape_ok(T, N, K)) return false;
   const int blocks = (T / 128) * (N / 128);
   hipLaunchKernelGGL((gemm_kernel<false, false, EPI_BIAS_ACT>), dim3(blocks), dim3(256), 0, s,
@@ -292,6 +285,7 @@ bool launch_gemm_nt(const uint16_t* x, const uint16_t* W, const uint16_t* bias, 
 bool launch_gemm_nn(const uint16_t* dy, const uint16_t* W, uint16_t* dx, int T, int N, int K,
                     hipStream_t s) {
   // dx[T][K] = dy[T][N] . W[N][K]: M = T, N' = K, reduction = N
+  if (launch_gemm256_nn(dy, W, dx, T, N, K, s)) return true;
   if (!gemm_shape_ok(T, K, N)) return false;
   const int blocks = (T / 128) * (K / 128);
   hipLaunchKernelGGL((gemm_kernel<false, true, EPI_BF16>), dim3(blocks), dim3(256), 0, s,
@@ -303,6 +297,7 @@ bool launch_gemm_nn(const uint16_t* dy, const uint16_t* W, uint16_t* dx, int T, 
 bool launch_gemm_wgrad(const uint16_t* dy, const uint16_t* x, float* dW, float* db, int T, int N,
                        int K, hipStream_t s) {
   // dW[N][K] += dy[T][N]^T . x[T][K]: M = N, N' = K, reduction = T (split over workgroups)
+  if (launch_gemm256_wgrad(dy, x, dW, db, T, N, K, s)) return true;
   if (!gemm_shape_ok(N, K, T)) return false;
   const int tiles = (N / 128) * (K / 128);
   int splits = (1024 + tiles - 1) / tiles;

@@ -1,0 +1,471 @@
+// 256 x 256 bf16 MFMA GEMM, 8-phase software pipeline (CDNA4 / gfx950).
+//
+// Same three Linear-layer products as gemm.hip (fwd "MK.NK", dgrad "MK.KN",
+// wgrad "KM.KN"), restructured for one workgroup per CU at high MFMA density:
+//
+// * 512 threads = 8 waves, 256 x 256 output tile, BK = 64, v_mfma_f32_16x16x32_bf16.
+// * LDS (one 128 KiB array): 2 K-tile buffers (even / odd K-tile) x 4 half-tile
+//   images {A rows 0-127, A rows 128-255, B rows 0-127, B rows 128-255} of
+//   16 KiB.  Images are written by global_load_lds_dwordx4 (lane-linear, so the
+//   XOR swizzle is applied to the per-lane global *source* address and undone on
+//   the read).  Row-form images ([128][64], 128-B rows) are read with
+//   ds_read_b128; transposed images ([64 k][128], 256-B rows: operands whose
+//   reduction dimension is outermost in memory) with ds_read_b64_tr_b16.
+// * A K-tile is computed in 4 phases, one 128 x 128 C quadrant per phase
+//   (A0.B0, A0.B1, A1.B1, A1.B0), each wave owning a 64 x 32 block of it (16
+//   MFMAs per phase).  Fragments are reused across phases (phase 4 reads
+//   nothing), so a K-tile costs 24 row-form LDS reads per wave instead of 48.
+// * One half-tile image is prefetched per phase; a counted `s_waitcnt vmcnt(4)`
+//   at phases 4 and 8 retires the next buffer while two half-tiles stay in
+//   flight across the barriers (no vmcnt(0) in the main loop, raw s_barrier).
+//   WAR: an image is restaged >= 2 phases after its last read; RAW: it is read
+//   >= 1 phase after the wait that retires it (both needed because the two
+//   wave groups run staggered by one barrier).
+// * Wave group 1 (waves 4-7) runs one barrier behind group 0, so on every SIMD
+//   one wave issues MFMAs while the other issues LDS reads and DMA.
+// * Workgroups are remapped so consecutive tiles (sharing an A panel) run on one XCD.
+//
+// Epilogues: bf16 (+bias, +activation, pre-activation copy) staged through LDS
+// as 16-B row stores, or fp32 atomic accumulation into the fp32 gradient buffer
+// (split-K wgrad) with the bias gradient reduced from the staged dy images.
+#include <cstdlib>
+
+#include "common.h"
+#include "launchers.h"
+#include "mfma.h"
+
+namespace dpa {
+namespace g256 {
+
+typedef __attribute__((address_space(3))) void lds_void;
+typedef const __attribute__((address_space(1))) void glob_void;
+typedef __attribute__((ext_vector_type(8))) __bf16 bf16x8_v;
+
+// LDS map (bytes): A images in [0, 64K), B images in [64K, 128K), so every
+// fragment read is one per-lane base VGPR + an immediate offset (< 64 KiB):
+//   A(buf, h) = buf * 32K + h * 16K,   B(buf, h) = 64K + buf * 32K + h * 16K
+constexpr int HALF = 16384;
+constexpr int B_REGION = 65536;
+__host__ __device__ constexpr int img_off(int buf, int h) { return buf * 2 * HALF + h * HALF; }
+
+enum { EPI_BF16 = 0, EPI_BIAS_ACT = 1, EPI_ATOMIC_F32 = 2 };
+
+__device__ __forceinline__ f32x4 mfma16(const bf16x8& a, const bf16x8& b, const f32x4& c) {
+  return __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8_v, a),
+                                                 __builtin_bit_cast(bf16x8_v, b), c, 0, 0, 0);
+}
+
+__device__ __forceinline__ uint32_t lds_u32(const void* p) {
+  return (uint32_t)reinterpret_cast<uintptr_t>((const __attribute__((address_space(3))) char*)p);
+}
+
+// Chunk XOR of a transposed image row: conflict-free ds_read_b64_tr_b16 for the
+// 16x16x32 operand (a 32-lane half reads rows {q, 8+q} (+16n) of two 16-B chunks).
+__device__ __forceinline__ int tr_x(int row) { return ((row & 3) << 1) | (((row >> 3) & 1) << 3); }
+
+__device__ __forceinline__ float act_f(float z, int act) {
+  switch (act) {
+    case 1: return 0.5f * z * (1.f + erff(z * 0.70710678118654752f));
+    case 2: return tanhf(z);
+    case 3: return z / (1.f + __expf(-z));
+    default: return z;
+  }
+}
+
+__device__ __forceinline__ void barrier() { asm volatile("s_barrier" ::: "memory"); }
+
+// ---- one operand (A or B) --------------------------------------------------
+template <bool TR>
+struct Operand {
+  const bf16_t* base;  // element (row 0 of this tile, k = 0) - wave-uniform
+  int64_t ld;
+  uint32_t off[2];     // byte offsets of this thread's two DMA pieces within a half image
+                       // (unsigned 32-bit: the DMA uses SGPR base + VGPR offset addressing)
+  uint32_t rd[4];      // LDS read byte offsets (relative to a half image)
+
+  // row0: first row (row form) / column (TR form) of the 256-wide tile; this
+  // wave's sub-block starts at row/col wsub * wrows of a half; region: LDS byte
+  // address of this operand's images.
+  __device__ __forceinline__ void init(const bf16_t* p, int64_t ld_, int row0, int w, int lane,
+                                       int wsub, int wrows, uint32_t region) {
+    ld = ld_;
+    base = TR ? p + row0 : p + (int64_t)row0 * ld_;
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const int piece = w * 2 + j;
+      if constexpr (TR) {
+        const int k = piece * 4 + (lane >> 4), phys = lane & 15;
+        off[j] = (uint32_t)(k * (int)ld_ + ((phys ^ tr_x(k)) << 3)) * 2u;
+      } else {
+        const int r = piece * 8 + (lane >> 3), phys = lane & 7;
+        off[j] = (uint32_t)(r * (int)ld_ + ((phys ^ ((r >> 1) & 7)) << 3)) * 2u;
+      }
+    }
+    const int g = lane >> 4, li = lane & 15;
+    if constexpr (TR) {
+      const int q = li >> 2, p = li & 3;
+      const int x = (q << 1) | ((g & 1) << 3);
+#pragma unroll
+      for (int c = 0; c < 4; ++c) {
+        const int cb = wsub * wrows + c * 16;
+        const int ch = ((cb >> 3) + (p >> 1)) ^ x;
+        rd[c] = region + (uint32_t)((8 * g + q) * 256 + ch * 16 + (p & 1) * 8);
+      }
+    } else {
+      const int row = wsub * wrows + li;
+      const int s = (row >> 1) & 7;
+#pragma unroll
+      for (int kk = 0; kk < 2; ++kk) rd[kk] = region + (uint32_t)(row * 128 + (((kk * 4 + g) ^ s) << 4));
+      rd[2] = rd[3] = 0;
+    }
+  }
+
+  // DMA one half image (h = 0/1) of K-tile t into LDS at `img`.
+  __device__ __forceinline__ void stage(char* img, int h, int t) const {
+    const char* src = reinterpret_cast<const char*>(TR ? base + (int64_t)t * 64 * ld + h * 128
+                                                       : base + (int64_t)h * 128 * ld + t * 64);
+    const int w = threadIdx.x >> 6;
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+      __builtin_amdgcn_global_load_lds((glob_void*)(src + off[j]),
+                                       (lds_void*)(img + (w * 2 + j) * 1024), 16, 0, 0);
+  }
+
+  // Fragment of 16-row (row form) / 16-column (TR form) block I, k-step KK, of
+  // the half image at byte offset IMG within the operand's region.  Issued from
+  // asm (no compiler vmcnt drain against the in-flight DMA); the caller retires
+  // it with lgkmcnt.
+  template <int IMG, int I, int KK>
+  __device__ __forceinline__ void frag(bf16x8& f) const {
+    if constexpr (TR) {
+      bf16x4 a, b;
+      asm volatile("ds_read_b64_tr_b16 %0, %1 offset:%2" : "=v"(a) : "v"(rd[I]), "i"(IMG + KK * 32 * 256));
+      asm volatile("ds_read_b64_tr_b16 %0, %1 offset:%2" : "=v"(b) : "v"(rd[I]), "i"(IMG + KK * 32 * 256 + 1024));
+      f = cat44(a, b);
+    } else {
+      asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(f) : "v"(rd[KK]), "i"(IMG + I * 2048));
+    }
+  }
+};
+
+template <int IMG, bool TR>
+__device__ __forceinline__ void read4(bf16x8 (&f)[4][2], const Operand<TR>& op) {
+  op.template frag<IMG, 0, 0>(f[0][0]); op.template frag<IMG, 0, 1>(f[0][1]);
+  op.template frag<IMG, 1, 0>(f[1][0]); op.template frag<IMG, 1, 1>(f[1][1]);
+  op.template frag<IMG, 2, 0>(f[2][0]); op.template frag<IMG, 2, 1>(f[2][1]);
+  op.template frag<IMG, 3, 0>(f[3][0]); op.template frag<IMG, 3, 1>(f[3][1]);
+}
+template <int IMG, bool TR>
+__device__ __forceinline__ void read2(bf16x8 (&f)[2][2], const Operand<TR>& op) {
+  op.template frag<IMG, 0, 0>(f[0][0]); op.template frag<IMG, 0, 1>(f[0][1]);
+  op.template frag<IMG, 1, 0>(f[1][0]); op.template frag<IMG, 1, 1>(f[1][1]);
+}
+
+// Bias-gradient partial sums from a transposed [64 k][128] dy image (at byte
+// offset IMG of the A region), read by the wave group that owns it: thread t
+// (0..255) sums column (t & 127) over rows 32*(t>>7) .. +31 with eight
+// ds_read_b64_tr_b16 (4 rows of its column each) into ONE register.
+// csa[0/1]: per-thread read bases for rows with bit 3 clear / set.
+template <int IMG>
+__device__ __forceinline__ void colsum_read(float& cs, const uint32_t (&csa)[2]) {
+#pragma unroll
+  for (int r = 0; r < 8; ++r) {
+    bf16x4 v;
+    asm volatile("ds_read_b64_tr_b16 %0, %1 offset:%2\n\ts_waitcnt lgkmcnt(0)"
+                 : "=v"(v) : "v"(csa[(r >> 1) & 1]), "i"(IMG + 4 * r * 256));
+#pragma unroll
+    for (int e = 0; e < 4; ++e) cs += __uint_as_float(((uint32_t)(uint16_t)v[e]) << 16);
+  }
+}
+
+template <int QA, int QB>
+__device__ __forceinline__ void mfma_quadrant(f32x4 (&acc)[2][2][4][2], const bf16x8 (&fa)[4][2],
+                                              const bf16x8 (&fb)[2][2]) {
+  __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+  for (int kk = 0; kk < 2; ++kk)
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < 2; ++j) acc[QA][QB][i][j] = mfma16(fa[i][kk], fb[j][kk], acc[QA][QB][i][j]);
+  __builtin_amdgcn_s_setprio(0);
+}
+
+// One phase P (0..7) of a 2-K-tile iteration; te = even K-tile of the iteration.
+template <int P, bool A_TR, bool B_TR, bool CS>
+__device__ __forceinline__ void phase(f32x4 (&acc)[2][2][4][2], bf16x8 (&fa)[4][2],
+                                      bf16x8 (&fb0)[2][2], bf16x8 (&fb1)[2][2], float& cs,
+                                      const Operand<A_TR>& opA, const Operand<B_TR>& opB,
+                                      char* smem, const uint32_t (&csa)[2], int te, bool more, bool do_cs,
+                                      int grp) {
+  constexpr int q = P & 3;
+  constexpr int bf = P < 4 ? 0 : 1;
+  char* const smB = smem + B_REGION;
+  // 1. LDS fragment reads (B first, then A)
+  if constexpr (q == 0) {
+    read2<img_off(bf, 0)>(fb0, opB);
+    __builtin_amdgcn_sched_barrier(0);
+    read4<img_off(bf, 0)>(fa, opA);
+  } else if constexpr (q == 1) {
+    read2<img_off(bf, 1)>(fb1, opB);
+  } else if constexpr (q == 2) {
+    read4<img_off(bf, 1)>(fa, opA);
+  }
+  // group 0 sums the A0 image, group 1 the A1 image (wave-uniform branch)
+  if constexpr (CS && q == 0) { if (do_cs && grp == 0) colsum_read<img_off(bf, 0)>(cs, csa); }
+  if constexpr (CS && q == 2) { if (do_cs && grp == 1) colsum_read<img_off(bf, 1)>(cs, csa); }
+  // 2. prefetch one half image (schedule in the header comment)
+  if constexpr (P == 0) opB.stage(smB + img_off(1, 1), 1, te + 1);
+  if constexpr (P == 1) opA.stage(smem + img_off(1, 1), 1, te + 1);
+  if constexpr (P == 2) { if (more) opA.stage(smem + img_off(0, 0), 0, te + 2); }
+  if constexpr (P == 3) {
+    if (more) {
+      opB.stage(smB + img_off(0, 0), 0, te + 2);
+      asm volatile("s_waitcnt vmcnt(4)" ::: "memory");  // odd K-tile te+1 landed
+    } else {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+  }
+  if constexpr (P == 4) { if (more) opB.stage(smB + img_off(0, 1), 1, te + 2); }
+  if constexpr (P == 5) { if (more) opA.stage(smem + img_off(0, 1), 1, te + 2); }
+  if constexpr (P == 6) { if (more) opA.stage(smem + img_off(1, 0), 0, te + 3); }
+  if constexpr (P == 7) {
+    if (more) {
+      opB.stage(smB + img_off(1, 0), 0, te + 3);
+      asm volatile("s_waitcnt vmcnt(4)" ::: "memory");  // even K-tile te+2 landed
+    }
+  }
+  // 3. barrier, retire reads, 16 MFMAs on one quadrant, barrier
+  barrier();
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_sched_barrier(0);
+  if constexpr (q == 0) mfma_quadrant<0, 0>(acc, fa, fb0);
+  if constexpr (q == 1) mfma_quadrant<0, 1>(acc, fa, fb1);
+  if constexpr (q == 2) mfma_quadrant<1, 1>(acc, fa, fb1);
+  if constexpr (q == 3) mfma_quadrant<1, 0>(acc, fa, fb0);
+  __builtin_amdgcn_sched_barrier(0);
+  barrier();
+}
+
+template <bool A_TR, bool B_TR, int EPI>
+__global__ void __launch_bounds__(512) gemm256_kernel(
+    const bf16_t* __restrict__ A, int64_t lda, const bf16_t* __restrict__ B, int64_t ldb, int M,
+    int N, int ktiles_total, int ktiles_per_split, int splits, bf16_t* __restrict__ C, int64_t ldc,
+    float* __restrict__ Cf, const bf16_t* __restrict__ bias, int act, bf16_t* __restrict__ Zout,
+    float* __restrict__ colsum) {
+  __shared__ __attribute__((aligned(1024))) char smem[2 * B_REGION];
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int wm = (w >> 2) & 1, wn = w & 3;  // 2 x 4 waves over a 128 x 128 quadrant
+  const int grp = __builtin_amdgcn_readfirstlane(w >> 2);
+  const int MT = M / 256, NT = N / 256;
+  const int tile = xcd_remap(blockIdx.x, MT * NT * splits);
+  const int nt = tile % NT, mt = (tile / NT) % MT, z = tile / (NT * MT);
+  const int m0 = mt * 256, n0 = nt * 256;
+  const int t0 = z * ktiles_per_split;
+  const int nk = min(ktiles_total - t0, ktiles_per_split);  // even, >= 2 (host guarantees)
+
+  Operand<A_TR> opA;
+  Operand<B_TR> opB;
+  const uint32_t sbase = lds_u32(smem);
+  opA.init(A + (A_TR ? (int64_t)t0 * 64 * lda : (int64_t)t0 * 64), lda, m0, w, lane, wm, 64, sbase);
+  opB.init(B + (B_TR ? (int64_t)t0 * 64 * ldb : (int64_t)t0 * 64), ldb, n0, w, lane, wn, 32,
+           sbase + B_REGION);
+
+  constexpr bool CS = (EPI == EPI_ATOMIC_F32) && A_TR;
+  const bool do_cs = CS && colsum != nullptr && nt == 0;
+  float cs = 0.f;
+
+  f32x4 acc[2][2][4][2];
+#pragma unroll
+  for (int a = 0; a < 2; ++a)
+#pragma unroll
+    for (int b = 0; b < 2; ++b)
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j) acc[a][b][i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  bf16x8 fa[4][2], fb0[2][2], fb1[2][2];
+  // colsum transposed-read bases: lane 4q+p of its 16-lane group addresses row
+  // 32*(t>>7) + 4r + q, columns 16*((t>>4)&7) + 4p .. +3
+  uint32_t csa[2];
+  {
+    const int t = tid & 255, q = (lane & 15) >> 2, p = lane & 3;
+#pragma unroll
+    for (int b3 = 0; b3 < 2; ++b3) {
+      const int row = q + 8 * b3;  // tr_x depends on row & 3 and row bit 3 only
+      const int ch = (2 * ((t >> 4) & 7) + (p >> 1)) ^ tr_x(row);
+      csa[b3] = sbase + (uint32_t)((32 * (t >> 7) + q) * 256 + ch * 16 + (p & 1) * 8);
+    }
+  }
+
+  // prologue: K-tile 0 complete; K-tile 1 halves A0, B0 in flight
+  char* const smB = smem + B_REGION;
+  opA.stage(smem + img_off(0, 0), 0, 0);
+  opB.stage(smB + img_off(0, 0), 0, 0);
+  opB.stage(smB + img_off(0, 1), 1, 0);
+  opA.stage(smem + img_off(0, 1), 1, 0);
+  opA.stage(smem + img_off(1, 0), 0, 1);
+  opB.stage(smB + img_off(1, 0), 0, 1);
+  asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+  barrier();
+  if (grp == 1) barrier();
+
+  const int niter = nk >> 1;
+  for (int it = 0; it < niter; ++it) {
+    const int te = 2 * it;
+    const bool more = it + 1 < niter;
+    phase<0, A_TR, B_TR, CS>(acc, fa, fb0, fb1, cs, opA, opB, smem, csa, te, more, do_cs, grp);
+    phase<1, A_TR, B_TR, CS>(acc, fa, fb0, fb1, cs, opA, opB, smem, csa, te, more, do_cs, grp);
+    phase<2, A_TR, B_TR, CS>(acc, fa, fb0, fb1, cs, opA, opB, smem, csa, te, more, do_cs, grp);
+    phase<3, A_TR, B_TR, CS>(acc, fa, fb0, fb1, cs, opA, opB, smem, csa, te, more, do_cs, grp);
+    phase<4, A_TR, B_TR, CS>(acc, fa, fb0, fb1, cs, opA, opB, smem, csa, te, more, do_cs, grp);
+    phase<5, A_TR, B_TR, CS>(acc, fa, fb0, fb1, cs, opA, opB, smem, csa, te, more, do_cs, grp);
+    phase<6, A_TR, B_TR, CS>(acc, fa, fb0, fb1, cs, opA, opB, smem, csa, te, more, do_cs, grp);
+    phase<7, A_TR, B_TR, CS>(acc, fa, fb0, fb1, cs, opA, opB, smem, csa, te, more, do_cs, grp);
+  }
+  if (grp == 0) barrier();  // re-align the groups; all LDS reads are retired past here
+
+  // ---- epilogue: acc[qa][qb][i][j] reg r -> row qa*128 + wm*64 + i*16 + 4*(lane>>4) + r,
+  //                                           col qb*128 + wn*32 + j*16 + (lane&15)
+  const int g4 = (lane >> 4) * 4, li = lane & 15;
+  if constexpr (EPI == EPI_ATOMIC_F32) {
+    if (do_cs) {
+      float* red = reinterpret_cast<float*>(smem);  // [2 row halves][256 cols]
+      const int t = tid & 255;
+      red[(t >> 7) * 256 + grp * 128 + (t & 127)] = cs;
+      __syncthreads();
+      if (tid < 256) atomicAdd(colsum + m0 + tid, red[tid] + red[256 + tid]);
+    }
+    // Stage each 128-row half of the fp32 tile in LDS ([128][256], 16-float blocks
+    // XOR-swizzled by row & 3), then add it with fully coalesced atomics (a wave
+    // covers 256 contiguous bytes of one gradient row).
+    float* ct = reinterpret_cast<float*>(smem);
+#pragma unroll
+    for (int qa = 0; qa < 2; ++qa) {
+      __syncthreads();
+#pragma unroll
+      for (int qb = 0; qb < 2; ++qb)
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+          for (int j = 0; j < 2; ++j)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+              const int row = wm * 64 + i * 16 + g4 + r;
+              const int col = (qb * 128 + wn * 32 + j * 16 + li) ^ ((row & 3) << 4);
+              ct[row * 256 + col] = acc[qa][qb][i][j][r];
+            }
+      __syncthreads();
+      float* dst = Cf + (int64_t)(m0 + qa * 128) * ldc + n0;
+#pragma unroll 4
+      for (int c = 0; c < 64; ++c) {
+        const int idx = tid + c * 512;
+        const int row = idx >> 8, col = idx & 255;
+        atomicAdd(dst + (int64_t)row * ldc + col, ct[row * 256 + (col ^ ((row & 3) << 4))]);
+      }
+    }
+  } else {
+    constexpr int LDC = 264;  // padded staging row (elements)
+    bf16_t* ct = reinterpret_cast<bf16_t*>(smem);
+    float bv[2][2] = {{0.f, 0.f}, {0.f, 0.f}};
+    if (EPI == EPI_BIAS_ACT && bias) {
+#pragma unroll
+      for (int qb = 0; qb < 2; ++qb)
+#pragma unroll
+        for (int j = 0; j < 2; ++j) bv[qb][j] = bf2f(bias[n0 + qb * 128 + wn * 32 + j * 16 + li]);
+    }
+#pragma unroll
+    for (int qa = 0; qa < 2; ++qa) {
+      if (qa) __syncthreads();  // previous half's rows have been stored
+#pragma unroll
+      for (int qb = 0; qb < 2; ++qb)
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+          for (int j = 0; j < 2; ++j)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+              const int row = wm * 64 + i * 16 + g4 + r;
+              const int col = qb * 128 + wn * 32 + j * 16 + li;
+              ct[row * LDC + col] = f2bf(acc[qa][qb][i][j][r] + bv[qb][j]);
+            }
+      __syncthreads();
+      // 128 rows x 32 chunks of 8 elements
+#pragma unroll 2
+      for (int c = 0; c < 8; ++c) {
+        const int idx = tid + c * 512;
+        const int row = idx >> 5, ch = idx & 31;
+        uint4 v = *reinterpret_cast<const uint4*>(ct + row * LDC + ch * 8);
+        const int64_t o = (int64_t)(m0 + qa * 128 + row) * ldc + n0 + ch * 8;
+        if (EPI == EPI_BIAS_ACT && act != 0) {
+          if (Zout) *reinterpret_cast<uint4*>(Zout + o) = v;
+          uint32_t wv[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+          for (int q = 0; q < 4; ++q) {
+            const float lo = act_f(__uint_as_float(wv[q] << 16), act);
+            const float hi = act_f(__uint_as_float(wv[q] & 0xffff0000u), act);
+            wv[q] = pack_bf2(lo, hi);
+          }
+          v = make_uint4(wv[0], wv[1], wv[2], wv[3]);
+        }
+        *reinterpret_cast<uint4*>(C + o) = v;
+      }
+    }
+  }
+}
+
+}  // namespace g256
+
+// Default on; DPA_GEMM256=0 or set_gemm256(false) routes every shape to gemm.hip.
+static int g_gemm256 = -1;
+void set_gemm256(bool on) { g_gemm256 = on ? 1 : 0; }
+static bool g256_enabled() {
+  if (g_gemm256 < 0) {
+    const char* e = std::getenv("DPA_GEMM256");
+    g_gemm256 = (e && e[0] == '0') ? 0 : 1;
+  }
+  return g_gemm256 != 0;
+}
+
+bool launch_gemm256_nt(const uint16_t* x, const uint16_t* W, const uint16_t* bias, uint16_t* y,
+                       uint16_t* z, int T, int N, int K, int act, hipStream_t s) {
+  if (!g256_enabled() || T % 256 || N % 256 || K % 128 || K < 128) return false;
+  hipLaunchKernelGGL((g256::gemm256_kernel<false, false, g256::EPI_BIAS_ACT>),
+                     dim3((T / 256) * (N / 256)), dim3(512), 0, s, (const bf16_t*)x, (int64_t)K,
+                     (const bf16_t*)W, (int64_t)K, T, N, K / 64, K / 64, 1, (bf16_t*)y, (int64_t)N,
+                     nullptr, (const bf16_t*)bias, act, (bf16_t*)z, nullptr);
+  return true;
+}
+
+bool launch_gemm256_nn(const uint16_t* dy, const uint16_t* W, uint16_t* dx, int T, int N, int K,
+                       hipStream_t s) {
+  // dx[T][K] = dy[T][N] . W[N][K]: M = T, N' = K, reduction = N
+  if (!g256_enabled() || T % 256 || K % 256 || N % 128 || N < 128) return false;
+  hipLaunchKernelGGL((g256::gemm256_kernel<false, true, g256::EPI_BF16>),
+                     dim3((T / 256) * (K / 256)), dim3(512), 0, s, (const bf16_t*)dy, (int64_t)N,
+                     (const bf16_t*)W, (int64_t)K, T, K, N / 64, N / 64, 1, (bf16_t*)dx, (int64_t)K,
+                     nullptr, nullptr, 0, nullptr, nullptr);
+  return true;
+}
+
+bool launch_gemm256_wgrad(const uint16_t* dy, const uint16_t* x, float* dW, float* db, int T,
+                          int N, int K, hipStream_t s) {
+  // dW[N][K] += dy[T][N]^T . x[T][K]: M = N, N' = K, reduction = T split over workgroups
+  if (!g256_enabled() || N % 256 || K % 256 || T % 128 || T < 128) return false;
+  const int tiles = (N / 256) * (K / 256);
+  const int ktot = T / 64;
+  int splits = (512 + tiles - 1) / tiles;
+  if (splits > ktot / 2) splits = ktot / 2;
+  if (splits < 1) splits = 1;
+  int kps = (ktot + splits - 1) / splits;
+  kps += kps & 1;
+  splits = (ktot + kps - 1) / kps;
+  hipLaunchKernelGGL((g256::gemm256_kernel<true, true, g256::EPI_ATOMIC_F32>),
+                     dim3(tiles * splits), dim3(512), 0, s, (const bf16_t*)dy, (int64_t)N,
+                     (const bf16_t*)x, (int64_t)K, N, K, ktot, kps, splits, nullptr, (int64_t)K, dW,
+                     nullptr, 0, nullptr, db);
+  return true;
+}
+
+}  // namespace dpa

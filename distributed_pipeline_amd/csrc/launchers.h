@@ -60,5 +60,14 @@ bool launch_gemm_nn(const uint16_t* dy, const uint16_t* W, uint16_t* dx, int T, 
                     hipStream_t s);
 bool launch_gemm_wgrad(const uint16_t* dy, const uint16_t* x, float* dW, float* db, int T, int N,
                        int K, hipStream_t s);
+// gemm256.hip: 256x256 8-phase variants (return false when the shape does not tile
+// or DPA_GEMM256=0); the launch_gemm_* entry points try them first.
+bool launch_gemm256_nt(const uint16_t* x, const uint16_t* W, const uint16_t* bias, uint16_t* y,
+                       uint16_t* z, int T, int N, int K, int act, hipStream_t s);
+bool launch_gemm256_nn(const uint16_t* dy, const uint16_t* W, uint16_t* dx, int T, int N, int K,
+                       hipStream_t s);
+void set_gemm256(bool on);
+bool launch_gemm256_wgrad(const uint16_t* dy, const uint16_t* x, float* dW, float* db, int T,
+                          int N, int K, hipStream_t s);
 
 }  // namespace dpa

@@ -107,6 +107,15 @@ __device__ __forceinline__ bf16x8 lds_tr_frag_nat(const char* lds, int r0, int c
   return cat44(ds_read_tr16(pa), ds_read_tr16(pb));
 }
 
+// Bijective XCD remap: workgroup ids with equal (id % 8) run on one XCD; give
+// each XCD a contiguous range of logical tile ids (neighbouring tiles share
+// operand panels in that XCD's L2).
+__device__ __forceinline__ int xcd_remap(int id, int total) {
+  const int q = total >> 3, r = total & 7, xcd = id & 7;
+  const int base = xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q;
+  return base + (id >> 3);
+}
+
 // Cheap 32-bit hash (lowbias32) for dropout masks inside matrix-core loops.
 __device__ __forceinline__ uint32_t lowbias32(uint32_t x) {
   x ^= x >> 16; x *= 0x7feb352du; x ^= x >> 15; x *= 0x846ca68bu; x ^= x >> 16;

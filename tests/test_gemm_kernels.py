@@ -10,14 +10,24 @@ def _ext():
     return get_ext(required=True)
 
 
+@pytest.fixture(params=[256, 128], ids=["tile256", "tile128"])
+def tile(request):
+    """Run each case on the 256x256 8-phase kernel (where the shape tiles) and on
+    the 128x128 kernel."""
+    _ext().set_gemm256(request.param == 256)
+    yield request.param
+    _ext().set_gemm256(True)
+
+
 def _close(a, r, tol=2e-2):
     err = (a.float() - r).abs().max().item()
     assert err <= tol * max(r.abs().max().item(), 1e-3), (err, r.abs().max().item())
 
 
 @pytest.mark.parametrize("T,K,N,act", [(256, 128, 128, 0), (512, 768, 2304, 0), (384, 768, 3072, 1),
-                                       (128, 256, 384, 2), (256, 128, 512, 3)])
-def test_gemm_nt_bias_act(T, K, N, act):
+                                       (128, 256, 384, 2), (256, 128, 512, 3), (768, 768, 3072, 1),
+                                       (256, 512, 512, 2), (1024, 128, 768, 3), (512, 3072, 768, 0)])
+def test_gemm_nt_bias_act(T, K, N, act, tile):
     torch.manual_seed(0)
     x = torch.randn(T, K, device="cuda").bfloat16()
     W = (torch.randn(N, K, device="cuda") * 0.05).bfloat16()
@@ -30,16 +40,18 @@ def test_gemm_nt_bias_act(T, K, N, act):
         _close(z, zr)
 
 
-@pytest.mark.parametrize("T,N,K", [(256, 128, 128), (512, 2304, 768), (384, 768, 3072)])
-def test_gemm_nn_dgrad(T, N, K):
+@pytest.mark.parametrize("T,N,K", [(256, 128, 128), (512, 2304, 768), (384, 768, 3072),
+                                   (768, 768, 3072), (512, 3072, 768), (256, 128, 256)])
+def test_gemm_nn_dgrad(T, N, K, tile):
     torch.manual_seed(0)
     dy = torch.randn(T, N, device="cuda").bfloat16()
     W = (torch.randn(N, K, device="cuda") * 0.05).bfloat16()
     _close(_ext().gemm_nn(dy, W), dy.float() @ W.float())
 
 
-@pytest.mark.parametrize("T,N,K", [(128, 128, 128), (4096, 768, 768), (8192, 2304, 768), (1024, 768, 3072)])
-def test_gemm_wgrad_accumulates(T, N, K):
+@pytest.mark.parametrize("T,N,K", [(128, 128, 128), (4096, 768, 768), (8192, 2304, 768), (1024, 768, 3072),
+                                   (640, 256, 256), (256, 512, 768), (32768, 768, 3072)])
+def test_gemm_wgrad_accumulates(T, N, K, tile):
     torch.manual_seed(0)
     dy = torch.randn(T, N, device="cuda").bfloat16()
     x = torch.randn(T, K, device="cuda").bfloat16()
