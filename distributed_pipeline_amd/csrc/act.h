@@ -1,0 +1,60 @@
+// Activation functions shared by the GEMM epilogues and the elementwise kernels.
+//
+// GELU is the exact (erf) form used by BERT, evaluated with the
+// Abramowitz-Stegun 7.1.26 rational approximation of erf (|error| < 1.5e-7,
+// far below bf16 resolution): one v_exp_f32 and one v_rcp_f32 instead of the
+// libm erff, and the same exp(-z^2/2) term serves the derivative's pdf.
+// Codes: 0 none, 1 gelu, 2 tanh, 3 silu.
+#pragma once
+#include <hip/hip_runtime.h>
+
+namespace dpa {
+
+// Phi(z) (standard normal cdf) and exp(-z^2/2)
+__device__ __forceinline__ float phi_cdf(float z, float& e) {
+  const float x = fabsf(z) * 0.70710678118654752f;
+  e = __expf(-x * x);
+  const float t = __builtin_amdgcn_rcpf(fmaf(0.3275911f, x, 1.f));
+  float p = fmaf(1.061405429f, t, -1.453152027f);
+  p = fmaf(p, t, 1.421413741f);
+  p = fmaf(p, t, -0.284496736f);
+  p = fmaf(p, t, 0.254829592f);
+  p *= t;
+  const float erf_abs = fmaf(-p, e, 1.f);
+  return 0.5f + 0.5f * copysignf(erf_abs, z);
+}
+
+__device__ __forceinline__ float gelu_f(float z) {
+  float e;
+  return z * phi_cdf(z, e);
+}
+
+__device__ __forceinline__ float dgelu_f(float z) {
+  float e;
+  const float c = phi_cdf(z, e);
+  return fmaf(z * 0.39894228040143268f, e, c);
+}
+
+__device__ __forceinline__ float act_apply(float z, int act) {
+  switch (act) {
+    case 1: return gelu_f(z);
+    case 2: return tanhf(z);
+    case 3: return z * __builtin_amdgcn_rcpf(1.f + __expf(-z));
+    default: return z;
+  }
+}
+
+// d act / dz given aux = z (gelu, silu) or y = tanh(z) (tanh)
+__device__ __forceinline__ float act_deriv(float a, int act) {
+  switch (act) {
+    case 1: return dgelu_f(a);
+    case 2: return 1.f - a * a;
+    case 3: {
+      const float sg = __builtin_amdgcn_rcpf(1.f + __expf(-a));
+      return sg * fmaf(a, 1.f - sg, 1.f);
+    }
+    default: return 1.f;
+  }
+}
+
+}  // namespace dpa

@@ -178,159 +178,100 @@ __global__ void __launch_bounds__(256) attn_fwd_kernel(const bf16_t* __restrict_
 }
 
 
-// register prefetch of one (batch, head): K, V rows (4 x 16 B per thread each) and the
-// wave's Q fragments (named registers: hipcc puts small arrays carried around the
-// persistent loop in scratch)
-struct AttPrefetch {
-  uint4 k0, k1, k2, k3, v0, v1, v2, v3;
-  bf16x8 q0, q1, q2, q3;
-};
-
-__device__ __forceinline__ uint4 ld16_row(const bf16_t* base, int64_t ld, int c, int L) {
-  const int row = c >> 3, ch = c & 7;
-  const int rr = row < L ? row : 0;
-  return *reinterpret_cast<const uint4*>(base + (int64_t)rr * ld + ch * 8);
-}
-
-__device__ __forceinline__ void attn_prefetch(const bf16_t* __restrict__ qkv, int bh, int H, int L,
-                                              int64_t ld, int tid, int q, bool q_ok, int hf,
-                                              AttPrefetch& f) {
-  const int b = bh / H, h = bh - b * H;
-  const bf16_t* qb = qkv + (int64_t)b * L * ld + (int64_t)h * HD;
-  const bf16_t* kb = qb + (int64_t)H * HD;
-  const bf16_t* vb = qb + 2LL * H * HD;
-  f.k0 = ld16_row(kb, ld, tid, L);
-  f.k1 = ld16_row(kb, ld, tid + 256, L);
-  f.k2 = ld16_row(kb, ld, tid + 512, L);
-  f.k3 = ld16_row(kb, ld, tid + 768, L);
-  f.v0 = ld16_row(vb, ld, tid, L);
-  f.v1 = ld16_row(vb, ld, tid + 256, L);
-  f.v2 = ld16_row(vb, ld, tid + 512, L);
-  f.v3 = ld16_row(vb, ld, tid + 768, L);
-  const bf16_t* qp = qb + (int64_t)(q_ok ? q : 0) * ld + 8 * hf;
-  f.q0 = ld_frag(qp);
-  f.q1 = ld_frag(qp + 16);
-  f.q2 = ld_frag(qp + 32);
-  f.q3 = ld_frag(qp + 48);
-}
-
-__device__ __forceinline__ void st16_lds(char* lds, int c, const uint4& v) {
-  *reinterpret_cast<uint4*>(lds + swz<128>(c >> 3, c & 7)) = v;
-}
-
 // L <= 128: every key of the (batch, head) fits one LDS image and the whole
 // S^T column of a query fits in registers -> exact softmax in one pass.
-// Persistent: each workgroup walks (batch, head) pairs; the next pair's K, V
-// (register-staged) and Q fragments are loaded while the current pair computes.
 template <bool CAUSAL>
 __global__ void __launch_bounds__(256) attn_fwd_small_kernel(const bf16_t* __restrict__ qkv,
                                                             bf16_t* __restrict__ out,
-                                                            float* __restrict__ lse, int B, int L,
-                                                            int H, float p, uint32_t seed,
-                                                            uint32_t offset) {
+                                                            float* __restrict__ lse, int L, int H,
+                                                            float p, uint32_t seed, uint32_t offset) {
   __shared__ __attribute__((aligned(16))) char smem[2 * 128 * 128];
   char* kt_lds = smem;
   char* vt_lds = smem + 128 * 128;
+  const int b = blockIdx.z, hd = blockIdx.y;
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, hf = lane >> 5;
   const int64_t ld = 3LL * H * HD;
-  const int nt = L >> 5;            // 32-key tiles (<= 4)
-  const int nbh = B * H;
+  const bf16_t* qb = qkv + (int64_t)b * L * ld + (int64_t)hd * HD;
+  const bf16_t* kb = qb + (int64_t)H * HD;
+  const bf16_t* vb = qb + 2LL * H * HD;
+  const int nt = L >> 5;  // 32-key tiles (<= 4)
+  for (int r0 = 0; r0 < L; r0 += 64) {
+    stage64(kt_lds + r0 * 128, kb, ld, r0, L, tid);
+    stage64(vt_lds + r0 * 128, vb, ld, r0, L, tid);
+  }
   const int qbase = w * 32;
   const int q = qbase + (lane & 31);
   const bool q_ok = q < L;
-  AttPrefetch pf;
-
-  int bh = blockIdx.x;
-  if (bh < nbh) attn_prefetch(qkv, bh, H, L, ld, tid, q, q_ok, hf, pf);
-  for (; bh < nbh; bh += gridDim.x) {
-    __syncthreads();  // previous pair done with the LDS images
-    // rows >= L hold junk that no key index reaches
-    st16_lds(kt_lds, tid, pf.k0);
-    st16_lds(kt_lds, tid + 256, pf.k1);
-    st16_lds(kt_lds, tid + 512, pf.k2);
-    st16_lds(kt_lds, tid + 768, pf.k3);
-    st16_lds(vt_lds, tid, pf.v0);
-    st16_lds(vt_lds, tid + 256, pf.v1);
-    st16_lds(vt_lds, tid + 512, pf.v2);
-    st16_lds(vt_lds, tid + 768, pf.v3);
-    bf16x8 qf[4] = {pf.q0, pf.q1, pf.q2, pf.q3};
-    if (!q_ok) {
+  bf16x8 qf[4];
 #pragma unroll
-      for (int s = 0; s < 4; ++s)
+  for (int s = 0; s < 4; ++s) {
+    if (q_ok) qf[s] = ld_frag(qb + (int64_t)q * ld + 16 * s + 8 * hf);
+    else for (int j = 0; j < 8; ++j) qf[s][j] = 0;
+  }
+  const DropCfg dc = make_drop(p, seed, offset, (uint32_t)(b * H + hd));
+  __syncthreads();
+  if (qbase >= L) return;  // whole wave idle (L < 128); no barrier follows
+  f32x16 acc[4];
+  float m = -INFINITY;
 #pragma unroll
-        for (int j = 0; j < 8; ++j) qf[s][j] = 0;
-    }
-    __syncthreads();
-    if (bh + (int)gridDim.x < nbh)  // in flight during the compute
-      attn_prefetch(qkv, bh + (int)gridDim.x, H, L, ld, tid, q, q_ok, hf, pf);
-
-    const int b = bh / H, hd = bh - b * H;
-    const DropCfg dc = make_drop(p, seed, offset, (uint32_t)bh);
-    if (qbase < L) {
-      f32x16 acc[4];
-      float m = -INFINITY;
+  for (int t = 0; t < 4; ++t) {
+    acc[t] = zero16();
+    if (t < nt) {
 #pragma unroll
-      for (int t = 0; t < 4; ++t) {
-        acc[t] = zero16();
-        if (t < nt) {
+      for (int s = 0; s < 4; ++s) acc[t] = mfma32(lds_frag<128>(kt_lds, t * 32 + (lane & 31), 2 * s + hf), qf[s], acc[t]);
 #pragma unroll
-          for (int s = 0; s < 4; ++s)
-            acc[t] = mfma32(lds_frag<128>(kt_lds, t * 32 + (lane & 31), 2 * s + hf), qf[s], acc[t]);
-#pragma unroll
-          for (int i = 0; i < 16; ++i) {
-            const int key = t * 32 + acc_row(i, hf);
-            float y = acc[t][i] * ATT_C;
-            if (CAUSAL && key > q) y = -INFINITY;
-            acc[t][i] = y;
-            m = fmaxf(m, y);
-          }
-        }
+      for (int i = 0; i < 16; ++i) {
+        const int key = t * 32 + acc_row(i, hf);
+        float y = acc[t][i] * ATT_C;
+        if (CAUSAL && key > q) y = -INFINITY;
+        acc[t][i] = y;
+        m = fmaxf(m, y);
       }
-      m = fmaxf(m, __shfl_xor(m, 32, 64));
-      float l = 0.f;
-#pragma unroll
-      for (int t = 0; t < 4; ++t)
-        if (t < nt)
-#pragma unroll
-          for (int i = 0; i < 16; ++i) {
-            const float e = exp2f(acc[t][i] - m);
-            acc[t][i] = e;
-            l += e;
-          }
-      l += __shfl_xor(l, 32, 64);
-      const float inv_l = 1.f / l;
-      if (hf == 0 && q_ok) lse[(int64_t)bh * L + q] = (m + log2f(l)) * LN2f;
-      f32x16 o[2];
-      o[0] = zero16();
-      o[1] = zero16();
-#pragma unroll
-      for (int t = 0; t < 4; ++t) {
-        if (t < nt) {
-#pragma unroll
-          for (int i = 0; i < 16; ++i) {
-            float pr = acc[t][i] * inv_l;
-            if (dc.on) pr = keep_bit(dc, q, t * 32 + acc_row(i, hf)) ? pr * dc.scale : 0.f;
-            acc[t][i] = pr;
-          }
-#pragma unroll
-          for (int s = 0; s < 2; ++s) {
-            const bf16x8 af = acc_to_frag(acc[t], s);
-#pragma unroll
-            for (int dt = 0; dt < 2; ++dt)
-              o[dt] = mfma32(af, lds_tr_frag<128>(vt_lds, t * 32 + 16 * s, dt * 32, lane), o[dt]);
-          }
-        }
-      }
-      bf16_t* ob = out + (int64_t)b * L * H * HD + (int64_t)hd * HD;
-#pragma unroll
-      for (int dt = 0; dt < 2; ++dt)
-#pragma unroll
-        for (int i = 0; i < 16; ++i) {
-          const int qq = qbase + acc_row(i, hf);
-          if (qq < L) ob[(int64_t)qq * H * HD + dt * 32 + (lane & 31)] = f2bf(o[dt][i]);
-        }
     }
   }
+  m = fmaxf(m, __shfl_xor(m, 32, 64));
+  float l = 0.f;
+#pragma unroll
+  for (int t = 0; t < 4; ++t)
+    if (t < nt)
+#pragma unroll
+      for (int i = 0; i < 16; ++i) {
+        const float e = exp2f(acc[t][i] - m);
+        acc[t][i] = e;
+        l += e;
+      }
+  l += __shfl_xor(l, 32, 64);
+  const float inv_l = 1.f / l;
+  if (hf == 0 && q_ok) lse[((int64_t)b * H + hd) * L + q] = (m + log2f(l)) * LN2f;
+  f32x16 o[2];
+  o[0] = zero16();
+  o[1] = zero16();
+#pragma unroll
+  for (int t = 0; t < 4; ++t) {
+    if (t < nt) {
+#pragma unroll
+      for (int i = 0; i < 16; ++i) {
+        float pr = acc[t][i] * inv_l;
+        if (dc.on) pr = keep_bit(dc, q, t * 32 + acc_row(i, hf)) ? pr * dc.scale : 0.f;
+        acc[t][i] = pr;
+      }
+#pragma unroll
+      for (int s = 0; s < 2; ++s) {
+        const bf16x8 af = acc_to_frag(acc[t], s);
+#pragma unroll
+        for (int dt = 0; dt < 2; ++dt)
+          o[dt] = mfma32(af, lds_tr_frag<128>(vt_lds, t * 32 + 16 * s, dt * 32, lane), o[dt]);
+      }
+    }
+  }
+  bf16_t* ob = out + (int64_t)b * L * H * HD + (int64_t)hd * HD;
+#pragma unroll
+  for (int dt = 0; dt < 2; ++dt)
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+      const int qq = qbase + acc_row(i, hf);
+      if (qq < L) ob[(int64_t)qq * H * HD + dt * 32 + (lane & 31)] = f2bf(o[dt][i]);
+    }
 }
 
 // delta[b,h,q] = sum_d dO * O
@@ -546,14 +487,12 @@ void launch_attn_fwd(const uint16_t* qkv, uint16_t* out, float* lse, int B, int 
                      bool causal, uint32_t seed, uint32_t offset, hipStream_t s) {
   dim3 grid((L + 127) / 128, H, B);
   if (L <= 128) {
-    const int nbh = B * H;
-    const int pg = nbh < 2048 ? nbh : 2048;  // persistent: ~8 workgroups per CU
     if (causal)
-      hipLaunchKernelGGL(attn_fwd_small_kernel<true>, dim3(pg), dim3(256), 0, s, (const bf16_t*)qkv,
-                         (bf16_t*)out, lse, B, L, H, p, seed, offset);
+      hipLaunchKernelGGL(attn_fwd_small_kernel<true>, grid, dim3(256), 0, s, (const bf16_t*)qkv,
+                         (bf16_t*)out, lse, L, H, p, seed, offset);
     else
-      hipLaunchKernelGGL(attn_fwd_small_kernel<false>, dim3(pg), dim3(256), 0, s, (const bf16_t*)qkv,
-                         (bf16_t*)out, lse, B, L, H, p, seed, offset);
+      hipLaunchKernelGGL(attn_fwd_small_kernel<false>, grid, dim3(256), 0, s, (const bf16_t*)qkv,
+                         (bf16_t*)out, lse, L, H, p, seed, offset);
     return;
   }
   if (causal)

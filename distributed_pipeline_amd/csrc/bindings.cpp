@@ -307,6 +307,23 @@ static at::Tensor gemm_nn(const at::Tensor& dy, const at::Tensor& W) {
   return dx;
 }
 
+// dz = (dy . W) * act'(aux); returns an undefined tensor when the shape does not
+// tile for the fused kernel (caller falls back to dgrad + separate act backward).
+static at::Tensor gemm_nn_dact(const at::Tensor& dy, const at::Tensor& W, const at::Tensor& aux,
+                               int64_t act) {
+  CHECK_DEV(dy); CHECK_BF16(dy); CHECK_BF16(W); CHECK_BF16(aux);
+  CHECK_CONTIG(dy); CHECK_CONTIG(W); CHECK_CONTIG(aux);
+  const int T = (int)dy.size(0), N = (int)dy.size(1), K = (int)W.size(1);
+  TORCH_CHECK(W.size(0) == N && aux.size(0) == T && aux.size(1) == K, "gemm_nn_dact shapes");
+  const c10::DeviceGuard guard(dy.device());
+  at::Tensor dz = at::empty({T, K}, dy.options());
+  if (!dpa::launch_gemm256_nn_dact(bf_ptr(dy), bf_ptr(W), bf_ptr(aux),
+                                   reinterpret_cast<uint16_t*>(dz.data_ptr()), T, N, K, (int)act,
+                                   cur_stream()))
+    return at::Tensor();
+  return dz;
+}
+
 static void gemm_wgrad(const at::Tensor& dy, const at::Tensor& x, at::Tensor& dW,
                        c10::optional<at::Tensor> db) {
   CHECK_DEV(dy); CHECK_BF16(dy); CHECK_BF16(x); CHECK_CONTIG(dy); CHECK_CONTIG(x);
@@ -342,6 +359,7 @@ PYBIND11_MODULE(_C, m) {
   m.def("attn_bwd", &attn_bwd, "fused attention backward -> dqkv");
   m.def("gemm_nt", &gemm_nt, "y = act(x W^T + b) (bf16 MFMA) -> (y, z_preact)");
   m.def("gemm_nn", &gemm_nn, "dx = dy W (bf16 MFMA)");
+  m.def("gemm_nn_dact", &gemm_nn_dact, "dz = (dy W) * act'(aux) (bf16 MFMA, fused act backward)");
   m.def("gemm_wgrad", &gemm_wgrad, "dW += dy^T x, db += colsum(dy) (fp32 atomics, split-K)");
   m.def("gemm_supported", &gemm_supported, "shape check for the native GEMMs");
   m.def("set_gemm256", &dpa::set_gemm256, "enable/disable the 256x256 8-phase GEMM path");

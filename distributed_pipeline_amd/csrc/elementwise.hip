@@ -7,6 +7,7 @@
 // vector per row), threadIdx.y strides rows; grid.y splits rows.  Column sums
 // stay in registers across all of a thread's rows, are reduced over the 4
 // row-lanes in LDS and added with one fp32 atomic per column per block.
+#include "act.h"
 #include "common.h"
 #include "launchers.h"
 
@@ -14,31 +15,9 @@ namespace dpa {
 
 enum Act { ACT_NONE = 0, ACT_GELU = 1, ACT_TANH = 2, ACT_SILU = 3 };
 
-__device__ __forceinline__ float act_f(float z, int act) {
-  switch (act) {
-    case ACT_GELU: return 0.5f * z * (1.f + erff(z * 0.70710678118654752f));
-    case ACT_TANH: return tanhf(z);
-    case ACT_SILU: return z / (1.f + __expf(-z));
-    default: return z;
-  }
-}
-
+__device__ __forceinline__ float act_f(float z, int act) { return act_apply(z, act); }
 // derivative given pre-activation z (gelu/silu) or output y (tanh)
-__device__ __forceinline__ float act_grad(float zy, int act) {
-  switch (act) {
-    case ACT_GELU: {
-      const float cdf = 0.5f * (1.f + erff(zy * 0.70710678118654752f));
-      const float pdf = 0.3989422804014327f * __expf(-0.5f * zy * zy);
-      return cdf + zy * pdf;
-    }
-    case ACT_TANH: return 1.f - zy * zy;
-    case ACT_SILU: {
-      const float s = 1.f / (1.f + __expf(-zy));
-      return s * (1.f + zy * (1.f - s));
-    }
-    default: return 1.f;
-  }
-}
+__device__ __forceinline__ float act_grad(float zy, int act) { return act_deriv(zy, act); }
 
 __device__ __forceinline__ void unpack8(const uint4& r, float* v) {
   const uint32_t w[4] = {r.x, r.y, r.z, r.w};

@@ -21,6 +21,7 @@
 // tiles straight into the fp32 gradient buffer with atomics (two 128-B row
 // segments per wave instruction): gradient accumulation across micro-batches
 // is fused into the GEMM, and db is reduced from the staged dy tiles.
+#include "act.h"
 #include "common.h"
 #include "launchers.h"
 #include "mfma.h"
@@ -32,14 +33,7 @@ enum GemmEpi { EPI_BF16 = 0, EPI_BIAS_ACT = 1, EPI_ATOMIC_F32 = 2 };
 typedef __attribute__((address_space(3))) void lds_void;
 typedef const __attribute__((address_space(1))) void glob_void;
 
-__device__ __forceinline__ float gemm_act(float z, int act) {
-  switch (act) {
-    case 1: return 0.5f * z * (1.f + erff(z * 0.70710678118654752f));
-    case 2: return tanhf(z);
-    case 3: return z / (1.f + __expf(-z));
-    default: return z;
-  }
-}
+__device__ __forceinline__ float gemm_act(float z, int act) { return act_apply(z, act); }
 
 // Operand tile: row form [128][64] (128-B rows) or transposed form [64][128] (256-B rows).
 template <bool TR>

@@ -30,6 +30,7 @@
 // (split-K wgrad) with the bias gradient reduced from the staged dy images.
 #include <cstdlib>
 
+#include "act.h"
 #include "common.h"
 #include "launchers.h"
 #include "mfma.h"
@@ -48,7 +49,9 @@ constexpr int HALF = 16384;
 constexpr int B_REGION = 65536;
 __host__ __device__ constexpr int img_off(int buf, int h) { return buf * 2 * HALF + h * HALF; }
 
-enum { EPI_BF16 = 0, EPI_BIAS_ACT = 1, EPI_ATOMIC_F32 = 2 };
+// EPI_DACT: dgrad with the previous layer's activation backward fused in:
+// C = (A.B) * act'(aux), aux = pre-activation z (gelu, silu) or output y (tanh).
+enum { EPI_BF16 = 0, EPI_BIAS_ACT = 1, EPI_ATOMIC_F32 = 2, EPI_DACT = 3 };
 
 __device__ __forceinline__ f32x4 mfma16(const bf16x8& a, const bf16x8& b, const f32x4& c) {
   return __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8_v, a),
@@ -63,14 +66,8 @@ __device__ __forceinline__ uint32_t lds_u32(const void* p) {
 // 16x16x32 operand (a 32-lane half reads rows {q, 8+q} (+16n) of two 16-B chunks).
 __device__ __forceinline__ int tr_x(int row) { return ((row & 3) << 1) | (((row >> 3) & 1) << 3); }
 
-__device__ __forceinline__ float act_f(float z, int act) {
-  switch (act) {
-    case 1: return 0.5f * z * (1.f + erff(z * 0.70710678118654752f));
-    case 2: return tanhf(z);
-    case 3: return z / (1.f + __expf(-z));
-    default: return z;
-  }
-}
+__device__ __forceinline__ float act_f(float z, int act) { return act_apply(z, act); }
+__device__ __forceinline__ float dact_f(float a, int act) { return act_deriv(a, act); }
 
 __device__ __forceinline__ void barrier() { asm volatile("s_barrier" ::: "memory"); }
 
@@ -378,6 +375,17 @@ __global__ void __launch_bounds__(512) gemm256_kernel(
 #pragma unroll
     for (int qa = 0; qa < 2; ++qa) {
       if (qa) __syncthreads();  // previous half's rows have been stored
+      // EPI_DACT: fetch this half's activation-backward operand before staging, so
+      // its latency overlaps the LDS round trip
+      uint4 av[8];
+      if constexpr (EPI == EPI_DACT) {
+#pragma unroll
+        for (int c = 0; c < 8; ++c) {
+          const int idx = tid + c * 512;
+          const int64_t o = (int64_t)(m0 + qa * 128 + (idx >> 5)) * ldc + n0 + (idx & 31) * 8;
+          av[c] = *reinterpret_cast<const uint4*>(Zout + o);
+        }
+      }
 #pragma unroll
       for (int qb = 0; qb < 2; ++qb)
 #pragma unroll
@@ -392,12 +400,24 @@ __global__ void __launch_bounds__(512) gemm256_kernel(
             }
       __syncthreads();
       // 128 rows x 32 chunks of 8 elements
-#pragma unroll 2
+#pragma unroll
       for (int c = 0; c < 8; ++c) {
         const int idx = tid + c * 512;
         const int row = idx >> 5, ch = idx & 31;
         uint4 v = *reinterpret_cast<const uint4*>(ct + row * LDC + ch * 8);
         const int64_t o = (int64_t)(m0 + qa * 128 + row) * ldc + n0 + ch * 8;
+        if constexpr (EPI == EPI_DACT) {
+          uint32_t wv[4] = {v.x, v.y, v.z, v.w};
+          const uint32_t aw[4] = {av[c].x, av[c].y, av[c].z, av[c].w};
+#pragma unroll
+          for (int q = 0; q < 4; ++q) {
+            const float lo = __uint_as_float(wv[q] << 16) * dact_f(__uint_as_float(aw[q] << 16), act);
+            const float hi = __uint_as_float(wv[q] & 0xffff0000u) *
+                             dact_f(__uint_as_float(aw[q] & 0xffff0000u), act);
+            wv[q] = pack_bf2(lo, hi);
+          }
+          v = make_uint4(wv[0], wv[1], wv[2], wv[3]);
+        }
         if (EPI == EPI_BIAS_ACT && act != 0) {
           if (Zout) *reinterpret_cast<uint4*>(Zout + o) = v;
           uint32_t wv[4] = {v.x, v.y, v.z, v.w};
@@ -449,13 +469,26 @@ bool launch_gemm256_nn(const uint16_t* dy, const uint16_t* W, uint16_t* dx, int 
   return true;
 }
 
+bool launch_gemm256_nn_dact(const uint16_t* dy, const uint16_t* W, const uint16_t* aux,
+                            uint16_t* dz, int T, int N, int K, int act, hipStream_t s) {
+  // dz[T][K] = (dy[T][N] . W[N][K]) * act'(aux[T][K])
+  if (!g256_enabled() || T % 256 || K % 256 || N % 128 || N < 128) return false;
+  hipLaunchKernelGGL((g256::gemm256_kernel<false, true, g256::EPI_DACT>),
+                     dim3((T / 256) * (K / 256)), dim3(512), 0, s, (const bf16_t*)dy, (int64_t)N,
+                     (const bf16_t*)W, (int64_t)K, T, K, N / 64, N / 64, 1, (bf16_t*)dz, (int64_t)K,
+                     nullptr, nullptr, act, (bf16_t*)aux, nullptr);
+  return true;
+}
+
 bool launch_gemm256_wgrad(const uint16_t* dy, const uint16_t* x, float* dW, float* db, int T,
                           int N, int K, hipStream_t s) {
   // dW[N][K] += dy[T][N]^T . x[T][K]: M = N, N' = K, reduction = T split over workgroups
   if (!g256_enabled() || N % 256 || K % 256 || T % 128 || T < 128) return false;
   const int tiles = (N / 256) * (K / 256);
   const int ktot = T / 64;
-  int splits = (512 + tiles - 1) / tiles;
+  // One 128 KiB workgroup per CU: size the grid to whole rounds of 256 CUs
+  // (floor, never a nearly-empty extra round; ~2 rounds for load balance).
+  int splits = 512 / tiles;
   if (splits > ktot / 2) splits = ktot / 2;
   if (splits < 1) splits = 1;
   int kps = (ktot + splits - 1) / splits;

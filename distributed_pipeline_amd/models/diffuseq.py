@@ -20,11 +20,7 @@ from torch import nn
 
 from ..ops import nn as ops
 from . import presets
-from .layers import BertEncoder, Embedding, LayerNorm, Linear
-
-
-class _Seq(nn.Sequential):
-    """Sequential whose index names match DiffuSeq (0 = first Linear, 2 = second)."""
+from .layers import MLP, BertEncoder, Embedding, LayerNorm, Linear
 
 
 class TransformerNetModel(nn.Module):
@@ -49,10 +45,8 @@ class TransformerNetModel(nn.Module):
             self.lm_head.weight = self.word_embedding.weight  # tied rounding head
 
         t4 = hidden_t_dim * 4
-        self.time_embed = nn.Sequential(Linear(hidden_t_dim, t4, act="silu"), nn.Identity(),
-                                        Linear(t4, H))
-        self.input_up_proj = nn.Sequential(Linear(input_dims, H, act="tanh"), nn.Identity(),
-                                           Linear(H, H))
+        self.time_embed = MLP(hidden_t_dim, t4, H, act="silu")
+        self.input_up_proj = MLP(input_dims, H, H, act="tanh")
         self.input_transformers = BertEncoder(H, cfg["num_layers"], cfg["num_heads"],
                                               cfg["intermediate_size"], dropout,
                                               eps=cfg["layer_norm_eps"], init_std=0.02)
@@ -60,8 +54,7 @@ class TransformerNetModel(nn.Module):
                              persistent=False)
         self.position_embeddings = Embedding(cfg["max_position_embeddings"], H, init_std=0.02)
         self.LayerNorm = LayerNorm(H, eps=cfg["layer_norm_eps"])
-        self.output_down_proj = nn.Sequential(Linear(H, H, act="tanh"), nn.Identity(),
-                                              Linear(H, input_dims))
+        self.output_down_proj = MLP(H, H, input_dims, act="tanh")
 
     # -- DiffuSeq API -------------------------------------------------------
     def get_embeds(self, input_ids):

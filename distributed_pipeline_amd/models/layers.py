@@ -47,6 +47,18 @@ class Linear(nn.Module):
         return f"in={self.in_features}, out={self.out_features}, act={self.act}"
 
 
+class MLP(nn.Sequential):
+    """Linear(act) -> Identity -> Linear with DiffuSeq's Sequential parameter names
+    (``0.*``, ``2.*``); runs as one fused op (see ``ops.mlp``)."""
+
+    def __init__(self, d_in, d_hidden, d_out, act, init_std=None):
+        super().__init__(Linear(d_in, d_hidden, act=act, init_std=init_std), nn.Identity(),
+                         Linear(d_hidden, d_out, init_std=init_std))
+
+    def forward(self, x):
+        return ops.mlp(x, self[0], self[2])
+
+
 class LayerNorm(nn.Module):
     def __init__(self, dim, eps=1e-12):
         super().__init__()
@@ -101,7 +113,7 @@ class BertLayer(nn.Module):
     def forward(self, x):
         a = self.attn_out(self.attn(x))
         h = self.attn_ln(a, residual=x, dropout=self.dropout)
-        f = self.ffn_out(self.ffn_in(h))
+        f = ops.mlp(h, self.ffn_in, self.ffn_out)
         return self.ffn_ln(f, residual=h, dropout=self.dropout)
 
 
@@ -133,7 +145,7 @@ class GPT2Block(nn.Module):
     def forward(self, x):
         h = self.attn_proj(self.attn(self.ln_1(x)))
         x = _residual_dropout(h, x, self.dropout, self.training)
-        h = self.mlp_proj(self.mlp_fc(self.ln_2(x)))
+        h = ops.mlp(self.ln_2(x), self.mlp_fc, self.mlp_proj)
         return _residual_dropout(h, x, self.dropout, self.training)
 
 

@@ -113,14 +113,18 @@ def _bias_act_bwd(dy2d, z, y, act, want_db):
     return dz, db
 
 
-# Linear GEMM routing (DPA_GEMM):
-#   "auto"   (default) - per product, the faster of the two measured on MI355X
-#            (tools/gemm_shapes_bench.py, profiles/): hand-written MFMA kernels
-#            for the fused cases - forward with a GELU/SiLU epilogue, and every
-#            weight-gradient GEMM (split-K, dW/db accumulated straight into the
-#            fp32 grad buffer) - and hipBLASLt for the plain bias-epilogue
-#            forward and the data-gradient GEMM;
-#   "native" - every Linear GEMM on the hand-written kernels;
+# Linear GEMM routing (DPA_GEMM), per product, from tools/gemm_shapes_bench.py on
+# MI355X at 262144 tokens (profiles/gemm_shapes_r1.jsonl):
+#   "auto"   (default) - weight-gradient GEMMs on the hand-written split-K MFMA
+#            kernel (dW/db accumulated straight into the fp32 grad buffer;
+#            770-985 TF vs hipBLASLt 330-815 TF), the MLP's hidden-layer data
+#            forward / data-gradient GEMMs on hipBLASLt (1000-1360 TF) with its
+#            bias epilogue, activations (and their backward) in our bias_act
+#            kernels - measured faster than the GELU / GELU'-epilogue MFMA GEMMs,
+#            whose epilogue VALU work cannot overlap the matrix cores at one
+#            workgroup per CU;
+#   "native" - every Linear GEMM on the hand-written kernels, incl. the fused
+#            activation-backward dgrad of ops.mlp;
 #   "blas"   - every Linear GEMM on hipBLASLt (plus separate epilogue kernels).
 GEMM_MODE = os.environ.get("DPA_GEMM", "auto")
 
@@ -136,7 +140,7 @@ def _route(x2, n_out, act):
         return False, False, False
     if GEMM_MODE == "native":
         return True, True, True
-    return act in ("gelu", "silu"), False, True
+    return False, False, True
 
 
 def _accumulate_wgrad(p, dz, x2, bias):
@@ -162,6 +166,45 @@ def _accumulate_wgrad(p, dz, x2, bias):
     return dw_out, db_out
 
 
+def _lin_fwd(x2, w16, b16, act, route):
+    """Forward GEMM (+bias, +activation) of one Linear -> (y, z).
+
+    z is the pre-activation, returned only when the activation backward needs it
+    (gelu/silu); tanh's backward uses y."""
+    if route[0]:
+        y, z = get_ext().gemm_nt(x2, w16, b16, _ACTS.index(act))
+    else:
+        if b16 is not None and x2.is_cuda:
+            z = torch.addmm(b16, x2, w16.t())  # hipBLASLt bias epilogue
+            b16_epi = None
+        else:
+            z = x2 @ w16.t()
+            b16_epi = b16
+        if b16_epi is not None or act != "none":
+            z, y = _bias_act_fwd(z, b16_epi, act)
+        else:
+            y = z
+    return y, (z if act in ("gelu", "silu") else None)
+
+
+def _lin_param_grads(w, b, dz, x2, native, db=None):
+    """(dW, db) of one Linear from its output-side gradient dz [T, N] and input x2.
+
+    native: split-K MFMA GEMM accumulating dW/db into the fp32 .grad buffers in
+    place (returns None grads).  Otherwise fp32-output GEMM; db is taken from
+    ``db`` when the caller already reduced it, else summed here."""
+    if native:
+        return _accumulate_wgrad(w, dz, x2, b)
+    dw = _mm_fp32(dz.t(), x2)
+    if b is not None and db is None:
+        db = dz.float().sum(0)
+    return dw, db
+
+
+def _dgrad(dz, w16, native):
+    return get_ext().gemm_nn(dz, w16) if native else dz @ w16
+
+
 class _LinearFn(torch.autograd.Function):
     """y = act(x W^T + b) in bf16 with fp32 master weights.
 
@@ -176,28 +219,10 @@ class _LinearFn(torch.autograd.Function):
         shp = x.shape
         x2 = x.reshape(-1, shp[-1])
         route = _route(x2, w16.shape[0], act)
-        if route[0]:
-            y, z = get_ext().gemm_nt(x2, w16, b16, _ACTS.index(act))
-            if act == "none":
-                z = None
-        else:
-            if act == "none" and b16 is not None and x2.is_cuda:
-                z = torch.addmm(b16, x2, w16.t())  # hipBLASLt bias epilogue
-                b16_epi = None
-            else:
-                z = x2 @ w16.t()
-                b16_epi = b16
-            if b16_epi is not None or act != "none":
-                z, y = _bias_act_fwd(z, b16_epi, act)
-            else:
-                y = z
-        # what the activation backward needs: tanh uses y, gelu/silu use z
-        keep_z = z if act in ("gelu", "silu") else None
-        keep_y = y if act == "tanh" else None
-        ctx.save_for_backward(x2, w16, keep_z, keep_y)
+        y, z = _lin_fwd(x2, w16, b16, act, route)
+        ctx.save_for_backward(x2, w16, z, y if act == "tanh" else None)
         ctx.params = (w, b)
         ctx.act = act
-        ctx.has_b = b is not None
         ctx.route = route
         ctx.shp = shp
         return y.reshape(*shp[:-1], w16.shape[0])
@@ -208,24 +233,13 @@ class _LinearFn(torch.autograd.Function):
         w, b = ctx.params
         dy2 = dy.reshape(-1, dy.shape[-1]).contiguous()
         _, nat_dgrad, nat_wgrad = ctx.route
-        if nat_wgrad:
-            dz = dy2
-            if ctx.act != "none":
-                dz, _ = _bias_act_bwd(dy2, z, y, ctx.act, False)
-            dx = None
-            if ctx.needs_input_grad[0]:
-                dx = get_ext().gemm_nn(dz, w16) if nat_dgrad else dz @ w16
-                dx = dx.reshape(ctx.shp)
-            dw = db = None
-            if ctx.needs_input_grad[1] or (ctx.has_b and ctx.needs_input_grad[2]):
-                dw, db = _accumulate_wgrad(w, dz, x2, b if ctx.has_b else None)
-            return dx, dw, db, None, None, None
-        if ctx.act != "none" or ctx.has_b:
-            dz, db = _bias_act_bwd(dy2, z, y, ctx.act, ctx.has_b)
+        want_db = b is not None and not nat_wgrad
+        if ctx.act != "none" or want_db:
+            dz, db = _bias_act_bwd(dy2, z, y, ctx.act, want_db)
         else:
             dz, db = dy2, None
-        dx = (dz @ w16).reshape(ctx.shp) if ctx.needs_input_grad[0] else None
-        dw = _mm_fp32(dz.t(), x2) if ctx.needs_input_grad[1] else None
+        dx = _dgrad(dz, w16, nat_dgrad).reshape(ctx.shp) if ctx.needs_input_grad[0] else None
+        dw, db = _lin_param_grads(w, b, dz, x2, nat_wgrad, db)
         return dx, dw, db, None, None, None
 
 
@@ -234,6 +248,63 @@ def linear(x, weight, bias=None, act="none"):
     if x.dtype == torch.float32:
         return _act_fwd(F.linear(x, weight, bias), act)
     return _LinearFn.apply(x, weight, bias, shadow(weight, x.dtype), shadow(bias, x.dtype), act)
+
+
+class _MLPFn(torch.autograd.Function):
+    """y = fc2(act(fc1(x))) as one op, so the backward can fuse fc1's activation
+    derivative into fc2's data-gradient GEMM epilogue (dz1 = (dy W2) * act'(z1)):
+    the [T, ffn] hidden gradient is written once, already multiplied, instead of
+    a dgrad GEMM followed by a separate activation-backward pass."""
+
+    @staticmethod
+    def forward(ctx, x, w1, b1, w2, b2, w1_16, b1_16, w2_16, b2_16, act):
+        shp = x.shape
+        x2 = x.reshape(-1, shp[-1])
+        r1 = _route(x2, w1_16.shape[0], act)
+        h, z1 = _lin_fwd(x2, w1_16, b1_16, act, r1)
+        r2 = _route(h, w2_16.shape[0], "none")
+        y, _ = _lin_fwd(h, w2_16, b2_16, "none", r2)
+        ctx.save_for_backward(x2, w1_16, w2_16, h, z1)
+        ctx.params = (w1, b1, w2, b2)
+        ctx.cfg = (act, r1, r2, shp)
+        return y.reshape(*shp[:-1], w2_16.shape[0])
+
+    @staticmethod
+    def backward(ctx, dy):
+        x2, w1_16, w2_16, h, z1 = ctx.saved_tensors
+        w1, b1, w2, b2 = ctx.params
+        act, r1, r2, shp = ctx.cfg
+        dy2 = dy.reshape(-1, dy.shape[-1]).contiguous()
+        # fc2 parameter grads
+        db2 = None
+        if b2 is not None and not r2[2]:
+            _, db2 = _bias_act_bwd(dy2, None, None, "none", True)
+        dw2, db2 = _lin_param_grads(w2, b2, dy2, h, r2[2], db2)
+        # fc1 output gradient with the activation backward fused into the dgrad epilogue
+        aux = h if act == "tanh" else z1
+        dz1 = None
+        if act != "none" and GEMM_MODE == "native" and _gemm_shape_ok(dy2, w2_16.shape[1]):
+            dz1 = get_ext().gemm_nn_dact(dy2, w2_16, aux, _ACTS.index(act))
+        db1 = None
+        want_db1 = b1 is not None and not r1[2]
+        if dz1 is None:
+            dh = _dgrad(dy2, w2_16, r2[1])
+            if act != "none" or want_db1:
+                dz1, db1 = _bias_act_bwd(dh, z1, h if act == "tanh" else None, act, want_db1)
+            else:
+                dz1 = dh
+        dx = _dgrad(dz1, w1_16, r1[1]).reshape(shp) if ctx.needs_input_grad[0] else None
+        dw1, db1 = _lin_param_grads(w1, b1, dz1, x2, r1[2], db1)
+        return dx, dw1, db1, dw2, db2, None, None, None, None, None
+
+
+def mlp(x, fc1, fc2):
+    """fc2(act(fc1(x))) for two ``layers.Linear`` modules (fc1 carries the activation)."""
+    if x.dtype == torch.float32 or not native_ok(x, kernel="gemm_nn_dact"):
+        return fc2(fc1(x))
+    dt = x.dtype
+    return _MLPFn.apply(x, fc1.weight, fc1.bias, fc2.weight, fc2.bias, shadow(fc1.weight, dt),
+                        shadow(fc1.bias, dt), shadow(fc2.weight, dt), shadow(fc2.bias, dt), fc1.act)
 
 
 # --------------------------------------------------------------------------- #

@@ -73,6 +73,17 @@ def main():
             ref = (dz @ w).float()
             rec.update(native_dgrad_ms=round(nd, 3), native_dgrad_TF=round(fl / nd / 1e9, 1),
                        native_dgrad_relerr=((dxn.float() - ref).abs().max() / ref.abs().max()).item())
+        if ext is not None and name == "ffn_in":
+            # fused-epilogue variants vs hipBLASLt + separate elementwise pass
+            z = torch.randn(T, N, device=dev).bfloat16()
+            dh = torch.randn(T, K, device=dev).bfloat16()   # grad arriving from ffn_out (width K)
+            w2 = (torch.randn(K, N, device=dev) * 0.02).bfloat16()  # ffn_out weight [768, 3072]
+            rec["gelu_fwd_native_ms"] = round(bench(lambda: ext.gemm_nt(x, w, b, 1)), 3)
+            rec["gelu_fwd_blas_plus_eltwise_ms"] = round(bench(
+                lambda: ext.bias_act_fwd(torch.mm(x, w.t()), b, 1)), 3)
+            rec["dgelu_dgrad_native_ms"] = round(bench(lambda: ext.gemm_nn_dact(dh, w2, z, 1)), 3)
+            rec["dgelu_dgrad_blas_plus_eltwise_ms"] = round(bench(
+                lambda: ext.bias_act_bwd(dh @ w2, z, 1, False)), 3)
         for k in tot:
             tot[k] += rec[f"{k}_ms"]
         print(json.dumps(rec), flush=True)
