@@ -485,6 +485,7 @@ __global__ void __launch_bounds__(256) attn_bwd_q_kernel(
 
 void launch_attn_fwd(const uint16_t* qkv, uint16_t* out, float* lse, int B, int L, int H, float p,
                      bool causal, uint32_t seed, uint32_t offset, hipStream_t s) {
+  if (launch_attn128_fwd(qkv, out, lse, B, L, H, p, causal, seed, offset, s)) return;
   dim3 grid((L + 127) / 128, H, B);
   if (L <= 128) {
     if (causal)
@@ -509,6 +510,7 @@ void launch_attn_bwd(const uint16_t* qkv, const uint16_t* out, const uint16_t* d
                      float* delta, uint16_t* dqkv, float* dq_acc, int B, int L, int H, float p,
                      bool causal, uint32_t seed, uint32_t offset, hipStream_t s) {
   (void)dq_acc;
+  if (launch_attn128_bwd(qkv, out, dout, lse, dqkv, B, L, H, p, causal, seed, offset, s)) return;
   const int64_t rows = (int64_t)B * L * H;
   hipLaunchKernelGGL(attn_delta_kernel, dim3((unsigned)((rows + 255) / 256)), dim3(256), 0, s,
                      (const bf16_t*)dout, (const bf16_t*)out, delta, B, L, H);

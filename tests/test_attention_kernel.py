@@ -27,7 +27,8 @@ def _ref(qkv, H, causal, keep=None, p=0.0):
 
 
 @pytest.mark.parametrize("B,L,H,causal", [(3, 128, 4, False), (2, 64, 2, False), (2, 256, 3, False),
-                                            (2, 128, 2, True), (1, 512, 2, True)])
+                                            (2, 128, 2, True), (1, 512, 2, True),
+                                            (48, 128, 12, False)])  # > #CUs items: persistent loop
 def test_attention_no_dropout(B, L, H, causal):
     torch.manual_seed(0)
     qkv = (torch.randn(B, L, 3 * H * 64, device="cuda") * 0.7).bfloat16()
