@@ -72,8 +72,10 @@ def is_initialized():
 def setup_dist(backend=None, silent=False):
     """Create the process group once; returns True when running distributed.
 
-    Reference: basic_utils/dist_util.py:57-85.  Same fallback semantics (an init
-    failure prints and continues single-process), but RCCL-specific setup:
+    Reference: basic_utils/dist_util.py:57-85.  Same fallback semantics for a
+    single-rank launch (an init failure prints and continues single-process);
+    with WORLD_SIZE > 1 the failure propagates so torchrun can restart the group
+    (the reference would silently train a lone replica).  RCCL-specific setup:
     device bound first, eager communicator init, finite timeout.
     """
     if is_initialized():
@@ -86,8 +88,19 @@ def setup_dist(backend=None, silent=False):
                 backend = os.environ.get("DPA_DIST_BACKEND") or ("nccl" if use_gpu else "gloo")
             # Fail fast on hung collectives rather than wedging the node.
             os.environ.setdefault("TORCH_NCCL_ASYNC_ERROR_HANDLING", "1")
-            kwargs = dict(backend=backend, init_method="env://",
-                          timeout=datetime.timedelta(seconds=DIST_TIMEOUT_S))
+            timeout = datetime.timedelta(seconds=DIST_TIMEOUT_S)
+            kwargs = dict(backend=backend, init_method="env://", timeout=timeout)
+            if os.environ.get("TORCHELASTIC_USE_AGENT_STORE") == "True":
+                # Under torchrun the agent's TCPStore outlives worker restarts; a
+                # restarted group reading the previous attempt's peer addresses
+                # fails to connect.  Namespace the store per restart attempt.
+                attempt = os.environ.get("TORCHELASTIC_RESTART_COUNT", "0")
+                world = int(os.environ["WORLD_SIZE"])
+                store = dist.TCPStore(os.environ["MASTER_ADDR"], int(os.environ["MASTER_PORT"]),
+                                      world, False, timeout=timeout)
+                kwargs = dict(backend=backend, timeout=timeout, rank=int(os.environ["RANK"]),
+                              world_size=world,
+                              store=dist.PrefixStore(f"dpa/attempt_{attempt}", store))
             if use_gpu:
                 torch.cuda.set_device(dev())
                 if backend == "nccl":
@@ -98,8 +111,14 @@ def setup_dist(backend=None, silent=False):
             if os.environ["LOCAL_RANK"] == "0" and not silent:
                 print("<INFO> torch.distributed setup success, using distributed setting..")
             return True
-        except Exception as exc:  # same fallback policy as the reference
-            if not silent:
+        except Exception as exc:
+            if int(os.environ.get("WORLD_SIZE", "1")) > 1:
+                # Launched as one of several ranks: silently continuing alone (the
+                # reference's fallback) would train a divergent single-process
+                # replica and deadlock its peers, e.g. after an elastic restart.
+                # Fail so the torchrun agent restarts the worker group instead.
+                raise
+            if not silent:  # single-rank launch: same fallback as the reference
                 print(f"<INFO> {exc.__class__.__qualname__}: {exc}")
             is_available.cache = False
 

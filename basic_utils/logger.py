@@ -163,31 +163,43 @@ class CSVOutputFormat(KVWriter):
 
 
 class TensorBoardOutputFormat(KVWriter):
-    """Scalars to TensorBoard via ``torch.utils.tensorboard`` (optional dependency)."""
+    """Scalars to TensorBoard: ``torch.utils.tensorboard`` when the ``tensorboard``
+    package is installed, else the built-in event-file writer (``tb_events``)."""
 
     def __init__(self, dir):
         os.makedirs(dir, exist_ok=True)
         self.dir = dir
         self.step = 1
+        self.writer = self.events = None
         try:
             from torch.utils.tensorboard import SummaryWriter
-        except Exception as exc:  # tensorboard not installed
-            raise RuntimeError("tensorboard output needs the `tensorboard` package") from exc
-        self.writer = SummaryWriter(log_dir=dir)
+            self.writer = SummaryWriter(log_dir=dir)
+        except Exception:  # tensorboard not installed
+            from .tb_events import EventFileWriter
+            self.events = EventFileWriter(dir)
 
     def writekvs(self, kvs):
+        scalars = {}
         for k, v in kvs.items():
             try:
-                self.writer.add_scalar(k, float(v), self.step)
+                scalars[k] = float(v)
             except (TypeError, ValueError):
                 pass
-        self.writer.flush()
+        if self.writer is not None:
+            for k, v in scalars.items():
+                self.writer.add_scalar(k, v, self.step)
+            self.writer.flush()
+        else:
+            self.events.add_scalars(scalars, self.step)
         self.step += 1
 
     def close(self):
         if self.writer is not None:
             self.writer.close()
             self.writer = None
+        if self.events is not None:
+            self.events.close()
+            self.events = None
 
 
 def make_output_format(format, ev_dir, log_suffix="", append=False):

@@ -127,7 +127,25 @@ class PerfSettings(S):
         = _(False, "Average logged metrics over ranks at dump time.")
 
 
-class YourSettings(PerfSettings, DiffusionSettings, ModelSettings):
+class RuntimeSettings(S):
+    """Observability, debugging and failure handling."""
+    nan_guard: Choice("off", "skip", "abort") \
+        = _("off", "Non-finite gradient norm: off | skip the optimizer step | abort.")
+    debug_anomaly: bool \
+        = _(False, "torch.autograd.set_detect_anomaly(True).")
+    consistency_check_interval: int \
+        = _(0, "Every N steps verify parameters are identical on all ranks (0 = off).")
+    profile_steps: str \
+        = _("", "torch.profiler window 'start:stop' (chrome trace in the run dir); empty = off.")
+    roctx: bool \
+        = _(False, "Emit roctx ranges (fwd/bwd/optimize/allreduce) for rocprofv3 --marker-trace.")
+    save_rng_state: bool \
+        = _(True, "Write rng_{step}_rank{r}.pt next to each checkpoint and restore it on resume.")
+    tensorboard: bool \
+        = _(False, "Also log scalars to TensorBoard event files (run_dir/tb).")
+
+
+class YourSettings(RuntimeSettings, PerfSettings, DiffusionSettings, ModelSettings):
     """Workload-specific settings (the reference's TODO mixin)."""
 
 
@@ -170,4 +188,4 @@ class TrainSettings(
 
 
 __all__ = ('TrainSettings', 'GeneralSettings', 'DataSettings', 'ModelSettings',
-           'DiffusionSettings', 'PerfSettings', 'YourSettings')
+           'DiffusionSettings', 'PerfSettings', 'RuntimeSettings', 'YourSettings')

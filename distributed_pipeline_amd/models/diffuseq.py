@@ -86,5 +86,20 @@ class TransformerNetModel(nn.Module):
         return self.output_down_proj(h)
 
 
+def _train_flops_per_sample(self, seq_len):
+    """Matmul FLOPs of one training sample (forward + backward = 3x forward for
+    trained weights): encoder Linears 6*P_lin per token, attention 12*L*H per
+    token per layer, the up/down projections, and the tied rounding head: the
+    decoder_nll CE (6*E*V per token) plus the forward-only logged nll (2*E*V)."""
+    cfg, H, E, L = self.cfg, self.hidden_size, self.input_dims, seq_len
+    F_ = cfg["intermediate_size"]
+    p_lin = cfg["num_layers"] * (4 * H * H + 2 * H * F_) + (E * H + H * H) * 2
+    per_tok = 6 * p_lin + 12 * L * H * cfg["num_layers"] + 8 * E * cfg["vocab_size"]
+    return per_tok * L
+
+
+TransformerNetModel.train_flops_per_sample = _train_flops_per_sample
+
+
 def count_params(model):
     return sum(p.numel() for p in model.parameters())

@@ -49,3 +49,17 @@ class GPT2LMModel(nn.Module):
         x = h[:, :-1].reshape(-1, H)
         tgt = labels[:, 1:].reshape(-1)
         return ops.linear_cross_entropy(x, self.wte.weight, None, tgt).view(B, L - 1)
+
+
+def _gpt2_train_flops_per_sample(self, seq_len):
+    """6*P_lin + causal attention (~6*L*H per layer, half of the full 12*L*H) per
+    token, plus the tied LM head (6*H*V), times seq_len."""
+    cfg = self.cfg
+    H, V, n = cfg["hidden_size"], cfg["vocab_size"], cfg["num_layers"]
+    F_ = cfg.get("intermediate_size") or 4 * H
+    per_tok = 6 * n * (4 * H * H + 2 * H * F_) + 6 * seq_len * H * n + 6 * H * V
+    return per_tok * seq_len
+
+
+GPT2LMModel.train_flops_per_sample = _gpt2_train_flops_per_sample
+

@@ -65,7 +65,8 @@ def main(namespace):
     dist_util.barrier()
 
     logger.configure(dir=args.checkpoint_path,
-                     format_strs=["log", "csv"] + (["stdout"] if rank == 0 else []),
+                     format_strs=["log", "csv"] + (["stdout"] if rank == 0 else [])
+                     + (["tensorboard"] if args.tensorboard and rank == 0 else []),
                      append=resuming)
     seed_all(args.seed)
 
@@ -117,7 +118,9 @@ def main(namespace):
         ddp_engine=args.ddp_engine, precision=args.precision, bucket_cap_mb=args.ddp_bucket_cap_mb,
         first_bucket_mb=args.ddp_first_bucket_mb, grad_reduce_dtype=args.grad_reduce_dtype,
         exec_microbatch=args.exec_microbatch, hip_graphs=args.hip_graphs,
-        log_cross_rank_mean=args.log_cross_rank_mean)
+        log_cross_rank_mean=args.log_cross_rank_mean, nan_guard=args.nan_guard,
+        debug_anomaly=args.debug_anomaly, consistency_check_interval=args.consistency_check_interval,
+        profile_steps=args.profile_steps, roctx=args.roctx, save_rng_state=args.save_rng_state)
     if args.model == "gpt2":
         loop = LMTrainLoop(**kwargs)
     else:

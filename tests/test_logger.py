@@ -70,3 +70,18 @@ def test_rank_suffix_from_RANK(tmp_path, monkeypatch):
     assert os.path.exists(tmp_path / "log-rank003.txt")
     monkeypatch.delenv("RANK")
     logger.configure(dir=str(tmp_path), format_strs=[])
+
+
+def test_tensorboard_events_roundtrip(tmp_path):
+    """Built-in event writer: valid TFRecord framing (CRC32C) + decodable scalars."""
+    from basic_utils import tb_events
+    assert tb_events.crc32c(b"123456789") == 0xE3069283  # CRC-32C check value
+    fmt = logger.make_output_format("tensorboard", str(tmp_path))
+    fmt.writekvs({"loss": 1.5, "step": 3, "name": "x"})
+    fmt.writekvs({"loss": 0.25})
+    fmt.close()
+    files = list((tmp_path / "tb").glob("events.out.tfevents.*"))
+    assert len(files) == 1
+    ev = tb_events.read_events(str(files[0]))
+    assert ev[0][0] == 1 and abs(ev[0][1]["loss"] - 1.5) < 1e-6 and ev[0][1]["step"] == 3.0
+    assert ev[1] == (2, {"loss": 0.25})

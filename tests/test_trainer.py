@@ -116,3 +116,72 @@ def test_microbatch_fusion_gives_same_gradients(tmp_path, monkeypatch):
     b.forward_backward(batch)
     torch.testing.assert_close(a.ddp_model.space.grad_flat, b.ddp_model.space.grad_flat,
                                rtol=1e-5, atol=1e-6)
+
+
+def test_throughput_keys_logged(tmp_path):
+    loop = _loop(tmp_path, "native", steps=4, save_interval=100)
+    loop.run_loop()
+    import csv
+    rows = list(csv.DictReader(open(tmp_path / "progress.csv")))
+    keys = set(rows[-1])
+    assert {"steps_per_sec", "samples_per_sec", "tokens_per_sec"} <= keys
+    assert float(rows[-1]["samples_per_sec"]) > 0
+
+
+@pytest.mark.parametrize("engine", ["native", "torch"])
+def test_nan_guard_skip_and_abort(tmp_path, engine):
+    loop = _loop(tmp_path / "s", engine, steps=3, save_interval=100, nan_guard="skip")
+    orig = loop.backward_from_losses
+
+    def poisoned(losses):
+        orig(losses)
+        if loop.step == 1:  # poison the second step's gradients
+            next(loop.model.parameters()).grad.view(-1)[0] = float("nan")
+    loop.backward_from_losses = poisoned
+    before = {}
+
+    def snap():
+        before.update({k: v.clone() for k, v in loop.model.state_dict().items()})
+    orig_opt = loop.optimize
+
+    def opt_spy():
+        if loop.step == 1:
+            snap()
+        orig_opt()
+        if loop.step == 1:  # skipped: parameters untouched, no NaN anywhere
+            for k, v in loop.model.state_dict().items():
+                assert torch.equal(v, before[k]), k
+    loop.optimize = opt_spy
+    loop.run_loop()
+    assert all(torch.isfinite(p).all() for p in loop.model.parameters())
+    loop2 = _loop(tmp_path / "a", engine, steps=3, save_interval=100, nan_guard="abort")
+    orig2 = loop2.backward_from_losses
+
+    def poisoned2(losses):
+        orig2(losses)
+        next(loop2.model.parameters()).grad.view(-1)[0] = float("inf")
+    loop2.backward_from_losses = poisoned2
+    with pytest.raises(FloatingPointError):
+        loop2.run_loop()
+
+
+def test_rng_state_sidecar_restores_streams(tmp_path):
+    loop = _loop(tmp_path, "native", steps=2, save_interval=100)
+    loop.run_loop()  # final save at step 2 -> rng_000002_rank0.pt
+    assert "rng_000002_rank0.pt" in os.listdir(tmp_path)
+    expect = torch.rand(4)
+    loop2 = _loop(tmp_path, "native", steps=3, save_interval=100, seed=123)  # different seed
+    assert loop2.resume_step == 2
+    torch.testing.assert_close(torch.rand(4), expect)
+
+
+def test_fault_injection_marker(tmp_path, monkeypatch):
+    """DP_FAULT_AT_STEP exits once per checkpoint dir (marker makes the restart proceed)."""
+    from utils import trainer as tr
+    monkeypatch.setenv("DP_FAULT_AT_STEP", "1")
+    exits = []
+    monkeypatch.setattr(tr.os, "_exit", lambda code: exits.append(code))
+    tr._maybe_inject_fault(0, str(tmp_path))
+    tr._maybe_inject_fault(1, str(tmp_path))
+    tr._maybe_inject_fault(1, str(tmp_path))
+    assert exits == [17]

@@ -26,6 +26,8 @@ import contextlib
 import copy
 import math
 import os
+import random
+import time
 
 import torch
 from torch.optim import AdamW
@@ -125,6 +127,15 @@ class TrainLoop:
             exec_microbatch=0,
             hip_graphs=False,
             log_cross_rank_mean=False,
+            # ---- observability / robustness (all optional) ----
+            nan_guard="off",
+            debug_anomaly=False,
+            consistency_check_interval=0,
+            profile_steps="",
+            roctx=False,
+            save_rng_state=True,
+            flops_per_sample=None,
+            peak_tflops=None,
     ):
         self.model = model
         self.data = data
@@ -164,6 +175,19 @@ class TrainLoop:
         if log_cross_rank_mean:
             logger.set_comm("dist")
 
+        self.nan_guard = nan_guard
+        self.consistency_check_interval = int(consistency_check_interval or 0)
+        self.roctx = bool(roctx) and torch.cuda.is_available()
+        self.save_rng_state = bool(save_rng_state)
+        self.flops_per_sample = flops_per_sample
+        self.peak_tflops = float(peak_tflops or os.environ.get("DPA_PEAK_TFLOPS", 2500.0))
+        self._profile_window = _parse_window(profile_steps)
+        self._profiler = None
+        self._tp = None  # (wall time, step) at the start of the throughput window
+        self._tokens_per_sample = None
+        if debug_anomaly:
+            torch.autograd.set_detect_anomaly(True)
+
         self._load_and_sync_parameters()
         self.device = next(self.model.parameters()).device
 
@@ -171,7 +195,8 @@ class TrainLoop:
             self._build_native(bucket_cap_mb, first_bucket_mb, grad_reduce_dtype)
         else:
             self._build_torch()
-        self._step_timer = None
+        if self.resume_step:
+            self._load_rng()
 
     def _build_native(self, bucket_cap_mb, first_bucket_mb, grad_reduce_dtype):
         from distributed_pipeline_amd.parallel.ddp import DDPEngine
@@ -267,8 +292,12 @@ class TrainLoop:
     def run_loop(self):
         while (not self.learning_steps
                or self.step + self.resume_step < self.learning_steps):
+            _maybe_inject_fault(self.step + self.resume_step, self.checkpoint_path)
+            self._profiler_tick()
             batch = next(self.data)
             self.run_step(batch)
+            if self.consistency_check_interval and self.step % self.consistency_check_interval == 0:
+                self.check_replica_consistency()
             if self.step % self.log_interval == 0:
                 logger.dumpkvs()
             if self.eval_data is not None and self.step % self.eval_interval == 0:
@@ -284,11 +313,65 @@ class TrainLoop:
             self.step += 1
         if (self.step - 1) % self.save_interval != 0:
             self.save()
+        self._profiler_stop()
 
     def run_step(self, batch):
-        self.forward_backward(batch)
-        self.optimize()
+        with self._range("forward_backward"):
+            self.forward_backward(batch)
+        with self._range("optimize"):
+            self.optimize()
         self.log_step()
+
+    # ------------------------------------------------------- observability
+    def _range(self, name):
+        """roctx range (``torch.cuda.nvtx`` is roctx on ROCm) when enabled."""
+        if not self.roctx:
+            return contextlib.nullcontext()
+        return torch.cuda.nvtx.range(name)
+
+    def _profiler_tick(self):
+        if self._profile_window is None:
+            return
+        start, stop = self._profile_window
+        step = self.step + self.resume_step
+        if step == start and self._profiler is None:
+            acts = [torch.profiler.ProfilerActivity.CPU]
+            if torch.cuda.is_available():
+                acts.append(torch.profiler.ProfilerActivity.CUDA)
+            self._profiler = torch.profiler.profile(activities=acts, record_shapes=False)
+            self._profiler.__enter__()
+        elif step == stop:
+            self._profiler_stop()
+
+    def _profiler_stop(self):
+        if self._profiler is None:
+            return
+        if torch.cuda.is_available():
+            torch.cuda.synchronize()
+        self._profiler.__exit__(None, None, None)
+        path = os.path.join(logger.get_dir() or ".", f"trace_rank{dist_util.get_rank()}.json")
+        self._profiler.export_chrome_trace(path)
+        logger.log(f"torch.profiler trace written to {path}")
+        self._profiler = None
+
+    def check_replica_consistency(self):
+        """Debug: parameters must be bit-identical on every rank."""
+        if not dist_util.is_initialized():
+            return
+        import torch.distributed as dist
+        params = [p.detach().reshape(-1) for p in self.model.parameters()]
+        flat = torch.cat(params).double()
+        sig = torch.stack([flat.sum(), (flat * flat).sum(),
+                           (flat * torch.arange(flat.numel(), device=flat.device, dtype=torch.float64)
+                            .remainder_(977)).sum()])
+        dev = dist_util.dev() if dist.get_backend() == "nccl" else torch.device("cpu")
+        sig = sig.to(dev)
+        mx, mn = sig.clone(), sig.clone()
+        dist.all_reduce(mx, op=dist.ReduceOp.MAX)
+        dist.all_reduce(mn, op=dist.ReduceOp.MIN)
+        if not torch.equal(mx, mn):
+            raise RuntimeError(f"replica divergence at step {self.step + self.resume_step}: "
+                               f"param signatures differ across ranks ({mn.tolist()} vs {mx.tolist()})")
 
     def _zero_grad(self):
         if self.engine_kind == "native":
@@ -326,10 +409,15 @@ class TrainLoop:
 
     def forward_backward(self, batch):
         self._zero_grad()
+        if self._tokens_per_sample is None and isinstance(batch, dict):
+            v = next(iter(batch.values()))
+            self._tokens_per_sample = int(v.shape[1]) if torch.is_tensor(v) and v.dim() > 1 else 1
         for i in range(0, self.get_batch_length(batch), self.exec_microbatch):
-            losses = self._common_forward(batch, i, self.exec_microbatch)
+            with self._range("forward"):
+                losses = self._common_forward(batch, i, self.exec_microbatch)
             self.log_loss_dict(mode="train", losses=losses)
-            self.backward_from_losses(losses)
+            with self._range("backward"):
+                self.backward_from_losses(losses)
 
     # ----------------------------------------------------------------- optimize
     def optimize(self):
@@ -337,7 +425,9 @@ class TrainLoop:
             return self._optimize_native()
         if self.gradient_clipping > 0:
             self.grad_clip()
-        self._log_grad_norm()
+        norm = self._log_grad_norm()
+        if norm is not None and not self._grad_finite_or_skip(norm):
+            return
         self._anneal_lr()
         self.opt.step()
         for rate, params in zip(self.ema_rate, self.ema_params):
@@ -345,13 +435,31 @@ class TrainLoop:
 
     def _optimize_native(self):
         eng = self.ddp_model
-        eng.finalize()
+        with self._range("allreduce_wait"):
+            eng.finalize()
         scale = 1.0 / eng.world_size
         max_norm = self.gradient_clipping if self.gradient_clipping > 0 else 0.0
         norm = self.opt.compute_grad_norm(grad_scale=scale, max_norm=max_norm)
+        if not self._grad_finite_or_skip(norm[0]):
+            return
         logger.logkv_mean("grad_norm", norm[2] if max_norm > 0 else norm[0])
         self._anneal_lr()
         self.opt.step(grad_scale=scale, clip=norm if max_norm > 0 else None)
+
+    def _grad_finite_or_skip(self, norm):
+        """Non-finite gradient guard: ``nan_guard`` = off | skip | abort.
+        The gradient norm is already reduced across ranks, so every rank takes the
+        same decision.  One host sync per step when enabled."""
+        if self.nan_guard == "off":
+            return True
+        if bool(torch.isfinite(norm).item()):
+            return True
+        step = self.step + self.resume_step
+        if self.nan_guard == "abort":
+            raise FloatingPointError(f"non-finite gradient norm at step {step}")
+        logger.log(f"non-finite gradient norm at step {step}: skipping the optimizer step")
+        logger.logkv_mean("skipped_steps", 1.0)
+        return False
 
     def grad_clip(self):
         max_grad_norm = self.gradient_clipping
@@ -374,10 +482,30 @@ class TrainLoop:
             return
         sq = torch.stack([g.float().pow(2).sum() for g in grads]).sum()
         logger.logkv_mean("grad_norm", sq.sqrt())
+        return sq.sqrt()
 
     def log_step(self):
         logger.logkv("step", self.step + self.resume_step)
         logger.logkv("samples", (self.step + self.resume_step + 1) * self.global_batch)
+        # Throughput over the log window (host clock; the per-window dumpkvs host
+        # sync keeps it aligned with the device).  SURVEY T-11 / 5.1.
+        now = time.perf_counter()
+        if self._tp is None:
+            self._tp = (now, self.step)
+        elif self.step % self.log_interval == 0 and self.step > self._tp[1]:
+            t0, s0 = self._tp
+            sps = (self.step - s0) / max(now - t0, 1e-9)
+            logger.logkv("steps_per_sec", sps)
+            logger.logkv("samples_per_sec", sps * self.global_batch)
+            if self._tokens_per_sample:
+                logger.logkv("tokens_per_sec", sps * self.global_batch * self._tokens_per_sample)
+            fps = self.flops_per_sample
+            if fps is None and hasattr(self, "model_flops_per_sample"):
+                fps = self.model_flops_per_sample()
+            if fps:
+                achieved = sps * self.global_batch * fps
+                logger.logkv("mfu", achieved / (self.peak_tflops * 1e12 * dist_util.get_world_size()))
+            self._tp = (now, self.step)
 
     # -------------------------------------------------------------- checkpoints
     def save(self):
@@ -385,7 +513,43 @@ class TrainLoop:
         for r, p in zip(self.ema_rate, self.ema_params):
             self._save_checkpoint(r, p)
         self._save_opt()
+        if self.save_rng_state:
+            self._save_rng()
         dist_util.barrier()
+
+    # RNG sidecar: rng_{N}_rank{r}.pt next to the reference layout,
+    # so a resumed run continues the same random streams.
+    def _rng_path(self, step):
+        return _join(self.checkpoint_path, f"rng_{step:06d}_rank{dist_util.get_rank()}.pt")
+
+    def _save_rng(self):
+        from distributed_pipeline_amd.ops.nn import RNG
+        import numpy as np
+        st = np.random.get_state()
+        state = {"torch": torch.get_rng_state(),
+                 "numpy": [st[0], torch.from_numpy(st[1].astype("int64")), int(st[2]), int(st[3]),
+                           float(st[4])],
+                 "python": _py_rng_to_plain(random.getstate()),
+                 "kernel_rng": [int(RNG.seed), int(RNG.counter)]}
+        if torch.cuda.is_available():
+            state["cuda"] = torch.cuda.get_rng_state()
+        _atomic_torch_save(state, self._rng_path(self.step + self.resume_step))
+
+    def _load_rng(self):
+        path = self._rng_path(self.resume_step)
+        if not self.save_rng_state or not _exists(path):
+            return
+        import numpy as np
+        from distributed_pipeline_amd.ops.nn import RNG
+        state = dist_util.load_state_dict(path, map_location="cpu")
+        torch.set_rng_state(state["torch"])
+        n = state["numpy"]
+        np.random.set_state((n[0], n[1].numpy().astype("uint32"), n[2], n[3], n[4]))
+        random.setstate(_py_rng_from_plain(state["python"]))
+        RNG.seed, RNG.counter = state["kernel_rng"]
+        if "cuda" in state and torch.cuda.is_available():
+            torch.cuda.set_rng_state(state["cuda"])
+        logger.log(f"restored RNG state from {path}")
 
     def _save_checkpoint(self, rate, params):
         state_dict = self._master_params_to_state_dict(params)
@@ -457,6 +621,41 @@ class TrainLoop:
     __call__ = run_loop
 
 
+def _parse_window(spec):
+    """``"a:b"`` -> (a, b) profiler step window, else None."""
+    if not spec:
+        return None
+    a, b = str(spec).split(":")
+    return int(a), int(b)
+
+
+def _maybe_inject_fault(step, ckpt_dir):
+    """Test-only fault injection: ``DP_FAULT_AT_STEP=N`` makes rank
+    ``DP_FAULT_RANK`` (default 0) exit abruptly when it reaches step N, once per
+    checkpoint directory (a marker file keeps the restarted run going), to
+    exercise torchrun ``--max_restarts`` + auto-resume."""
+    at = os.environ.get("DP_FAULT_AT_STEP")
+    if at is None or step != int(at):
+        return
+    if dist_util.get_rank() != int(os.environ.get("DP_FAULT_RANK", "0")):
+        return
+    marker = os.path.join(ckpt_dir or ".", f".fault_injected_{step}")
+    if os.path.exists(marker):
+        return
+    with open(marker, "w") as f:
+        f.write("1")
+    logger.log(f"DP_FAULT_AT_STEP={step}: injecting a crash on rank {dist_util.get_rank()}")
+    os._exit(17)
+
+
+def _py_rng_to_plain(st):
+    return [st[0], list(st[1]), st[2]]
+
+
+def _py_rng_from_plain(st):
+    return (st[0], tuple(st[1]), st[2])
+
+
 def _to_cpu(obj):
     if torch.is_tensor(obj):
         return obj.detach().cpu()
@@ -514,6 +713,11 @@ class DiffusionTrainLoop(TrainLoop):
         if hasattr(self.schedule_sampler, "update_with_local_losses") and torch.is_grad_enabled():
             self.schedule_sampler.update_with_local_losses(t, losses["loss"].detach())
         return losses
+
+    def model_flops_per_sample(self):
+        """Model FLOPs per training sample (fwd+bwd, for the logged MFU)."""
+        fn = getattr(self.model, "train_flops_per_sample", None)
+        return fn(self._tokens_per_sample) if fn and self._tokens_per_sample else None
 
     def backward_from_losses(self, losses):
         w = self._last_weights
@@ -581,6 +785,10 @@ class LMTrainLoop(TrainLoop):
     def compute_losses(self, micro_batch):
         per_tok = self.ddp_model(micro_batch["input_ids"], labels=micro_batch["labels"])
         return {"loss": per_tok.mean(-1)}
+
+    def model_flops_per_sample(self):
+        fn = getattr(self.model, "train_flops_per_sample", None)
+        return fn(self._tokens_per_sample) if fn and self._tokens_per_sample else None
 
     def backward_from_losses(self, losses):
         (losses["loss"].mean() * self.loss_scale).backward()
