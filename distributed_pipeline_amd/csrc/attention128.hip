@@ -3,8 +3,9 @@
 // through LDS with global_load_lds prefetch, so the HBM traffic of item i+1
 // overlaps the matrix-core work of item i.
 //
-// Both kernels: grid = #CUs, 256 threads (4 waves), items (b, h) strided over
-// the grid, two LDS buffers (ping-pong).  All LDS accesses are inline asm so
+// Both kernels: grid = 2 x #CUs persistent workgroups of 256 threads (4 waves),
+// two resident per CU so every SIMD holds one wave of each and hides the other's
+// LDS / MFMA / load latencies; items (b, h) strided over the grid.  All LDS accesses are inline asm so
 // hipcc never drains the in-flight LDS-DMA with a vmcnt(0) before them.
 //
 // Forward (per item): S^T = K Q^T with the keys of a 32-query block in the
@@ -93,6 +94,18 @@ __device__ __forceinline__ void lgkm0() {
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
   __builtin_amdgcn_sched_barrier(0);
 }
+// s_waitcnt vmcnt(n) for the counts the pipelines use (immediate operand).
+__device__ __forceinline__ void wait_vm(int n) {
+  switch (n) {
+    case 5: asm volatile("s_waitcnt vmcnt(5)" ::: "memory"); break;
+    case 10: asm volatile("s_waitcnt vmcnt(10)" ::: "memory"); break;
+    case 12: asm volatile("s_waitcnt vmcnt(12)" ::: "memory"); break;
+    case 17: asm volatile("s_waitcnt vmcnt(17)" ::: "memory"); break;
+    case 22: asm volatile("s_waitcnt vmcnt(22)" ::: "memory"); break;
+    default: asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); break;
+  }
+}
+
 __device__ __forceinline__ void barrier() {
   asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
   __builtin_amdgcn_sched_barrier(0);
@@ -154,45 +167,52 @@ __device__ __forceinline__ float bfhi(uint32_t w) { return __uint_as_float(w & 0
 // ============================================================================
 // forward
 // ============================================================================
-__global__ void __launch_bounds__(256) attn128_fwd_kernel(const bf16_t* __restrict__ qkv,
-                                                         bf16_t* __restrict__ out,
-                                                         float* __restrict__ lse, int B, int H,
-                                                         float p, uint32_t seed, uint32_t offset) {
-  // buffer b at b * 48K: Q, K, V images
-  __shared__ __attribute__((aligned(1024))) char smem[2 * 3 * IMG];
-  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, hf = lane >> 5;
+__global__ void __launch_bounds__(256, 2) attn128_fwd_kernel(const bf16_t* __restrict__ qkv,
+                                                            bf16_t* __restrict__ out,
+                                                            float* __restrict__ lse, int B, int H,
+                                                            float p, uint32_t seed, uint32_t offset) {
+  // two workgroups per CU (8 waves: one wave of each on every SIMD hides the
+  // other's latencies); per workgroup 2 stages at s * 32K: K, V images.  Q goes
+  // straight to fragment registers (each wave needs only its 32 queries).
+  __shared__ __attribute__((aligned(1024))) char smem[2 * 2 * IMG];
+  const int w = threadIdx.x >> 6;
   const int nitems = B * H;
   const int64_t ld = 3LL * H * HD, ldo = (int64_t)H * HD;
   const uint32_t sb = lds_u32(smem);
 
-  auto issue = [&](int item, int buf) {
+  bf16x8 qpf[4];
+  const int tid = threadIdx.x, lane = tid & 63, hf = lane >> 5;
+  auto issue = [&](int item, int stg) {
     const int b = item / H, hd = item - b * H;
     const bf16_t* qb = qkv + (int64_t)b * L * ld + (int64_t)hd * HD;
-    char* base = smem + buf * 3 * IMG;
-    dma_img(base, qb, ld, w, lane);
-    dma_img(base + IMG, qb + (int64_t)H * HD, ld, w, lane);
-    dma_img(base + 2 * IMG, qb + 2LL * H * HD, ld, w, lane);
+    char* base = smem + stg * 2 * IMG;
+    dma_img(base, qb + (int64_t)H * HD, ld, w, lane);
+    dma_img(base + IMG, qb + 2LL * H * HD, ld, w, lane);
+    const bf16_t* qrow = qb + (int64_t)(w * 32 + (lane & 31)) * ld;
+#pragma unroll
+    for (int s = 0; s < 4; ++s) qpf[s] = ld_frag(qrow + 16 * s + 8 * hf);
   };
 
+  const int G = gridDim.x;
   int item = blockIdx.x;
   if (item < nitems) issue(item, 0);
-  for (int k = 0; item < nitems; ++k, item += gridDim.x) {
+  for (int k = 0; item < nitems; ++k, item += G) {
     const int cur = k & 1;
-    // this item's DMA landed; the previous item's 5 stores (lse + 4 O rows) may
-    // still be in flight (issued last, retired in order)
+    // This item's K/V DMA and Q loads landed; only the previous item's 5 stores
+    // (lse + 4 O rows) were issued after them (in-order retire).
     if (k == 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     else asm volatile("s_waitcnt vmcnt(5)" ::: "memory");
     barrier();
-    if (item + (int)gridDim.x < nitems) issue(item + gridDim.x, cur ^ 1);
-    const uint32_t qi = sb + cur * 3 * IMG, ki = qi + IMG, vi = qi + 2 * IMG;
+    bf16x8 qf[4];
+#pragma unroll
+    for (int s = 0; s < 4; ++s) qf[s] = qpf[s];
+    if (item + G < nitems) issue(item + G, cur ^ 1);
+    const uint32_t ki = sb + cur * 2 * IMG, vi = ki + IMG;
     const int b = item / H, hd = item - b * H;
     const DropCfg dc = make_drop(p, seed, offset, (uint32_t)item);
     const int q = w * 32 + (lane & 31);
 
     // S^T (keys in registers, query on the lane)
-    bf16x8 qf[4];
-#pragma unroll
-    for (int s = 0; s < 4; ++s) qf[s] = frag_r(qi, w * 32, s, lane);
     f32x16 acc[4];
 #pragma unroll
     for (int t = 0; t < 4; ++t) {
@@ -247,8 +267,9 @@ __global__ void __launch_bounds__(256) attn128_fwd_kernel(const bf16_t* __restri
         for (int dt = 0; dt < 2; ++dt) o[dt] = mfma32(af, vf[dt], o[dt]);
       }
     }
-    // stage O (rows = queries) in the Q image (dead: every wave passed its reads)
+    // stage O (rows = queries) in the K image (dead: every wave passed its S^T)
     barrier();
+    const uint32_t qi = ki;
 #pragma unroll
     for (int dt = 0; dt < 2; ++dt)
 #pragma unroll
@@ -271,53 +292,221 @@ __global__ void __launch_bounds__(256) attn128_fwd_kernel(const bf16_t* __restri
 // ============================================================================
 // backward
 // ============================================================================
-// LDS: buffers b = 0, 1 at b * 64K: Q, K, V, dO images; at 128K: lse2[128], delta[128]
-constexpr int BWD_BUF = 4 * IMG;
-constexpr int BWD_STATS = 2 * BWD_BUF;
+// ---- immediate-offset LDS access (per-lane base VGPR + compile-time offset) --
+template <int IMM>
+__device__ __forceinline__ bf16x8 rd128o(uint32_t a) {
+  bf16x8 f;
+  asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(f) : "v"(a), "i"(IMM));
+  return f;
+}
+template <int IMM>
+__device__ __forceinline__ f32x4 rdf4o(uint32_t a) {
+  f32x4 f;
+  asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(f) : "v"(a), "i"(IMM));
+  return f;
+}
+template <int IMM>
+__device__ __forceinline__ bf16x4 rdtro(uint32_t a) {
+  bf16x4 f;
+  asm volatile("ds_read_b64_tr_b16 %0, %1 offset:%2" : "=v"(f) : "v"(a), "i"(IMM));
+  return f;
+}
+template <int IMM>
+__device__ __forceinline__ void wr16o(uint32_t a, uint16_t v) {
+  asm volatile("ds_write_b16 %0, %1 offset:%2" ::"v"(a), "v"((uint32_t)v), "i"(IMM) : "memory");
+}
 
-__global__ void __launch_bounds__(256) attn128_bwd_kernel(
+// LDS (one stage per workgroup, two workgroups per CU so that one's loads
+// overlap the other's math): Q, dO, K images; then lse2[128], delta[128].  V never
+// goes through LDS: each wave needs only its 32 keys' V rows (fragment registers).
+// Every fragment read is one of a handful of per-lane base addresses plus an
+// immediate: the XOR swizzles are chosen so the tile offsets never interact
+// with the lane bits (derivations at the bases below).
+constexpr int BWD_BUF = 3 * IMG;
+constexpr int BWD_STATS = BWD_BUF;
+constexpr int I_Q = 0, I_DO = IMG, I_K = 2 * IMG;
+
+struct BwdBases {
+  uint32_t rb[4];     // row-form fragment, k-step s: row (lane & 31), chunk 2s + h
+  uint32_t tp;        // transposed (permuted k) fragment of a Q / dO image, r0 = 0, dt = 0
+  uint32_t tn1[2], tn2[2];  // transposed (natural k) fragment of the K image, per dt
+  uint32_t ts1, ts2;  // transposed (natural k) fragment of the dS^T image, this wave's queries
+  uint32_t stat;      // lse2 / delta rows 4h..: + 4 * (32t + 8g)
+  uint32_t ost;       // unswizzled output staging: row 32w + 4h, col lane & 31
+  uint32_t cpy;       // copy-out: row tid >> 3, chunk tid & 7 (unswizzled)
+};
+
+__device__ __forceinline__ BwdBases bwd_bases(int lane, int w, int tid) {
+  BwdBases B;
+  const int h = lane >> 5, g = lane >> 4, li = lane & 15, q = li >> 2, p = li & 3;
+  const int cp = 2 * (g & 1) + (p >> 1);  // chunk within a 32-column block
+  const int e = (p & 1) * 8;
+  const int r = lane & 31, sw_r = (r >> 1) & 7;
+#pragma unroll
+  for (int s = 0; s < 4; ++s) B.rb[s] = (uint32_t)(r * 128 + (((2 * s + h) ^ sw_r) << 4));
+  // frag_tp rows r0 + 4h + q (+8): swizzle (2h + q/2) for r0 % 16 == 0; dt -> +64 /
+  // second read +1024 + (1 - dt) * 64
+  B.tp = (uint32_t)((4 * h + q) * 128 + ((cp ^ ((2 * h + (q >> 1)) & 7)) << 4) + e);
+  // frag_tn (K) rows r0 + 8h + q and +4: swizzle (4h + q/2) and (4h + 2 + q/2)
+#pragma unroll
+  for (int dt = 0; dt < 2; ++dt) {
+    B.tn1[dt] = (uint32_t)((8 * h + q) * 128 + (((4 * dt + cp) ^ ((4 * h + (q >> 1)) & 7)) << 4) + e);
+    B.tn2[dt] = (uint32_t)((8 * h + q + 4) * 128 + (((4 * dt + cp) ^ ((4 * h + 2 + (q >> 1)) & 7)) << 4) + e);
+  }
+  // dS^T image (256-B rows, XOR ((row&3)<<2)|((row>>2)&3)), rows r0 + 8h + q (+4),
+  // columns 32w + 16(g&1) + 4p
+  B.ts1 = (uint32_t)((8 * h + q) * 256 + (((4 * w + cp) ^ ((q << 2) | (2 * h))) << 4) + e);
+  B.ts2 = (uint32_t)((8 * h + q + 4) * 256 + (((4 * w + cp) ^ ((q << 2) | (2 * h + 1))) << 4) + e);
+  B.stat = (uint32_t)(BWD_STATS + 16 * h);
+  B.ost = (uint32_t)((32 * w + 4 * h) * 128 + (lane & 31) * 2);
+  B.cpy = (uint32_t)((tid >> 3) * 128 + (tid & 7) * 16);
+  return B;
+}
+
+// S = Q K^T and dP = dO V^T for query tile T (this wave's 32 keys on the lane)
+template <int T, int S>
+__device__ __forceinline__ void bwd_sdp_step(f32x16& sacc, f32x16& dpacc, uint32_t base,
+                                             const BwdBases& B, uint32_t kbase,
+                                             const bf16x8 (&vf)[4]) {
+  const bf16x8 qf = rd128o<I_Q + T * 32 * 128>(base + B.rb[S]);
+  const bf16x8 df = rd128o<I_DO + T * 32 * 128>(base + B.rb[S]);
+  const bf16x8 kf = rd128o<I_K>(kbase + B.rb[S]);  // this wave's keys (re-read: VGPR budget)
+  lgkm0();
+  sacc = mfma32(qf, kf, sacc);
+  dpacc = mfma32(df, vf[S], dpacc);
+}
+
+// dV += dropout(P)^T dO and dK += dS^T Q for k-step S of tile T, output columns DT
+template <int T, int S, int DT>
+__device__ __forceinline__ void bwd_dkv_step(f32x16 (&dv)[2], f32x16 (&dk)[2], const bf16x8& pf,
+                                             const bf16x8& sf, uint32_t base, const BwdBases& B) {
+  constexpr int R0 = (T * 32 + 16 * S) * 128;
+  const bf16x8 tdo = cat44(rdtro<I_DO + R0 + DT * 64>(base + B.tp),
+                           rdtro<I_DO + R0 + 1024 + (1 - DT) * 64>(base + B.tp));
+  const bf16x8 tq = cat44(rdtro<I_Q + R0 + DT * 64>(base + B.tp),
+                          rdtro<I_Q + R0 + 1024 + (1 - DT) * 64>(base + B.tp));
+  lgkm0();
+  dv[DT] = mfma32(pf, tdo, dv[DT]);
+  dk[DT] = mfma32(sf, tq, dk[DT]);
+}
+
+template <int T, int G>
+__device__ __forceinline__ void bwd_pds(f32x16& sacc, f32x16& dpacc, uint32_t base,
+                                        const BwdBases& B, const DropCfg& dc, int key, int hf) {
+  const f32x4 lv = rdf4o<T * 128 + G * 32>(base + B.stat);
+  const f32x4 dl = rdf4o<T * 128 + G * 32 + 512>(base + B.stat);
+  lgkm0();
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    const int i = 4 * G + r;
+    const float pr = exp2f(sacc[i] * ATT_C - lv[r]);
+    float pd = pr, dpd = dpacc[i];
+    if (dc.on) {
+      const bool kp = keep_bit(dc, T * 32 + 8 * G + 4 * hf + r, key);
+      pd = kp ? pr * dc.scale : 0.f;
+      dpd = kp ? dpd * dc.scale : 0.f;
+    }
+    sacc[i] = pd;
+    dpacc[i] = pr * (dpd - dl[r]);
+  }
+}
+
+template <int T>
+__device__ __forceinline__ void bwd_tile(f32x16 (&dv)[2], f32x16 (&dk)[2], uint4 (&dsb)[2],
+                                         uint32_t base, const BwdBases& B, uint32_t kbase,
+                                         const bf16x8 (&vf)[4], const DropCfg& dc, int key, int hf) {
+  f32x16 sacc = zero16(), dpacc = zero16();
+  bwd_sdp_step<T, 0>(sacc, dpacc, base, B, kbase, vf);
+  bwd_sdp_step<T, 1>(sacc, dpacc, base, B, kbase, vf);
+  bwd_sdp_step<T, 2>(sacc, dpacc, base, B, kbase, vf);
+  bwd_sdp_step<T, 3>(sacc, dpacc, base, B, kbase, vf);
+  // P, dS on this lane's query rows 32T + 8g + 4h + r (statistics read per group g)
+  bwd_pds<T, 0>(sacc, dpacc, base, B, dc, key, hf);
+  bwd_pds<T, 1>(sacc, dpacc, base, B, dc, key, hf);
+  bwd_pds<T, 2>(sacc, dpacc, base, B, dc, key, hf);
+  bwd_pds<T, 3>(sacc, dpacc, base, B, dc, key, hf);
+  {
+    const bf16x8 pf = acc_to_frag(sacc, 0), sf = acc_to_frag(dpacc, 0);
+    dsb[0] = __builtin_bit_cast(uint4, sf);
+    bwd_dkv_step<T, 0, 0>(dv, dk, pf, sf, base, B);
+    bwd_dkv_step<T, 0, 1>(dv, dk, pf, sf, base, B);
+  }
+  {
+    const bf16x8 pf = acc_to_frag(sacc, 1), sf = acc_to_frag(dpacc, 1);
+    dsb[1] = __builtin_bit_cast(uint4, sf);
+    bwd_dkv_step<T, 1, 0>(dv, dk, pf, sf, base, B);
+    bwd_dkv_step<T, 1, 1>(dv, dk, pf, sf, base, B);
+  }
+}
+
+template <int KS>
+__device__ __forceinline__ void bwd_dq_step(f32x16 (&dq)[2], uint32_t base, const BwdBases& B) {
+  const bf16x8 af = cat44(rdtro<KS * 16 * 256>(base + B.ts1), rdtro<KS * 16 * 256>(base + B.ts2));
+  const bf16x8 b0 = cat44(rdtro<I_K + KS * 16 * 128>(base + B.tn1[0]),
+                          rdtro<I_K + KS * 16 * 128>(base + B.tn2[0]));
+  const bf16x8 b1 = cat44(rdtro<I_K + KS * 16 * 128>(base + B.tn1[1]),
+                          rdtro<I_K + KS * 16 * 128>(base + B.tn2[1]));
+  lgkm0();
+  dq[0] = mfma32(af, b0, dq[0]);
+  dq[1] = mfma32(af, b1, dq[1]);
+}
+
+template <int X, int DT>
+__device__ __forceinline__ void bwd_stage_out(const f32x16& acc, float scale, uint32_t a) {
+#pragma unroll
+  for (int i = 0; i < 16; ++i) {
+    // row 32w + 4h + (i&3) + 8(i>>2), column DT*32 + (lane&31): all but the lane part immediate
+    switch (i) {
+#define DPA_ST(I) case I: wr16o<X * IMG + ((I & 3) + 8 * (I >> 2)) * 128 + DT * 64>(a, f2bf(acc[I] * scale)); break;
+      DPA_ST(0) DPA_ST(1) DPA_ST(2) DPA_ST(3) DPA_ST(4) DPA_ST(5) DPA_ST(6) DPA_ST(7)
+      DPA_ST(8) DPA_ST(9) DPA_ST(10) DPA_ST(11) DPA_ST(12) DPA_ST(13) DPA_ST(14) DPA_ST(15)
+#undef DPA_ST
+    }
+  }
+}
+
+__global__ void __launch_bounds__(256, 2) attn128_bwd_kernel(
     const bf16_t* __restrict__ qkv, const bf16_t* __restrict__ out, const bf16_t* __restrict__ dout,
     const float* __restrict__ lse, bf16_t* __restrict__ dqkv, int B, int H, float p, uint32_t seed,
     uint32_t offset) {
   __shared__ __attribute__((aligned(1024))) char smem[BWD_STATS + 2 * L * 4];
-  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, hf = lane >> 5;
   const int nitems = B * H;
   const int64_t ld = 3LL * H * HD, ldo = (int64_t)H * HD;
   const uint32_t sb = lds_u32(smem);
-  const uint32_t s_lse = sb + BWD_STATS, s_del = s_lse + L * 4;
+  const int w = threadIdx.x >> 6;
+  const int kb = w * 32;
 
-  // register prefetch of O (delta) and LSE: thread -> row tid >> 1, half tid & 1
-  uint4 opf[4];
-  float lpf = 0.f;
-  auto prefetch = [&](int item) {
-    const int b = item / H, hd = item - b * H;
-    const bf16_t* orow = out + ((int64_t)b * L + (tid >> 1)) * ldo + (int64_t)hd * HD + (tid & 1) * 32;
-#pragma unroll
-    for (int c = 0; c < 4; ++c) opf[c] = *reinterpret_cast<const uint4*>(orow + c * 8);
-    if (tid < L) lpf = lse[(int64_t)item * L + tid];
-  };
-  auto issue = [&](int item, int buf) {
+  const int G = gridDim.x;
+  for (int item = blockIdx.x; item < nitems; item += G) {
+    // Every lane-dependent quantity is derived from the thread id through an
+    // opaque zero, once per item: otherwise LICM hoists ~150 per-lane constants
+    // (fragment addresses, DMA offsets, per-query hash terms) out of the item
+    // loop, where they overflow the 256-VGPR budget of 2 waves/SIMD and spill.
+    uint32_t z0;
+    asm volatile("v_mov_b32 %0, 0" : "=v"(z0));
+    const int tid = (int)(threadIdx.x + z0), lane = tid & 63, hf = lane >> 5;
+    const int key = kb + (lane & 31);
+    const BwdBases BB = bwd_bases(lane, w, tid);
+    const uint32_t base = sb;
     const int b = item / H, hd = item - b * H;
     const bf16_t* qb = qkv + (int64_t)b * L * ld + (int64_t)hd * HD;
-    char* base = smem + buf * BWD_BUF;
-    dma_img(base, qb, ld, w, lane);
-    dma_img(base + IMG, qb + (int64_t)H * HD, ld, w, lane);
-    dma_img(base + 2 * IMG, qb + 2LL * H * HD, ld, w, lane);
-    dma_img(base + 3 * IMG, dout + (int64_t)b * L * ldo + (int64_t)hd * HD, ldo, w, lane);
-  };
-
-  int item = blockIdx.x;
-  if (item < nitems) {
-    issue(item, 0);
-    prefetch(item);
-  }
-  for (int k = 0; item < nitems; ++k, item += gridDim.x) {
-    const int cur = k & 1;
-    const uint32_t qi = sb + cur * BWD_BUF, ki = qi + IMG, vi = qi + 2 * IMG, di = qi + 3 * IMG;
-    // this item's DMA + O/LSE prefetch landed; the previous item's 12 output
-    // stores (issued last, retired in order) may still be in flight
-    if (k == 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    else asm volatile("s_waitcnt vmcnt(12)" ::: "memory");
+    dma_img(smem + I_Q, qb, ld, w, lane);
+    dma_img(smem + I_DO, dout + (int64_t)b * L * ldo + (int64_t)hd * HD, ldo, w, lane);
+    dma_img(smem + I_K, qb + (int64_t)H * HD, ld, w, lane);
+    uint4 opf[4];
+    {
+      const bf16_t* orow = out + ((int64_t)b * L + (tid >> 1)) * ldo + (int64_t)hd * HD + (tid & 1) * 32;
+#pragma unroll
+      for (int c = 0; c < 4; ++c) opf[c] = *reinterpret_cast<const uint4*>(orow + c * 8);
+    }
+    bf16x8 vf[4];
+    {
+      const bf16_t* vrow = qb + (int64_t)key * ld + 2LL * H * HD;
+#pragma unroll
+      for (int s = 0; s < 4; ++s) vf[s] = ld_frag(vrow + 16 * s + 8 * hf);
+    }
+    const float lpf = tid < L ? lse[(int64_t)item * L + tid] : 0.f;
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     barrier();
     // delta = rowsum(dO * O) and lse (log2 units) -> LDS
     {
@@ -325,7 +514,7 @@ __global__ void __launch_bounds__(256) attn128_bwd_kernel(
       float s = 0.f;
 #pragma unroll
       for (int c = 0; c < 4; ++c) {
-        const bf16x8 dv = rd128(di + off_r(row, half * 4 + c));
+        const bf16x8 dv = rd128(base + I_DO + off_r(row, half * 4 + c));
         lgkm0();
         const uint32_t ow[4] = {opf[c].x, opf[c].y, opf[c].z, opf[c].w};
 #pragma unroll
@@ -335,136 +524,64 @@ __global__ void __launch_bounds__(256) attn128_bwd_kernel(
         }
       }
       s += __shfl_xor(s, 1, 64);
-      if (half == 0) wr_b32(s_del + row * 4, __float_as_uint(s));
-      if (tid < L) wr_b32(s_lse + tid * 4, __float_as_uint(lpf * LOG2Ef));
-    }
-    const int nxt = item + gridDim.x;
-    if (nxt < nitems) {
-      issue(nxt, cur ^ 1);
-      prefetch(nxt);
+      if (half == 0) wr_b32(base + BWD_STATS + 512 + row * 4, __float_as_uint(s));
+      if (tid < L) wr_b32(base + BWD_STATS + tid * 4, __float_as_uint(lpf * LOG2Ef));
     }
     barrier();
 
-    const int b = item / H, hd = item - b * H;
     const DropCfg dc = make_drop(p, seed, offset, (uint32_t)item);
-    const int kb = w * 32, key = kb + (lane & 31);
-    bf16x8 kf[4], vf[4];
-#pragma unroll
-    for (int s = 0; s < 4; ++s) {
-      kf[s] = frag_r(ki, kb, s, lane);
-      vf[s] = frag_r(vi, kb, s, lane);
-    }
-    lgkm0();
+    const uint32_t kbase = base + kb * 128;
     f32x16 dk[2], dv[2];
     uint4 dsb[4][2];  // dS as bf16 (the exact A-operand packing), 8 registers per tile
     dk[0] = zero16(); dk[1] = zero16(); dv[0] = zero16(); dv[1] = zero16();
-#pragma unroll
-    for (int t = 0; t < 4; ++t) {
-      f32x16 sacc = zero16(), dpacc = zero16();
-      {
-        bf16x8 qf[4], df[4];
-#pragma unroll
-        for (int s = 0; s < 4; ++s) {
-          qf[s] = frag_r(qi, t * 32, s, lane);
-          df[s] = frag_r(di, t * 32, s, lane);
-        }
-        lgkm0();
-#pragma unroll
-        for (int s = 0; s < 4; ++s) {
-          sacc = mfma32(qf[s], kf[s], sacc);
-          dpacc = mfma32(df[s], vf[s], dpacc);
-        }
-      }
-      // lse2 / delta of this lane's query rows 32t + 8g + 4h + r (r = 0..3)
-#pragma unroll
-      for (int g = 0; g < 4; ++g) {
-        const f32x4 lv = rd_f4(s_lse + (t * 32 + 8 * g + 4 * hf) * 4);
-        const f32x4 dl = rd_f4(s_del + (t * 32 + 8 * g + 4 * hf) * 4);
-        lgkm0();
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const int i = 4 * g + r;
-          const int qq = t * 32 + 8 * g + 4 * hf + r;
-          const float pr = exp2f(sacc[i] * ATT_C - lv[r]);
-          float pd = pr, dpd = dpacc[i];
-          if (dc.on) {
-            const bool kp = keep_bit(dc, qq, key);
-            pd = kp ? pr * dc.scale : 0.f;
-            dpd = kp ? dpd * dc.scale : 0.f;
-          }
-          sacc[i] = pd;
-          dpacc[i] = pr * (dpd - dl[r]);
-        }
-      }
-#pragma unroll
-      for (int s = 0; s < 2; ++s) {
-        const bf16x8 pf = acc_to_frag(sacc, s);
-        const bf16x8 sf = acc_to_frag(dpacc, s);
-        dsb[t][s] = __builtin_bit_cast(uint4, sf);
-        bf16x8 tdo[2], tq[2];
-#pragma unroll
-        for (int dt = 0; dt < 2; ++dt) {
-          tdo[dt] = frag_tp(di, t * 32 + 16 * s, dt * 32, lane);
-          tq[dt] = frag_tp(qi, t * 32 + 16 * s, dt * 32, lane);
-        }
-        lgkm0();
-#pragma unroll
-        for (int dt = 0; dt < 2; ++dt) {
-          dv[dt] = mfma32(pf, tdo[dt], dv[dt]);
-          dk[dt] = mfma32(sf, tq[dt], dk[dt]);
-        }
-      }
-    }
-    // dS^T -> LDS (over V / dO of this buffer, dead once every wave is here)
+    bwd_tile<0>(dv, dk, dsb[0], base, BB, kbase, vf, dc, key, hf);
+    bwd_tile<1>(dv, dk, dsb[1], base, BB, kbase, vf, dc, key, hf);
+    bwd_tile<2>(dv, dk, dsb[2], base, BB, kbase, vf, dc, key, hf);
+    bwd_tile<3>(dv, dk, dsb[3], base, BB, kbase, vf, dc, key, hf);
+    // dS^T -> LDS over Q + dO (dead once every wave is here): [128 keys][128 q], 256-B rows
     barrier();
-    const uint32_t si = vi;  // [128 keys][128 queries], 256-B rows (32 KiB: V + dO)
+    {
+      const int fk = ((key & 3) << 2) | ((key >> 2) & 3);
+      const uint32_t rowa = base + key * 256 + 8 * hf;
 #pragma unroll
-    for (int t = 0; t < 4; ++t)
+      for (int t = 0; t < 4; ++t)
 #pragma unroll
-      for (int g = 0; g < 4; ++g) {
-        // group g = registers 4g..4g+3 = elements 4(g&1).. of fragment g>>1
-        const int q0 = t * 32 + 8 * g + 4 * hf;
-        const uint4 v = dsb[t][g >> 1];
-        const uint32_t lo = (g & 1) ? v.z : v.x, hi = (g & 1) ? v.w : v.y;
-        wr_b64(si + off_s(key, q0 >> 3) + (q0 & 7) * 2, lo, hi);
-      }
+        for (int g = 0; g < 4; ++g) {
+          const uint4 v = dsb[t][g >> 1];
+          const uint32_t lo = (g & 1) ? v.z : v.x, hi = (g & 1) ? v.w : v.y;
+          wr_b64(rowa + (((4 * t + g) ^ fk) << 4), lo, hi);
+        }
+    }
     barrier();
     // dQ for queries 32w..32w+31: sum over keys of dS[q][key] K[key][d]
     f32x16 dq[2];
     dq[0] = zero16();
     dq[1] = zero16();
-#pragma unroll
-    for (int ks = 0; ks < 8; ++ks) {
-      const bf16x8 af = frag_tn_s(si, ks * 16, w * 32, lane);
-      bf16x8 bk[2];
-#pragma unroll
-      for (int dt = 0; dt < 2; ++dt) bk[dt] = frag_tn_r(ki, ks * 16, dt * 32, lane);
-      lgkm0();
-#pragma unroll
-      for (int dt = 0; dt < 2; ++dt) dq[dt] = mfma32(af, bk[dt], dq[dt]);
-    }
-    // stage dQ (rows = queries of wave w), dK, dV (rows = keys of wave w) in Q/K/V images
+    bwd_dq_step<0>(dq, base, BB); bwd_dq_step<1>(dq, base, BB);
+    bwd_dq_step<2>(dq, base, BB); bwd_dq_step<3>(dq, base, BB);
+    bwd_dq_step<4>(dq, base, BB); bwd_dq_step<5>(dq, base, BB);
+    bwd_dq_step<6>(dq, base, BB); bwd_dq_step<7>(dq, base, BB);
+    // stage dQ (rows = queries of wave w), dK, dV (rows = keys of wave w), unswizzled
     barrier();
-#pragma unroll
-    for (int dt = 0; dt < 2; ++dt)
-#pragma unroll
-      for (int i = 0; i < 16; ++i) {
-        const int row = w * 32 + acc_row(i, hf), col = dt * 32 + (lane & 31);
-        const uint32_t o = off_r(row, col >> 3) + (col & 7) * 2;
-        wr_b16(qi + o, f2bf(dq[dt][i] * 0.125f));
-        wr_b16(ki + o, f2bf(dk[dt][i] * 0.125f));
-        wr_b16(vi + o, f2bf(dv[dt][i]));
-      }
+    const uint32_t oa = base + BB.ost;
+    bwd_stage_out<0, 0>(dq[0], 0.125f, oa); bwd_stage_out<0, 1>(dq[1], 0.125f, oa);
+    bwd_stage_out<1, 0>(dk[0], 0.125f, oa); bwd_stage_out<1, 1>(dk[1], 0.125f, oa);
+    bwd_stage_out<2, 0>(dv[0], 1.f, oa);    bwd_stage_out<2, 1>(dv[1], 1.f, oa);
     barrier();
     bf16_t* gb = dqkv + (int64_t)b * L * ld + (int64_t)hd * HD;
-#pragma unroll
-    for (int c = 0; c < 12; ++c) {
-      const int idx = tid + c * 256;          // 3 tensors x 128 rows x 8 chunks
-      const int x = idx >> 10, row = (idx >> 3) & 127, ch = idx & 7;
-      const bf16x8 v = rd128(qi + x * IMG + off_r(row, ch));
-      lgkm0();
-      *reinterpret_cast<bf16x8*>(gb + (int64_t)row * ld + (int64_t)x * H * HD + ch * 8) = v;
-    }
+    const uint32_t ca = base + BB.cpy;
+    const int crow = tid >> 3, cch = tid & 7;
+#define DPA_CP(C)                                                                         \
+  {                                                                                       \
+    const bf16x8 v = rd128o<(C >> 2) * IMG + (C & 3) * 4096>(ca);                         \
+    lgkm0();                                                                              \
+    *reinterpret_cast<bf16x8*>(gb + (int64_t)(crow + 32 * (C & 3)) * ld +                 \
+                               (int64_t)(C >> 2) * H * HD + cch * 8) = v;                \
+  }
+    DPA_CP(0) DPA_CP(1) DPA_CP(2) DPA_CP(3) DPA_CP(4) DPA_CP(5)
+    DPA_CP(6) DPA_CP(7) DPA_CP(8) DPA_CP(9) DPA_CP(10) DPA_CP(11)
+#undef DPA_CP
+    barrier();  // staging fully read before the next item's DMA lands on it
   }
 }
 
@@ -493,8 +610,8 @@ static int num_cus() {
 bool launch_attn128_fwd(const uint16_t* qkv, uint16_t* out, float* lse, int B, int Lq, int H,
                         float p, bool causal, uint32_t seed, uint32_t offset, hipStream_t s) {
   if (Lq != a128::L || causal || !a128::enabled()) return false;
-  const int items = B * H;
-  const int grid = items < a128::num_cus() ? items : a128::num_cus();
+  const int items = B * H, slots = 2 * a128::num_cus();
+  const int grid = items < slots ? items : slots;
   hipLaunchKernelGGL(a128::attn128_fwd_kernel, dim3(grid), dim3(256), 0, s, (const bf16_t*)qkv,
                      (bf16_t*)out, lse, B, H, p, seed, offset);
   return true;
@@ -504,8 +621,8 @@ bool launch_attn128_bwd(const uint16_t* qkv, const uint16_t* out, const uint16_t
                         const float* lse, uint16_t* dqkv, int B, int Lq, int H, float p, bool causal,
                         uint32_t seed, uint32_t offset, hipStream_t s) {
   if (Lq != a128::L || causal || !a128::enabled()) return false;
-  const int items = B * H;
-  const int grid = items < a128::num_cus() ? items : a128::num_cus();
+  const int items = B * H, slots = 2 * a128::num_cus();
+  const int grid = items < slots ? items : slots;
   hipLaunchKernelGGL(a128::attn128_bwd_kernel, dim3(grid), dim3(256), 0, s, (const bf16_t*)qkv,
                      (const bf16_t*)out, (const bf16_t*)dout, lse, (bf16_t*)dqkv, B, H, p, seed,
                      offset);

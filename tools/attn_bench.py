@@ -37,6 +37,12 @@ def main():
     ext = get_ext(required=True)
     B, H, L = a.B, a.H, a.L
     qkv = (torch.randn(B, L, 3 * H * 64, device="cuda") * 0.5).bfloat16()
+    # memory-pattern probes: contiguous copy vs per-head 128-B-segment gather
+    gb = qkv.numel() * 2 * 2 / 1e9
+    t_c = bench(lambda: qkv.clone())
+    t_p = bench(lambda: qkv.view(B, L, 3, H, 64).permute(0, 2, 3, 1, 4).contiguous())
+    print(json.dumps({"copy_contig_GBps": round(gb / t_c * 1e3, 1),
+                      "copy_head_gather_GBps": round(gb / t_p * 1e3, 1)}), flush=True)
     for p in sorted({0.0, a.p}):
         out, lse = ext.attn_fwd(qkv, H, p, False, 1, 0)
         dout = torch.randn_like(out)
