@@ -15,12 +15,13 @@
 //   (A0.B0, A0.B1, A1.B1, A1.B0), each wave owning a 64 x 32 block of it (16
 //   MFMAs per phase).  Fragments are reused across phases (phase 4 reads
 //   nothing), so a K-tile costs 24 row-form LDS reads per wave instead of 48.
-// * One half-tile image is prefetched per phase; a counted `s_waitcnt vmcnt(4)`
-//   at phases 4 and 8 retires the next buffer while two half-tiles stay in
-//   flight across the barriers (no vmcnt(0) in the main loop, raw s_barrier).
-//   WAR: an image is restaged >= 2 phases after its last read; RAW: it is read
-//   >= 1 phase after the wait that retires it (both needed because the two
-//   wave groups run staggered by one barrier).
+// * One half-tile image is prefetched per phase and a counted `s_waitcnt
+//   vmcnt(8)` in every phase retires the half staged four phases earlier, so four
+//   half-tiles (64 KiB) stay in flight across the barriers (no vmcnt(0) in the
+//   main loop, raw s_barrier).  The staging slots satisfy, for every half:
+//   restaged >= 2 phases after its last read (WAR) and first read >= 1 phase
+//   after the wait that retires it (RAW), both needed because the two wave
+//   groups run staggered by one barrier.
 // * Wave group 1 (waves 4-7) runs one barrier behind group 0, so on every SIMD
 //   one wave issues MFMAs while the other issues LDS reads and DMA.
 // * Workgroups are remapped so consecutive tiles (sharing an A panel) run on one XCD.
@@ -211,27 +212,19 @@ __device__ __forceinline__ void phase(f32x4 (&acc)[2][2][4][2], bf16x8 (&fa)[4][
   // group 0 sums the A0 image, group 1 the A1 image (wave-uniform branch)
   if constexpr (CS && q == 0) { if (do_cs && grp == 0) colsum_read<img_off(bf, 0)>(cs, csa); }
   if constexpr (CS && q == 2) { if (do_cs && grp == 1) colsum_read<img_off(bf, 1)>(cs, csa); }
-  // 2. prefetch one half image (schedule in the header comment)
+  // 2. prefetch one half image (schedule in the header comment), then retire the
+  //    half staged 4 phases ago (4 half-tiles = 8 DMA ops stay in flight); in the
+  //    last iteration fewer halves are issued, so drain instead.
   if constexpr (P == 0) opB.stage(smB + img_off(1, 1), 1, te + 1);
   if constexpr (P == 1) opA.stage(smem + img_off(1, 1), 1, te + 1);
   if constexpr (P == 2) { if (more) opA.stage(smem + img_off(0, 0), 0, te + 2); }
-  if constexpr (P == 3) {
-    if (more) {
-      opB.stage(smB + img_off(0, 0), 0, te + 2);
-      asm volatile("s_waitcnt vmcnt(4)" ::: "memory");  // odd K-tile te+1 landed
-    } else {
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    }
-  }
+  if constexpr (P == 3) { if (more) opB.stage(smB + img_off(0, 0), 0, te + 2); }
   if constexpr (P == 4) { if (more) opB.stage(smB + img_off(0, 1), 1, te + 2); }
   if constexpr (P == 5) { if (more) opA.stage(smem + img_off(0, 1), 1, te + 2); }
   if constexpr (P == 6) { if (more) opA.stage(smem + img_off(1, 0), 0, te + 3); }
-  if constexpr (P == 7) {
-    if (more) {
-      opB.stage(smB + img_off(1, 0), 0, te + 3);
-      asm volatile("s_waitcnt vmcnt(4)" ::: "memory");  // even K-tile te+2 landed
-    }
-  }
+  if constexpr (P == 7) { if (more) opB.stage(smB + img_off(1, 0), 0, te + 3); }
+  if (more) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+  else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   // 3. barrier, retire reads, 16 MFMAs on one quadrant, barrier
   barrier();
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
@@ -304,7 +297,7 @@ __global__ void __launch_bounds__(512) gemm256_kernel(
   opA.stage(smem + img_off(0, 1), 1, 0);
   opA.stage(smem + img_off(1, 0), 0, 1);
   opB.stage(smB + img_off(1, 0), 0, 1);
-  asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+  asm volatile("s_waitcnt vmcnt(8)" ::: "memory");  // K-tile 0 halves A0, B0 landed
   barrier();
   if (grp == 1) barrier();
 
