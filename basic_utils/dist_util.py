@@ -157,9 +157,13 @@ def barrier(*args, **kwargs):
 
 
 def dev():
-    """Device of this rank: ``cuda:{LOCAL_RANK}`` (a HIP device) or cpu."""
+    """Device of this rank: ``cuda:{LOCAL_RANK}`` (a HIP device) or cpu.
+
+    With more local ranks than visible GPUs (test setups: several gloo ranks on
+    one GPU) ranks wrap around the visible devices."""
     if _cuda_available():
-        return torch.device(f"cuda:{os.environ.get('LOCAL_RANK', '0')}")
+        lr = int(os.environ.get('LOCAL_RANK', '0'))
+        return torch.device(f"cuda:{lr % max(torch.cuda.device_count(), 1)}")
     return torch.device("cpu")
 
 
