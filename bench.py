@@ -152,7 +152,7 @@ def main():
     out = {
         "metric": METRIC,
         "value": round(value, 4),
-        "unit": "steps/s summed over GPUs (1 step = 2048 samples x 128 tokens per GPU)",
+        "unit": f"steps/s summed over GPUs (1 step = {a.batch_size} samples x {a.seq_len} tokens per GPU)",
         "n_gpus": world,
         "steps": a.steps,
         "warmup": a.warmup,

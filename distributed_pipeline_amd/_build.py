@@ -73,6 +73,8 @@ def build(force=False, jobs=None, debug=False, verbose=True):
     headers = glob.glob(os.path.join(CSRC, "*.h"))
     kernels = sorted(glob.glob(os.path.join(CSRC, "*.hip")))
     binding = os.path.join(CSRC, "bindings.cpp")
+    # host-side C++ (torch / c10d APIs): compiled with the binding flags
+    host_cpp = sorted(glob.glob(os.path.join(CSRC, "comm", "*.cpp")))
     opt = ["-O0", "-g"] if debug else ["-O3"]
     common = ["-std=c++17", "-fPIC", "--offload-arch=" + ARCH, "-D__HIP_PLATFORM_AMD__=1",
               "-Wno-unused-result", "-Wno-unused-command-line-argument"] + opt
@@ -84,8 +86,8 @@ def build(force=False, jobs=None, debug=False, verbose=True):
 
     jobs_todo = []
     objects = []
-    for src in kernels + [binding]:
-        flags = bind_flags if src == binding else common
+    for src in kernels + [binding] + host_cpp:
+        flags = bind_flags if (src == binding or src in host_cpp) else common
         key = _hash_files([src] + headers, " ".join(flags))
         obj = os.path.join(BUILD, os.path.basename(src) + "." + key + ".o")
         objects.append(obj)

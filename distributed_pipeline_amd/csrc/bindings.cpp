@@ -9,6 +9,10 @@
 
 #include "launchers.h"
 
+namespace dpa {
+void register_comm(pybind11::module& m);  // comm/reducer.cpp
+}
+
 #define CHECK_DEV(x) TORCH_CHECK((x).is_cuda(), #x " must be a HIP tensor")
 #define CHECK_CONTIG(x) TORCH_CHECK((x).is_contiguous(), #x " must be contiguous")
 #define CHECK_F32(x) TORCH_CHECK((x).scalar_type() == at::kFloat, #x " must be float32")
@@ -347,6 +351,7 @@ static bool gemm_supported(int64_t M, int64_t N, int64_t K) {
 
 PYBIND11_MODULE(_C, m) {
   m.doc() = "distributed_pipeline_amd native gfx950 kernels";
+  dpa::register_comm(m);
   m.def("sqnorm", &sqnorm, "flat grad L2 norm + clip coefficient (device)");
   m.def("adamw_ema", &adamw_ema, "fused AdamW + EMA + bf16 shadow refresh");
   m.def("ema_update", &ema_update, "flat EMA update");

@@ -1,0 +1,163 @@
+// Native bucket reducer of the DDP engine (SURVEY N-1: the role of torch's C++
+// DDP Reducer, reference utils/trainer.py:115-128), designed around the flat
+// gradient buffer instead of per-parameter copies:
+//
+// * Buckets are contiguous [begin, end) slices of ONE flat fp32 gradient buffer
+//   (the parameters' .grad are views into it), so a bucket is reduced in place:
+//   no copy-in / copy-out, no per-bucket staging.
+// * mark_ready(param) is called from the parameters' post-accumulate-grad hooks
+//   (autograd worker thread).  A per-bucket pending counter reaches zero when
+//   the bucket's last gradient has been accumulated; ready buckets are launched
+//   strictly in bucket order so every rank issues the same collective sequence
+//   (one all-reduce per bucket per step, RCCL over xGMI on the GPU).
+// * Optional bf16 wire format: the slice is packed into a persistent bf16 comm
+//   buffer, reduced, and unpacked at finalize (fp32 master gradients keep full
+//   precision locally; only the wire is narrow).
+// * The 1/world average is NOT applied here: the fused AdamW kernel folds it
+//   into its gradient scale.
+//
+// The collectives are issued through the c10d ProcessGroup object the Python
+// side created (RCCL "nccl" on ROCm, gloo on CPU), so stream ordering follows
+// the backend: RCCL work is enqueued after the producing kernels of the
+// current stream and completion is awaited in finalize().
+#include <torch/extension.h>
+#include <torch/csrc/distributed/c10d/ProcessGroup.hpp>
+#include <torch/csrc/distributed/c10d/Work.hpp>
+
+#include <mutex>
+#include <stdexcept>
+#include <vector>
+
+namespace dpa {
+
+class BucketReducer {
+ public:
+  BucketReducer(c10::intrusive_ptr<c10d::ProcessGroup> pg, at::Tensor grad_flat,
+                std::vector<int64_t> bounds, std::vector<int64_t> param_bucket, bool bf16_wire)
+      : pg_(std::move(pg)), grad_(std::move(grad_flat)), bounds_(std::move(bounds)),
+        bucket_of_(std::move(param_bucket)), bf16_(bf16_wire) {
+    TORCH_CHECK(grad_.is_contiguous() && grad_.dim() == 1, "grad_flat must be a 1-D contiguous tensor");
+    TORCH_CHECK(bounds_.size() >= 2 && bounds_.front() == 0 && bounds_.back() <= grad_.numel(),
+                "bucket bounds must start at 0 and stay inside the flat buffer");
+    const int nb = (int)bounds_.size() - 1;
+    size_.assign(nb, 0);
+    for (int64_t b : bucket_of_) {
+      TORCH_CHECK(b >= 0 && b < nb, "param bucket index out of range");
+      size_[b] += 1;
+    }
+    for (int b = 0; b < nb; ++b) TORCH_CHECK(size_[b] > 0, "empty bucket ", b);
+    pending_ = size_;
+    work_.resize(nb);
+    launched_.assign(nb, false);
+    if (bf16_) comm_ = at::empty({grad_.numel()}, grad_.options().dtype(at::kBFloat16));
+  }
+
+  // Called at forward time when gradient synchronisation is enabled (torch-DDP
+  // semantics: the no_sync decision is taken when the graph is built).
+  void arm() {
+    std::lock_guard<std::mutex> g(mu_);
+    pending_ = size_;
+    std::fill(launched_.begin(), launched_.end(), false);
+    for (auto& w : work_) w.reset();
+    next_ = 0;
+    armed_ = true;
+  }
+
+  void disarm() {
+    std::lock_guard<std::mutex> g(mu_);
+    armed_ = false;
+  }
+
+  bool armed() const { return armed_; }
+
+  void mark_ready(int64_t param_index) {
+    std::lock_guard<std::mutex> g(mu_);
+    if (!armed_) return;
+    TORCH_CHECK(param_index >= 0 && param_index < (int64_t)bucket_of_.size(), "bad param index");
+    const int b = (int)bucket_of_[param_index];
+    TORCH_CHECK(pending_[b] > 0, "parameter ", param_index, " marked ready twice in one backward");
+    if (--pending_[b] == 0) launch_ready_in_order();
+  }
+
+  // Launch whatever has not been launched (e.g. unused parameters, or graph
+  // replays without hooks), wait for every bucket, unpack the bf16 wire.
+  void finalize() {
+    std::lock_guard<std::mutex> g(mu_);
+    if (!armed_) return;
+    const int nb = (int)launched_.size();
+    for (int b = next_; b < nb; ++b) launch(b);
+    next_ = nb;
+    for (int b = 0; b < nb; ++b) {
+      if (work_[b]) {
+        work_[b]->wait();
+        work_[b].reset();
+        if (bf16_) slice(grad_, b).copy_(slice(comm_, b));
+      }
+    }
+    armed_ = false;
+  }
+
+  // Reduce every bucket now (graph mode: backward ran without hooks).
+  void reduce_all() {
+    arm();
+    finalize();
+  }
+
+  int64_t num_buckets() const { return (int64_t)launched_.size(); }
+  int64_t next_bucket() const { return next_; }
+  std::vector<int64_t> pending() const {
+    return std::vector<int64_t>(pending_.begin(), pending_.end());
+  }
+
+ private:
+  at::Tensor slice(const at::Tensor& t, int b) const { return t.slice(0, bounds_[b], bounds_[b + 1]); }
+
+  void launch_ready_in_order() {
+    const int nb = (int)launched_.size();
+    while (next_ < nb && pending_[next_] == 0) launch(next_++);
+  }
+
+  void launch(int b) {
+    if (launched_[b]) return;
+    at::Tensor view = slice(grad_, b);
+    if (bf16_) {
+      at::Tensor wire = slice(comm_, b);
+      wire.copy_(view);
+      view = wire;
+    }
+    std::vector<at::Tensor> ts{view};
+    work_[b] = pg_->allreduce(ts);
+    launched_[b] = true;
+  }
+
+  c10::intrusive_ptr<c10d::ProcessGroup> pg_;
+  at::Tensor grad_, comm_;
+  std::vector<int64_t> bounds_;
+  std::vector<int64_t> bucket_of_;
+  std::vector<int> size_, pending_;
+  std::vector<c10::intrusive_ptr<c10d::Work>> work_;
+  std::vector<bool> launched_;
+  int next_ = 0;
+  bool armed_ = false;
+  bool bf16_;
+  std::mutex mu_;
+};
+
+void register_comm(pybind11::module& m) {
+  pybind11::class_<BucketReducer>(m, "BucketReducer")
+      .def(pybind11::init<c10::intrusive_ptr<c10d::ProcessGroup>, at::Tensor, std::vector<int64_t>,
+                          std::vector<int64_t>, bool>(),
+           pybind11::arg("process_group"), pybind11::arg("grad_flat"), pybind11::arg("bounds"),
+           pybind11::arg("param_bucket"), pybind11::arg("bf16_wire") = false)
+      .def("arm", &BucketReducer::arm)
+      .def("disarm", &BucketReducer::disarm)
+      .def("armed", &BucketReducer::armed)
+      .def("mark_ready", &BucketReducer::mark_ready, pybind11::call_guard<pybind11::gil_scoped_release>())
+      .def("finalize", &BucketReducer::finalize, pybind11::call_guard<pybind11::gil_scoped_release>())
+      .def("reduce_all", &BucketReducer::reduce_all, pybind11::call_guard<pybind11::gil_scoped_release>())
+      .def("num_buckets", &BucketReducer::num_buckets)
+      .def("next_bucket", &BucketReducer::next_bucket)
+      .def("pending", &BucketReducer::pending);
+}
+
+}  // namespace dpa

@@ -3,7 +3,10 @@ Native data-parallel engine (SURVEY N-1/P-DP/P-GA): the MI355X replacement for
 ``torch.nn.parallel.DistributedDataParallel`` as used by the reference trainer
 (reference: utils/trainer.py:115-128, 209-221).
 
-Design (xGMI/RCCL-first rather than a translation of the C++ Reducer):
+Design (xGMI/RCCL-first rather than a translation of torch's C++ Reducer).  The
+bucket bookkeeping and collective launches run in the native ``BucketReducer``
+(``csrc/comm/reducer.cpp``) when the extension is present; the Python code here
+implements the same protocol for the single-GPU multi-rank test transport.
 
 * Gradients live in ONE flat fp32 buffer (:class:`FlatParamSpace`); buckets are
   contiguous slices of it, so a bucket all-reduce reads/writes the gradients
@@ -31,11 +34,13 @@ Design (xGMI/RCCL-first rather than a translation of the C++ Reducer):
   fires; :meth:`finalize` then launches every bucket after the replay.
 """
 import contextlib
+import os
 
 import torch
 import torch.distributed as dist
 from torch import nn
 
+from ..ops._ext import get_ext
 from .flat import FlatParamSpace
 
 _MiB = 1024 * 1024
@@ -91,22 +96,34 @@ class DDPEngine(nn.Module):
             for p in b.params:
                 self._bucket_of[id(p)] = b
         self._hooks = []
-        if self.distributed:
-            self._verify_shapes()
-            if broadcast_from_rank0:
-                self.broadcast_parameters()
-            for p in self.space.layout:
-                hook = self._make_hook(p)
-                # Fires once per backward per leaf, also when a fused op wrote the
-                # gradient in place and returned None for it (AccumulateGrad still
-                # runs), so no op-side notification is needed.
-                self._hooks.append(p.register_post_accumulate_grad_hook(hook))
         self._comm_buf = None
         # gloo on device tensors is only a test transport (several ranks sharing one
         # GPU): stage each bucket through host memory synchronously so its ordering
         # w.r.t. the producing kernels is explicit.  RCCL ("nccl") orders via events.
         self._host_sync_before_comm = (self.distributed and self.space.device.type == "cuda"
                                        and dist.get_backend(self.pg) == "gloo")
+        # Native C++ bucket reducer (csrc/comm/reducer.cpp) for the real transports;
+        # the Python implementation below stays as the reference / test transport.
+        self._native = None
+        if (self.distributed and not self._host_sync_before_comm
+                and os.environ.get("DPA_NATIVE_REDUCER", "1") != "0"):
+            ext = get_ext(required=False)
+            if ext is not None and hasattr(ext, "BucketReducer"):
+                pg = self.pg or dist.distributed_c10d._get_default_group()
+                bounds = [b.start for b in self.buckets] + [self.buckets[-1].end]
+                param_bucket = [self._bucket_of[id(p)].index for p in self.space.layout]
+                self._native = ext.BucketReducer(pg, self.space.grad_flat, bounds, param_bucket,
+                                                 self.reduce_dtype == torch.bfloat16)
+        if self.distributed:
+            self._verify_shapes()
+            if broadcast_from_rank0:
+                self.broadcast_parameters()
+            for i, p in enumerate(self.space.layout):
+                hook = self._make_hook(p, i)
+                # Fires once per backward per leaf, also when a fused op wrote the
+                # gradient in place and returned None for it (AccumulateGrad still
+                # runs), so no op-side notification is needed.
+                self._hooks.append(p.register_post_accumulate_grad_hook(hook))
 
     # -- setup ---------------------------------------------------------------
     def _coll_device(self):
@@ -135,7 +152,9 @@ class DDPEngine(nn.Module):
     def forward(self, *args, **kwargs):
         if self.distributed and torch.is_grad_enabled() and self.training:
             self._armed = self._sync_enabled
-            if self._armed:
+            if self._native is not None:
+                self._native.arm() if self._armed else self._native.disarm()
+            elif self._armed:
                 for b in self.buckets:
                     b.pending = len(b.params)
                     b.work = None
@@ -153,7 +172,14 @@ class DDPEngine(nn.Module):
             self._sync_enabled = prev
 
     # -- reduction ----------------------------------------------------------------
-    def _make_hook(self, p):
+    def _make_hook(self, p, index):
+        if self._native is not None:
+            native = self._native
+
+            def native_hook(_param):
+                native.mark_ready(index)  # no-op unless armed
+            return native_hook
+
         def hook(_param):
             if not self._armed:
                 return
@@ -199,6 +225,10 @@ class DDPEngine(nn.Module):
         """Wait for (and launch any not-yet-launched) bucket reductions."""
         if not self.distributed or not self._armed:
             return
+        if self._native is not None:
+            self._native.finalize()
+            self._armed = False
+            return
         for b in self.buckets[self._next_launch:]:
             self._launch(b)
         self._next_launch = len(self.buckets)
@@ -215,6 +245,9 @@ class DDPEngine(nn.Module):
     def reduce_all_now(self):
         """Graph mode: backward ran without hooks; reduce every bucket now."""
         if not self.distributed:
+            return
+        if self._native is not None:
+            self._native.reduce_all()
             return
         self._armed = True
         for b in self.buckets:

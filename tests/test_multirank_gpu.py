@@ -43,7 +43,7 @@ def _worker(rank, world, port, q):
                                              dict(input_ids=ids[rank, mb], input_mask=mask[rank, mb]))
             terms["loss"].mean().backward()
         eng.finalize()
-        q.put((rank, eng.space.grad_flat.cpu(), len(eng.buckets)))
+        q.put((rank, eng.space.grad_flat.cpu().numpy().copy(), len(eng.buckets)))
     finally:
         dist.destroy_process_group()
 
@@ -60,6 +60,7 @@ def test_two_ranks_one_gpu_gradients_agree():
         p.join(timeout=60)
         assert p.exitcode == 0
     (_, g0, nb), (_, g1, _) = res
+    g0, g1 = torch.from_numpy(g0), torch.from_numpy(g1)
     assert nb > 3
     assert torch.isfinite(g0).all() and g0.abs().sum() > 0
     torch.testing.assert_close(g0, g1, rtol=0, atol=0)  # all-reduced sums identical on both ranks
