@@ -8,12 +8,14 @@
 #pragma once
 #include <hip/hip_runtime.h>
 
+#include "common.h"
+
 namespace dpa {
 
 // Phi(z) (standard normal cdf) and exp(-z^2/2)
 __device__ __forceinline__ float phi_cdf(float z, float& e) {
   const float x = fabsf(z) * 0.70710678118654752f;
-  e = __expf(-x * x);
+  e = fexp(-x * x);
   const float t = __builtin_amdgcn_rcpf(fmaf(0.3275911f, x, 1.f));
   float p = fmaf(1.061405429f, t, -1.453152027f);
   p = fmaf(p, t, 1.421413741f);
@@ -39,7 +41,7 @@ __device__ __forceinline__ float act_apply(float z, int act) {
   switch (act) {
     case 1: return gelu_f(z);
     case 2: return tanhf(z);
-    case 3: return z * __builtin_amdgcn_rcpf(1.f + __expf(-z));
+    case 3: return z * __builtin_amdgcn_rcpf(1.f + fexp(-z));
     default: return z;
   }
 }
@@ -50,7 +52,7 @@ __device__ __forceinline__ float act_deriv(float a, int act) {
     case 1: return dgelu_f(a);
     case 2: return 1.f - a * a;
     case 3: {
-      const float sg = __builtin_amdgcn_rcpf(1.f + __expf(-a));
+      const float sg = __builtin_amdgcn_rcpf(1.f + fexp(-a));
       return sg * fmaf(a, 1.f - sg, 1.f);
     }
     default: return 1.f;

@@ -121,15 +121,15 @@ __global__ void __launch_bounds__(256) attn_fwd_kernel(const bf16_t* __restrict_
 #pragma unroll
     for (int t = 0; t < 2; ++t)
 #pragma unroll
-      for (int i = 0; i < 16; ++i) add += exp2f(acc[t][i] - mn);
-    l = l * exp2f(m - mn) + add;
+      for (int i = 0; i < 16; ++i) add += fexp2(acc[t][i] - mn);
+    l = l * fexp2(m - mn) + add;
     m = mn;
     __syncthreads();
   }
   {
     const float m2 = __shfl_xor(m, 32, 64), l2 = __shfl_xor(l, 32, 64);
     const float M = fmaxf(m, m2);
-    l = l * exp2f(m - M) + l2 * exp2f(m2 - M);
+    l = l * fexp2(m - M) + l2 * fexp2(m2 - M);
     m = M;
   }
   const float lse2 = m + log2f(l);
@@ -151,7 +151,7 @@ __global__ void __launch_bounds__(256) attn_fwd_kernel(const bf16_t* __restrict_
 #pragma unroll
       for (int i = 0; i < 16; ++i) {
         const int key = kv0 + t * 32 + acc_row(i, hf);
-        float pr = exp2f(acc[i] * ATT_C - lse2);
+        float pr = fexp2(acc[i] * ATT_C - lse2);
         if (CAUSAL && key > q) pr = 0.f;
         if (dc.on) pr = keep_bit(dc, q, key) ? pr * dc.scale : 0.f;
         acc[i] = pr;
@@ -236,7 +236,7 @@ __global__ void __launch_bounds__(256) attn_fwd_small_kernel(const bf16_t* __res
     if (t < nt)
 #pragma unroll
       for (int i = 0; i < 16; ++i) {
-        const float e = exp2f(acc[t][i] - m);
+        const float e = fexp2(acc[t][i] - m);
         acc[t][i] = e;
         l += e;
       }
@@ -363,7 +363,7 @@ __global__ void __launch_bounds__(256) attn_bwd_kv_kernel(
       for (int i = 0; i < 16; ++i) {
         const int r = qt * 32 + acc_row(i, hf);
         const int qq = q0 + r;
-        float pr = exp2f(sacc[i] * ATT_C - s_lse[r]);
+        float pr = fexp2(sacc[i] * ATT_C - s_lse[r]);
         if ((CAUSAL && key > qq) || !k_ok || qq >= L) pr = 0.f;
         float pd = pr, dpd = dpacc[i];
         if (dc.on) {
@@ -458,7 +458,7 @@ __global__ void __launch_bounds__(256) attn_bwd_q_kernel(
 #pragma unroll
       for (int i = 0; i < 16; ++i) {
         const int kk = kv0 + t * 32 + acc_row(i, hf);
-        float pr = exp2f(sacc[i] * ATT_C - lse2);
+        float pr = fexp2(sacc[i] * ATT_C - lse2);
         if ((CAUSAL && kk > q) || !q_ok || kk >= L) pr = 0.f;
         float dpd = dpacc[i];
         if (dc.on) dpd = keep_bit(dc, q, kk) ? dpd * dc.scale : 0.f;

@@ -238,7 +238,7 @@ __global__ void __launch_bounds__(256, 2) attn128_fwd_kernel(const bf16_t* __res
     for (int t = 0; t < 4; ++t)
 #pragma unroll
       for (int i = 0; i < 16; ++i) {
-        const float e = exp2f(acc[t][i] - m);
+        const float e = fexp2(acc[t][i] - m);
         acc[t][i] = e;
         l += e;
       }
@@ -399,7 +399,7 @@ __device__ __forceinline__ void bwd_pds(f32x16& sacc, f32x16& dpacc, uint32_t ba
 #pragma unroll
   for (int r = 0; r < 4; ++r) {
     const int i = 4 * G + r;
-    const float pr = exp2f(sacc[i] * ATT_C - lv[r]);
+    const float pr = fexp2(sacc[i] * ATT_C - lv[r]);
     float pd = pr, dpd = dpacc[i];
     if (dc.on) {
       const bool kp = keep_bit(dc, T * 32 + 8 * G + 4 * hf + r, key);

@@ -89,4 +89,10 @@ __device__ __forceinline__ float u32_to_unit(uint32_t x) {  // [0,1)
   return (float)(x >> 8) * (1.0f / 16777216.0f);
 }
 
+// Raw v_exp_f32 (2^x): no denormal range reduction (the libm exp2f adds a
+// compare / select / ldexp around every call); results below 2^-126 flush to 0,
+// which is exact enough for softmax / activation math.
+__device__ __forceinline__ float fexp2(float x) { return __builtin_amdgcn_exp2f(x); }
+__device__ __forceinline__ float fexp(float x) { return __builtin_amdgcn_exp2f(x * 1.4426950408889634f); }
+
 }  // namespace dpa

@@ -59,6 +59,14 @@ void launch_attn_bwd(const uint16_t* qkv, const uint16_t* out, const uint16_t* d
                      float* delta, uint16_t* dqkv, float* dq_acc, int B, int L, int H, float p,
                      bool causal, uint32_t seed, uint32_t offset, hipStream_t s);
 
+// ---- xent2.hip: E = 128 LDS-DMA pipelined fused linear-CE (used by xent.hip) ----
+bool launch_lxent2_fwd(const uint16_t* x, const uint16_t* W, const uint16_t* b, const int64_t* tgt,
+                       int N, int V, int E, int splits, int vps, float* loss, float* lse,
+                       float* part_m, float* part_s, float* tgt_logit, hipStream_t s);
+bool launch_lxent2_dx(const uint16_t* x, const uint16_t* W, const uint16_t* b, const int64_t* tgt,
+                      const float* lse, const float* dloss, int N, int V, int E, int splits, int vps,
+                      uint16_t* dx, float* dx_acc, hipStream_t s);
+
 // ---- gemm.hip (bf16 MFMA GEMMs of Linear layers) ----------------------------------
 bool launch_gemm_nt(const uint16_t* x, const uint16_t* W, const uint16_t* bias, uint16_t* y,
                     uint16_t* z, int T, int N, int K, int act, hipStream_t s);

@@ -103,46 +103,45 @@ __global__ void __launch_bounds__(256) lxent_fwd_kernel(
     stage.store(wt, tid);
     if (tid < 64) {
       const int v = v0 + tid;
-      bt[tid] = (v < V) ? (bias ? bf2f(bias[v]) : 0.f) : 0.f;
+      bt[tid] = (v < vend) ? (bias ? bf2f(bias[v]) : 0.f) : -INFINITY;
     }
     __syncthreads();
     if (v0 + 64 < vend) stage.load(W, v0 + 64, V, tid);  // prefetch next tile behind the MFMAs
 
+    // Accumulators start at the bias of their vocabulary rows (-inf for rows past
+    // the split / vocabulary), so no per-element bias add or tail test remains.
     f32x16 acc[2];
 #pragma unroll
     for (int vt = 0; vt < 2; ++vt) {
-      acc[vt] = zero16();
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        const f32x4 bv = *reinterpret_cast<const f32x4*>(bt + vt * 32 + 8 * g + 4 * h);
+#pragma unroll
+        for (int r = 0; r < 4; ++r) acc[vt][4 * g + r] = bv[r];
+      }
 #pragma unroll
       for (int s = 0; s < KS; ++s)
         acc[vt] = mfma32(lds_frag<ROWB>(wt, vt * 32 + (lane & 31), 2 * s + h), xf[s], acc[vt]);
     }
-    const bool tail = (v0 + 64 > V);
     float tmax = -INFINITY;
 #pragma unroll
-    for (int vt = 0; vt < 2; ++vt) {
+    for (int vt = 0; vt < 2; ++vt)
 #pragma unroll
-      for (int i = 0; i < 16; ++i) {
-        const int r = vt * 32 + acc_row(i, h);
-        float y = (acc[vt][i] + bt[r]) * LOG2E;
-        if (tail && v0 + r >= V) y = -INFINITY;
-        acc[vt][i] = y;
-        tmax = fmaxf(tmax, y);
-      }
-    }
-    const float mn = fmaxf(m, tmax);
+      for (int i = 0; i < 16; i += 2) tmax = fmaxf(tmax, fmaxf(acc[vt][i], acc[vt][i + 1]));
+    const float mn = fmaxf(m, tmax * LOG2E);
     float add = 0.f;
 #pragma unroll
     for (int vt = 0; vt < 2; ++vt)
 #pragma unroll
-      for (int i = 0; i < 16; ++i) add += exp2f(acc[vt][i] - mn);
-    ssum = ssum * exp2f(m - mn) + add;
+      for (int i = 0; i < 16; ++i) add += fexp2(fmaf(acc[vt][i], LOG2E, -mn));
+    ssum = ssum * fexp2(m - mn) + add;
     m = mn;
     const int64_t r = tg - v0;
     if (r >= 0 && r < 64 && v0 + r < vend) {
       const int rr = (int)r & 31, vt = (int)r >> 5;
       if (((rr >> 2) & 1) == h) {
         const int i = (rr & 3) + 4 * (rr >> 3);
-        tl = (vt ? sel16(acc[1], i) : sel16(acc[0], i)) * LN2;
+        tl = vt ? sel16(acc[1], i) : sel16(acc[0], i);
       }
     }
     __syncthreads();
@@ -151,7 +150,7 @@ __global__ void __launch_bounds__(256) lxent_fwd_kernel(
   const float m2 = __shfl_xor(m, 32, 64), s2 = __shfl_xor(ssum, 32, 64);
   const float tl2 = __shfl_xor(tl, 32, 64);
   const float M = fmaxf(m, m2);
-  const float S = ssum * exp2f(m - M) + s2 * exp2f(m2 - M);
+  const float S = ssum * fexp2(m - M) + s2 * fexp2(m2 - M);
   tl = fmaxf(tl, tl2);
   if (h == 0 && tok_ok) {
     if (gridDim.y == 1) {
@@ -176,7 +175,7 @@ __global__ void __launch_bounds__(256) lxent_combine_kernel(
   float M = -1e30f;
   for (int s = 0; s < S; ++s) M = fmaxf(M, part_m[(int64_t)s * N + t]);
   float sum = 0.f;
-  for (int s = 0; s < S; ++s) sum += part_s[(int64_t)s * N + t] * exp2f(part_m[(int64_t)s * N + t] - M);
+  for (int s = 0; s < S; ++s) sum += part_s[(int64_t)s * N + t] * fexp2(part_m[(int64_t)s * N + t] - M);
   const float lse = (M + log2f(sum)) * LN2;
   const int64_t tg = target[t];
   const bool valid = tg >= 0 && tg < V;
@@ -223,24 +222,31 @@ __global__ void __launch_bounds__(256) lxent_dx_kernel(
     stage.store(wt, tid);
     if (tid < 64) {
       const int v = v0 + tid;
-      bt[tid] = (v < V) ? (bias ? bf2f(bias[v]) : 0.f) : 0.f;
+      bt[tid] = (v < vend) ? (bias ? bf2f(bias[v]) : 0.f) : -INFINITY;
     }
     __syncthreads();
     if (v0 + 64 < vend) stage.load(W, v0 + 64, V, tid);
 
 #pragma unroll
     for (int vt = 0; vt < 2; ++vt) {
-      f32x16 acc = zero16();
+      f32x16 acc;
+#pragma unroll
+      for (int g4 = 0; g4 < 4; ++g4) {
+        const f32x4 bv = *reinterpret_cast<const f32x4*>(bt + vt * 32 + 8 * g4 + 4 * h);
+#pragma unroll
+        for (int r = 0; r < 4; ++r) acc[4 * g4 + r] = bv[r];
+      }
 #pragma unroll
       for (int s = 0; s < KS; ++s)
         acc = mfma32(lds_frag<ROWB>(wt, vt * 32 + (lane & 31), 2 * s + h), xf[s], acc);
+      // dS = g * (softmax - onehot(target)); rows past the split come out as 0
 #pragma unroll
-      for (int i = 0; i < 16; ++i) {
-        const int r = vt * 32 + acc_row(i, h);
-        const int v = v0 + r;
-        float p = exp2f((acc[i] + bt[r]) * LOG2E - lse2);
-        p = (v < vend) ? p : 0.f;
-        acc[i] = g * (p - ((int64_t)v == tg ? 1.f : 0.f));
+      for (int i = 0; i < 16; ++i) acc[i] = g * fexp2(fmaf(acc[i], LOG2E, -lse2));
+      const int64_t rt = tg - (v0 + vt * 32);
+      if (rt >= 0 && rt < 32 && tg < vend && ((rt >> 2) & 1) == h) {
+        const int it = ((int)rt & 3) + 4 * ((int)rt >> 3);
+#pragma unroll
+        for (int i = 0; i < 16; ++i) acc[i] -= (i == it) ? g : 0.f;
       }
       // dx[t][k] += sum_v dS[v][t] W[v][k]   (dS as A operand, W read transposed)
 #pragma unroll
@@ -294,7 +300,8 @@ __global__ void __launch_bounds__(512) lxent_dw_kernel(
     if (v_ok) wf[s] = ld_frag(W + (int64_t)v * E + 16 * s + 8 * h);
     else for (int j = 0; j < 8; ++j) wf[s][j] = 0;
   }
-  const float bv = (v_ok && bias) ? bf2f(bias[v]) : 0.f;
+  // rows past the vocabulary start at -inf: their softmax (and gradient) is 0
+  const float bv = v_ok ? (bias ? bf2f(bias[v]) : 0.f) : -INFINITY;
 
   f32x16 dacc[KT];
 #pragma unroll
@@ -324,17 +331,28 @@ __global__ void __launch_bounds__(512) lxent_dw_kernel(
     __syncthreads();
 #pragma unroll
     for (int tt = 0; tt < 2; ++tt) {
-      f32x16 acc = zero16();  // S'[t][v]: rows = tokens, cols = vocab (lane)
+      f32x16 acc;  // S'[t][v]: rows = tokens, cols = vocab (lane); starts at the bias
+#pragma unroll
+      for (int i = 0; i < 16; ++i) acc[i] = bv;
 #pragma unroll
       for (int s = 0; s < KS; ++s)
         acc = mfma32(lds_frag<ROWB>(xt, tt * 32 + (lane & 31), 2 * s + h), wf[s], acc);
 #pragma unroll
-      for (int i = 0; i < 16; ++i) {
-        const int r = tt * 32 + acc_row(i, h);
-        const float p = exp2f((acc[i] + bv) * LOG2E - s_lse[r]);
-        const float d = v_ok ? s_g[r] * (p - (s_tg[r] == v ? 1.f : 0.f)) : 0.f;
-        acc[i] = d;
-        dbs += d;
+      for (int g4 = 0; g4 < 4; ++g4) {
+        // per-token scalars of rows tt*32 + 8 g4 + 4 h + r, one 16-byte read each
+        const int rb = tt * 32 + 8 * g4 + 4 * h;
+        const f32x4 l4 = *reinterpret_cast<const f32x4*>(s_lse + rb);
+        const f32x4 g4v = *reinterpret_cast<const f32x4*>(s_g + rb);
+        const int4 t4 = *reinterpret_cast<const int4*>(s_tg + rb);
+        const int tgs[4] = {t4.x, t4.y, t4.z, t4.w};
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int i = 4 * g4 + r;
+          const float gp = g4v[r] * fexp2(fmaf(acc[i], LOG2E, -l4[r]));
+          const float d = (tgs[r] == v) ? gp - g4v[r] : gp;
+          acc[i] = d;
+          dbs += d;
+        }
       }
 #pragma unroll
       for (int s = 0; s < 2; ++s) {
@@ -394,8 +412,10 @@ static void fwd_impl(const bf16_t* x, const bf16_t* W, const bf16_t* b, const in
   float* pm = ws;
   float* ps = ws + (int64_t)Sx * N;
   float* tl = ws + 2 * (int64_t)Sx * N;
-  hipLaunchKernelGGL(lxent_fwd_kernel<E>, dim3(tb, Sx), dim3(256), 0, st, x, W, b, tgt, N, V, vps,
-                     loss, lse, pm, ps, tl);
+  if (!launch_lxent2_fwd((const uint16_t*)x, (const uint16_t*)W, (const uint16_t*)b, tgt, N, V, E, Sx,
+                         vps, loss, lse, pm, ps, tl, st))
+    hipLaunchKernelGGL(lxent_fwd_kernel<E>, dim3(tb, Sx), dim3(256), 0, st, x, W, b, tgt, N, V, vps,
+                       loss, lse, pm, ps, tl);
   if (Sx > 1)
     hipLaunchKernelGGL(lxent_combine_kernel, dim3((N + 255) / 256), dim3(256), 0, st, pm, ps, tl,
                        tgt, N, V, Sx, loss, lse);
@@ -425,8 +445,10 @@ static void dx_impl(const bf16_t* x, const bf16_t* W, const bf16_t* b, const int
   const int S = dx_acc ? pick_splits(tb, vchunks, 1024) : 1;
   const int vps = ((vchunks + S - 1) / S) * 64;
   const int Sx = (V + vps - 1) / vps;
-  hipLaunchKernelGGL(lxent_dx_kernel<E>, dim3(tb, Sx), dim3(256), 0, st, x, W, b, tgt, lse, dl, N,
-                     V, vps, (bf16_t*)dx, Sx > 1 ? dx_acc : nullptr);
+  if (!launch_lxent2_dx((const uint16_t*)x, (const uint16_t*)W, (const uint16_t*)b, tgt, lse, dl, N,
+                        V, E, Sx, vps, dx, Sx > 1 ? dx_acc : nullptr, st))
+    hipLaunchKernelGGL(lxent_dx_kernel<E>, dim3(tb, Sx), dim3(256), 0, st, x, W, b, tgt, lse, dl, N,
+                       V, vps, (bf16_t*)dx, Sx > 1 ? dx_acc : nullptr);
   if (Sx > 1) {
     const int64_t n = (int64_t)N * E;
     hipLaunchKernelGGL(f32_to_bf16_kernel, dim3((unsigned)((n / 4 + 255) / 256 + 1)), dim3(256), 0,
