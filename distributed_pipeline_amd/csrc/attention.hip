@@ -506,11 +506,13 @@ void launch_attn_fwd(const uint16_t* qkv, uint16_t* out, float* lse, int B, int 
 
 bool attn_bwd_needs_dq_acc(int L) { (void)L; return false; }
 
-void launch_attn_bwd(const uint16_t* qkv, const uint16_t* out, const uint16_t* dout, const float* lse,
-                     float* delta, uint16_t* dqkv, float* dq_acc, int B, int L, int H, float p,
-                     bool causal, uint32_t seed, uint32_t offset, hipStream_t s) {
+bool launch_attn_bwd(const uint16_t* qkv, const uint16_t* out, const uint16_t* dout, const float* lse,
+                     float* delta, uint16_t* dqkv, float* dq_acc, float* colpart, float* dbias, int B,
+                     int L, int H, float p, bool causal, uint32_t seed, uint32_t offset, hipStream_t s) {
   (void)dq_acc;
-  if (launch_attn128_bwd(qkv, out, dout, lse, dqkv, B, L, H, p, causal, seed, offset, s)) return;
+  if (launch_attn128_bwd(qkv, out, dout, lse, dqkv, colpart, dbias, B, L, H, p, causal, seed, offset,
+                         s))
+    return dbias != nullptr;
   const int64_t rows = (int64_t)B * L * H;
   hipLaunchKernelGGL(attn_delta_kernel, dim3((unsigned)((rows + 255) / 256)), dim3(256), 0, s,
                      (const bf16_t*)dout, (const bf16_t*)out, delta, B, L, H);
@@ -526,6 +528,7 @@ void launch_attn_bwd(const uint16_t* qkv, const uint16_t* out, const uint16_t* d
     hipLaunchKernelGGL(attn_bwd_q_kernel<false>, grid, dim3(256), 0, s, (const bf16_t*)qkv,
                        (const bf16_t*)dout, lse, delta, (bf16_t*)dqkv, L, H, p, seed, offset);
   }
+  return false;
 }
 
 }  // namespace dpa

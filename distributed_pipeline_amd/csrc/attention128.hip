@@ -90,6 +90,14 @@ __device__ __forceinline__ void wr_b64(uint32_t a, uint32_t lo, uint32_t hi) {
   u32x2 v = {lo, hi};
   asm volatile("ds_write_b64 %0, %1" ::"v"(a), "v"(v) : "memory");
 }
+__device__ __forceinline__ void wr_f4(uint32_t a, const f32x4& v) {
+  asm volatile("ds_write_b128 %0, %1" ::"v"(a), "v"(v) : "memory");
+}
+__device__ __forceinline__ float rd_f1(uint32_t a) {
+  float f;
+  asm volatile("ds_read_b32 %0, %1" : "=v"(f) : "v"(a));
+  return f;
+}
 __device__ __forceinline__ void lgkm0() {
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
   __builtin_amdgcn_sched_barrier(0);
@@ -467,8 +475,8 @@ __device__ __forceinline__ void bwd_stage_out(const f32x16& acc, float scale, ui
 
 __global__ void __launch_bounds__(256, 2) attn128_bwd_kernel(
     const bf16_t* __restrict__ qkv, const bf16_t* __restrict__ out, const bf16_t* __restrict__ dout,
-    const float* __restrict__ lse, bf16_t* __restrict__ dqkv, int B, int H, float p, uint32_t seed,
-    uint32_t offset) {
+    const float* __restrict__ lse, bf16_t* __restrict__ dqkv, float* __restrict__ colpart, int B,
+    int H, float p, uint32_t seed, uint32_t offset) {
   __shared__ __attribute__((aligned(1024))) char smem[BWD_STATS + 2 * L * 4];
   const int nitems = B * H;
   const int64_t ld = 3LL * H * HD, ldo = (int64_t)H * HD;
@@ -571,18 +579,62 @@ __global__ void __launch_bounds__(256, 2) attn128_bwd_kernel(
     bf16_t* gb = dqkv + (int64_t)b * L * ld + (int64_t)hd * HD;
     const uint32_t ca = base + BB.cpy;
     const int crow = tid >> 3, cch = tid & 7;
+    // Column sums of the bf16 dQ/dK/dV this item writes (the qkv bias gradient,
+    // so the wgrad GEMM needs no column-sum pass): each thread sums its 4 rows.
+    float cs[3][8];
 #define DPA_CP(C)                                                                         \
   {                                                                                       \
     const bf16x8 v = rd128o<(C >> 2) * IMG + (C & 3) * 4096>(ca);                         \
     lgkm0();                                                                              \
     *reinterpret_cast<bf16x8*>(gb + (int64_t)(crow + 32 * (C & 3)) * ld +                 \
                                (int64_t)(C >> 2) * H * HD + cch * 8) = v;                \
+    _Pragma("unroll") for (int j = 0; j < 8; ++j) {                                       \
+      const float f = __uint_as_float((uint32_t)(uint16_t)v[j] << 16);                    \
+      cs[C >> 2][j] = (C & 3) ? cs[C >> 2][j] + f : f;                                    \
+    }                                                                                     \
   }
     DPA_CP(0) DPA_CP(1) DPA_CP(2) DPA_CP(3) DPA_CP(4) DPA_CP(5)
     DPA_CP(6) DPA_CP(7) DPA_CP(8) DPA_CP(9) DPA_CP(10) DPA_CP(11)
 #undef DPA_CP
     barrier();  // staging fully read before the next item's DMA lands on it
+    if (colpart != nullptr) {
+      // [32 row groups][192 columns] fp32 partials over the (now free) staging area
+      const uint32_t pa = base + (uint32_t)(crow * 192 + cch * 8) * 4;
+#pragma unroll
+      for (int q = 0; q < 3; ++q) {
+        wr_f4(pa + q * 256, f32x4{cs[q][0], cs[q][1], cs[q][2], cs[q][3]});
+        wr_f4(pa + q * 256 + 16, f32x4{cs[q][4], cs[q][5], cs[q][6], cs[q][7]});
+      }
+      barrier();
+      if (tid < 192) {
+        // inline-asm LDS reads carry no implicit wait: load all, lgkmcnt(0), then add
+        float v[32];
+#pragma unroll
+        for (int r = 0; r < 32; ++r) v[r] = rd_f1(base + (uint32_t)(r * 192 + tid) * 4);
+        lgkm0();
+        float t = 0.f;
+#pragma unroll
+        for (int r = 0; r < 32; ++r) t += v[r];
+        colpart[(int64_t)item * 192 + tid] = t;
+      }
+      barrier();
+    }
   }
+}
+
+// db[q*H*64 + h*64 + d] += sum_b colpart[(b*H + h)*192 + q*64 + d]: grid (H*3, chunks of B)
+__global__ void __launch_bounds__(256) colpart_reduce_kernel(const float* __restrict__ colpart,
+                                                             float* __restrict__ db, int B, int H,
+                                                             int bchunk) {
+  __shared__ float red[4][64];
+  const int hq = blockIdx.x, h = hq / 3, q = hq - 3 * h;
+  const int d = threadIdx.x & 63, r = threadIdx.x >> 6;
+  const int b0 = blockIdx.y * bchunk, b1 = min(B, b0 + bchunk);
+  float t = 0.f;
+  for (int b = b0 + r; b < b1; b += 4) t += colpart[((int64_t)b * H + h) * 192 + q * 64 + d];
+  red[r][d] = t;
+  __syncthreads();
+  if (r == 0) atomicAdd(db + q * H * HD + h * HD + d, red[0][d] + red[1][d] + red[2][d] + red[3][d]);
 }
 
 static bool enabled() {
@@ -618,14 +670,21 @@ bool launch_attn128_fwd(const uint16_t* qkv, uint16_t* out, float* lse, int B, i
 }
 
 bool launch_attn128_bwd(const uint16_t* qkv, const uint16_t* out, const uint16_t* dout,
-                        const float* lse, uint16_t* dqkv, int B, int Lq, int H, float p, bool causal,
-                        uint32_t seed, uint32_t offset, hipStream_t s) {
+                        const float* lse, uint16_t* dqkv, float* colpart, float* dbias, int B,
+                        int Lq, int H, float p, bool causal, uint32_t seed, uint32_t offset,
+                        hipStream_t s) {
   if (Lq != a128::L || causal || !a128::enabled()) return false;
   const int items = B * H, slots = 2 * a128::num_cus();
   const int grid = items < slots ? items : slots;
   hipLaunchKernelGGL(a128::attn128_bwd_kernel, dim3(grid), dim3(256), 0, s, (const bf16_t*)qkv,
-                     (const bf16_t*)out, (const bf16_t*)dout, lse, (bf16_t*)dqkv, B, H, p, seed,
-                     offset);
+                     (const bf16_t*)out, (const bf16_t*)dout, lse, (bf16_t*)dqkv,
+                     dbias ? colpart : nullptr, B, H, p, seed, offset);
+  if (dbias) {
+    const int bchunk = 64, nch = (B + bchunk - 1) / bchunk;
+    hipMemsetAsync(dbias, 0, sizeof(float) * 3 * H * a128::HD, s);
+    hipLaunchKernelGGL(a128::colpart_reduce_kernel, dim3(3 * H, nch), dim3(256), 0, s, colpart,
+                       dbias, B, H, bchunk);
+  }
   return true;
 }
 

@@ -187,7 +187,8 @@ static std::vector<at::Tensor> add_ln_fwd(const at::Tensor& y, c10::optional<at:
 static std::vector<at::Tensor> add_ln_bwd(const at::Tensor& dout, const at::Tensor& hs,
                                           const at::Tensor& mean, const at::Tensor& rstd,
                                           const at::Tensor& g, double p, int64_t seed,
-                                          int64_t offset, bool need_dres, bool need_dy) {
+                                          int64_t offset, bool need_dres, bool need_dy,
+                                          bool want_dyb) {
   CHECK_DEV(dout); CHECK_BF16(dout); CHECK_CONTIG(dout); CHECK_BF16(hs); CHECK_CONTIG(hs);
   const int64_t R = dout.size(0);
   const int D = (int)dout.size(1);
@@ -198,16 +199,18 @@ static std::vector<at::Tensor> add_ln_bwd(const at::Tensor& dout, const at::Tens
   auto f32 = dout.options().dtype(at::kFloat);
   const int nb = dpa::ln_bwd_blocks(R);
   (void)nb;
-  at::Tensor part;
+  at::Tensor dyb;
+  if (need_dy && want_dyb) dyb = at::empty({D}, f32);
   at::Tensor dg = at::empty({D}, f32), db = at::empty({D}, f32);
   bool ok = dpa::launch_add_ln_bwd(
       bf_ptr(dout), bf_ptr(hs), mean.data_ptr<float>(), rstd.data_ptr<float>(), bf_ptr(g),
       need_dres ? reinterpret_cast<uint16_t*>(dres.data_ptr()) : nullptr,
-      need_dy ? reinterpret_cast<uint16_t*>(dy.data_ptr()) : nullptr, nullptr,
+      need_dy ? reinterpret_cast<uint16_t*>(dy.data_ptr()) : nullptr,
+      dyb.defined() ? dyb.data_ptr<float>() : nullptr,
       dg.data_ptr<float>(), db.data_ptr<float>(), R, D, (float)p, (uint32_t)seed, (uint32_t)offset,
       cur_stream());
   TORCH_CHECK(ok, "add_ln_bwd: unsupported hidden size ", D);
-  return {dres, dy, dg, db};
+  return {dres, dy, dg, db, dyb};
 }
 
 // ---- bias + activation epilogues ------------------------------------------------------
@@ -263,22 +266,29 @@ static std::vector<at::Tensor> attn_fwd(const at::Tensor& qkv, int64_t heads, do
   return {out, lse};
 }
 
-static at::Tensor attn_bwd(const at::Tensor& dout, const at::Tensor& qkv, const at::Tensor& out,
-                           const at::Tensor& lse, int64_t heads, double p, bool causal, int64_t seed,
-                           int64_t offset) {
+static std::vector<at::Tensor> attn_bwd(const at::Tensor& dout, const at::Tensor& qkv,
+                                        const at::Tensor& out, const at::Tensor& lse, int64_t heads,
+                                        double p, bool causal, int64_t seed, int64_t offset,
+                                        bool want_db) {
   CHECK_DEV(dout); CHECK_BF16(dout); CHECK_CONTIG(dout); CHECK_CONTIG(out); CHECK_CONTIG(qkv);
   const int B = (int)qkv.size(0), L = (int)qkv.size(1), H = (int)heads;
   TORCH_CHECK(dout.sizes() == out.sizes(), "dout shape");
   const c10::DeviceGuard guard(qkv.device());
   at::Tensor dqkv = at::empty_like(qkv);
-  at::Tensor delta = at::empty({B, H, L}, qkv.options().dtype(at::kFloat));
-  at::Tensor dq;
-  if (dpa::attn_bwd_needs_dq_acc(L)) dq = at::zeros({B, L, H, 64}, qkv.options().dtype(at::kFloat));
-  dpa::launch_attn_bwd(bf_ptr(qkv), bf_ptr(out), bf_ptr(dout), lse.data_ptr<float>(),
-                       delta.data_ptr<float>(), reinterpret_cast<uint16_t*>(dqkv.data_ptr()),
-                       dq.defined() ? dq.data_ptr<float>() : nullptr, B, L, H, (float)p, causal,
-                       (uint32_t)seed, (uint32_t)offset, cur_stream());
-  return dqkv;
+  auto f32 = qkv.options().dtype(at::kFloat);
+  at::Tensor delta = at::empty({B, H, L}, f32);
+  at::Tensor dq, colpart, db;
+  if (dpa::attn_bwd_needs_dq_acc(L)) dq = at::zeros({B, L, H, 64}, f32);
+  if (want_db) {
+    colpart = at::empty({(int64_t)B * H * 192}, f32);
+    db = at::empty({3 * H * 64}, f32);
+  }
+  const bool got = dpa::launch_attn_bwd(
+      bf_ptr(qkv), bf_ptr(out), bf_ptr(dout), lse.data_ptr<float>(), delta.data_ptr<float>(),
+      reinterpret_cast<uint16_t*>(dqkv.data_ptr()), dq.defined() ? dq.data_ptr<float>() : nullptr,
+      want_db ? colpart.data_ptr<float>() : nullptr, want_db ? db.data_ptr<float>() : nullptr, B, L,
+      H, (float)p, causal, (uint32_t)seed, (uint32_t)offset, cur_stream());
+  return {dqkv, got ? db : at::Tensor()};
 }
 
 // ---- GEMMs ---------------------------------------------------------------------------
@@ -357,11 +367,16 @@ PYBIND11_MODULE(_C, m) {
   m.def("ema_update", &ema_update, "flat EMA update");
   m.def("cast_bf16", &cast_bf16, "flat fp32->bf16");
   m.def("add_ln_fwd", &add_ln_fwd, "LN(dropout(y)+res) -> (out, hsave, mean, rstd)");
-  m.def("add_ln_bwd", &add_ln_bwd, "backward of add_ln_fwd -> (dres, dy, dgamma, dbeta)");
+  m.def("add_ln_bwd", &add_ln_bwd, "backward of add_ln_fwd -> (dres, dy, dgamma, dbeta, colsum(dy))",
+        py::arg("dout"), py::arg("hsave"), py::arg("mean"), py::arg("rstd"), py::arg("gamma"),
+        py::arg("p"), py::arg("seed"), py::arg("offset"), py::arg("need_dres"), py::arg("need_dy"),
+        py::arg("want_dy_colsum") = false);
   m.def("bias_act_fwd", &bias_act_fwd, "z += bias (in place); y = act(z) -> (z, y)");
   m.def("bias_act_bwd", &bias_act_bwd, "dz = dy*act'(zy); db = colsum(dz) -> (dz, db)");
   m.def("attn_fwd", &attn_fwd, "fused attention forward (head_dim 64) -> (out, lse)");
-  m.def("attn_bwd", &attn_bwd, "fused attention backward -> dqkv");
+  m.def("attn_bwd", &attn_bwd, "fused attention backward -> (dqkv, colsum(dqkv) or None)",
+        py::arg("dout"), py::arg("qkv"), py::arg("out"), py::arg("lse"), py::arg("heads"), py::arg("p"),
+        py::arg("causal"), py::arg("seed"), py::arg("offset"), py::arg("want_db") = false);
   m.def("gemm_nt", &gemm_nt, "y = act(x W^T + b) (bf16 MFMA) -> (y, z_preact)");
   m.def("gemm_nn", &gemm_nn, "dx = dy W (bf16 MFMA)");
   m.def("gemm_nn_dact", &gemm_nn_dact, "dz = (dy W) * act'(aux) (bf16 MFMA, fused act backward)");

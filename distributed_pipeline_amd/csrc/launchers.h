@@ -34,8 +34,9 @@ bool launch_add_ln_fwd(const uint16_t* y, const uint16_t* res, const uint16_t* g
                        uint16_t* out, uint16_t* hsave, float* mean, float* rstd, int64_t R, int D,
                        float p, float eps, uint32_t seed, uint32_t off, hipStream_t s);
 int ln_bwd_blocks(int64_t R);
+// dyb (nullable): column sums of dy (the bias gradient of the layer producing y)
 bool launch_add_ln_bwd(const uint16_t* dout, const uint16_t* hsave, const float* mean,
-                       const float* rstd, const uint16_t* g, uint16_t* dres, uint16_t* dy, float* part,
+                       const float* rstd, const uint16_t* g, uint16_t* dres, uint16_t* dy, float* dyb,
                        float* dg, float* db, int64_t R, int D, float p, uint32_t seed, uint32_t off,
                        hipStream_t s);
 
@@ -52,12 +53,16 @@ bool attn_bwd_needs_dq_acc(int L);
 // attention128.hip: persistent L = 128 bidirectional kernels (false: not applicable)
 bool launch_attn128_fwd(const uint16_t* qkv, uint16_t* out, float* lse, int B, int L, int H,
                         float p, bool causal, uint32_t seed, uint32_t offset, hipStream_t s);
+// colpart [B*H][192] fp32 scratch; when dbias != nullptr also writes the column sums of
+// dqkv (the qkv bias gradient) into dbias [3*H*64] (overwritten).
 bool launch_attn128_bwd(const uint16_t* qkv, const uint16_t* out, const uint16_t* dout,
-                        const float* lse, uint16_t* dqkv, int B, int L, int H, float p, bool causal,
-                        uint32_t seed, uint32_t offset, hipStream_t s);
-void launch_attn_bwd(const uint16_t* qkv, const uint16_t* out, const uint16_t* dout, const float* lse,
-                     float* delta, uint16_t* dqkv, float* dq_acc, int B, int L, int H, float p,
-                     bool causal, uint32_t seed, uint32_t offset, hipStream_t s);
+                        const float* lse, uint16_t* dqkv, float* colpart, float* dbias, int B,
+                        int L, int H, float p, bool causal, uint32_t seed, uint32_t offset,
+                        hipStream_t s);
+// Returns true when the column sums of dqkv were written to dbias (L == 128 path).
+bool launch_attn_bwd(const uint16_t* qkv, const uint16_t* out, const uint16_t* dout, const float* lse,
+                     float* delta, uint16_t* dqkv, float* dq_acc, float* colpart, float* dbias, int B,
+                     int L, int H, float p, bool causal, uint32_t seed, uint32_t offset, hipStream_t s);
 
 // ---- xent2.hip: E = 128 LDS-DMA pipelined fused linear-CE (used by xent.hip) ----
 bool launch_lxent2_fwd(const uint16_t* x, const uint16_t* W, const uint16_t* b, const int64_t* tgt,

@@ -123,16 +123,16 @@ __global__ void __launch_bounds__(256) add_ln_bwd_kernel(
     const bf16_t* __restrict__ dout, const bf16_t* __restrict__ hsave,
     const float* __restrict__ mean_in, const float* __restrict__ rstd_in,
     const bf16_t* __restrict__ gamma, bf16_t* __restrict__ dres, bf16_t* __restrict__ dy,
-    float* __restrict__ part_dg, float* __restrict__ part_db, int64_t R, float p, uint32_t seed,
-    uint32_t offset) {
+    float* __restrict__ dyb, float* __restrict__ part_dg, float* __restrict__ part_db, int64_t R,
+    float p, uint32_t seed, uint32_t offset) {
   constexpr int D = VEC * 64;
-  __shared__ float red[2][4][D];
+  __shared__ float red[3][4][D];
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int col0 = lane * VEC;
-  float g[VEC], adg[VEC], adb[VEC];
+  float g[VEC], adg[VEC], adb[VEC], ady[VEC];
   RowIO<VEC>::load(gamma + col0, g);
 #pragma unroll
-  for (int i = 0; i < VEC; ++i) { adg[i] = 0.f; adb[i] = 0.f; }
+  for (int i = 0; i < VEC; ++i) { adg[i] = 0.f; adb[i] = 0.f; ady[i] = 0.f; }
   const float sc = p > 0.f ? 1.f / (1.f - p) : 1.f;
   for (int64_t row = (int64_t)blockIdx.x * 4 + w; row < R; row += (int64_t)gridDim.x * 4) {
     float h[VEC], d[VEC];
@@ -164,18 +164,25 @@ __global__ void __launch_bounds__(256) add_ln_bwd_kernel(
         for (int i = 0; i < VEC; ++i) d[i] = keep[i] ? d[i] * sc : 0.f;
       }
       RowIO<VEC>::store(dy + row * D + col0, d);
+      if (dyb) {
+        // bias gradient of the layer that produced y: column sums of the bf16 dy
+#pragma unroll
+        for (int i = 0; i < VEC; ++i) ady[i] += bf2f(f2bf(d[i]));
+      }
     }
   }
 #pragma unroll
   for (int i = 0; i < VEC; ++i) {
     red[0][w][col0 + i] = adg[i];
     red[1][w][col0 + i] = adb[i];
+    red[2][w][col0 + i] = ady[i];
   }
   __syncthreads();
-  // one fp32 atomic per column per block (dg/db zeroed by the launcher)
+  // one fp32 atomic per column per block (dg/db/dyb zeroed by the launcher)
   for (int c = threadIdx.x; c < D; c += blockDim.x) {
     atomicAdd(part_dg + c, red[0][0][c] + red[0][1][c] + red[0][2][c] + red[0][3][c]);
     atomicAdd(part_db + c, red[1][0][c] + red[1][1][c] + red[1][2][c] + red[1][3][c]);
+    if (dyb) atomicAdd(dyb + c, red[2][0][c] + red[2][1][c] + red[2][2][c] + red[2][3][c]);
   }
 }
 
@@ -217,23 +224,23 @@ int ln_bwd_blocks(int64_t R) {
 template <int VEC>
 static void ln_bwd_impl(const uint16_t* dout, const uint16_t* hsave, const float* mean,
                         const float* rstd, const uint16_t* g, uint16_t* dres, uint16_t* dy,
-                        float* part, float* dg, float* db, int64_t R, float p, uint32_t seed,
+                        float* dyb, float* dg, float* db, int64_t R, float p, uint32_t seed,
                         uint32_t off, hipStream_t s) {
   constexpr int D = VEC * 64;
   const int nb = ln_bwd_blocks(R);
-  (void)part;
   hipMemsetAsync(dg, 0, sizeof(float) * D, s);
   hipMemsetAsync(db, 0, sizeof(float) * D, s);
+  if (dyb) hipMemsetAsync(dyb, 0, sizeof(float) * D, s);
   hipLaunchKernelGGL(add_ln_bwd_kernel<VEC>, dim3(nb), dim3(256), 0, s, (const bf16_t*)dout,
                      (const bf16_t*)hsave, mean, rstd, (const bf16_t*)g, (bf16_t*)dres, (bf16_t*)dy,
-                     dg, db, R, p, seed, off);
+                     dy ? dyb : nullptr, dg, db, R, p, seed, off);
 }
 
 bool launch_add_ln_bwd(const uint16_t* dout, const uint16_t* hsave, const float* mean,
-                       const float* rstd, const uint16_t* g, uint16_t* dres, uint16_t* dy, float* part,
+                       const float* rstd, const uint16_t* g, uint16_t* dres, uint16_t* dy, float* dyb,
                        float* dg, float* db, int64_t R, int D, float p, uint32_t seed, uint32_t off,
                        hipStream_t s) {
-  DPA_LN_DISPATCH(D, ln_bwd_impl, dout, hsave, mean, rstd, g, dres, dy, part, dg, db, R, p, seed,
+  DPA_LN_DISPATCH(D, ln_bwd_impl, dout, hsave, mean, rstd, g, dres, dy, dyb, dg, db, R, p, seed,
                   off, s)
   return true;
 }

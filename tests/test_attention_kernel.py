@@ -39,7 +39,12 @@ def test_attention_no_dropout(B, L, H, causal):
     torch.testing.assert_close(out.float(), ref_o, rtol=2e-2, atol=2e-2)
     dout = torch.randn_like(ref_o)
     ref_o.backward(dout)
-    dqkv = _ext().attn_bwd(dout.bfloat16(), qkv, out, lse, H, 0.0, causal, 1, 0)
+    dqkv, dbias = _ext().attn_bwd(dout.bfloat16(), qkv, out, lse, H, 0.0, causal, 1, 0, True)
+    if L == 128 and not causal:  # persistent L=128 kernel also column-sums dqkv (qkv bias grad)
+        ref_db = dqkv.float().sum((0, 1))
+        torch.testing.assert_close(dbias, ref_db, rtol=1e-3, atol=1e-3 * ref_db.abs().max().item())
+    else:
+        assert dbias is None
     g = x.grad
     for i, name in enumerate("qkv"):
         a = dqkv.view(B, L, 3, H * 64)[:, :, i].float()
@@ -73,5 +78,5 @@ def test_attention_dropout_consistent_with_mask():
     torch.testing.assert_close(out.float(), ref_o, rtol=3e-2, atol=3e-2)
     dout = torch.randn_like(ref_o)
     ref_o.backward(dout)
-    dqkv = _ext().attn_bwd(dout.bfloat16(), qkv, out, lse, H, p, False, 11, 5)
+    dqkv, _ = _ext().attn_bwd(dout.bfloat16(), qkv, out, lse, H, p, False, 11, 5)
     torch.testing.assert_close(dqkv.float(), x.grad, rtol=5e-2, atol=5e-2 * x.grad.abs().max().item())

@@ -39,8 +39,12 @@ def test_diffuseq_native_bf16_matches_fp32(monkeypatch):
         terms["loss"].mean().backward()
         return {k: v.detach().float() for k, v in terms.items()}
 
+    from distributed_pipeline_amd.ops import nn as opsnn
     tr = run(ref)
+    taken0 = opsnn.DB_HANDOFF_STATS["taken"]
     tn = run(eng)
+    # per layer: attention (qkv), out-proj LN and FFN LN hand their bias grads over
+    assert opsnn.DB_HANDOFF_STATS["taken"] - taken0 >= 3 * CFG["num_layers"]
     for k in ("mse", "decoder_nll", "loss", "nll"):
         torch.testing.assert_close(tn[k], tr[k], rtol=3e-2, atol=3e-2, msg=k)
     gr, gn = _grads(ref), _grads(nat)

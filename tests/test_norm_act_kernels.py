@@ -28,8 +28,10 @@ def test_add_ln_no_dropout(R, D, res):
     torch.testing.assert_close(out.float(), ref, rtol=2e-2, atol=2e-2)
     dout = torch.randn(R, D, device="cuda").bfloat16()
     ref.backward(dout.float())
-    dres, dy, dg, db = _ext().add_ln_bwd(dout, hs, mean, rstd, g, 0.0, 1, 0, res, True)
+    dres, dy, dg, db, dyb = _ext().add_ln_bwd(dout, hs, mean, rstd, g, 0.0, 1, 0, res, True, True)
     torch.testing.assert_close(dy.float(), h.grad, rtol=2e-2, atol=2e-2)
+    ref_dyb = dy.float().sum(0)  # column sums of the emitted bf16 dy (next layer's bias grad)
+    torch.testing.assert_close(dyb, ref_dyb, rtol=1e-3, atol=1e-3 * ref_dyb.abs().max().item())
     if res:
         torch.testing.assert_close(dres.float(), h.grad, rtol=2e-2, atol=2e-2)
     torch.testing.assert_close(dg, gf.grad, rtol=1e-2, atol=1e-2 * gf.grad.abs().max().item())
@@ -51,8 +53,9 @@ def test_add_ln_dropout_statistics_and_consistency():
     assert torch.equal(hs, hs2) and not torch.equal(hs, hs3)
     # backward regenerates the same mask: dy is zero exactly where dropped
     dout = torch.randn(R, D, device="cuda").bfloat16()
-    _, dy, _, _ = _ext().add_ln_bwd(dout, hs, mean, rstd, g, p, 7, 3, False, True)
+    _, dy, _, _, dyb = _ext().add_ln_bwd(dout, hs, mean, rstd, g, p, 7, 3, False, True, True)
     assert torch.equal(dy == 0, hs == 0)
+    torch.testing.assert_close(dyb, dy.float().sum(0), rtol=1e-3, atol=1e-2)
 
 
 @pytest.mark.parametrize("act", ["none", "gelu", "tanh", "silu"])

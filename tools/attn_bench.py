@@ -48,11 +48,13 @@ def main():
         dout = torch.randn_like(out)
         f = bench(lambda: ext.attn_fwd(qkv, H, p, False, 1, 0))
         b = bench(lambda: ext.attn_bwd(dout, qkv, out, lse, H, p, False, 1, 0))
+        bdb = bench(lambda: ext.attn_bwd(dout, qkv, out, lse, H, p, False, 1, 0, True))
         gb_f = (qkv.numel() + out.numel()) * 2 / 1e9
         gb_b = (qkv.numel() * 2 + out.numel() * 2) * 2 / 1e9
         print(json.dumps({"B": B, "H": H, "L": L, "p": p, "attn128": os.environ.get("DPA_ATTN128", "1"),
                           "fwd_ms": round(f, 3), "fwd_GBps": round(gb_f / f * 1e3, 1),
                           "bwd_ms": round(b, 3), "bwd_GBps": round(gb_b / b * 1e3, 1),
+                          "bwd_with_bias_colsum_ms": round(bdb, 3),
                           "fwd_us_per_item_per_cu": round(f * 1e3 / (B * H / 256), 2),
                           "bwd_us_per_item_per_cu": round(b * 1e3 / (B * H / 256), 2)}), flush=True)
 

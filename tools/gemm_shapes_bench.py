@@ -59,8 +59,10 @@ def main():
             gacc.zero_()
             ext.gemm_wgrad(dz, x, gacc, None)
             err = (gacc - ref).abs().max().item() / ref.abs().max().item()
+            gb = torch.zeros(N, device=dev)
+            nwb = bench(lambda: ext.gemm_wgrad(dz, x, gacc, gb))
             rec.update(native_wgrad_ms=round(nw, 3), native_wgrad_TF=round(fl / nw / 1e9, 1),
-                       native_wgrad_relerr=err)
+                       native_wgrad_relerr=err, native_wgrad_with_db_ms=round(nwb, 3))
         if ext is not None and hasattr(ext, "gemm_nt"):
             nf = bench(lambda: ext.gemm_nt(x, w, b, 0))
             y = ext.gemm_nt(x, w, b, 0)[0]
