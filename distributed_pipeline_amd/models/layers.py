@@ -111,10 +111,12 @@ class BertLayer(nn.Module):
         self.ffn_ln = LayerNorm(hidden, eps)
 
     def forward(self, x):
-        a = self.attn_out(self.attn(x))
-        h = self.attn_ln(a, residual=x, dropout=self.dropout)
-        f = ops.mlp(h, self.ffn_in, self.ffn_out)
-        return self.ffn_ln(f, residual=h, dropout=self.dropout)
+        # each post-LN sublayer runs as one fused op on the HIP path (the op owns
+        # both uses of its input, so the residual-branch gradient is accumulated
+        # by the dgrad GEMM); the composed ops otherwise
+        h = ops.attn_add_ln(x, self.attn.qkv, self.attn_out, self.attn_ln, self.attn.heads,
+                            self.attn.dropout, self.dropout, self.training)
+        return ops.mlp_add_ln(h, self.ffn_in, self.ffn_out, self.ffn_ln, self.dropout, self.training)
 
 
 class BertEncoder(nn.Module):

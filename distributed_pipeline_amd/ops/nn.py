@@ -193,7 +193,7 @@ def _lin_fwd(x2, w16, b16, act, route):
 # here and the Linear's backward takes it, so the wgrad GEMM does not reduce dz
 # a second time (measured: +30% wgrad time for the in-GEMM column sum).
 _DB_OFFER = [None]
-DB_HANDOFF_STATS = {"offered": 0, "taken": 0}
+DB_HANDOFF_STATS = {"offered": 0, "taken": 0, "fused_sublayers": 0}
 
 
 def _offer_db(g, db):
@@ -282,6 +282,53 @@ def linear(x, weight, bias=None, act="none"):
     return _LinearFn.apply(x, weight, bias, shadow(weight, x.dtype), shadow(bias, x.dtype), act)
 
 
+def _dgrad_acc(dz, w16, native, dx_acc):
+    """dx = dz @ W (+ dx_acc).  With hipBLASLt the residual-branch gradient is
+    accumulated by the GEMM itself (beta = 1, in place on ``dx_acc``), which
+    replaces autograd's separate bf16 add of the two branches."""
+    if dx_acc is None:
+        return _dgrad(dz, w16, native)
+    if not native and dz.is_cuda:
+        return dx_acc.addmm_(dz, w16)
+    return dx_acc.add_(_dgrad(dz, w16, native))
+
+
+def _mlp_fwd(x2, w1_16, b1_16, w2_16, b2_16, act):
+    r1 = _route(x2, w1_16.shape[0], act)
+    h, z1 = _lin_fwd(x2, w1_16, b1_16, act, r1)
+    r2 = _route(h, w2_16.shape[0], "none")
+    y, _ = _lin_fwd(h, w2_16, b2_16, "none", r2)
+    return y, h, z1, (act, r1, r2)
+
+
+def _mlp_bwd(dy2, x2, w1_16, w2_16, h, z1, params, cfg, need_dx, db2=None, dx_acc=None):
+    """Backward of fc2(act(fc1(x))) -> (dx, dw1, db1, dw2, db2)."""
+    w1, b1, w2, b2 = params
+    act, r1, r2 = cfg
+    # fc2 parameter grads
+    if db2 is None and b2 is not None:
+        db2 = _take_db(dy2)
+    if b2 is not None and db2 is None and not r2[2]:
+        _, db2 = _bias_act_bwd(dy2, None, None, "none", True)
+    dw2, db2 = _lin_param_grads(w2, b2, dy2, h, r2[2], db2)
+    # fc1 output gradient (activation backward fused into the dgrad epilogue in native mode)
+    aux = h if act == "tanh" else z1
+    dz1 = None
+    if act != "none" and GEMM_MODE == "native" and _gemm_shape_ok(dy2, w2_16.shape[1]):
+        dz1 = get_ext().gemm_nn_dact(dy2, w2_16, aux, _ACTS.index(act))
+    db1 = None
+    if dz1 is None:
+        dh = _dgrad(dy2, w2_16, r2[1])
+        if act != "none" or b1 is not None:
+            # the activation backward reads dh anyway: it also sums db1
+            dz1, db1 = _bias_act_bwd(dh, z1, h if act == "tanh" else None, act, b1 is not None)
+        else:
+            dz1 = dh
+    dx = _dgrad_acc(dz1, w1_16, r1[1], dx_acc) if need_dx else None
+    dw1, db1 = _lin_param_grads(w1, b1, dz1, x2, r1[2], db1)
+    return dx, dw1, db1, dw2, db2
+
+
 class _MLPFn(torch.autograd.Function):
     """y = fc2(act(fc1(x))) as one op, so the backward can fuse fc1's activation
     derivative into fc2's data-gradient GEMM epilogue (dz1 = (dy W2) * act'(z1)):
@@ -292,42 +339,159 @@ class _MLPFn(torch.autograd.Function):
     def forward(ctx, x, w1, b1, w2, b2, w1_16, b1_16, w2_16, b2_16, act):
         shp = x.shape
         x2 = x.reshape(-1, shp[-1])
-        r1 = _route(x2, w1_16.shape[0], act)
-        h, z1 = _lin_fwd(x2, w1_16, b1_16, act, r1)
-        r2 = _route(h, w2_16.shape[0], "none")
-        y, _ = _lin_fwd(h, w2_16, b2_16, "none", r2)
+        y, h, z1, cfg = _mlp_fwd(x2, w1_16, b1_16, w2_16, b2_16, act)
         ctx.save_for_backward(x2, w1_16, w2_16, h, z1)
         ctx.params = (w1, b1, w2, b2)
-        ctx.cfg = (act, r1, r2, shp)
+        ctx.cfg = cfg
+        ctx.shp = shp
         return y.reshape(*shp[:-1], w2_16.shape[0])
 
     @staticmethod
     def backward(ctx, dy):
         x2, w1_16, w2_16, h, z1 = ctx.saved_tensors
-        w1, b1, w2, b2 = ctx.params
-        act, r1, r2, shp = ctx.cfg
         dy2 = dy.reshape(-1, dy.shape[-1]).contiguous()
-        # fc2 parameter grads
-        db2 = _take_db(dy2) if b2 is not None else None
-        if b2 is not None and db2 is None and not r2[2]:
-            _, db2 = _bias_act_bwd(dy2, None, None, "none", True)
-        dw2, db2 = _lin_param_grads(w2, b2, dy2, h, r2[2], db2)
-        # fc1 output gradient with the activation backward fused into the dgrad epilogue
-        aux = h if act == "tanh" else z1
-        dz1 = None
-        if act != "none" and GEMM_MODE == "native" and _gemm_shape_ok(dy2, w2_16.shape[1]):
-            dz1 = get_ext().gemm_nn_dact(dy2, w2_16, aux, _ACTS.index(act))
-        db1 = None
-        want_db1 = b1 is not None  # free inside the activation backward pass
-        if dz1 is None:
-            dh = _dgrad(dy2, w2_16, r2[1])
-            if act != "none" or want_db1:
-                dz1, db1 = _bias_act_bwd(dh, z1, h if act == "tanh" else None, act, want_db1)
-            else:
-                dz1 = dh
-        dx = _dgrad(dz1, w1_16, r1[1]).reshape(shp) if ctx.needs_input_grad[0] else None
-        dw1, db1 = _lin_param_grads(w1, b1, dz1, x2, r1[2], db1)
+        dx, dw1, db1, dw2, db2 = _mlp_bwd(dy2, x2, w1_16, w2_16, h, z1, ctx.params, ctx.cfg,
+                                          ctx.needs_input_grad[0])
+        if dx is not None:
+            dx = dx.reshape(ctx.shp)
         return dx, dw1, db1, dw2, db2, None, None, None, None, None
+
+
+class _MLPLNFn(torch.autograd.Function):
+    """Post-LN FFN sublayer as one op: out = LN(dropout(fc2(act(fc1(x)))) + x).
+
+    Owning both uses of x lets the backward hand the LayerNorm's residual
+    gradient to fc1's dgrad GEMM as its accumulator (one GEMM writes
+    dx = dres + dz1 W1) and the LN backward's column sum of dy to fc2 as its
+    bias gradient - no autograd-side add of the two branch gradients."""
+
+    @staticmethod
+    def forward(ctx, x, w1, b1, w2, b2, lw, lb, w1_16, b1_16, w2_16, b2_16, lw16, lb16, act, p, eps,
+                seed, off):
+        shp = x.shape
+        x2 = x.reshape(-1, shp[-1])
+        y, h, z1, cfg = _mlp_fwd(x2, w1_16, b1_16, w2_16, b2_16, act)
+        out, hsave, mean, rstd = get_ext().add_ln_fwd(y, x2, lw16, lb16, float(p), float(eps), seed,
+                                                      off)
+        ctx.save_for_backward(x2, w1_16, w2_16, h, z1, hsave, mean, rstd, lw16)
+        ctx.params = (w1, b1, w2, b2)
+        ctx.cfg = cfg
+        ctx.ln = (p, seed, off)
+        ctx.shp = shp
+        return out.reshape(shp)
+
+    @staticmethod
+    def backward(ctx, dout):
+        x2, w1_16, w2_16, h, z1, hsave, mean, rstd, lw16 = ctx.saved_tensors
+        p, seed, off = ctx.ln
+        need_dx = ctx.needs_input_grad[0]
+        dres, dy, dlw, dlb, dyb = get_ext().add_ln_bwd(
+            dout.reshape(-1, dout.shape[-1]).contiguous(), hsave, mean, rstd, lw16, float(p), seed,
+            off, need_dx, True, True)
+        dx, dw1, db1, dw2, db2 = _mlp_bwd(dy, x2, w1_16, w2_16, h, z1, ctx.params, ctx.cfg, need_dx,
+                                          db2=dyb, dx_acc=dres)
+        if dx is not None:
+            dx = dx.reshape(ctx.shp)
+        return (dx, dw1, db1, dw2, db2, dlw, dlb) + (None,) * 11
+
+
+class _AttnLNFn(torch.autograd.Function):
+    """Post-LN self-attention sublayer as one op:
+    out = LN(dropout(Wo attn(Wqkv x + bqkv) + bo) + x)   (bidirectional).
+
+    Backward: LN backward (with the column sum of its dy = bo's gradient) ->
+    out-proj dgrad/wgrad -> attention backward (with the column sum of dqkv =
+    bqkv's gradient) -> qkv wgrad and a dgrad GEMM that accumulates onto the
+    LN's residual gradient in place."""
+
+    @staticmethod
+    def forward(ctx, x, wq, bq, wo, bo, lw, lb, wq16, bq16, wo16, bo16, lw16, lb16, heads, p_attn,
+                p, eps, seed_a, off_a, seed_l, off_l):
+        shp = x.shape
+        B, L, D = shp
+        x2 = x.reshape(-1, D)
+        rq = _route(x2, wq16.shape[0], "none")
+        qkv, _ = _lin_fwd(x2, wq16, bq16, "none", rq)
+        qkv3 = qkv.view(B, L, wq16.shape[0])
+        o, lse = get_ext().attn_fwd(qkv3, heads, float(p_attn), False, seed_a, off_a)
+        o2 = o.view(-1, o.shape[-1])
+        ro = _route(o2, wo16.shape[0], "none")
+        y, _ = _lin_fwd(o2, wo16, bo16, "none", ro)
+        out, hsave, mean, rstd = get_ext().add_ln_fwd(y, x2, lw16, lb16, float(p), float(eps), seed_l,
+                                                      off_l)
+        ctx.save_for_backward(x2, qkv3, o, lse, wq16, wo16, hsave, mean, rstd, lw16)
+        ctx.params = (wq, bq, wo, bo)
+        ctx.cfg = (heads, p_attn, seed_a, off_a, p, seed_l, off_l, rq, ro)
+        ctx.shp = shp
+        return out.reshape(shp)
+
+    @staticmethod
+    def backward(ctx, dout):
+        x2, qkv3, o, lse, wq16, wo16, hsave, mean, rstd, lw16 = ctx.saved_tensors
+        wq, bq, wo, bo = ctx.params
+        heads, p_attn, seed_a, off_a, p, seed_l, off_l, rq, ro = ctx.cfg
+        need_dx = ctx.needs_input_grad[0]
+        ext = get_ext()
+        dres, dy, dlw, dlb, dyb = ext.add_ln_bwd(
+            dout.reshape(-1, dout.shape[-1]).contiguous(), hsave, mean, rstd, lw16, float(p), seed_l,
+            off_l, need_dx, True, True)
+        # out projection
+        o2 = o.view(-1, o.shape[-1])
+        do = _dgrad(dy, wo16, ro[1])
+        dwo, dbo = _lin_param_grads(wo, bo, dy, o2, ro[2], dyb if bo is not None else None)
+        # attention
+        dqkv, dbq = ext.attn_bwd(do.view(o.shape), qkv3, o, lse, heads, float(p_attn), False, seed_a,
+                                 off_a, bq is not None)
+        dz = dqkv.view(-1, dqkv.shape[-1])
+        if bq is not None and dbq is None and not rq[2]:
+            _, dbq = _bias_act_bwd(dz, None, None, "none", True)
+        dx = _dgrad_acc(dz, wq16, rq[1], dres) if need_dx else None
+        dwq, dbq = _lin_param_grads(wq, bq, dz, x2, rq[2], dbq)
+        if dx is not None:
+            dx = dx.reshape(ctx.shp)
+        return (dx, dwq, dbq, dwo, dbo, dlw, dlb) + (None,) * 14
+
+
+def _ln_block_ok(x, *lins):
+    if x.dtype != torch.bfloat16 or x.dim() != 3 or not native_ok(x, kernel="add_ln_fwd"):
+        return False
+    D = x.shape[-1]
+    return D % 64 == 0 and D <= 2048 and all(lin.weight.dtype == torch.float32 for lin in lins)
+
+
+def mlp_add_ln(x, fc1, fc2, ln, p=0.0, training=True):
+    """Post-LN FFN sublayer LN(dropout(fc2(act(fc1(x)))) + x) as one fused op."""
+    p = p if training else 0.0
+    if not _ln_block_ok(x, fc1, fc2):
+        f = mlp(x, fc1, fc2)
+        return add_dropout_layernorm(f, x, ln.weight, ln.bias, p, ln.eps, training)
+    dt = x.dtype
+    seed, off = RNG.next()
+    DB_HANDOFF_STATS["fused_sublayers"] += 1
+    return _MLPLNFn.apply(x.contiguous(), fc1.weight, fc1.bias, fc2.weight, fc2.bias, ln.weight,
+                          ln.bias, shadow(fc1.weight, dt), shadow(fc1.bias, dt), shadow(fc2.weight, dt),
+                          shadow(fc2.bias, dt), shadow(ln.weight, dt), shadow(ln.bias, dt), fc1.act, p,
+                          ln.eps, seed, off)
+
+
+def attn_add_ln(x, qkv, out_proj, ln, heads, p_attn=0.0, p=0.0, training=True):
+    """Post-LN bidirectional self-attention sublayer LN(dropout(Wo attn(Wqkv x)) + x) as one op."""
+    p_attn = p_attn if training else 0.0
+    p = p if training else 0.0
+    B, L, D = x.shape if x.dim() == 3 else (0, 0, 0)
+    if (not _ln_block_ok(x, qkv, out_proj) or qkv.act != "none" or out_proj.act != "none"
+            or D % heads or D // heads != 64 or L % 64 or L > 1024
+            or not native_ok(x, kernel="attn_fwd")):
+        a = out_proj(attention(qkv(x), heads, p_attn, False, training))
+        return add_dropout_layernorm(a, x, ln.weight, ln.bias, p, ln.eps, training)
+    dt = x.dtype
+    seed_a, off_a = RNG.next()
+    seed_l, off_l = RNG.next()
+    DB_HANDOFF_STATS["fused_sublayers"] += 1
+    return _AttnLNFn.apply(x.contiguous(), qkv.weight, qkv.bias, out_proj.weight, out_proj.bias,
+                           ln.weight, ln.bias, shadow(qkv.weight, dt), shadow(qkv.bias, dt),
+                           shadow(out_proj.weight, dt), shadow(out_proj.bias, dt), shadow(ln.weight, dt),
+                           shadow(ln.bias, dt), heads, p_attn, p, ln.eps, seed_a, off_a, seed_l, off_l)
 
 
 def mlp(x, fc1, fc2):
