@@ -49,6 +49,8 @@ def parse():
     ap.add_argument("--bucket-cap-mb", type=float, default=32.0)
     ap.add_argument("--first-bucket-mb", type=float, default=4.0)
     ap.add_argument("--hip-graphs", type=int, default=0)
+    ap.add_argument("--zero1", type=int, default=0, help="ZeRO-1 sharded optimizer (N > 1)")
+    ap.add_argument("--grad-wire", default="fp32", choices=["fp32", "bf16"])
     ap.add_argument("--data-workers", type=int, default=2)
     ap.add_argument("--log-interval", type=int, default=20)
     ap.add_argument("--json-out", default=None)
@@ -102,7 +104,8 @@ def main():
               checkpoint_path=logdir, gradient_clipping=0.0, ddp_engine=engine,
               precision=precision, bucket_cap_mb=a.bucket_cap_mb,
               first_bucket_mb=a.first_bucket_mb, exec_microbatch=exec_mb,
-              hip_graphs=bool(a.hip_graphs))
+              hip_graphs=bool(a.hip_graphs), shard_optimizer=bool(a.zero1),
+              grad_reduce_dtype=a.grad_wire)
     if a.model == "gpt2":
         loop = LMTrainLoop(**kw)
     else:

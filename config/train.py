@@ -115,6 +115,8 @@ class PerfSettings(S):
         = _(4.0, "First (last-layer) bucket size (MiB) so communication starts early.")
     grad_reduce_dtype: Choice("fp32", "bf16") \
         = _("fp32", "Dtype on the wire for the gradient all-reduce.")
+    shard_optimizer: bool \
+        = _(False, "ZeRO-1: reduce-scatter gradients and shard AdamW moments + EMAs over the data-parallel ranks.")
     use_hip_kernels: bool \
         = _(True, "Use the hand-written gfx950 kernels (required on GPU).")
     exec_microbatch: int \

@@ -355,6 +355,181 @@ static void gemm_wgrad(const at::Tensor& dy, const at::Tensor& x, at::Tensor& dW
   TORCH_CHECK(ok, "gemm_wgrad: unsupported shape");
 }
 
+// ---- row softmax cross-entropy (chunked wide-E linear-CE) ------------------------------
+static void check_i64(const at::Tensor& t, const char* name) {
+  TORCH_CHECK(t.is_cuda() && t.scalar_type() == at::kLong && t.is_contiguous(), name,
+              " must be a contiguous int64 HIP tensor");
+}
+
+static std::vector<at::Tensor> xent_rows_fwd(const at::Tensor& lg, int64_t V, const at::Tensor& tgt) {
+  CHECK_DEV(lg); CHECK_BF16(lg); CHECK_CONTIG(lg); CHECK_ALIGNED(lg);
+  check_i64(tgt, "target");
+  TORCH_CHECK(lg.dim() == 2 && lg.size(1) % 8 == 0 && V > 0 && V <= lg.size(1),
+              "logits [R, ld] with ld % 8 == 0 and V <= ld");
+  TORCH_CHECK(tgt.numel() == lg.size(0), "target [R]");
+  const c10::DeviceGuard guard(lg.device());
+  auto f32 = lg.options().dtype(at::kFloat);
+  at::Tensor loss = at::empty({lg.size(0)}, f32), lse = at::empty({lg.size(0)}, f32);
+  dpa::launch_xent_rows_fwd(bf_ptr(lg), lg.size(1), (int)V, tgt.data_ptr<int64_t>(), lg.size(0),
+                            loss.data_ptr<float>(), lse.data_ptr<float>(), cur_stream());
+  return {loss, lse};
+}
+
+static void xent_rows_bwd_(at::Tensor& lg, int64_t V, const at::Tensor& tgt, const at::Tensor& lse,
+                           const at::Tensor& dloss) {
+  CHECK_DEV(lg); CHECK_BF16(lg); CHECK_CONTIG(lg); CHECK_ALIGNED(lg);
+  check_i64(tgt, "target");
+  CHECK_F32(lse); CHECK_F32(dloss); CHECK_CONTIG(lse); CHECK_CONTIG(dloss);
+  TORCH_CHECK(lg.dim() == 2 && lg.size(1) % 8 == 0 && V > 0 && V <= lg.size(1), "logits [R, ld]");
+  const int64_t R = lg.size(0);
+  TORCH_CHECK(tgt.numel() == R && lse.numel() == R && dloss.numel() == R, "per-row tensors [R]");
+  const c10::DeviceGuard guard(lg.device());
+  dpa::launch_xent_rows_bwd(reinterpret_cast<uint16_t*>(lg.data_ptr()), lg.size(1), (int)V,
+                            tgt.data_ptr<int64_t>(), lse.data_ptr<float>(), dloss.data_ptr<float>(), R,
+                            cur_stream());
+}
+
+// ---- DiffuSeq diffusion kernels ------------------------------------------------------------
+static void check_diffusion_common(const at::Tensor& ids, const at::Tensor& t, const at::Tensor& W) {
+  check_i64(ids, "ids");
+  check_i64(t, "t");
+  CHECK_DEV(W); CHECK_F32(W); CHECK_CONTIG(W); CHECK_ALIGNED(W);
+  TORCH_CHECK(ids.dim() == 2 && t.dim() == 1 && t.size(0) == ids.size(0), "ids [B, L], t [B]");
+  TORCH_CHECK(W.dim() == 2 && W.size(1) % 4 == 0, "W [V, E] with E % 4 == 0");
+}
+
+static std::vector<at::Tensor> emb_qsample_fwd(const at::Tensor& ids, const at::Tensor& mask,
+                                               const at::Tensor& t, const at::Tensor& W,
+                                               const at::Tensor& sa, const at::Tensor& s1a, double std0,
+                                               int64_t seed, int64_t offset, bool want_x16) {
+  check_diffusion_common(ids, t, W);
+  check_i64(mask, "mask");
+  TORCH_CHECK(mask.sizes() == ids.sizes(), "mask [B, L]");
+  CHECK_DEV(sa); CHECK_F32(sa); CHECK_CONTIG(sa); CHECK_DEV(s1a); CHECK_F32(s1a); CHECK_CONTIG(s1a);
+  TORCH_CHECK(sa.numel() == s1a.numel() && sa.numel() > 0, "schedule tables [T]");
+  const int64_t B = ids.size(0), L = ids.size(1), E = W.size(1);
+  const c10::DeviceGuard guard(W.device());
+  auto bf = W.options().dtype(at::kBFloat16);
+  at::Tensor xs = at::empty({B, L, E}, W.options()), xt = at::empty({B, L, E}, bf), x16;
+  if (want_x16) x16 = at::empty({B, L, E}, bf);
+  if (B * L > 0)
+    dpa::launch_emb_qsample_fwd(ids.data_ptr<int64_t>(), mask.data_ptr<int64_t>(), t.data_ptr<int64_t>(),
+                                W.data_ptr<float>(), sa.data_ptr<float>(), s1a.data_ptr<float>(), B * L,
+                                (int)L, (int)E, (int)W.size(0), (float)std0, (uint32_t)seed,
+                                (uint32_t)offset, xs.data_ptr<float>(),
+                                want_x16 ? reinterpret_cast<uint16_t*>(x16.data_ptr()) : nullptr,
+                                reinterpret_cast<uint16_t*>(xt.data_ptr()), cur_stream());
+  return {xs, x16, xt};
+}
+
+static void emb_qsample_bwd(const at::Tensor& ids, const at::Tensor& mask, const at::Tensor& t,
+                            const at::Tensor& sa, c10::optional<at::Tensor> d_xs,
+                            c10::optional<at::Tensor> d_xs16, c10::optional<at::Tensor> d_xt,
+                            at::Tensor& dW) {
+  check_diffusion_common(ids, t, dW);
+  check_i64(mask, "mask");
+  CHECK_DEV(sa); CHECK_F32(sa); CHECK_CONTIG(sa);
+  const int64_t B = ids.size(0), L = ids.size(1), E = dW.size(1), n = B * L * E;
+  const float* p_xs = nullptr;
+  const uint16_t* p_xs16 = nullptr;
+  const uint16_t* p_xt16 = nullptr;
+  const float* p_xt32 = nullptr;
+  if (d_xs.has_value() && d_xs->defined()) {
+    CHECK_F32((*d_xs)); CHECK_CONTIG((*d_xs));
+    TORCH_CHECK(d_xs->numel() == n, "d_x_start size");
+    p_xs = d_xs->data_ptr<float>();
+  }
+  if (d_xs16.has_value() && d_xs16->defined()) {
+    CHECK_BF16((*d_xs16)); CHECK_CONTIG((*d_xs16));
+    TORCH_CHECK(d_xs16->numel() == n, "d_x_start16 size");
+    p_xs16 = bf_ptr(*d_xs16);
+  }
+  if (d_xt.has_value() && d_xt->defined()) {
+    CHECK_CONTIG((*d_xt));
+    TORCH_CHECK(d_xt->numel() == n, "d_x_t size");
+    if (d_xt->scalar_type() == at::kBFloat16) p_xt16 = bf_ptr(*d_xt);
+    else { CHECK_F32((*d_xt)); p_xt32 = d_xt->data_ptr<float>(); }
+  }
+  const c10::DeviceGuard guard(dW.device());
+  if (n > 0)
+    dpa::launch_emb_qsample_bwd(ids.data_ptr<int64_t>(), mask.data_ptr<int64_t>(), t.data_ptr<int64_t>(),
+                                sa.data_ptr<float>(), p_xs, p_xs16, p_xt16, p_xt32, B * L, (int)L, (int)E,
+                                (int)dW.size(0), dW.data_ptr<float>(), cur_stream());
+}
+
+static void check_loss_inputs(const at::Tensor& xs, const at::Tensor& out, const at::Tensor& ids,
+                              const at::Tensor& t, const at::Tensor& W) {
+  check_diffusion_common(ids, t, W);
+  CHECK_DEV(xs); CHECK_F32(xs); CHECK_CONTIG(xs); CHECK_ALIGNED(xs);
+  CHECK_DEV(out); CHECK_CONTIG(out);
+  TORCH_CHECK(out.scalar_type() == at::kBFloat16 || out.scalar_type() == at::kFloat,
+              "model output must be bf16 or fp32");
+  TORCH_CHECK(xs.dim() == 3 && xs.size(0) == ids.size(0) && xs.size(1) == ids.size(1) &&
+                  xs.size(2) == W.size(1) && out.sizes() == xs.sizes(),
+              "x_start / output [B, L, E] matching ids and W");
+}
+
+static std::vector<at::Tensor> diff_loss_fwd(const at::Tensor& xs, const at::Tensor& out,
+                                             const at::Tensor& ids, const at::Tensor& t,
+                                             const at::Tensor& W, double sa_last) {
+  check_loss_inputs(xs, out, ids, t, W);
+  const int64_t B = xs.size(0), L = xs.size(1), E = xs.size(2);
+  const c10::DeviceGuard guard(xs.device());
+  at::Tensor mse = at::empty({B}, xs.options()), tT = at::empty({B}, xs.options());
+  if (B > 0)
+    dpa::launch_diff_loss_fwd(xs.data_ptr<float>(), out.data_ptr(), out.scalar_type() == at::kBFloat16,
+                              ids.data_ptr<int64_t>(), t.data_ptr<int64_t>(), W.data_ptr<float>(), (int)B,
+                              (int)L, (int)E, (int)W.size(0), (float)sa_last, mse.data_ptr<float>(),
+                              tT.data_ptr<float>(), cur_stream());
+  return {mse, tT};
+}
+
+static std::vector<at::Tensor> diff_loss_bwd(const at::Tensor& xs, const at::Tensor& out,
+                                             const at::Tensor& ids, const at::Tensor& t,
+                                             const at::Tensor& W, c10::optional<at::Tensor> dmse,
+                                             c10::optional<at::Tensor> dtT, double sa_last, bool need_dout,
+                                             bool need_dxs, c10::optional<at::Tensor> dW) {
+  check_loss_inputs(xs, out, ids, t, W);
+  const int64_t B = xs.size(0), L = xs.size(1), E = xs.size(2);
+  const float* pm = nullptr;
+  const float* pt = nullptr;
+  if (dmse.has_value() && dmse->defined()) {
+    CHECK_F32((*dmse)); CHECK_CONTIG((*dmse)); TORCH_CHECK(dmse->numel() == B, "dmse [B]");
+    pm = dmse->data_ptr<float>();
+  }
+  if (dtT.has_value() && dtT->defined()) {
+    CHECK_F32((*dtT)); CHECK_CONTIG((*dtT)); TORCH_CHECK(dtT->numel() == B, "dtT [B]");
+    pt = dtT->data_ptr<float>();
+  }
+  float* pw = nullptr;
+  if (dW.has_value() && dW->defined()) {
+    CHECK_F32((*dW)); CHECK_CONTIG((*dW)); TORCH_CHECK(dW->sizes() == W.sizes(), "dW like W");
+    pw = dW->data_ptr<float>();
+  }
+  const c10::DeviceGuard guard(xs.device());
+  at::Tensor d_out, d_xs;
+  if (need_dout) d_out = at::empty_like(out);
+  if (need_dxs) d_xs = at::empty_like(xs);
+  if (B > 0 && (need_dout || need_dxs || pw))
+    dpa::launch_diff_loss_bwd(xs.data_ptr<float>(), out.data_ptr(), out.scalar_type() == at::kBFloat16,
+                              ids.data_ptr<int64_t>(), t.data_ptr<int64_t>(), W.data_ptr<float>(), pm, pt,
+                              (int)B, (int)L, (int)E, (int)W.size(0), (float)sa_last,
+                              need_dout ? d_out.data_ptr() : nullptr,
+                              need_dxs ? d_xs.data_ptr<float>() : nullptr, pw, cur_stream());
+  return {d_out, d_xs};
+}
+
+static at::Tensor timestep_emb(const at::Tensor& ts, int64_t dim, double max_period) {
+  CHECK_DEV(ts); CHECK_F32(ts); CHECK_CONTIG(ts);
+  TORCH_CHECK(ts.dim() == 1 && dim > 0, "timesteps [B]");
+  const c10::DeviceGuard guard(ts.device());
+  at::Tensor out = at::empty({ts.size(0), dim}, ts.options().dtype(at::kBFloat16));
+  if (ts.numel() > 0)
+    dpa::launch_timestep_emb(ts.data_ptr<float>(), (int)ts.size(0), (int)dim, (float)max_period,
+                             reinterpret_cast<uint16_t*>(out.data_ptr()), cur_stream());
+  return out;
+}
+
 static bool gemm_supported(int64_t M, int64_t N, int64_t K) {
   return M % 128 == 0 && N % 128 == 0 && K % 128 == 0;
 }
@@ -385,4 +560,12 @@ PYBIND11_MODULE(_C, m) {
   m.def("set_gemm256", &dpa::set_gemm256, "enable/disable the 256x256 8-phase GEMM path");
   m.def("lxent_fwd", &lxent_fwd, "fused linear + cross-entropy forward -> (loss, lse)");
   m.def("lxent_bwd", &lxent_bwd, "fused linear + cross-entropy backward -> (dx, dW fp32, db fp32)");
+  m.def("xent_rows_fwd", &xent_rows_fwd, "row softmax-CE over bf16 logits [R, ld] -> (loss, lse)");
+  m.def("xent_rows_bwd_", &xent_rows_bwd_, "in place: logits -> dloss * (softmax - onehot)");
+  m.def("emb_qsample_fwd", &emb_qsample_fwd,
+        "DiffuSeq embedding gather + x_start noise + masked q_sample -> (x_start, x_start bf16, x_t bf16)");
+  m.def("emb_qsample_bwd", &emb_qsample_bwd, "scatter-add of the q_sample gradients into dW (fp32)");
+  m.def("diff_loss_fwd", &diff_loss_fwd, "DiffuSeq per-sample (mse, tT) losses");
+  m.def("diff_loss_bwd", &diff_loss_bwd, "backward of diff_loss_fwd -> (d_out, d_x_start)");
+  m.def("timestep_emb", &timestep_emb, "sinusoidal timestep embedding [cos | sin] -> bf16");
 }

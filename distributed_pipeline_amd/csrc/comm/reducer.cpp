@@ -15,6 +15,9 @@
 //   precision locally; only the wire is narrow).
 // * The 1/world average is NOT applied here: the fused AdamW kernel folds it
 //   into its gradient scale.
+// * ZeRO-1 mode (a shard buffer is given): each bucket is REDUCE-SCATTERED
+//   instead: this rank's summed chunk of bucket b lands at shard_offsets[b] of
+//   the compact shard buffer (bucket lengths are multiples of the world size).
 //
 // The collectives are issued through the c10d ProcessGroup object the Python
 // side created (RCCL "nccl" on ROCm, gloo on CPU), so stream ordering follows
@@ -33,7 +36,8 @@ namespace dpa {
 class BucketReducer {
  public:
   BucketReducer(c10::intrusive_ptr<c10d::ProcessGroup> pg, at::Tensor grad_flat,
-                std::vector<int64_t> bounds, std::vector<int64_t> param_bucket, bool bf16_wire)
+                std::vector<int64_t> bounds, std::vector<int64_t> param_bucket, bool bf16_wire,
+                c10::optional<at::Tensor> shard_out, std::vector<int64_t> shard_offsets)
       : pg_(std::move(pg)), grad_(std::move(grad_flat)), bounds_(std::move(bounds)),
         bucket_of_(std::move(param_bucket)), bf16_(bf16_wire) {
     TORCH_CHECK(grad_.is_contiguous() && grad_.dim() == 1, "grad_flat must be a 1-D contiguous tensor");
@@ -50,6 +54,22 @@ class BucketReducer {
     work_.resize(nb);
     launched_.assign(nb, false);
     if (bf16_) comm_ = at::empty({grad_.numel()}, grad_.options().dtype(at::kBFloat16));
+    if (shard_out.has_value() && shard_out->defined()) {
+      rs_ = true;
+      shard_ = *shard_out;
+      shard_off_ = std::move(shard_offsets);
+      world_ = pg_->getSize();
+      TORCH_CHECK(shard_.is_contiguous() && shard_.scalar_type() == grad_.scalar_type(),
+                  "shard buffer must be contiguous and of the gradient dtype");
+      TORCH_CHECK((int)shard_off_.size() == nb, "one shard offset per bucket");
+      for (int b = 0; b < nb; ++b) {
+        const int64_t n = bounds_[b + 1] - bounds_[b];
+        TORCH_CHECK(n % world_ == 0, "bucket ", b, " is not divisible by the world size");
+        TORCH_CHECK(shard_off_[b] >= 0 && shard_off_[b] + n / world_ <= shard_.numel(),
+                    "shard offset out of range");
+      }
+      if (bf16_) comm_out_ = at::empty({shard_.numel()}, grad_.options().dtype(at::kBFloat16));
+    }
   }
 
   // Called at forward time when gradient synchronisation is enabled (torch-DDP
@@ -91,7 +111,10 @@ class BucketReducer {
       if (work_[b]) {
         work_[b]->wait();
         work_[b].reset();
-        if (bf16_) slice(grad_, b).copy_(slice(comm_, b));
+        if (bf16_) {
+          if (rs_) chunk(shard_, b).copy_(chunk(comm_out_, b));
+          else slice(grad_, b).copy_(slice(comm_, b));
+        }
       }
     }
     armed_ = false;
@@ -111,6 +134,10 @@ class BucketReducer {
 
  private:
   at::Tensor slice(const at::Tensor& t, int b) const { return t.slice(0, bounds_[b], bounds_[b + 1]); }
+  // this rank's reduce-scatter output for bucket b inside a compact shard buffer
+  at::Tensor chunk(const at::Tensor& t, int b) const {
+    return t.narrow(0, shard_off_[b], (bounds_[b + 1] - bounds_[b]) / world_);
+  }
 
   void launch_ready_in_order() {
     const int nb = (int)launched_.size();
@@ -125,13 +152,21 @@ class BucketReducer {
       wire.copy_(view);
       view = wire;
     }
-    std::vector<at::Tensor> ts{view};
-    work_[b] = pg_->allreduce(ts);
+    if (rs_) {
+      at::Tensor out = chunk(bf16_ ? comm_out_ : shard_, b);
+      work_[b] = pg_->_reduce_scatter_base(out, view);
+    } else {
+      std::vector<at::Tensor> ts{view};
+      work_[b] = pg_->allreduce(ts);
+    }
     launched_[b] = true;
   }
 
   c10::intrusive_ptr<c10d::ProcessGroup> pg_;
-  at::Tensor grad_, comm_;
+  at::Tensor grad_, comm_, shard_, comm_out_;
+  std::vector<int64_t> shard_off_;
+  int64_t world_ = 1;
+  bool rs_ = false;
   std::vector<int64_t> bounds_;
   std::vector<int64_t> bucket_of_;
   std::vector<int> size_, pending_;
@@ -146,9 +181,12 @@ class BucketReducer {
 void register_comm(pybind11::module& m) {
   pybind11::class_<BucketReducer>(m, "BucketReducer")
       .def(pybind11::init<c10::intrusive_ptr<c10d::ProcessGroup>, at::Tensor, std::vector<int64_t>,
-                          std::vector<int64_t>, bool>(),
+                          std::vector<int64_t>, bool, c10::optional<at::Tensor>,
+                          std::vector<int64_t>>(),
            pybind11::arg("process_group"), pybind11::arg("grad_flat"), pybind11::arg("bounds"),
-           pybind11::arg("param_bucket"), pybind11::arg("bf16_wire") = false)
+           pybind11::arg("param_bucket"), pybind11::arg("bf16_wire") = false,
+           pybind11::arg("shard_out") = pybind11::none(),
+           pybind11::arg("shard_offsets") = std::vector<int64_t>())
       .def("arm", &BucketReducer::arm)
       .def("disarm", &BucketReducer::disarm)
       .def("armed", &BucketReducer::armed)

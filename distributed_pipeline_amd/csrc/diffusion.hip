@@ -1,0 +1,302 @@
+// DiffuSeq diffusion-side kernels (SURVEY K-M1..K-M4, K-M13; the workload the
+// reference trainer was adapted for, reference utils/trainer.py:1-4, Appendix B):
+//
+//   emb_qsample_fwd : x0_mean = W[ids] (fp32 word embedding: the diffusion space)
+//                     x_start = x0_mean + std0 * eps0
+//                     x_t     = mask ? sqrt(abar_t) x_start + sqrt(1-abar_t) eps : x_start
+//                     -> x_start fp32, x_start bf16 (rounding-head input), x_t bf16 (model input).
+//                     eps0 / eps are generated in-kernel (counter-based Philox + Box-Muller), so
+//                     the noise tensors never exist in memory.
+//   emb_qsample_bwd : dW[ids] += d_xstart + d_xstart16 + (mask ? sqrt(abar_t) : 1) d_x_t
+//                     (fp32 atomics straight into the tied embedding's gradient; the tied
+//                     rounding head's dW comes from the fused linear-CE kernel)
+//   diff_loss_fwd   : per sample  mse = mean((target - out)^2), target = t==0 ? x0_mean : x_start
+//                                 tT  = mean((sqrt(abar_{T-1}) x_start)^2)
+//   diff_loss_bwd   : d_out, d_xstart (fp32) and, for t==0 samples, dW[ids] += d x0_mean
+//   timestep_emb    : [cos(t f_j) | sin(t f_j)], f_j = 10000^(-j/half) -> bf16
+//
+// Forward layout: a token row of E fp32 values is owned by E/4 consecutive lanes
+// (16-byte vectors), so every load/store is part of a full 128-byte line.  The
+// scatter-add backward is element-per-lane instead: one wave-instruction's 64
+// atomics then cover 256 contiguous bytes, the shape the memory-side atomic
+// units serve at full rate (MI355X_MICROARCH, Global float atomics).
+//
+// Timestep indices are trusted to lie in [0, T) (they come from the schedule
+// sampler); token ids outside [0, V) contribute nothing.
+#include "common.h"
+#include "launchers.h"
+
+namespace dpa {
+
+// Four standard normals for (seed, stream, element-group) via one Philox call.
+__device__ __forceinline__ void normal4(uint32_t seed, uint32_t stream, uint32_t offset,
+                                        uint64_t grp, float out[4]) {
+  uint32_t r[4];
+  philox4(seed, 0x2545F491u ^ stream, (uint32_t)grp, (uint32_t)(grp >> 32), offset, stream, r);
+#pragma unroll
+  for (int k = 0; k < 2; ++k) {
+    // u1 in (0, 1]: never log(0)
+    const float u1 = ((float)(r[2 * k] >> 8) + 1.0f) * (1.0f / 16777216.0f);
+    const float u2 = (float)(r[2 * k + 1] >> 8) * (1.0f / 16777216.0f);
+    const float rad = sqrtf(-2.0f * __logf(u1));
+    float s, c;
+    __sincosf(6.283185307179586f * u2, &s, &c);
+    out[2 * k] = rad * c;
+    out[2 * k + 1] = rad * s;
+  }
+}
+
+__device__ __forceinline__ f32x4 load4_bf(const bf16_t* p) {
+  const uint2 raw = *reinterpret_cast<const uint2*>(p);
+  f32x4 r;
+  r[0] = __uint_as_float(raw.x << 16);
+  r[1] = __uint_as_float(raw.x & 0xffff0000u);
+  r[2] = __uint_as_float(raw.y << 16);
+  r[3] = __uint_as_float(raw.y & 0xffff0000u);
+  return r;
+}
+
+__device__ __forceinline__ void store4_bf(bf16_t* p, const f32x4& v) {
+  uint2 raw;
+  raw.x = pack_bf2(v[0], v[1]);
+  raw.y = pack_bf2(v[2], v[3]);
+  *reinterpret_cast<uint2*>(p) = raw;
+}
+
+__global__ void __launch_bounds__(256) emb_qsample_fwd_kernel(
+    const int64_t* __restrict__ ids, const int64_t* __restrict__ mask, const int64_t* __restrict__ t,
+    const float* __restrict__ W, const float* __restrict__ sa, const float* __restrict__ s1a,
+    int64_t NT, int L, int E, int V, float std0, uint32_t seed, uint32_t offset,
+    float* __restrict__ x_start, bf16_t* __restrict__ x_start16, bf16_t* __restrict__ x_t) {
+  const int vpr = E >> 2;  // 16-byte vectors per row
+  const int64_t n = NT * vpr;
+  for (int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; q < n;
+       q += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t tok = q / vpr;
+    const int c = (int)(q - tok * vpr) * 4;
+    const int64_t id = ids[tok];
+    f32x4 x0 = {0.f, 0.f, 0.f, 0.f};
+    if (id >= 0 && id < V) x0 = *reinterpret_cast<const f32x4*>(W + id * E + c);
+    float e0[4], e1[4];
+    normal4(seed, 0u, offset, (uint64_t)q, e0);
+    normal4(seed, 1u, offset, (uint64_t)q, e1);
+    const bool noised = mask[tok] != 0;
+    const int64_t ts = t[tok / L];
+    const float a = noised ? sa[ts] : 1.f, b = noised ? s1a[ts] : 0.f;
+    f32x4 xs, xt;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      xs[k] = x0[k] + std0 * e0[k];
+      xt[k] = a * xs[k] + b * e1[k];
+    }
+    const int64_t o = tok * E + c;
+    *reinterpret_cast<f32x4*>(x_start + o) = xs;
+    if (x_start16) store4_bf(x_start16 + o, xs);
+    store4_bf(x_t + o, xt);
+  }
+}
+
+// Gradients are bf16 (d_xs16, d_xt16) or fp32 (d_xs, d_xt32); any may be null.
+__global__ void __launch_bounds__(256) emb_qsample_bwd_kernel(
+    const int64_t* __restrict__ ids, const int64_t* __restrict__ mask, const int64_t* __restrict__ t,
+    const float* __restrict__ sa, const float* __restrict__ d_xs, const bf16_t* __restrict__ d_xs16,
+    const bf16_t* __restrict__ d_xt16, const float* __restrict__ d_xt32, int64_t NT, int L, int E,
+    int V, float* __restrict__ dW) {
+  const int64_t n = NT * E;
+  for (int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; q < n;
+       q += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t tok = q / E;
+    const int c = (int)(q - tok * E);
+    const int64_t id = ids[tok];
+    if (id < 0 || id >= V) continue;
+    float g = 0.f;
+    if (d_xs) g = d_xs[q];
+    if (d_xs16) g += bf2f(d_xs16[q]);
+    if (d_xt16 || d_xt32) {
+      const float a = mask[tok] != 0 ? sa[t[tok / L]] : 1.f;
+      g += a * (d_xt16 ? bf2f(d_xt16[q]) : d_xt32[q]);
+    }
+    atomicAdd(dW + id * E + c, g);
+  }
+}
+
+// One workgroup per sample: reductions over the sample's L*E elements.
+template <bool OUT_BF16>
+__global__ void __launch_bounds__(256) diff_loss_fwd_kernel(
+    const float* __restrict__ x_start, const void* __restrict__ out_, const int64_t* __restrict__ ids,
+    const int64_t* __restrict__ t, const float* __restrict__ W, int L, int E, int V, float sa_last,
+    float* __restrict__ mse, float* __restrict__ tT) {
+  __shared__ float red[2][4];
+  const int b = blockIdx.x;
+  const bool t0 = t[b] == 0;
+  const int vpr = E >> 2;
+  const int64_t base = (int64_t)b * L * E;
+  float s_mse = 0.f, s_tt = 0.f;
+  for (int q = threadIdx.x; q < L * vpr; q += blockDim.x) {
+    const int tok = q / vpr, c = (q - tok * vpr) * 4;
+    const int64_t o = base + (int64_t)tok * E + c;
+    const f32x4 xs = *reinterpret_cast<const f32x4*>(x_start + o);
+    f32x4 y;
+    if (OUT_BF16) y = load4_bf(reinterpret_cast<const bf16_t*>(out_) + o);
+    else y = *reinterpret_cast<const f32x4*>(reinterpret_cast<const float*>(out_) + o);
+    f32x4 tg = xs;
+    if (t0) {
+      const int64_t id = ids[(int64_t)b * L + tok];
+      tg = (id >= 0 && id < V) ? *reinterpret_cast<const f32x4*>(W + id * E + c)
+                               : f32x4{0.f, 0.f, 0.f, 0.f};
+    }
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const float d = tg[k] - y[k];
+      s_mse += d * d;
+      s_tt += xs[k] * xs[k];
+    }
+  }
+  s_mse = wave_sum(s_mse);
+  s_tt = wave_sum(s_tt);
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  if (lane == 0) {
+    red[0][w] = s_mse;
+    red[1][w] = s_tt;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const float inv = 1.f / (float)(L * E);
+    float a = 0.f, c = 0.f;
+    for (int i = 0; i < (int)(blockDim.x >> 6); ++i) {
+      a += red[0][i];
+      c += red[1][i];
+    }
+    mse[b] = a * inv;
+    tT[b] = c * inv * sa_last * sa_last;
+  }
+}
+
+template <bool OUT_BF16>
+__global__ void __launch_bounds__(256) diff_loss_bwd_kernel(
+    const float* __restrict__ x_start, const void* __restrict__ out_, const int64_t* __restrict__ ids,
+    const int64_t* __restrict__ t, const float* __restrict__ W, const float* __restrict__ dmse,
+    const float* __restrict__ dtT, int B, int L, int E, int V, float sa_last,
+    void* __restrict__ d_out_, float* __restrict__ d_xs, float* __restrict__ dW) {
+  const int vpr = E >> 2;
+  const int64_t n = (int64_t)B * L * vpr;
+  const float inv = 1.f / (float)(L * E);
+  for (int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; q < n;
+       q += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t tok = q / vpr;
+    const int c = (int)(q - tok * vpr) * 4;
+    const int b = (int)(tok / L);
+    const int64_t o = tok * E + c;
+    const f32x4 xs = *reinterpret_cast<const f32x4*>(x_start + o);
+    f32x4 y;
+    if (OUT_BF16) y = load4_bf(reinterpret_cast<const bf16_t*>(out_) + o);
+    else y = *reinterpret_cast<const f32x4*>(reinterpret_cast<const float*>(out_) + o);
+    const bool t0 = t[b] == 0;
+    const float gm = dmse ? dmse[b] * 2.f * inv : 0.f;
+    const float gt = dtT ? dtT[b] * 2.f * inv * sa_last * sa_last : 0.f;
+    f32x4 tg = xs;
+    const int64_t id = ids[tok];
+    const bool id_ok = id >= 0 && id < V;
+    if (t0) tg = id_ok ? *reinterpret_cast<const f32x4*>(W + id * E + c) : f32x4{0.f, 0.f, 0.f, 0.f};
+    f32x4 dy, dx;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const float r = y[k] - tg[k];
+      dy[k] = gm * r;
+      dx[k] = gt * xs[k] - (t0 ? 0.f : gm * r);
+    }
+    if (d_out_) {
+      if (OUT_BF16) store4_bf(reinterpret_cast<bf16_t*>(d_out_) + o, dy);
+      else *reinterpret_cast<f32x4*>(reinterpret_cast<float*>(d_out_) + o) = dy;
+    }
+    if (d_xs) *reinterpret_cast<f32x4*>(d_xs + o) = dx;
+    if (t0 && dW && id_ok) {  // d x0_mean of the t == 0 branch -> tied embedding rows (rare)
+#pragma unroll
+      for (int k = 0; k < 4; ++k) atomicAdd(dW + id * E + c + k, -dy[k]);
+    }
+  }
+}
+
+__global__ void __launch_bounds__(256) timestep_emb_kernel(const float* __restrict__ ts, int B, int dim,
+                                                           float log_max_period,
+                                                           bf16_t* __restrict__ out) {
+  const int half = dim >> 1;
+  const int64_t n = (int64_t)B * dim;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    const int b = (int)(i / dim), j = (int)(i - (int64_t)b * dim);
+    float v = 0.f;
+    if (j < 2 * half) {
+      const int jj = j < half ? j : j - half;
+      const float f = expf(-log_max_period * (float)jj / (float)half);
+      const float a = ts[b] * f;
+      v = j < half ? cosf(a) : sinf(a);
+    }
+    out[i] = f2bf(v);
+  }
+}
+
+static inline unsigned grid_cap(int64_t n, int cap) {
+  int64_t g = (n + 255) / 256;
+  if (g < 1) g = 1;
+  if (g > cap) g = cap;
+  return (unsigned)g;
+}
+
+bool launch_emb_qsample_fwd(const int64_t* ids, const int64_t* mask, const int64_t* t, const float* W,
+                            const float* sa, const float* s1a, int64_t NT, int L, int E, int V,
+                            float std0, uint32_t seed, uint32_t offset, float* x_start,
+                            uint16_t* x_start16, uint16_t* x_t, hipStream_t s) {
+  if (E % 4 != 0 || L <= 0) return false;
+  hipLaunchKernelGGL(emb_qsample_fwd_kernel, dim3(grid_cap(NT * (E / 4), 256 * 16)), dim3(256), 0, s,
+                     ids, mask, t, W, sa, s1a, NT, L, E, V, std0, seed, offset, x_start,
+                     (bf16_t*)x_start16, (bf16_t*)x_t);
+  return true;
+}
+
+bool launch_emb_qsample_bwd(const int64_t* ids, const int64_t* mask, const int64_t* t, const float* sa,
+                            const float* d_xs, const uint16_t* d_xs16, const uint16_t* d_xt16,
+                            const float* d_xt32, int64_t NT, int L, int E, int V, float* dW,
+                            hipStream_t s) {
+  if (L <= 0 || E <= 0) return false;
+  hipLaunchKernelGGL(emb_qsample_bwd_kernel, dim3(grid_cap(NT * E, 256 * 16)), dim3(256), 0, s, ids,
+                     mask, t, sa, d_xs, (const bf16_t*)d_xs16, (const bf16_t*)d_xt16, d_xt32, NT, L,
+                     E, V, dW);
+  return true;
+}
+
+bool launch_diff_loss_fwd(const float* x_start, const void* out, bool out_bf16, const int64_t* ids,
+                          const int64_t* t, const float* W, int B, int L, int E, int V, float sa_last,
+                          float* mse, float* tT, hipStream_t s) {
+  if (E % 4 != 0 || B <= 0) return false;
+  if (out_bf16)
+    hipLaunchKernelGGL(diff_loss_fwd_kernel<true>, dim3(B), dim3(256), 0, s, x_start, out, ids, t, W, L,
+                       E, V, sa_last, mse, tT);
+  else
+    hipLaunchKernelGGL(diff_loss_fwd_kernel<false>, dim3(B), dim3(256), 0, s, x_start, out, ids, t, W,
+                       L, E, V, sa_last, mse, tT);
+  return true;
+}
+
+bool launch_diff_loss_bwd(const float* x_start, const void* out, bool out_bf16, const int64_t* ids,
+                          const int64_t* t, const float* W, const float* dmse, const float* dtT, int B,
+                          int L, int E, int V, float sa_last, void* d_out, float* d_xs, float* dW,
+                          hipStream_t s) {
+  if (E % 4 != 0 || B <= 0) return false;
+  const unsigned g = grid_cap((int64_t)B * L * (E / 4), 256 * 16);
+  if (out_bf16)
+    hipLaunchKernelGGL(diff_loss_bwd_kernel<true>, dim3(g), dim3(256), 0, s, x_start, out, ids, t, W,
+                       dmse, dtT, B, L, E, V, sa_last, d_out, d_xs, dW);
+  else
+    hipLaunchKernelGGL(diff_loss_bwd_kernel<false>, dim3(g), dim3(256), 0, s, x_start, out, ids, t, W,
+                       dmse, dtT, B, L, E, V, sa_last, d_out, d_xs, dW);
+  return true;
+}
+
+void launch_timestep_emb(const float* ts, int B, int dim, float max_period, uint16_t* out,
+                         hipStream_t s) {
+  hipLaunchKernelGGL(timestep_emb_kernel, dim3(grid_cap((int64_t)B * dim, 1024)), dim3(256), 0, s, ts,
+                     B, dim, logf(max_period), (bf16_t*)out);
+}
+
+}  // namespace dpa

@@ -72,6 +72,31 @@ bool launch_lxent2_dx(const uint16_t* x, const uint16_t* W, const uint16_t* b, c
                       const float* lse, const float* dloss, int N, int V, int E, int splits, int vps,
                       uint16_t* dx, float* dx_acc, hipStream_t s);
 
+// ---- xent_rows.hip: row softmax-CE over materialised logits (wide-E chunked path) ----
+bool launch_xent_rows_fwd(const uint16_t* lg, int64_t ld, int V, const int64_t* tgt, int64_t R,
+                          float* loss, float* lse, hipStream_t s);
+bool launch_xent_rows_bwd(uint16_t* lg, int64_t ld, int V, const int64_t* tgt, const float* lse,
+                          const float* dloss, int64_t R, hipStream_t s);
+
+// ---- diffusion.hip: DiffuSeq q_sample / diffusion losses / timestep embedding ------
+bool launch_emb_qsample_fwd(const int64_t* ids, const int64_t* mask, const int64_t* t, const float* W,
+                            const float* sa, const float* s1a, int64_t NT, int L, int E, int V,
+                            float std0, uint32_t seed, uint32_t offset, float* x_start,
+                            uint16_t* x_start16, uint16_t* x_t, hipStream_t s);
+bool launch_emb_qsample_bwd(const int64_t* ids, const int64_t* mask, const int64_t* t, const float* sa,
+                            const float* d_xs, const uint16_t* d_xs16, const uint16_t* d_xt16,
+                            const float* d_xt32, int64_t NT, int L, int E, int V, float* dW,
+                            hipStream_t s);
+bool launch_diff_loss_fwd(const float* x_start, const void* out, bool out_bf16, const int64_t* ids,
+                          const int64_t* t, const float* W, int B, int L, int E, int V, float sa_last,
+                          float* mse, float* tT, hipStream_t s);
+bool launch_diff_loss_bwd(const float* x_start, const void* out, bool out_bf16, const int64_t* ids,
+                          const int64_t* t, const float* W, const float* dmse, const float* dtT, int B,
+                          int L, int E, int V, float sa_last, void* d_out, float* d_xs, float* dW,
+                          hipStream_t s);
+void launch_timestep_emb(const float* ts, int B, int dim, float max_period, uint16_t* out,
+                         hipStream_t s);
+
 // ---- gemm.hip (bf16 MFMA GEMMs of Linear layers) ----------------------------------
 bool launch_gemm_nt(const uint16_t* x, const uint16_t* W, const uint16_t* bias, uint16_t* y,
                     uint16_t* z, int T, int N, int K, int act, hipStream_t s);

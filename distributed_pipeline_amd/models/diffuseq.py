@@ -74,7 +74,7 @@ class TransformerNetModel(nn.Module):
     def forward(self, x, timesteps):
         dt = self.compute_dtype
         B, L, _ = x.shape
-        temb = ops.timestep_embedding(timesteps, self.hidden_t_dim).to(dt)
+        temb = ops.timestep_embedding(timesteps, self.hidden_t_dim, dtype=dt)
         emb_t = self.time_embed(temb)                                        # [B, H]
         emb_x = self.input_up_proj(x.to(dt))                                 # [B, L, H]
         pos = self.position_embeddings(self.position_ids[:, :L], dt)         # [1, L, H]

@@ -107,12 +107,50 @@ class GaussianDiffusion:
     def training_losses(self, model, *args, **kwargs):
         return self.training_losses_seq2seq(model, *args, **kwargs)
 
+    # Take the fused HIP path (csrc/diffusion.hip) for bf16 models on a GPU; the
+    # PyTorch formulas below stay the CPU / fp32 path and the kernels' oracle.
+    fused = True
+
+    def _fused_ok(self, net, noise):
+        if noise is not None or not GaussianDiffusion.fused:
+            return False
+        emb = getattr(net, "word_embedding", None)
+        if emb is None or getattr(net, "compute_dtype", None) != torch.bfloat16:
+            return False
+        from ..ops import diffusion as dops
+        return dops.available(emb.weight)
+
+    def _training_losses_fused(self, model, net, t, input_ids, input_mask, compute_nll):
+        """Same terms as below; embedding gather + noise + q_sample and the mse/tT
+        reductions each run as one kernel (noise drawn in-kernel, never stored)."""
+        from ..ops import diffusion as dops
+        W = net.word_embedding.weight
+        dev = W.device
+        x_start, x_start16, x_t = dops.emb_qsample(
+            W, input_ids, input_mask, t, self._table("sqrt_alphas_cumprod", dev),
+            self._table("sqrt_one_minus_alphas_cumprod", dev),
+            float(self.sqrt_one_minus_alphas_cumprod[0]))
+        model_out = model(x_t, self.scale_timesteps(t))                       # x0_hat (bf16)
+        sa_last = float(self.sqrt_alphas_cumprod[self.num_timesteps - 1])
+        mse, tT_loss = dops.diffusion_mse(x_start, model_out, input_ids, t, W, sa_last)
+        terms = {"mse": mse}
+        decoder_nll = self.token_discrete_loss(x_start16, net, input_ids)
+        if compute_nll:
+            with torch.no_grad():
+                terms["nll"] = self.token_discrete_loss(model_out.detach(), net, input_ids,
+                                                        mask=input_mask)
+        terms["decoder_nll"] = decoder_nll
+        terms["loss"] = mse + decoder_nll + tT_loss
+        return terms
+
     def training_losses_seq2seq(self, model, x_start_unused, t, model_kwargs, noise=None,
                                 compute_nll=True):
         """DiffuSeq loss terms, each [B] fp32.  ``model`` may be wrapped (DDP engine)."""
         net = getattr(model, "module", model)
         input_ids = model_kwargs["input_ids"]
         input_mask = model_kwargs["input_mask"]
+        if self._fused_ok(net, noise):
+            return self._training_losses_fused(model, net, t, input_ids, input_mask, compute_nll)
         x0_mean = net.get_embeds(input_ids)                                  # [B, L, E] fp32
         std0 = float(self.sqrt_one_minus_alphas_cumprod[0])
         x_start = x0_mean + std0 * torch.randn_like(x0_mean)

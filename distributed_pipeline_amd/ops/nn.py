@@ -655,15 +655,103 @@ class _LinearXentFn(torch.autograd.Function):
         return dx, dw, db, None, None, None
 
 
+def _pad_vocab(w16, b16, mult=256):
+    """Vocabulary rows padded to a multiple of ``mult`` (zero rows; their logits are
+    masked by the row kernels), so every logits row is 16-byte aligned and the
+    weight-gradient GEMM tiles."""
+    V = w16.shape[0]
+    Vp = (V + mult - 1) // mult * mult
+    if Vp == V:
+        return w16, b16
+    wp = torch.zeros(Vp, w16.shape[1], dtype=w16.dtype, device=w16.device)
+    wp[:V].copy_(w16)
+    bp = None
+    if b16 is not None:
+        bp = torch.zeros(Vp, dtype=b16.dtype, device=b16.device)
+        bp[:V].copy_(b16)
+    return wp, bp
+
+
+def _chunk_logits(xc, wp, bp):
+    return torch.addmm(bp, xc, wp.t()) if bp is not None else xc @ wp.t()
+
+
+class _ChunkedLinearXentFn(torch.autograd.Function):
+    """Per-token CE for WIDE inputs (E > 256, e.g. GPT-2's 768 x 50257 LM head): the
+    logits of one token chunk at a time come from hipBLASLt into a [chunk, Vp] bf16
+    buffer and the row kernels of ``csrc/xent_rows.hip`` turn them into (loss, lse) -
+    in backward into dlogits in place - so the [N, V] logits never exist whole.
+    Backward recomputes each chunk's logits (one GEMM) rather than storing them."""
+
+    @staticmethod
+    def forward(ctx, x, w, b, w16, b16, target, chunk):
+        ext = get_ext()
+        N, V = x.shape[0], w16.shape[0]
+        wp, bp = _pad_vocab(w16, b16)
+        loss = torch.empty(N, dtype=torch.float32, device=x.device)
+        lse = torch.empty(N, dtype=torch.float32, device=x.device)
+        for s in range(0, N, chunk):
+            e = min(N, s + chunk)
+            lg = _chunk_logits(x[s:e], wp, bp)
+            l_c, lse_c = ext.xent_rows_fwd(lg, V, target[s:e])
+            loss[s:e].copy_(l_c)
+            lse[s:e].copy_(lse_c)
+        ctx.save_for_backward(x, w16, b16, target, lse)
+        ctx.params = (w, b)
+        ctx.chunk = chunk
+        return loss
+
+    @staticmethod
+    def backward(ctx, dloss):
+        x, w16, b16, target, lse = ctx.saved_tensors
+        w, b = ctx.params
+        ext = get_ext()
+        N, E, V = x.shape[0], x.shape[1], w16.shape[0]
+        wp, bp = _pad_vocab(w16, b16)
+        Vp = wp.shape[0]
+        dloss = dloss.contiguous().float()
+        need_dx, need_dw, need_db = ctx.needs_input_grad[0], ctx.needs_input_grad[1], (
+            b is not None and ctx.needs_input_grad[2])
+        dx = torch.empty_like(x) if need_dx else None
+        dwp = torch.zeros(Vp, E, dtype=torch.float32, device=x.device) if need_dw else None
+        db = torch.zeros(V, dtype=torch.float32, device=x.device) if need_db else None
+        native_wgrad = need_dw and Vp % 256 == 0 and E % 256 == 0 and hasattr(ext, "gemm_wgrad")
+        for s in range(0, N, ctx.chunk):
+            e = min(N, s + ctx.chunk)
+            dlg = _chunk_logits(x[s:e], wp, bp)
+            ext.xent_rows_bwd_(dlg, V, target[s:e], lse[s:e], dloss[s:e])
+            if need_dx:
+                torch.mm(dlg, wp, out=dx[s:e])
+            if need_dw:
+                if native_wgrad and (e - s) % 128 == 0:
+                    ext.gemm_wgrad(dlg, x[s:e], dwp, None)   # split-K MFMA, fp32 accumulate
+                else:
+                    dwp.add_(_mm_fp32(dlg.t(), x[s:e]))
+            if need_db:
+                db.add_(dlg[:, :V].float().sum(0))
+        dw = dwp[:V] if need_dw else None
+        return dx, dw, db, None, None, None, None
+
+
+# tokens per logits chunk of the wide-E path: about 0.5 GiB of bf16 logits
+_XENT_CHUNK_BYTES = int(os.environ.get("DPA_XENT_CHUNK_MB", "512")) << 20
+
+
 def linear_cross_entropy(x, weight, bias, target):
     """Per-token CE of logits = x @ W^T + b against ``target`` without materialising logits.
 
-    x: [N, E]; weight: [V, E]; target: [N] int64 -> loss [N] fp32.
+    x: [N, E]; weight: [V, E]; target: [N] int64 -> loss [N] fp32.  E in {128, 256}:
+    fully fused MFMA kernels (csrc/xent.hip); wider E: chunked hipBLASLt logits +
+    row kernels (csrc/xent_rows.hip).
     """
-    if (x.dtype == torch.bfloat16 and native_ok(x, kernel="lxent_fwd")
-            and x.shape[-1] in (128, 256)):
+    if x.dtype == torch.bfloat16 and native_ok(x, kernel="lxent_fwd") and x.shape[-1] in (128, 256):
         return _LinearXentFn.apply(x.contiguous(), weight, bias, shadow(weight, x.dtype),
                                    shadow(bias, x.dtype), target.contiguous())
+    if x.dtype == torch.bfloat16 and native_ok(x, kernel="xent_rows_fwd") and x.dim() == 2:
+        Vp = (weight.shape[0] + 255) // 256 * 256
+        chunk = max(256, (_XENT_CHUNK_BYTES // (Vp * 2)) // 256 * 256)
+        return _ChunkedLinearXentFn.apply(x.contiguous(), weight, bias, shadow(weight, x.dtype),
+                                          shadow(bias, x.dtype), target.contiguous(), chunk)
     logits = linear(x, weight, bias)
     return F.cross_entropy(logits.float(), target, reduction="none")
 
@@ -693,8 +781,17 @@ def embedding(ids, weight, dtype):
     return _EmbFn.apply(ids, weight, shadow(weight, dtype))
 
 
-def timestep_embedding(timesteps, dim, max_period=10000):
-    """Sinusoidal embedding [cos | sin] (DiffuSeq / guided-diffusion convention)."""
+def timestep_embedding(timesteps, dim, max_period=10000, dtype=None):
+    """Sinusoidal embedding [cos | sin] (DiffuSeq / guided-diffusion convention).
+
+    bf16 on a HIP device: one kernel writes the bf16 embedding (csrc/diffusion.hip)."""
+    if dtype == torch.bfloat16 and native_ok(timesteps, kernel="timestep_emb"):
+        return get_ext().timestep_emb(timesteps.float().contiguous(), int(dim), float(max_period))
+    emb = _timestep_embedding_ref(timesteps, dim, max_period)
+    return emb if dtype is None else emb.to(dtype)
+
+
+def _timestep_embedding_ref(timesteps, dim, max_period=10000):
     half = dim // 2
     freqs = torch.exp(-math.log(max_period) *
                       torch.arange(half, dtype=torch.float32, device=timesteps.device) / half)

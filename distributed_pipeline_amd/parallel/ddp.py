@@ -32,6 +32,11 @@ implements the same protocol for the single-GPU multi-rank test transport.
   checksum all-reduce (replaces DDP's per-tensor broadcast, SURVEY X-4).
 * HIP-graph mode: when backward runs inside a captured graph no Python hook
   fires; :meth:`finalize` then launches every bucket after the replay.
+* ZeRO-1 (``shard_optimizer=True``, parallel/zero.py): buckets are padded to a
+  multiple of world x 16 elements and REDUCE-SCATTERED instead of all-reduced;
+  rank r receives the summed r-th chunk of every bucket in a compact
+  ``grad_shard`` buffer, the sharded optimizer updates only those elements and
+  :meth:`gather_params` all-gathers the updated fp32 chunks back in place.
 """
 import contextlib
 import os
@@ -41,9 +46,23 @@ import torch.distributed as dist
 from torch import nn
 
 from ..ops._ext import get_ext
-from .flat import FlatParamSpace
+from .flat import ALIGN, FlatParamSpace, layout_order
 
 _MiB = 1024 * 1024
+
+
+def bucket_members(numels, cap_mb, first_mb):
+    """Bucket membership (lists of layout indices) of parameters with these element
+    counts, by the same rule as :func:`plan_buckets` - computable before the flat
+    space exists (the sharded engine pads the space at these bucket ends)."""
+    groups, cur, off, cur_start, limit = [], [], 0, 0, first_mb * _MiB
+    for i, n in enumerate(numels):
+        cur.append(i)
+        off = (off + n + ALIGN - 1) // ALIGN * ALIGN
+        if (off - cur_start) * 4 >= limit or i == len(numels) - 1:
+            groups.append(cur)
+            cur, cur_start, limit = [], off, cap_mb * _MiB
+    return groups
 
 
 def plan_buckets(space, cap_mb, first_mb):
@@ -76,14 +95,23 @@ class _Bucket:
 class DDPEngine(nn.Module):
     def __init__(self, module, *, device=None, bucket_cap_mb=32.0, first_bucket_mb=4.0,
                  shadow_dtype=None, process_group=None, reduce_dtype=torch.float32,
-                 broadcast_from_rank0=True, space=None):
+                 broadcast_from_rank0=True, space=None, shard_optimizer=False):
         super().__init__()
         self.module = module
         self.pg = process_group
-        self.space = space or FlatParamSpace(module.parameters(), device=device,
-                                             shadow_dtype=shadow_dtype)
         self.distributed = dist.is_available() and dist.is_initialized()
         self.world_size = dist.get_world_size(self.pg) if self.distributed else 1
+        self.rank = dist.get_rank(self.pg) if self.distributed else 0
+        self.sharded = bool(shard_optimizer) and self.distributed and self.world_size > 1
+        if space is None:
+            kw = {}
+            if self.sharded:
+                # pad every bucket end so each bucket splits into world equal 16-aligned chunks
+                layout = layout_order(module.parameters())
+                groups = bucket_members([p.numel() for p in layout], bucket_cap_mb, first_bucket_mb)
+                kw = dict(break_after={g[-1] for g in groups}, break_align=self.world_size * ALIGN)
+            space = FlatParamSpace(module.parameters(), device=device, shadow_dtype=shadow_dtype, **kw)
+        self.space = space
         self.reduce_dtype = reduce_dtype
         self._sync_enabled = True
         self._armed = False
@@ -97,15 +125,31 @@ class DDPEngine(nn.Module):
                 self._bucket_of[id(p)] = b
         self._hooks = []
         self._comm_buf = None
+        self._comm_out = None
+        self.grad_shard = None
+        self.shard_chunks = []  # per bucket: (flat start of this rank's chunk, length, shard offset)
+        if self.sharded:
+            off = 0
+            for b in self.buckets:
+                n = b.end - b.start
+                if n % (self.world_size * ALIGN):
+                    raise RuntimeError(f"bucket {b.index} ({n} elements) is not world-divisible")
+                c = n // self.world_size
+                self.shard_chunks.append((b.start + self.rank * c, c, off))
+                off += c
+            self.grad_shard = torch.zeros(off, dtype=torch.float32, device=self.space.device)
         # gloo on device tensors is only a test transport (several ranks sharing one
         # GPU): stage each bucket through host memory synchronously so its ordering
         # w.r.t. the producing kernels is explicit.  RCCL ("nccl") orders via events.
+        self._backend = dist.get_backend(self.pg) if self.distributed else None
         self._host_sync_before_comm = (self.distributed and self.space.device.type == "cuda"
-                                       and dist.get_backend(self.pg) == "gloo")
+                                       and self._backend == "gloo")
         # Native C++ bucket reducer (csrc/comm/reducer.cpp) for the real transports;
         # the Python implementation below stays as the reference / test transport.
+        # The sharded (reduce-scatter) mode needs a backend with reduce_scatter: RCCL.
         self._native = None
         if (self.distributed and not self._host_sync_before_comm
+                and (not self.sharded or self._backend == "nccl")
                 and os.environ.get("DPA_NATIVE_REDUCER", "1") != "0"):
             ext = get_ext(required=False)
             if ext is not None and hasattr(ext, "BucketReducer"):
@@ -113,7 +157,9 @@ class DDPEngine(nn.Module):
                 bounds = [b.start for b in self.buckets] + [self.buckets[-1].end]
                 param_bucket = [self._bucket_of[id(p)].index for p in self.space.layout]
                 self._native = ext.BucketReducer(pg, self.space.grad_flat, bounds, param_bucket,
-                                                 self.reduce_dtype == torch.bfloat16)
+                                                 self.reduce_dtype == torch.bfloat16,
+                                                 self.grad_shard if self.sharded else None,
+                                                 [c[2] for c in self.shard_chunks])
         if self.distributed:
             self._verify_shapes()
             if broadcast_from_rank0:
@@ -197,10 +243,40 @@ class DDPEngine(nn.Module):
             self._launch(b)
             self._next_launch += 1
 
+    def _wire(self):
+        if self._comm_buf is None:
+            self._comm_buf = torch.empty(self.space.numel, dtype=self.reduce_dtype,
+                                         device=self.space.device)
+        return self._comm_buf
+
+    def _launch_sharded(self, b, view):
+        s, c, off = self.shard_chunks[b.index]
+        out = self.grad_shard[off:off + c]
+        if self._backend != "nccl":
+            # gloo (CPU tests / host-staged transport) has no reduce_scatter: all-reduce
+            # the bucket and keep this rank's chunk (same sums, twice the traffic)
+            full = view.to("cpu") if view.is_cuda else view.clone()
+            dist.all_reduce(full, group=self.pg)
+            out.copy_(full[s - b.start:s - b.start + c])
+            b.work = None
+        elif self.reduce_dtype == torch.float32:
+            b.work = dist.reduce_scatter_tensor(out, view, group=self.pg, async_op=True)
+        else:
+            wire = self._wire()[b.start:b.end]
+            wire.copy_(view)
+            if self._comm_out is None:
+                self._comm_out = torch.empty_like(self.grad_shard, dtype=self.reduce_dtype)
+            wout = self._comm_out[off:off + c]
+            b.work = (dist.reduce_scatter_tensor(wout, wire, group=self.pg, async_op=True), wout, out)
+        b.launched = True
+
     def _launch(self, b):
         if b.launched:
             return
         view = self.space.grad_flat[b.start:b.end]
+        if self.sharded:
+            self._launch_sharded(b, view)
+            return
         if self._host_sync_before_comm:
             # test transport: stage through host memory synchronously (gloo's own
             # device-tensor path is not used)
@@ -257,7 +333,44 @@ class DDPEngine(nn.Module):
 
     def average_gradients(self):
         if self.world_size > 1:
-            self.space.grad_flat.mul_(1.0 / self.world_size)
+            (self.grad_shard if self.sharded else self.space.grad_flat).mul_(1.0 / self.world_size)
+
+    # -- ZeRO-1 helpers -----------------------------------------------------------------
+    def all_gather_chunks(self, full):
+        """``full`` is a flat buffer laid out like the parameters whose per-bucket chunk
+        ``shard_chunks[b]`` is valid on each owning rank: gather every bucket in place."""
+        for b, (s, c, _off) in zip(self.buckets, self.shard_chunks):
+            whole = full[b.start:b.end]
+            mine = full[s:s + c]
+            if self._host_sync_before_comm:  # gloo on device tensors: host-staged
+                host = whole.to("cpu")
+                dist.all_gather_into_tensor(host, host[s - b.start:s - b.start + c].clone(),
+                                            group=self.pg)
+                whole.copy_(host)
+            elif self._backend == "nccl":
+                dist.all_gather_into_tensor(whole, mine, group=self.pg)  # in place
+            else:
+                dist.all_gather_into_tensor(whole, mine.clone(), group=self.pg)
+
+    def gather_params(self):
+        """After the sharded optimizer step: every rank's updated fp32 chunks to every
+        rank, then the bf16 compute shadow is refreshed from the full master buffer."""
+        if not self.sharded:
+            return
+        self.all_gather_chunks(self.space.param_flat)
+        self.space.refresh_shadow()
+
+    def all_reduce_sum_(self, t):
+        """Small control-plane sum (e.g. the squared grad norm) on this engine's transport."""
+        if not self.distributed:
+            return t
+        if self._host_sync_before_comm:
+            host = t.to("cpu")
+            dist.all_reduce(host, group=self.pg)
+            t.copy_(host)
+        else:
+            dist.all_reduce(t, group=self.pg)
+        return t
 
     def zero_grad(self, set_to_none=False):  # noqa: ARG002 - flat grads are never None
         self.space.zero_grad()

@@ -15,6 +15,8 @@ all-reduce buckets fill in order.  Every parameter starts on a 16-element
 (64-byte) boundary so views are aligned for 16-byte vector loads; the total is
 padded to a multiple of 64 elements.
 """
+import math
+
 import torch
 
 ALIGN = 16
@@ -24,24 +26,44 @@ def _round_up(x, a):
     return (x + a - 1) // a * a
 
 
+def unique_trainable(params):
+    """Trainable parameters without duplicates (a tied weight appears once), in order."""
+    seen, uniq = set(), []
+    for p in params:
+        if id(p) not in seen and p.requires_grad:
+            seen.add(id(p))
+            uniq.append(p)
+    return uniq
+
+
+def layout_order(params, reverse=True):
+    """The order :class:`FlatParamSpace` lays ``params`` out in."""
+    uniq = unique_trainable(params)
+    return list(reversed(uniq)) if reverse else uniq
+
+
 class FlatParamSpace:
-    def __init__(self, params, device=None, shadow_dtype=None, reverse=True):
-        params = list(params)
-        seen, uniq = set(), []
-        for p in params:
-            if id(p) not in seen and p.requires_grad:
-                seen.add(id(p))
-                uniq.append(p)
+    """``break_after`` (layout indices) + ``break_align``: after each of those
+    parameters the next offset is rounded up to a multiple of ``break_align``
+    elements, so the sharded engine (ZeRO-1, parallel/zero.py) can cut every
+    gradient bucket into world-size equal, aligned chunks."""
+
+    def __init__(self, params, device=None, shadow_dtype=None, reverse=True, break_after=(),
+                 break_align=ALIGN):
+        uniq = unique_trainable(params)
         self.params = uniq                       # model.parameters() order
         self.layout = list(reversed(uniq)) if reverse else list(uniq)
         device = torch.device(device) if device is not None else uniq[0].device
         self.device = device
         self.offsets = {}
+        breaks = set(break_after)
         off = 0
-        for p in self.layout:
+        for i, p in enumerate(self.layout):
             self.offsets[id(p)] = off
             off = _round_up(off + p.numel(), ALIGN)
-        self.numel = _round_up(max(off, ALIGN), 64)
+            if i in breaks:
+                off = _round_up(off, break_align)
+        self.numel = _round_up(max(off, ALIGN), math.lcm(64, break_align))
         self.param_flat = torch.zeros(self.numel, dtype=torch.float32, device=device)
         self.grad_flat = torch.zeros(self.numel, dtype=torch.float32, device=device)
         self.shadow_flat = (torch.zeros(self.numel, dtype=shadow_dtype, device=device)

@@ -33,13 +33,17 @@ class FusedAdamW:
                      weight_decay=float(weight_decay))
         group["params"] = list(space.params)
         self.param_groups = [group]
-        self.exp_avg = space.new_like()
-        self.exp_avg_sq = space.new_like()
         self.step_count = 0
-        self.ema_rates = [float(r) for r in ema_rates]
-        self.ema_flats = [space.new_like("copy") for _ in self.ema_rates]
         self._partial = torch.empty(2048, dtype=torch.float32, device=space.device)
         self.norm_buf = torch.zeros(3, dtype=torch.float32, device=space.device)
+        self._init_state(ema_rates)
+
+    def _init_state(self, ema_rates):
+        """Moments and EMA buffers (full flat buffers; the ZeRO subclass shards them)."""
+        self.exp_avg = self.space.new_like()
+        self.exp_avg_sq = self.space.new_like()
+        self.ema_rates = [float(r) for r in ema_rates]
+        self.ema_flats = [self.space.new_like("copy") for _ in self.ema_rates]
 
     # -- EMA views (list of per-parameter tensors, model.parameters() order) ----
     def ema_params(self, i):
@@ -64,6 +68,17 @@ class FusedAdamW:
 
     def zero_grad(self, set_to_none=False):  # noqa: ARG002
         self.space.zero_grad()
+
+    def load_ema(self, i, tensors=None, broadcast=None):
+        """Set EMA ``i`` from per-parameter tensors (model.parameters() order, e.g. a
+        loaded ``ema_*.pt``; None keeps the current values), then ``broadcast`` the flat
+        buffer from rank 0 when given."""
+        if tensors is not None:
+            with torch.no_grad():
+                for dst, src in zip(self.ema_params(i), tensors):
+                    dst.copy_(src)
+        if broadcast is not None:
+            broadcast(self.ema_flats[i])
 
     # -- torch.optim.AdamW-compatible state ------------------------------------------
     def state_dict(self):

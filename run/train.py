@@ -117,6 +117,7 @@ def main(namespace):
         eval_interval=args.eval_interval, eval_callbacks=[],
         ddp_engine=args.ddp_engine, precision=args.precision, bucket_cap_mb=args.ddp_bucket_cap_mb,
         first_bucket_mb=args.ddp_first_bucket_mb, grad_reduce_dtype=args.grad_reduce_dtype,
+        shard_optimizer=args.shard_optimizer,
         exec_microbatch=args.exec_microbatch, hip_graphs=args.hip_graphs,
         log_cross_rank_mean=args.log_cross_rank_mean, nan_guard=args.nan_guard,
         debug_anomaly=args.debug_anomaly, consistency_check_interval=args.consistency_check_interval,

@@ -86,9 +86,12 @@ def _rccl_worker(port, wire, q):
         mask[:, :32] = 0
         t = torch.randint(0, 100, (4,), generator=g).cuda()
 
+        from distributed_pipeline_amd.ops.nn import RNG
+
         def run(sync):
             eng.zero_grad()
             torch.manual_seed(99)
+            RNG.counter = 0  # same in-kernel noise / dropout streams in both runs
             with (torch.enable_grad() if sync else eng.no_sync()):
                 terms = diff.training_losses(eng, None, t, dict(input_ids=ids, input_mask=mask))
             terms["loss"].mean().backward()

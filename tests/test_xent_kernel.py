@@ -58,3 +58,32 @@ def test_linear_cross_entropy_autograd_matches_torch():
     torch.testing.assert_close(loss, ref, rtol=2e-3, atol=2e-3)
     torch.testing.assert_close(W.grad, Wr.grad, rtol=2e-2, atol=2e-2 * Wr.grad.abs().max().item())
     torch.testing.assert_close(x.grad.float(), xr.grad, rtol=2e-2, atol=2e-2 * xr.grad.abs().max().item())
+
+
+@pytest.mark.parametrize("N,V,E,with_bias,chunk_mb", [(1000, 50257, 768, False, 16),
+                                                      (300, 1000, 512, True, 1)])
+def test_chunked_linear_cross_entropy_wide_E(N, V, E, with_bias, chunk_mb, monkeypatch):
+    """Wide-E path (GPT-2 LM head): hipBLASLt chunk logits + csrc/xent_rows.hip row
+    kernels, several chunks (incl. a ragged last one), ignored targets, padding columns."""
+    monkeypatch.setattr(ops, "_XENT_CHUNK_BYTES", chunk_mb << 20)
+    torch.manual_seed(2)
+    x = (torch.randn(N, E, device="cuda") * 0.05).bfloat16().requires_grad_(True)
+    W = torch.nn.Parameter(torch.randn(V, E, device="cuda") * 0.5)
+    b = torch.nn.Parameter(torch.randn(V, device="cuda") * 0.1) if with_bias else None
+    tgt = torch.randint(0, V, (N,), device="cuda")
+    tgt[::11] = -100
+    loss = ops.linear_cross_entropy(x, W, b, tgt)
+    g = torch.rand(N, device="cuda")
+    (loss * g).sum().backward()
+    xr = x.detach().float().requires_grad_(True)
+    Wr = W.detach().bfloat16().float().requires_grad_(True)
+    br = b.detach().bfloat16().float().requires_grad_(True) if with_bias else None
+    logits = xr @ Wr.t() + (br if with_bias else 0)
+    ref = torch.nn.functional.cross_entropy(logits, tgt.clamp_min(0), reduction="none")
+    ref = torch.where(tgt < 0, torch.zeros_like(ref), ref)
+    (ref * g).sum().backward()
+    torch.testing.assert_close(loss, ref, rtol=1e-2, atol=3e-2)
+    torch.testing.assert_close(x.grad.float(), xr.grad, rtol=3e-2, atol=3e-2 * xr.grad.abs().max().item())
+    torch.testing.assert_close(W.grad, Wr.grad, rtol=3e-2, atol=2e-2 * Wr.grad.abs().max().item())
+    if with_bias:
+        torch.testing.assert_close(b.grad, br.grad, rtol=3e-2, atol=2e-2 * br.grad.abs().max().item())

@@ -124,6 +124,7 @@ class TrainLoop:
             bucket_cap_mb=32.0,
             first_bucket_mb=4.0,
             grad_reduce_dtype="fp32",
+            shard_optimizer=False,
             exec_microbatch=0,
             hip_graphs=False,
             log_cross_rank_mean=False,
@@ -154,6 +155,7 @@ class TrainLoop:
         self.gradient_clipping = gradient_clipping
         self.engine_kind = ddp_engine
         self.precision = precision
+        self.shard_optimizer = bool(shard_optimizer)
         self.hip_graphs = bool(hip_graphs)
 
         # Executed micro-batch: a multiple of the semantic one; the loss of a
@@ -201,28 +203,39 @@ class TrainLoop:
     def _build_native(self, bucket_cap_mb, first_bucket_mb, grad_reduce_dtype):
         from distributed_pipeline_amd.parallel.ddp import DDPEngine
         from distributed_pipeline_amd.parallel.optimizer import FusedAdamW
+        from distributed_pipeline_amd.parallel.zero import ZeroFusedAdamW
         shadow = torch.bfloat16 if self.precision == "bf16" else None
         self.ddp_model = DDPEngine(
             self.model, device=self.device, bucket_cap_mb=bucket_cap_mb,
             first_bucket_mb=first_bucket_mb, shadow_dtype=shadow,
-            reduce_dtype=torch.bfloat16 if grad_reduce_dtype == "bf16" else torch.float32)
+            reduce_dtype=torch.bfloat16 if grad_reduce_dtype == "bf16" else torch.float32,
+            shard_optimizer=self.shard_optimizer)
         self.use_ddp = self.ddp_model.distributed
         self.model_params = list(self.model.parameters())
         self.master_params = self.model_params
-        self.opt = FusedAdamW(self.ddp_model.space, lr=self.lr, weight_decay=self.weight_decay,
-                              ema_rates=self.ema_rate)
+        opt_cls = ZeroFusedAdamW if self.ddp_model.sharded else FusedAdamW
+        self.opt = opt_cls(self.ddp_model if self.ddp_model.sharded else self.ddp_model.space,
+                           lr=self.lr, weight_decay=self.weight_decay, ema_rates=self.ema_rate)
         if self.resume_step:
             self._load_optimizer_state()
             for i, rate in enumerate(self.ema_rate):
-                loaded = self._load_ema_parameters(rate)
-                if loaded is not None:
-                    with torch.no_grad():
-                        for dst, src in zip(self.opt.ema_params(i), loaded):
-                            dst.copy_(src)
-                self.ddp_model.broadcast_flat(self.opt.ema_flats[i])
-        self.ema_params = [self.opt.ema_params(i) for i in range(len(self.ema_rate))]
+                self.opt.load_ema(i, self._load_ema_parameters(rate),
+                                  broadcast=self.ddp_model.broadcast_flat)
         if torch.cuda.is_available():
             torch.cuda.empty_cache()
+
+    @property
+    def ema_params(self):
+        """Per-rate lists of EMA tensors (model.parameters() order).  Native engine:
+        views of the fused optimizer's flat EMA buffers; with ``shard_optimizer`` each
+        access gathers the shards (a collective: call it on every rank)."""
+        if self.engine_kind == "native" and getattr(self, "opt", None) is not None:
+            return [self.opt.ema_params(i) for i in range(len(self.ema_rate))]
+        return self._ema_params
+
+    @ema_params.setter
+    def ema_params(self, value):
+        self._ema_params = value
 
     def _build_torch(self):
         from torch.nn.parallel.distributed import DistributedDataParallel
