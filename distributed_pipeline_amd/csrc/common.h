@@ -22,16 +22,19 @@ __device__ __forceinline__ float bf2f(bf16_t h) {
   return __uint_as_float(((uint32_t)h) << 16);
 }
 
-// Round-to-nearest-even f32 -> bf16 (NaN-preserving).
-__device__ __forceinline__ bf16_t f2bf(float f) {
-  uint32_t u = __float_as_uint(f);
-  if ((u & 0x7fffffffu) > 0x7f800000u) return (bf16_t)((u >> 16) | 0x40u);
-  u += 0x7fffu + ((u >> 16) & 1u);
-  return (bf16_t)(u >> 16);
-}
+// Round-to-nearest-even f32 -> bf16 (NaN-preserving) on CDNA4's hardware
+// converter: v_cvt_pk_bf16_f32 rounds two floats into one packed dword in a
+// single VALU op (the bit-twiddled RNE costs ~6 ops per element, which made the
+// activation / LayerNorm epilogues VALU-bound rather than HBM-bound).
+typedef __attribute__((ext_vector_type(2))) __bf16 bf16x2_hw;
 
 __device__ __forceinline__ uint32_t pack_bf2(float lo, float hi) {
-  return (uint32_t)f2bf(lo) | ((uint32_t)f2bf(hi) << 16);
+  const f32x2 v = {lo, hi};
+  return __builtin_bit_cast(uint32_t, __builtin_convertvector(v, bf16x2_hw));
+}
+
+__device__ __forceinline__ bf16_t f2bf(float f) {
+  return __builtin_bit_cast(bf16_t, (__bf16)f);
 }
 
 // ---- wave64 reductions ----------------------------------------------------

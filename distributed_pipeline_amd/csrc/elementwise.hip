@@ -14,6 +14,7 @@
 namespace dpa {
 
 enum Act { ACT_NONE = 0, ACT_GELU = 1, ACT_TANH = 2, ACT_SILU = 3 };
+constexpr int kUnroll = 4;
 
 __device__ __forceinline__ float act_f(float z, int act) { return act_apply(z, act); }
 // derivative given pre-activation z (gelu/silu) or output y (tanh)
@@ -45,17 +46,31 @@ __global__ void __launch_bounds__(256) bias_act_fwd_kernel(bf16_t* __restrict__ 
   float b[8];
   if (bias) unpack8(*reinterpret_cast<const uint4*>(bias + c8), b);
   else for (int k = 0; k < 8; ++k) b[k] = 0.f;
-  for (int64_t r = (int64_t)blockIdx.y * 4 + threadIdx.y; r < R; r += (int64_t)gridDim.y * 4) {
-    const int64_t o = r * N + c8;
-    float v[8];
-    unpack8(*reinterpret_cast<const uint4*>(z + o), v);
+  const int64_t S = (int64_t)gridDim.y * 4;
+  // kUnroll rows per trip, all loads issued before any math: enough 16-byte
+  // requests in flight per CU to cover HBM latency at full occupancy.
+  for (int64_t r0 = (int64_t)blockIdx.y * 4 + threadIdx.y; r0 < R; r0 += S * kUnroll) {
+    uint4 raw[kUnroll];
 #pragma unroll
-    for (int k = 0; k < 8; ++k) v[k] = bf2f(f2bf(v[k] + b[k]));  // z is stored rounded
-    if (bias) *reinterpret_cast<uint4*>(z + o) = pack8(v);
-    if (y) {
+    for (int u = 0; u < kUnroll; ++u) {
+      const int64_t r = r0 + u * S;
+      if (r < R) raw[u] = *reinterpret_cast<const uint4*>(z + r * N + c8);
+    }
 #pragma unroll
-      for (int k = 0; k < 8; ++k) v[k] = act_f(v[k], act);
-      *reinterpret_cast<uint4*>(y + o) = pack8(v);
+    for (int u = 0; u < kUnroll; ++u) {
+      const int64_t r = r0 + u * S;
+      if (r >= R) break;
+      const int64_t o = r * N + c8;
+      float v[8];
+      unpack8(raw[u], v);
+#pragma unroll
+      for (int k = 0; k < 8; ++k) v[k] = bf2f(f2bf(v[k] + b[k]));  // z is stored rounded
+      if (bias) *reinterpret_cast<uint4*>(z + o) = pack8(v);
+      if (y) {
+#pragma unroll
+        for (int k = 0; k < 8; ++k) v[k] = act_f(v[k], act);
+        *reinterpret_cast<uint4*>(y + o) = pack8(v);
+      }
     }
   }
 }
@@ -71,19 +86,34 @@ __global__ void __launch_bounds__(256) bias_act_bwd_kernel(const bf16_t* __restr
 #pragma unroll
   for (int k = 0; k < 8; ++k) acc[k] = 0.f;
   if (c8 < N) {
-    for (int64_t r = (int64_t)blockIdx.y * 4 + threadIdx.y; r < R; r += (int64_t)gridDim.y * 4) {
-      const int64_t o = r * N + c8;
-      float d[8];
-      unpack8(*reinterpret_cast<const uint4*>(dy + o), d);
-      if (act != ACT_NONE) {
-        float zz[8];
-        unpack8(*reinterpret_cast<const uint4*>(zy + o), zz);
+    const int64_t S = (int64_t)gridDim.y * 4;
+    const bool has_aux = act != ACT_NONE;
+    for (int64_t r0 = (int64_t)blockIdx.y * 4 + threadIdx.y; r0 < R; r0 += S * kUnroll) {
+      uint4 rd[kUnroll], rz[kUnroll];
 #pragma unroll
-        for (int k = 0; k < 8; ++k) d[k] *= act_grad(zz[k], act);
+      for (int u = 0; u < kUnroll; ++u) {
+        const int64_t r = r0 + u * S;
+        if (r < R) {
+          rd[u] = *reinterpret_cast<const uint4*>(dy + r * N + c8);
+          if (has_aux) rz[u] = *reinterpret_cast<const uint4*>(zy + r * N + c8);
+        }
       }
-      if (dz) *reinterpret_cast<uint4*>(dz + o) = pack8(d);
 #pragma unroll
-      for (int k = 0; k < 8; ++k) acc[k] += bf2f(f2bf(d[k]));
+      for (int u = 0; u < kUnroll; ++u) {
+        const int64_t r = r0 + u * S;
+        if (r >= R) break;
+        float d[8];
+        unpack8(rd[u], d);
+        if (has_aux) {
+          float zz[8];
+          unpack8(rz[u], zz);
+#pragma unroll
+          for (int k = 0; k < 8; ++k) d[k] *= act_grad(zz[k], act);
+        }
+        if (dz) *reinterpret_cast<uint4*>(dz + r * N + c8) = pack8(d);
+#pragma unroll
+        for (int k = 0; k < 8; ++k) acc[k] += bf2f(f2bf(d[k]));
+      }
     }
   }
   if (!db) return;

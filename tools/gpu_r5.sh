@@ -1,0 +1,9 @@
+set -o pipefail
+cd $GRAFT_REPO_ROOT
+export TMPDIR=/tmp
+mkdir -p gpurun_out
+timeout -k 10 900 python -u -m pytest tests -m gpu -v --timeout 300 --timeout-method thread > gpurun_out/r5_pytest_gpu.log 2>&1
+echo "pytest exit=$?" >> gpurun_out/r5_pytest_gpu.log
+timeout -k 10 400 python -u bench.py --steps 10 --warmup 3 > gpurun_out/r5_bench.log 2>&1 && \
+timeout -k 10 400 rocprofv3 --kernel-trace --stats -d gpurun_out/r5_prof -o run -- python bench.py --steps 5 --warmup 2 > gpurun_out/r5_prof.log 2>&1
+echo "exit=$?"
