@@ -4,6 +4,13 @@ Policy: on a machine with a visible HIP device the extension is REQUIRED -
 every op that has a gfx950 kernel runs it, and a missing/broken build raises
 immediately instead of silently falling back to eager PyTorch.  On CPU-only
 hosts (unit tests) ops use their PyTorch reference implementations.
+
+Debug mode: ``DPA_SYNC_CHECK=1`` returns a proxy of the module whose
+functions synchronise the device after every native call and re-raise any HIP
+error together with the op name and its tensor shapes/dtypes, so an
+asynchronous fault (out-of-bounds access, bad launch) is attributed to the
+kernel that caused it rather than to whatever op synchronises next.  The cost
+is one device sync per op; use it for debugging only.
 """
 import importlib
 import os
@@ -12,6 +19,41 @@ import torch
 
 _EXT = None
 _ERR = None
+
+
+def _describe(args):
+    out = []
+    for a in args:
+        if isinstance(a, torch.Tensor):
+            out.append(f"Tensor{tuple(a.shape)}:{str(a.dtype).replace('torch.', '')}@{a.device}")
+        else:
+            out.append(type(a).__name__ if not isinstance(a, (int, float, bool)) else repr(a))
+    return ", ".join(out)
+
+
+class _SyncChecked:
+    """Module proxy: every pybind function call is followed by a device sync."""
+
+    def __init__(self, mod):
+        self._mod = mod
+
+    def __getattr__(self, name):
+        attr = getattr(self._mod, name)
+        if type(attr).__name__ != "builtin_function_or_method":
+            return attr
+
+        def checked(*args, **kwargs):
+            try:
+                out = attr(*args, **kwargs)
+                if torch.cuda.is_available():
+                    torch.cuda.synchronize()
+            except Exception as exc:  # noqa: BLE001
+                raise RuntimeError(f"[DPA_SYNC_CHECK] native op {name}({_describe(args)}) failed: "
+                                   f"{exc}") from exc
+            return out
+
+        checked.__name__ = name
+        return checked
 
 
 def gpu_present():
@@ -24,6 +66,8 @@ def get_ext(required=None):
     if _EXT is None and _ERR is None:
         try:
             _EXT = importlib.import_module("distributed_pipeline_amd._C")
+            if os.environ.get("DPA_SYNC_CHECK", "0") == "1":
+                _EXT = _SyncChecked(_EXT)
         except Exception as exc:  # noqa: BLE001
             _ERR = exc
     if required is None:
