@@ -534,7 +534,7 @@ static bool gemm_supported(int64_t M, int64_t N, int64_t K) {
   return M % 128 == 0 && N % 128 == 0 && K % 128 == 0;
 }
 
-PYBIND11_MODULE(_C, m) {
+PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.doc() = "distributed_pipeline_amd native gfx950 kernels";
   dpa::register_comm(m);
   m.def("sqnorm", &sqnorm, "flat grad L2 norm + clip coefficient (device)");

@@ -65,7 +65,9 @@ def get_ext(required=None):
     global _EXT, _ERR
     if _EXT is None and _ERR is None:
         try:
-            _EXT = importlib.import_module("distributed_pipeline_amd._C")
+            # DPA_EXT selects an alternative build of the same sources, e.g. the
+            # host-ASan build ``_C_asan`` of tools/asan_build.py
+            _EXT = importlib.import_module("distributed_pipeline_amd." + os.environ.get("DPA_EXT", "_C"))
             if os.environ.get("DPA_SYNC_CHECK", "0") == "1":
                 _EXT = _SyncChecked(_EXT)
         except Exception as exc:  # noqa: BLE001
