@@ -51,6 +51,28 @@ __device__ __forceinline__ bool keep_bit(const DropCfg& d, int q, int key) {
   return r >= d.thr16;
 }
 
+// softmax scale in the exp2 domain and the 1/sqrt(D) gradient scale
+template <int D>
+__device__ __forceinline__ constexpr float att_c() { return D == 64 ? ATT_C : 1.4426950408889634f * 0.08838834764831845f; }
+template <int D>
+__device__ __forceinline__ constexpr float rsqrt_d() { return D == 64 ? 0.125f : 0.08838834764831845f; }
+
+// stage a [64 rows][D] bf16 tile (rows r0.., stride `ld` elements) -> swizzled LDS
+// rows of 2*D bytes; 64*D/8 16-byte chunks over 256 threads
+template <int D>
+__device__ __forceinline__ void stage_tile(char* lds, const bf16_t* __restrict__ src, int64_t ld,
+                                           int r0, int nrows, int tid) {
+  constexpr int CPR = D / 8;  // chunks per row
+#pragma unroll
+  for (int i = 0; i < 64 * CPR / 256; ++i) {
+    const int c = tid + i * 256;
+    const int row = c / CPR, ch = c % CPR;
+    uint4 v = make_uint4(0, 0, 0, 0);
+    if (r0 + row < nrows) v = *reinterpret_cast<const uint4*>(src + (int64_t)(r0 + row) * ld + ch * 8);
+    *reinterpret_cast<uint4*>(lds + swz<2 * D>(row, ch)) = v;
+  }
+}
+
 // stage a [64 rows][64 d] bf16 tile (rows r0.., stride `ld` elements) -> swizzled LDS
 __device__ __forceinline__ void stage64(char* lds, const bf16_t* __restrict__ src, int64_t ld,
                                         int r0, int nrows, int tid) {
@@ -67,26 +89,26 @@ __device__ __forceinline__ void stage64(char* lds, const bf16_t* __restrict__ sr
 // ---------------------------------------------------------------------------
 // forward
 // ---------------------------------------------------------------------------
-template <bool CAUSAL>
+template <int D, bool CAUSAL>
 __global__ void __launch_bounds__(256) attn_fwd_kernel(const bf16_t* __restrict__ qkv,
                                                       bf16_t* __restrict__ out, float* __restrict__ lse,
                                                       int L, int H, float p, uint32_t seed,
                                                       uint32_t offset) {
-  __shared__ __attribute__((aligned(16))) char smem[2 * 64 * 128];
+  __shared__ __attribute__((aligned(16))) char smem[2 * 64 * 2 * D];
   char* kt_lds = smem;
-  char* vt_lds = smem + 64 * 128;
+  char* vt_lds = smem + 64 * 2 * D;
   const int b = blockIdx.z, hd = blockIdx.y;
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, hf = lane >> 5;
-  const int64_t ld = 3LL * H * HD;  // token stride
-  const bf16_t* qb = qkv + (int64_t)b * L * ld + (int64_t)hd * HD;
-  const bf16_t* kb = qb + (int64_t)H * HD;
-  const bf16_t* vb = qb + 2LL * H * HD;
+  const int64_t ld = 3LL * H * D;  // token stride
+  const bf16_t* qb = qkv + (int64_t)b * L * ld + (int64_t)hd * D;
+  const bf16_t* kb = qb + (int64_t)H * D;
+  const bf16_t* vb = qb + 2LL * H * D;
   const int qbase = blockIdx.x * 128 + w * 32;
   const int q = qbase + (lane & 31);
   const bool q_ok = q < L;
-  bf16x8 qf[4];
+  bf16x8 qf[D / 16];
 #pragma unroll
-  for (int s = 0; s < 4; ++s) {
+  for (int s = 0; s < D / 16; ++s) {
     if (q_ok) qf[s] = ld_frag(qb + (int64_t)q * ld + 16 * s + 8 * hf);
     else for (int j = 0; j < 8; ++j) qf[s][j] = 0;
   }
@@ -96,14 +118,14 @@ __global__ void __launch_bounds__(256) attn_fwd_kernel(const bf16_t* __restrict_
   // ---- pass 1: row statistics -------------------------------------------------
   float m = -1e30f, l = 0.f;
   for (int kv0 = 0; kv0 < kv_end; kv0 += 64) {
-    stage64(kt_lds, kb, ld, kv0, L, tid);
+    stage_tile<D>(kt_lds, kb, ld, kv0, L, tid);
     __syncthreads();
     f32x16 acc[2];
 #pragma unroll
     for (int t = 0; t < 2; ++t) {
       acc[t] = zero16();
 #pragma unroll
-      for (int s = 0; s < 4; ++s) acc[t] = mfma32(lds_frag<128>(kt_lds, t * 32 + (lane & 31), 2 * s + hf), qf[s], acc[t]);
+      for (int s = 0; s < D / 16; ++s) acc[t] = mfma32(lds_frag<2 * D>(kt_lds, t * 32 + (lane & 31), 2 * s + hf), qf[s], acc[t]);
     }
     float tmax = -INFINITY;
 #pragma unroll
@@ -111,7 +133,7 @@ __global__ void __launch_bounds__(256) attn_fwd_kernel(const bf16_t* __restrict_
 #pragma unroll
       for (int i = 0; i < 16; ++i) {
         const int key = kv0 + t * 32 + acc_row(i, hf);
-        float y = acc[t][i] * ATT_C;
+        float y = acc[t][i] * att_c<D>();
         if (CAUSAL && key > q) y = -INFINITY;
         acc[t][i] = y;
         tmax = fmaxf(tmax, y);
@@ -136,22 +158,22 @@ __global__ void __launch_bounds__(256) attn_fwd_kernel(const bf16_t* __restrict_
   if (hf == 0 && q_ok) lse[((int64_t)b * H + hd) * L + q] = lse2 * LN2f;
 
   // ---- pass 2: O = dropout(P) V --------------------------------------------------
-  f32x16 o[2];
-  o[0] = zero16();
-  o[1] = zero16();
+  f32x16 o[D / 32];
+#pragma unroll
+  for (int dt = 0; dt < D / 32; ++dt) o[dt] = zero16();
   for (int kv0 = 0; kv0 < kv_end; kv0 += 64) {
-    stage64(kt_lds, kb, ld, kv0, L, tid);
-    stage64(vt_lds, vb, ld, kv0, L, tid);
+    stage_tile<D>(kt_lds, kb, ld, kv0, L, tid);
+    stage_tile<D>(vt_lds, vb, ld, kv0, L, tid);
     __syncthreads();
 #pragma unroll
     for (int t = 0; t < 2; ++t) {
       f32x16 acc = zero16();
 #pragma unroll
-      for (int s = 0; s < 4; ++s) acc = mfma32(lds_frag<128>(kt_lds, t * 32 + (lane & 31), 2 * s + hf), qf[s], acc);
+      for (int s = 0; s < D / 16; ++s) acc = mfma32(lds_frag<2 * D>(kt_lds, t * 32 + (lane & 31), 2 * s + hf), qf[s], acc);
 #pragma unroll
       for (int i = 0; i < 16; ++i) {
         const int key = kv0 + t * 32 + acc_row(i, hf);
-        float pr = fexp2(acc[i] * ATT_C - lse2);
+        float pr = fexp2(acc[i] * att_c<D>() - lse2);
         if (CAUSAL && key > q) pr = 0.f;
         if (dc.on) pr = keep_bit(dc, q, key) ? pr * dc.scale : 0.f;
         acc[i] = pr;
@@ -160,20 +182,20 @@ __global__ void __launch_bounds__(256) attn_fwd_kernel(const bf16_t* __restrict_
       for (int s = 0; s < 2; ++s) {
         const bf16x8 af = acc_to_frag(acc, s);
 #pragma unroll
-        for (int dt = 0; dt < 2; ++dt)
-          o[dt] = mfma32(af, lds_tr_frag<128>(vt_lds, t * 32 + 16 * s, dt * 32, lane), o[dt]);
+        for (int dt = 0; dt < D / 32; ++dt)
+          o[dt] = mfma32(af, lds_tr_frag<2 * D>(vt_lds, t * 32 + 16 * s, dt * 32, lane), o[dt]);
       }
     }
     __syncthreads();
   }
   // o[dt] reg i: row = query qbase + acc_row(i,hf), col = d (dt*32 + lane&31)
-  bf16_t* ob = out + (int64_t)b * L * H * HD + (int64_t)hd * HD;
+  bf16_t* ob = out + (int64_t)b * L * H * D + (int64_t)hd * D;
 #pragma unroll
-  for (int dt = 0; dt < 2; ++dt)
+  for (int dt = 0; dt < D / 32; ++dt)
 #pragma unroll
     for (int i = 0; i < 16; ++i) {
       const int qq = qbase + acc_row(i, hf);
-      if (qq < L) ob[(int64_t)qq * H * HD + dt * 32 + (lane & 31)] = f2bf(o[dt][i]);
+      if (qq < L) ob[(int64_t)qq * H * D + dt * 32 + (lane & 31)] = f2bf(o[dt][i]);
     }
 }
 
@@ -275,6 +297,7 @@ __global__ void __launch_bounds__(256) attn_fwd_small_kernel(const bf16_t* __res
 }
 
 // delta[b,h,q] = sum_d dO * O
+template <int D>
 __global__ void __launch_bounds__(256) attn_delta_kernel(const bf16_t* __restrict__ dout,
                                                         const bf16_t* __restrict__ out,
                                                         float* __restrict__ delta, int B, int L, int H) {
@@ -283,11 +306,11 @@ __global__ void __launch_bounds__(256) attn_delta_kernel(const bf16_t* __restric
   const int hd = (int)(idx % H);
   const int64_t bq = idx / H;
   const int q = (int)(bq % L), b = (int)(bq / L);
-  const bf16_t* d = dout + idx * HD;
-  const bf16_t* o = out + idx * HD;
+  const bf16_t* d = dout + idx * D;
+  const bf16_t* o = out + idx * D;
   float s = 0.f;
 #pragma unroll
-  for (int c = 0; c < 8; ++c) {
+  for (int c = 0; c < D / 8; ++c) {
     uint4 a = *reinterpret_cast<const uint4*>(d + c * 8);
     uint4 bb = *reinterpret_cast<const uint4*>(o + c * 8);
     const uint32_t aw[4] = {a.x, a.y, a.z, a.w}, bw[4] = {bb.x, bb.y, bb.z, bb.w};
@@ -307,29 +330,29 @@ __global__ void __launch_bounds__(256) attn_delta_kernel(const bf16_t* __restric
 //   dV += dropout(P)^T dO,  dK += dS^T Q   with dS = P (dropout'(dP) - delta),
 // both straight from the accumulators (dO / Q read transposed from LDS).
 // ---------------------------------------------------------------------------
-template <bool CAUSAL>
+template <int D, bool CAUSAL>
 __global__ void __launch_bounds__(256) attn_bwd_kv_kernel(
     const bf16_t* __restrict__ qkv, const bf16_t* __restrict__ dout, const float* __restrict__ lse,
     const float* __restrict__ delta, bf16_t* __restrict__ dqkv, int L, int H, float p,
     uint32_t seed, uint32_t offset) {
-  __shared__ __attribute__((aligned(16))) char smem[2 * 64 * 128 + 2 * 64 * 4];
+  __shared__ __attribute__((aligned(16))) char smem[2 * 64 * 2 * D + 2 * 64 * 4];
   char* qt_lds = smem;
-  char* dot_lds = smem + 64 * 128;
-  float* s_lse = reinterpret_cast<float*>(smem + 2 * 64 * 128);
+  char* dot_lds = smem + 64 * 2 * D;
+  float* s_lse = reinterpret_cast<float*>(smem + 2 * 64 * 2 * D);
   float* s_del = s_lse + 64;
   const int b = blockIdx.z, hd = blockIdx.y;
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, hf = lane >> 5;
-  const int64_t ld = 3LL * H * HD, ldo = (int64_t)H * HD;
-  const bf16_t* qb = qkv + (int64_t)b * L * ld + (int64_t)hd * HD;
-  const bf16_t* kb = qb + (int64_t)H * HD;
-  const bf16_t* vb = qb + 2LL * H * HD;
-  const bf16_t* dob = dout + (int64_t)b * L * ldo + (int64_t)hd * HD;
+  const int64_t ld = 3LL * H * D, ldo = (int64_t)H * D;
+  const bf16_t* qb = qkv + (int64_t)b * L * ld + (int64_t)hd * D;
+  const bf16_t* kb = qb + (int64_t)H * D;
+  const bf16_t* vb = qb + 2LL * H * D;
+  const bf16_t* dob = dout + (int64_t)b * L * ldo + (int64_t)hd * D;
   const int kbase = blockIdx.x * 128 + w * 32;
   const int key = kbase + (lane & 31);
   const bool k_ok = key < L;
-  bf16x8 kf[4], vf[4];
+  bf16x8 kf[D / 16], vf[D / 16];
 #pragma unroll
-  for (int s = 0; s < 4; ++s) {
+  for (int s = 0; s < D / 16; ++s) {
     if (k_ok) {
       kf[s] = ld_frag(kb + (int64_t)key * ld + 16 * s + 8 * hf);
       vf[s] = ld_frag(vb + (int64_t)key * ld + 16 * s + 8 * hf);
@@ -339,12 +362,13 @@ __global__ void __launch_bounds__(256) attn_bwd_kv_kernel(
   }
   const DropCfg dc = make_drop(p, seed, offset, (uint32_t)(b * H + hd));
   const int64_t lrow = ((int64_t)b * H + hd) * L;
-  f32x16 dk[2], dv[2];
-  dk[0] = zero16(); dk[1] = zero16(); dv[0] = zero16(); dv[1] = zero16();
+  f32x16 dk[D / 32], dv[D / 32];
+#pragma unroll
+  for (int dt = 0; dt < D / 32; ++dt) { dk[dt] = zero16(); dv[dt] = zero16(); }
   const int qbeg = CAUSAL ? (int)blockIdx.x * 128 : 0;
   for (int q0 = qbeg; q0 < L; q0 += 64) {
-    stage64(qt_lds, qb, ld, q0, L, tid);
-    stage64(dot_lds, dob, ldo, q0, L, tid);
+    stage_tile<D>(qt_lds, qb, ld, q0, L, tid);
+    stage_tile<D>(dot_lds, dob, ldo, q0, L, tid);
     if (tid < 64) {
       const bool ok = q0 + tid < L;
       s_lse[tid] = ok ? lse[lrow + q0 + tid] * 1.4426950408889634f : 0.f;
@@ -355,15 +379,15 @@ __global__ void __launch_bounds__(256) attn_bwd_kv_kernel(
     for (int qt = 0; qt < 2; ++qt) {
       f32x16 sacc = zero16(), dpacc = zero16();
 #pragma unroll
-      for (int s = 0; s < 4; ++s) {
-        sacc = mfma32(lds_frag<128>(qt_lds, qt * 32 + (lane & 31), 2 * s + hf), kf[s], sacc);
-        dpacc = mfma32(lds_frag<128>(dot_lds, qt * 32 + (lane & 31), 2 * s + hf), vf[s], dpacc);
+      for (int s = 0; s < D / 16; ++s) {
+        sacc = mfma32(lds_frag<2 * D>(qt_lds, qt * 32 + (lane & 31), 2 * s + hf), kf[s], sacc);
+        dpacc = mfma32(lds_frag<2 * D>(dot_lds, qt * 32 + (lane & 31), 2 * s + hf), vf[s], dpacc);
       }
 #pragma unroll
       for (int i = 0; i < 16; ++i) {
         const int r = qt * 32 + acc_row(i, hf);
         const int qq = q0 + r;
-        float pr = fexp2(sacc[i] * ATT_C - s_lse[r]);
+        float pr = fexp2(sacc[i] * att_c<D>() - s_lse[r]);
         if ((CAUSAL && key > qq) || !k_ok || qq >= L) pr = 0.f;
         float pd = pr, dpd = dpacc[i];
         if (dc.on) {
@@ -379,23 +403,23 @@ __global__ void __launch_bounds__(256) attn_bwd_kv_kernel(
         const bf16x8 pf = acc_to_frag(sacc, s);
         const bf16x8 sf = acc_to_frag(dpacc, s);
 #pragma unroll
-        for (int dt = 0; dt < 2; ++dt) {
-          dv[dt] = mfma32(pf, lds_tr_frag<128>(dot_lds, qt * 32 + 16 * s, dt * 32, lane), dv[dt]);
-          dk[dt] = mfma32(sf, lds_tr_frag<128>(qt_lds, qt * 32 + 16 * s, dt * 32, lane), dk[dt]);
+        for (int dt = 0; dt < D / 32; ++dt) {
+          dv[dt] = mfma32(pf, lds_tr_frag<2 * D>(dot_lds, qt * 32 + 16 * s, dt * 32, lane), dv[dt]);
+          dk[dt] = mfma32(sf, lds_tr_frag<2 * D>(qt_lds, qt * 32 + 16 * s, dt * 32, lane), dk[dt]);
         }
       }
     }
     __syncthreads();
   }
 #pragma unroll
-  for (int dt = 0; dt < 2; ++dt)
+  for (int dt = 0; dt < D / 32; ++dt)
 #pragma unroll
     for (int i = 0; i < 16; ++i) {
       const int kk = kbase + acc_row(i, hf);
       if (kk < L) {
-        bf16_t* base = dqkv + ((int64_t)b * L + kk) * ld + (int64_t)hd * HD + dt * 32 + (lane & 31);
-        base[(int64_t)H * HD] = f2bf(dk[dt][i] * 0.125f);
-        base[2LL * H * HD] = f2bf(dv[dt][i]);
+        bf16_t* base = dqkv + ((int64_t)b * L + kk) * ld + (int64_t)hd * D + dt * 32 + (lane & 31);
+        base[(int64_t)H * D] = f2bf(dk[dt][i] * rsqrt_d<D>());
+        base[2LL * H * D] = f2bf(dv[dt][i]);
       }
     }
 }
@@ -407,27 +431,27 @@ __global__ void __launch_bounds__(256) attn_bwd_kv_kernel(
 //   dQ += dS K with dS^T fed as the A operand and K read transposed.
 // No atomics: each workgroup owns its queries' dQ rows completely.
 // ---------------------------------------------------------------------------
-template <bool CAUSAL>
+template <int D, bool CAUSAL>
 __global__ void __launch_bounds__(256) attn_bwd_q_kernel(
     const bf16_t* __restrict__ qkv, const bf16_t* __restrict__ dout, const float* __restrict__ lse,
     const float* __restrict__ delta, bf16_t* __restrict__ dqkv, int L, int H, float p,
     uint32_t seed, uint32_t offset) {
-  __shared__ __attribute__((aligned(16))) char smem[2 * 64 * 128];
+  __shared__ __attribute__((aligned(16))) char smem[2 * 64 * 2 * D];
   char* kt_lds = smem;
-  char* vt_lds = smem + 64 * 128;
+  char* vt_lds = smem + 64 * 2 * D;
   const int b = blockIdx.z, hd = blockIdx.y;
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, hf = lane >> 5;
-  const int64_t ld = 3LL * H * HD, ldo = (int64_t)H * HD;
-  const bf16_t* qb = qkv + (int64_t)b * L * ld + (int64_t)hd * HD;
-  const bf16_t* kb = qb + (int64_t)H * HD;
-  const bf16_t* vb = qb + 2LL * H * HD;
-  const bf16_t* dob = dout + (int64_t)b * L * ldo + (int64_t)hd * HD;
+  const int64_t ld = 3LL * H * D, ldo = (int64_t)H * D;
+  const bf16_t* qb = qkv + (int64_t)b * L * ld + (int64_t)hd * D;
+  const bf16_t* kb = qb + (int64_t)H * D;
+  const bf16_t* vb = qb + 2LL * H * D;
+  const bf16_t* dob = dout + (int64_t)b * L * ldo + (int64_t)hd * D;
   const int qbase = blockIdx.x * 128 + w * 32;
   const int q = qbase + (lane & 31);
   const bool q_ok = q < L;
-  bf16x8 qf[4], df[4];
+  bf16x8 qf[D / 16], df[D / 16];
 #pragma unroll
-  for (int s = 0; s < 4; ++s) {
+  for (int s = 0; s < D / 16; ++s) {
     if (q_ok) {
       qf[s] = ld_frag(qb + (int64_t)q * ld + 16 * s + 8 * hf);
       df[s] = ld_frag(dob + (int64_t)q * ldo + 16 * s + 8 * hf);
@@ -439,26 +463,26 @@ __global__ void __launch_bounds__(256) attn_bwd_q_kernel(
   const float lse2 = q_ok ? lse[lrow + q] * 1.4426950408889634f : 0.f;
   const float dlt = q_ok ? delta[lrow + q] : 0.f;
   const DropCfg dc = make_drop(p, seed, offset, (uint32_t)(b * H + hd));
-  f32x16 dq[2];
-  dq[0] = zero16();
-  dq[1] = zero16();
+  f32x16 dq[D / 32];
+#pragma unroll
+  for (int dt = 0; dt < D / 32; ++dt) dq[dt] = zero16();
   const int kv_end = CAUSAL ? min(L, (int)blockIdx.x * 128 + 128) : L;
   for (int kv0 = 0; kv0 < kv_end; kv0 += 64) {
-    stage64(kt_lds, kb, ld, kv0, L, tid);
-    stage64(vt_lds, vb, ld, kv0, L, tid);
+    stage_tile<D>(kt_lds, kb, ld, kv0, L, tid);
+    stage_tile<D>(vt_lds, vb, ld, kv0, L, tid);
     __syncthreads();
 #pragma unroll 1
     for (int t = 0; t < 2; ++t) {
       f32x16 sacc = zero16(), dpacc = zero16();
 #pragma unroll
-      for (int s = 0; s < 4; ++s) {
-        sacc = mfma32(lds_frag<128>(kt_lds, t * 32 + (lane & 31), 2 * s + hf), qf[s], sacc);
-        dpacc = mfma32(lds_frag<128>(vt_lds, t * 32 + (lane & 31), 2 * s + hf), df[s], dpacc);
+      for (int s = 0; s < D / 16; ++s) {
+        sacc = mfma32(lds_frag<2 * D>(kt_lds, t * 32 + (lane & 31), 2 * s + hf), qf[s], sacc);
+        dpacc = mfma32(lds_frag<2 * D>(vt_lds, t * 32 + (lane & 31), 2 * s + hf), df[s], dpacc);
       }
 #pragma unroll
       for (int i = 0; i < 16; ++i) {
         const int kk = kv0 + t * 32 + acc_row(i, hf);
-        float pr = fexp2(sacc[i] * ATT_C - lse2);
+        float pr = fexp2(sacc[i] * att_c<D>() - lse2);
         if ((CAUSAL && kk > q) || !q_ok || kk >= L) pr = 0.f;
         float dpd = dpacc[i];
         if (dc.on) dpd = keep_bit(dc, q, kk) ? dpd * dc.scale : 0.f;
@@ -468,26 +492,39 @@ __global__ void __launch_bounds__(256) attn_bwd_q_kernel(
       for (int s = 0; s < 2; ++s) {
         const bf16x8 sf = acc_to_frag(sacc, s);
 #pragma unroll
-        for (int dt = 0; dt < 2; ++dt)
-          dq[dt] = mfma32(sf, lds_tr_frag<128>(kt_lds, t * 32 + 16 * s, dt * 32, lane), dq[dt]);
+        for (int dt = 0; dt < D / 32; ++dt)
+          dq[dt] = mfma32(sf, lds_tr_frag<2 * D>(kt_lds, t * 32 + 16 * s, dt * 32, lane), dq[dt]);
       }
     }
     __syncthreads();
   }
 #pragma unroll
-  for (int dt = 0; dt < 2; ++dt)
+  for (int dt = 0; dt < D / 32; ++dt)
 #pragma unroll
     for (int i = 0; i < 16; ++i) {
       const int qq = qbase + acc_row(i, hf);
-      if (qq < L) dqkv[((int64_t)b * L + qq) * ld + (int64_t)hd * HD + dt * 32 + (lane & 31)] = f2bf(dq[dt][i] * 0.125f);
+      if (qq < L) dqkv[((int64_t)b * L + qq) * ld + (int64_t)hd * D + dt * 32 + (lane & 31)] = f2bf(dq[dt][i] * rsqrt_d<D>());
     }
 }
 
-void launch_attn_fwd(const uint16_t* qkv, uint16_t* out, float* lse, int B, int L, int H, float p,
-                     bool causal, uint32_t seed, uint32_t offset, hipStream_t s) {
-  if (launch_attn128_fwd(qkv, out, lse, B, L, H, p, causal, seed, offset, s)) return;
+template <int D>
+static void attn_fwd_general(const uint16_t* qkv, uint16_t* out, float* lse, int B, int L, int H,
+                             float p, bool causal, uint32_t seed, uint32_t offset, hipStream_t s) {
   dim3 grid((L + 127) / 128, H, B);
+  if (causal)
+    hipLaunchKernelGGL((attn_fwd_kernel<D, true>), grid, dim3(256), 0, s, (const bf16_t*)qkv,
+                       (bf16_t*)out, lse, L, H, p, seed, offset);
+  else
+    hipLaunchKernelGGL((attn_fwd_kernel<D, false>), grid, dim3(256), 0, s, (const bf16_t*)qkv,
+                       (bf16_t*)out, lse, L, H, p, seed, offset);
+}
+
+void launch_attn_fwd(const uint16_t* qkv, uint16_t* out, float* lse, int B, int L, int H, int D,
+                     float p, bool causal, uint32_t seed, uint32_t offset, hipStream_t s) {
+  if (D == 128) return attn_fwd_general<128>(qkv, out, lse, B, L, H, p, causal, seed, offset, s);
+  if (launch_attn128_fwd(qkv, out, lse, B, L, H, p, causal, seed, offset, s)) return;
   if (L <= 128) {
+    dim3 grid((L + 127) / 128, H, B);
     if (causal)
       hipLaunchKernelGGL(attn_fwd_small_kernel<true>, grid, dim3(256), 0, s, (const bf16_t*)qkv,
                          (bf16_t*)out, lse, L, H, p, seed, offset);
@@ -496,38 +533,45 @@ void launch_attn_fwd(const uint16_t* qkv, uint16_t* out, float* lse, int B, int 
                          (bf16_t*)out, lse, L, H, p, seed, offset);
     return;
   }
-  if (causal)
-    hipLaunchKernelGGL(attn_fwd_kernel<true>, grid, dim3(256), 0, s, (const bf16_t*)qkv,
-                       (bf16_t*)out, lse, L, H, p, seed, offset);
-  else
-    hipLaunchKernelGGL(attn_fwd_kernel<false>, grid, dim3(256), 0, s, (const bf16_t*)qkv,
-                       (bf16_t*)out, lse, L, H, p, seed, offset);
+  attn_fwd_general<64>(qkv, out, lse, B, L, H, p, causal, seed, offset, s);
 }
 
 bool attn_bwd_needs_dq_acc(int L) { (void)L; return false; }
 
-bool launch_attn_bwd(const uint16_t* qkv, const uint16_t* out, const uint16_t* dout, const float* lse,
-                     float* delta, uint16_t* dqkv, float* dq_acc, float* colpart, float* dbias, int B,
-                     int L, int H, float p, bool causal, uint32_t seed, uint32_t offset, hipStream_t s) {
-  (void)dq_acc;
-  if (launch_attn128_bwd(qkv, out, dout, lse, dqkv, colpart, dbias, B, L, H, p, causal, seed, offset,
-                         s))
-    return dbias != nullptr;
+template <int D>
+static void attn_bwd_general(const uint16_t* qkv, const uint16_t* out, const uint16_t* dout,
+                             const float* lse, float* delta, uint16_t* dqkv, int B, int L, int H,
+                             float p, bool causal, uint32_t seed, uint32_t offset, hipStream_t s) {
   const int64_t rows = (int64_t)B * L * H;
-  hipLaunchKernelGGL(attn_delta_kernel, dim3((unsigned)((rows + 255) / 256)), dim3(256), 0, s,
+  hipLaunchKernelGGL(attn_delta_kernel<D>, dim3((unsigned)((rows + 255) / 256)), dim3(256), 0, s,
                      (const bf16_t*)dout, (const bf16_t*)out, delta, B, L, H);
   dim3 grid((L + 127) / 128, H, B);
   if (causal) {
-    hipLaunchKernelGGL(attn_bwd_kv_kernel<true>, grid, dim3(256), 0, s, (const bf16_t*)qkv,
+    hipLaunchKernelGGL((attn_bwd_kv_kernel<D, true>), grid, dim3(256), 0, s, (const bf16_t*)qkv,
                        (const bf16_t*)dout, lse, delta, (bf16_t*)dqkv, L, H, p, seed, offset);
-    hipLaunchKernelGGL(attn_bwd_q_kernel<true>, grid, dim3(256), 0, s, (const bf16_t*)qkv,
+    hipLaunchKernelGGL((attn_bwd_q_kernel<D, true>), grid, dim3(256), 0, s, (const bf16_t*)qkv,
                        (const bf16_t*)dout, lse, delta, (bf16_t*)dqkv, L, H, p, seed, offset);
   } else {
-    hipLaunchKernelGGL(attn_bwd_kv_kernel<false>, grid, dim3(256), 0, s, (const bf16_t*)qkv,
+    hipLaunchKernelGGL((attn_bwd_kv_kernel<D, false>), grid, dim3(256), 0, s, (const bf16_t*)qkv,
                        (const bf16_t*)dout, lse, delta, (bf16_t*)dqkv, L, H, p, seed, offset);
-    hipLaunchKernelGGL(attn_bwd_q_kernel<false>, grid, dim3(256), 0, s, (const bf16_t*)qkv,
+    hipLaunchKernelGGL((attn_bwd_q_kernel<D, false>), grid, dim3(256), 0, s, (const bf16_t*)qkv,
                        (const bf16_t*)dout, lse, delta, (bf16_t*)dqkv, L, H, p, seed, offset);
   }
+}
+
+bool launch_attn_bwd(const uint16_t* qkv, const uint16_t* out, const uint16_t* dout, const float* lse,
+                     float* delta, uint16_t* dqkv, float* dq_acc, float* colpart, float* dbias, int B,
+                     int L, int H, int D, float p, bool causal, uint32_t seed, uint32_t offset,
+                     hipStream_t s) {
+  (void)dq_acc;
+  if (D == 128) {
+    attn_bwd_general<128>(qkv, out, dout, lse, delta, dqkv, B, L, H, p, causal, seed, offset, s);
+    return false;
+  }
+  if (launch_attn128_bwd(qkv, out, dout, lse, dqkv, colpart, dbias, B, L, H, p, causal, seed, offset,
+                         s))
+    return dbias != nullptr;
+  attn_bwd_general<64>(qkv, out, dout, lse, delta, dqkv, B, L, H, p, causal, seed, offset, s);
   return false;
 }
 

@@ -253,15 +253,17 @@ static std::vector<at::Tensor> bias_act_bwd(const at::Tensor& dy, const at::Tens
 static std::vector<at::Tensor> attn_fwd(const at::Tensor& qkv, int64_t heads, double p, bool causal,
                                         int64_t seed, int64_t offset) {
   CHECK_DEV(qkv); CHECK_BF16(qkv); CHECK_CONTIG(qkv);
-  TORCH_CHECK(qkv.dim() == 3, "qkv must be [B, L, 3*H*64]");
+  TORCH_CHECK(qkv.dim() == 3, "qkv must be [B, L, 3*H*D]");
   const int B = (int)qkv.size(0), L = (int)qkv.size(1), H = (int)heads;
-  TORCH_CHECK(qkv.size(2) == 3LL * H * 64, "attn: head_dim must be 64");
+  TORCH_CHECK(H > 0 && qkv.size(2) % (3LL * H) == 0, "attn: qkv width must be 3*H*D");
+  const int D = (int)(qkv.size(2) / (3LL * H));
+  TORCH_CHECK(D == 64 || D == 128, "attn: head_dim must be 64 or 128");
   TORCH_CHECK(L % 64 == 0, "attn: L must be a multiple of 64");
   const c10::DeviceGuard guard(qkv.device());
-  at::Tensor out = at::empty({B, L, (int64_t)H * 64}, qkv.options());
+  at::Tensor out = at::empty({B, L, (int64_t)H * D}, qkv.options());
   at::Tensor lse = at::empty({B, H, L}, qkv.options().dtype(at::kFloat));
   dpa::launch_attn_fwd(bf_ptr(qkv), reinterpret_cast<uint16_t*>(out.data_ptr()),
-                       lse.data_ptr<float>(), B, L, H, (float)p, causal, (uint32_t)seed,
+                       lse.data_ptr<float>(), B, L, H, D, (float)p, causal, (uint32_t)seed,
                        (uint32_t)offset, cur_stream());
   return {out, lse};
 }
@@ -273,21 +275,26 @@ static std::vector<at::Tensor> attn_bwd(const at::Tensor& dout, const at::Tensor
   CHECK_DEV(dout); CHECK_BF16(dout); CHECK_CONTIG(dout); CHECK_CONTIG(out); CHECK_CONTIG(qkv);
   const int B = (int)qkv.size(0), L = (int)qkv.size(1), H = (int)heads;
   TORCH_CHECK(dout.sizes() == out.sizes(), "dout shape");
+  TORCH_CHECK(H > 0 && qkv.size(2) % (3LL * H) == 0, "attn: qkv width must be 3*H*D");
+  const int D = (int)(qkv.size(2) / (3LL * H));
+  TORCH_CHECK(D == 64 || D == 128, "attn: head_dim must be 64 or 128");
+  TORCH_CHECK(L % 64 == 0 && out.size(2) == (int64_t)H * D, "attn_bwd: shapes");
+  TORCH_CHECK(lse.numel() == (int64_t)B * H * L, "attn_bwd: lse shape");
   const c10::DeviceGuard guard(qkv.device());
   at::Tensor dqkv = at::empty_like(qkv);
   auto f32 = qkv.options().dtype(at::kFloat);
   at::Tensor delta = at::empty({B, H, L}, f32);
   at::Tensor dq, colpart, db;
-  if (dpa::attn_bwd_needs_dq_acc(L)) dq = at::zeros({B, L, H, 64}, f32);
+  if (dpa::attn_bwd_needs_dq_acc(L)) dq = at::zeros({B, L, H, D}, f32);
   if (want_db) {
     colpart = at::empty({(int64_t)B * H * 192}, f32);
-    db = at::empty({3 * H * 64}, f32);
+    db = at::empty({3 * H * D}, f32);
   }
   const bool got = dpa::launch_attn_bwd(
       bf_ptr(qkv), bf_ptr(out), bf_ptr(dout), lse.data_ptr<float>(), delta.data_ptr<float>(),
       reinterpret_cast<uint16_t*>(dqkv.data_ptr()), dq.defined() ? dq.data_ptr<float>() : nullptr,
       want_db ? colpart.data_ptr<float>() : nullptr, want_db ? db.data_ptr<float>() : nullptr, B, L,
-      H, (float)p, causal, (uint32_t)seed, (uint32_t)offset, cur_stream());
+      H, D, (float)p, causal, (uint32_t)seed, (uint32_t)offset, cur_stream());
   return {dqkv, got ? db : at::Tensor()};
 }
 
@@ -548,7 +555,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("want_dy_colsum") = false);
   m.def("bias_act_fwd", &bias_act_fwd, "z += bias (in place); y = act(z) -> (z, y)");
   m.def("bias_act_bwd", &bias_act_bwd, "dz = dy*act'(zy); db = colsum(dz) -> (dz, db)");
-  m.def("attn_fwd", &attn_fwd, "fused attention forward (head_dim 64) -> (out, lse)");
+  m.def("attn_fwd", &attn_fwd, "fused attention forward (head_dim 64/128) -> (out, lse)");
   m.def("attn_bwd", &attn_bwd, "fused attention backward -> (dqkv, colsum(dqkv) or None)",
         py::arg("dout"), py::arg("qkv"), py::arg("out"), py::arg("lse"), py::arg("heads"), py::arg("p"),
         py::arg("causal"), py::arg("seed"), py::arg("offset"), py::arg("want_db") = false);

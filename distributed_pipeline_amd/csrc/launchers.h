@@ -46,9 +46,9 @@ void launch_bias_act_fwd(uint16_t* z, const uint16_t* bias, uint16_t* y, int64_t
 void launch_bias_act_bwd(const uint16_t* dy, const uint16_t* zy, uint16_t* dz, float* db, int64_t R,
                          int N, int act, hipStream_t s);
 
-// ---- attention.hip (head_dim 64, dropout, causal) ---------------------------------
-void launch_attn_fwd(const uint16_t* qkv, uint16_t* out, float* lse, int B, int L, int H, float p,
-                     bool causal, uint32_t seed, uint32_t offset, hipStream_t s);
+// ---- attention.hip (head_dim 64 or 128, dropout, causal) ---------------------------------
+void launch_attn_fwd(const uint16_t* qkv, uint16_t* out, float* lse, int B, int L, int H, int D,
+                     float p, bool causal, uint32_t seed, uint32_t offset, hipStream_t s);
 bool attn_bwd_needs_dq_acc(int L);
 // attention128.hip: persistent L = 128 bidirectional kernels (false: not applicable)
 bool launch_attn128_fwd(const uint16_t* qkv, uint16_t* out, float* lse, int B, int L, int H,
@@ -62,7 +62,8 @@ bool launch_attn128_bwd(const uint16_t* qkv, const uint16_t* out, const uint16_t
 // Returns true when the column sums of dqkv were written to dbias (L == 128 path).
 bool launch_attn_bwd(const uint16_t* qkv, const uint16_t* out, const uint16_t* dout, const float* lse,
                      float* delta, uint16_t* dqkv, float* dq_acc, float* colpart, float* dbias, int B,
-                     int L, int H, float p, bool causal, uint32_t seed, uint32_t offset, hipStream_t s);
+                     int L, int H, int D, float p, bool causal, uint32_t seed, uint32_t offset,
+                     hipStream_t s);
 
 // ---- xent2.hip: E = 128 LDS-DMA pipelined fused linear-CE (used by xent.hip) ----
 bool launch_lxent2_fwd(const uint16_t* x, const uint16_t* W, const uint16_t* b, const int64_t* tgt,

@@ -480,7 +480,7 @@ def attn_add_ln(x, qkv, out_proj, ln, heads, p_attn=0.0, p=0.0, training=True):
     p = p if training else 0.0
     B, L, D = x.shape if x.dim() == 3 else (0, 0, 0)
     if (not _ln_block_ok(x, qkv, out_proj) or qkv.act != "none" or out_proj.act != "none"
-            or D % heads or D // heads != 64 or L % 64 or L > 1024
+            or D % heads or D // heads not in (64, 128) or L % 64 or L > 1024
             or not native_ok(x, kernel="attn_fwd")):
         a = out_proj(attention(qkv(x), heads, p_attn, False, training))
         return add_dropout_layernorm(a, x, ln.weight, ln.bias, p, ln.eps, training)
@@ -625,7 +625,7 @@ def attention(qkv, n_heads, p=0.0, causal=False, training=True):
     B, L, three_hd = qkv.shape
     hd = three_hd // 3
     D = hd // n_heads
-    if (qkv.dtype == torch.bfloat16 and native_ok(qkv, kernel="attn_fwd") and D == 64
+    if (qkv.dtype == torch.bfloat16 and native_ok(qkv, kernel="attn_fwd") and D in (64, 128)
             and L % 64 == 0 and L <= 1024):
         seed, off = RNG.next()
         return _AttnFn.apply(qkv.contiguous(), n_heads, p, causal, seed, off)
