@@ -46,3 +46,19 @@ def test_elastic_restart_after_injected_crash_resumes(tmp_path):
     assert "loading model from checkpoint" in out and "model_000001.pt" in out  # resumed
     assert (tmp_path / "ck" / ".fault_injected_2").exists()
     assert (tmp_path / "ck" / "model_000003.pt").exists()  # and finished
+
+
+def test_allreduce_sweep_tool_runs_on_gloo_ranks():
+    """tools/bench_allreduce.py (bucket-size sweep) on 2 CPU ranks."""
+    import json
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ, OMP_NUM_THREADS="1")
+    out = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+                          "--master-addr", "127.0.0.1", "--master-port", str(find_free_port()),
+                          os.path.join(root, "tools", "bench_allreduce.py"), "--backend", "gloo",
+                          "--sizes-mb", "0.25,1", "--iters", "2", "--warmup", "1"],
+                         capture_output=True, text=True, timeout=180, env=env, cwd=root)
+    assert out.returncode == 0, out.stderr[-2000:]
+    rows = [json.loads(l) for l in out.stdout.splitlines() if l.startswith("{")]
+    assert [r["size_mb"] for r in rows] == [0.25, 1.0]
+    assert all(r["world"] == 2 and r["algbw_GBps"] > 0 for r in rows)
