@@ -28,10 +28,14 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--tokens", type=int, default=262144)
     ap.add_argument("--native", action="store_true")
+    ap.add_argument("--hidden", type=int, default=768, help="2048 for DiffuSeq-XL")
+    ap.add_argument("--ffn", type=int, default=0, help="default 4 x hidden")
     a = ap.parse_args()
+    Hd = a.hidden
+    F = a.ffn or 4 * Hd
     T = a.tokens
     dev = "cuda"
-    shapes = [("qkv", 768, 2304), ("attn_out", 768, 768), ("ffn_in", 768, 3072), ("ffn_out", 3072, 768)]
+    shapes = [("qkv", Hd, 3 * Hd), ("attn_out", Hd, Hd), ("ffn_in", Hd, F), ("ffn_out", F, Hd)]
     tot = {"fwd": 0.0, "dgrad": 0.0, "wgrad": 0.0}
     ext = None
     if a.native:
@@ -79,7 +83,7 @@ def main():
             # fused-epilogue variants vs hipBLASLt + separate elementwise pass
             z = torch.randn(T, N, device=dev).bfloat16()
             dh = torch.randn(T, K, device=dev).bfloat16()   # grad arriving from ffn_out (width K)
-            w2 = (torch.randn(K, N, device=dev) * 0.02).bfloat16()  # ffn_out weight [768, 3072]
+            w2 = (torch.randn(K, N, device=dev) * 0.02).bfloat16()  # ffn_out weight [hidden, ffn]
             rec["gelu_fwd_native_ms"] = round(bench(lambda: ext.gemm_nt(x, w, b, 1)), 3)
             rec["gelu_fwd_blas_plus_eltwise_ms"] = round(bench(
                 lambda: ext.bias_act_fwd(torch.mm(x, w.t()), b, 1)), 3)
