@@ -19,6 +19,8 @@
 // Dropout: keep/drop bits come from a per-(query, key-pair) hash of
 //   (seed, offset, batch*head), so forward and backward agree without storing
 //   a mask.
+#include <cstdlib>
+
 #include "common.h"
 #include "launchers.h"
 #include "mfma.h"
@@ -70,6 +72,37 @@ __device__ __forceinline__ void stage_tile(char* lds, const bf16_t* __restrict__
     uint4 v = make_uint4(0, 0, 0, 0);
     if (r0 + row < nrows) v = *reinterpret_cast<const uint4*>(src + (int64_t)(r0 + row) * ld + ch * 8);
     *reinterpret_cast<uint4*>(lds + swz<2 * D>(row, ch)) = v;
+  }
+}
+
+// register-staged variant of stage_tile: global -> registers (issued early, so the
+// loads of tile t+1 are in flight while tile t is computed), registers -> LDS later
+template <int D>
+struct TileRegs {
+  static constexpr int N = 64 * (D / 8) / 256;
+  uint4 v[N];
+};
+
+template <int D>
+__device__ __forceinline__ void tile_load(TileRegs<D>& r, const bf16_t* __restrict__ src, int64_t ld,
+                                          int r0, int nrows, int tid) {
+  constexpr int CPR = D / 8;
+#pragma unroll
+  for (int i = 0; i < TileRegs<D>::N; ++i) {
+    const int c = tid + i * 256;
+    const int row = c / CPR, ch = c % CPR;
+    r.v[i] = make_uint4(0, 0, 0, 0);
+    if (r0 + row < nrows) r.v[i] = *reinterpret_cast<const uint4*>(src + (int64_t)(r0 + row) * ld + ch * 8);
+  }
+}
+
+template <int D>
+__device__ __forceinline__ void tile_store(char* lds, const TileRegs<D>& r, int tid) {
+  constexpr int CPR = D / 8;
+#pragma unroll
+  for (int i = 0; i < TileRegs<D>::N; ++i) {
+    const int c = tid + i * 256;
+    *reinterpret_cast<uint4*>(lds + swz<2 * D>(c / CPR, c % CPR)) = r.v[i];
   }
 }
 
@@ -199,6 +232,122 @@ __global__ void __launch_bounds__(256) attn_fwd_kernel(const bf16_t* __restrict_
     }
 }
 
+
+// Single-pass variant (online softmax): per 64-key tile, S^T = K Q^T, the
+// per-query running max is combined across the two lane halves (both halves
+// feed the same O rows through the MFMA k dimension, so they must share it),
+// P = exp2(S - m) goes straight into O += P^T V, and O is rescaled by
+// exp2(m_old - m_new).  O's rows live on accumulator registers, not lanes, so a
+// register's factor is fetched from the lane that owns that query (one
+// ds_bpermute per register per tile).  K is read once instead of twice.
+template <int D, bool CAUSAL>
+__global__ void __launch_bounds__(256) attn_fwd_online_kernel(const bf16_t* __restrict__ qkv,
+                                                             bf16_t* __restrict__ out,
+                                                             float* __restrict__ lse, int L, int H,
+                                                             float p, uint32_t seed, uint32_t offset) {
+  __shared__ __attribute__((aligned(16))) char smem[2 * 64 * 2 * D];
+  char* kt_lds = smem;
+  char* vt_lds = smem + 64 * 2 * D;
+  const int b = blockIdx.z, hd = blockIdx.y;
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, hf = lane >> 5;
+  const int64_t ld = 3LL * H * D;
+  const bf16_t* qb = qkv + (int64_t)b * L * ld + (int64_t)hd * D;
+  const bf16_t* kb = qb + (int64_t)H * D;
+  const bf16_t* vb = qb + 2LL * H * D;
+  const int qbase = blockIdx.x * 128 + w * 32;
+  const int q = qbase + (lane & 31);
+  const bool q_ok = q < L;
+  bf16x8 qf[D / 16];
+#pragma unroll
+  for (int s = 0; s < D / 16; ++s) {
+    if (q_ok) qf[s] = ld_frag(qb + (int64_t)q * ld + 16 * s + 8 * hf);
+    else for (int j = 0; j < 8; ++j) qf[s][j] = 0;
+  }
+  const DropCfg dc = make_drop(p, seed, offset, (uint32_t)(b * H + hd));
+  const int kv_end = CAUSAL ? min(L, (int)blockIdx.x * 128 + 128) : L;
+  // source lane (in this half's numbering) of the query that register i of O belongs to
+  int src[16];
+#pragma unroll
+  for (int i = 0; i < 16; ++i) src[i] = acc_row(i, hf);
+  float m = -1e30f, l = 0.f;
+  f32x16 o[D / 32];
+#pragma unroll
+  for (int dt = 0; dt < D / 32; ++dt) o[dt] = zero16();
+  TileRegs<D> kr, vr;
+  tile_load<D>(kr, kb, ld, 0, L, tid);
+  tile_load<D>(vr, vb, ld, 0, L, tid);
+  for (int kv0 = 0; kv0 < kv_end; kv0 += 64) {
+    tile_store<D>(kt_lds, kr, tid);
+    tile_store<D>(vt_lds, vr, tid);
+    __syncthreads();
+    if (kv0 + 64 < kv_end) {  // next tile's loads overlap this tile's matrix-core work
+      tile_load<D>(kr, kb, ld, kv0 + 64, L, tid);
+      tile_load<D>(vr, vb, ld, kv0 + 64, L, tid);
+    }
+    f32x16 acc[2];
+    float tmax = -1e30f;
+#pragma unroll
+    for (int t = 0; t < 2; ++t) {
+      acc[t] = zero16();
+#pragma unroll
+      for (int s = 0; s < D / 16; ++s)
+        acc[t] = mfma32(lds_frag<2 * D>(kt_lds, t * 32 + (lane & 31), 2 * s + hf), qf[s], acc[t]);
+#pragma unroll
+      for (int i = 0; i < 16; ++i) {
+        const int key = kv0 + t * 32 + acc_row(i, hf);
+        float y = acc[t][i] * att_c<D>();
+        if ((CAUSAL && key > q) || key >= L) y = -INFINITY;
+        acc[t][i] = y;
+        tmax = fmaxf(tmax, y);
+      }
+    }
+    tmax = fmaxf(tmax, __shfl_xor(tmax, 32, 64));
+    const float mn = fmaxf(m, tmax);
+    const float alpha = fexp2(m - mn);
+    m = mn;
+    float add = 0.f;
+#pragma unroll
+    for (int t = 0; t < 2; ++t)
+#pragma unroll
+      for (int i = 0; i < 16; ++i) {
+        const int key = kv0 + t * 32 + acc_row(i, hf);
+        float pr = fexp2(acc[t][i] - mn);
+        add += pr;
+        if (dc.on) pr = keep_bit(dc, q, key) ? pr * dc.scale : 0.f;
+        acc[t][i] = pr;
+      }
+    l = l * alpha + add;
+    // rescale O rows by their query's alpha
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+      const float f = __shfl(alpha, src[i] + 32 * hf, 64);
+#pragma unroll
+      for (int dt = 0; dt < D / 32; ++dt) o[dt][i] *= f;
+    }
+#pragma unroll
+    for (int t = 0; t < 2; ++t)
+#pragma unroll
+      for (int s = 0; s < 2; ++s) {
+        const bf16x8 af = acc_to_frag(acc[t], s);
+#pragma unroll
+        for (int dt = 0; dt < D / 32; ++dt)
+          o[dt] = mfma32(af, lds_tr_frag<2 * D>(vt_lds, t * 32 + 16 * s, dt * 32, lane), o[dt]);
+      }
+    __syncthreads();
+  }
+  l += __shfl_xor(l, 32, 64);
+  if (hf == 0 && q_ok) lse[((int64_t)b * H + hd) * L + q] = (m + log2f(l)) * LN2f;
+  const float inv_l = 1.f / l;
+  bf16_t* ob = out + (int64_t)b * L * H * D + (int64_t)hd * D;
+#pragma unroll
+  for (int i = 0; i < 16; ++i) {
+    const float f = __shfl(inv_l, src[i] + 32 * hf, 64);
+    const int qq = qbase + acc_row(i, hf);
+#pragma unroll
+    for (int dt = 0; dt < D / 32; ++dt)
+      if (qq < L) ob[(int64_t)qq * H * D + dt * 32 + (lane & 31)] = f2bf(o[dt][i] * f);
+  }
+}
 
 // L <= 128: every key of the (batch, head) fits one LDS image and the whole
 // S^T column of a query fits in registers -> exact softmax in one pass.
@@ -366,15 +515,22 @@ __global__ void __launch_bounds__(256) attn_bwd_kv_kernel(
 #pragma unroll
   for (int dt = 0; dt < D / 32; ++dt) { dk[dt] = zero16(); dv[dt] = zero16(); }
   const int qbeg = CAUSAL ? (int)blockIdx.x * 128 : 0;
+  TileRegs<D> qr, dr;  // register prefetch of the next query tile (Q, dO)
+  tile_load<D>(qr, qb, ld, qbeg, L, tid);
+  tile_load<D>(dr, dob, ldo, qbeg, L, tid);
   for (int q0 = qbeg; q0 < L; q0 += 64) {
-    stage_tile<D>(qt_lds, qb, ld, q0, L, tid);
-    stage_tile<D>(dot_lds, dob, ldo, q0, L, tid);
+    tile_store<D>(qt_lds, qr, tid);
+    tile_store<D>(dot_lds, dr, tid);
     if (tid < 64) {
       const bool ok = q0 + tid < L;
       s_lse[tid] = ok ? lse[lrow + q0 + tid] * 1.4426950408889634f : 0.f;
       s_del[tid] = ok ? delta[lrow + q0 + tid] : 0.f;
     }
     __syncthreads();
+    if (q0 + 64 < L) {
+      tile_load<D>(qr, qb, ld, q0 + 64, L, tid);
+      tile_load<D>(dr, dob, ldo, q0 + 64, L, tid);
+    }
 #pragma unroll 1
     for (int qt = 0; qt < 2; ++qt) {
       f32x16 sacc = zero16(), dpacc = zero16();
@@ -467,10 +623,17 @@ __global__ void __launch_bounds__(256) attn_bwd_q_kernel(
 #pragma unroll
   for (int dt = 0; dt < D / 32; ++dt) dq[dt] = zero16();
   const int kv_end = CAUSAL ? min(L, (int)blockIdx.x * 128 + 128) : L;
+  TileRegs<D> kr, vr;  // register prefetch of the next key tile (K, V)
+  tile_load<D>(kr, kb, ld, 0, L, tid);
+  tile_load<D>(vr, vb, ld, 0, L, tid);
   for (int kv0 = 0; kv0 < kv_end; kv0 += 64) {
-    stage_tile<D>(kt_lds, kb, ld, kv0, L, tid);
-    stage_tile<D>(vt_lds, vb, ld, kv0, L, tid);
+    tile_store<D>(kt_lds, kr, tid);
+    tile_store<D>(vt_lds, vr, tid);
     __syncthreads();
+    if (kv0 + 64 < kv_end) {
+      tile_load<D>(kr, kb, ld, kv0 + 64, L, tid);
+      tile_load<D>(vr, vb, ld, kv0 + 64, L, tid);
+    }
 #pragma unroll 1
     for (int t = 0; t < 2; ++t) {
       f32x16 sacc = zero16(), dpacc = zero16();
@@ -511,11 +674,24 @@ template <int D>
 static void attn_fwd_general(const uint16_t* qkv, uint16_t* out, float* lse, int B, int L, int H,
                              float p, bool causal, uint32_t seed, uint32_t offset, hipStream_t s) {
   dim3 grid((L + 127) / 128, H, B);
+  static const bool two_pass = [] {
+    const char* e = getenv("DPA_ATTN_TWOPASS");
+    return e != nullptr && e[0] == '1';
+  }();
+  if (two_pass) {
+    if (causal)
+      hipLaunchKernelGGL((attn_fwd_kernel<D, true>), grid, dim3(256), 0, s, (const bf16_t*)qkv,
+                         (bf16_t*)out, lse, L, H, p, seed, offset);
+    else
+      hipLaunchKernelGGL((attn_fwd_kernel<D, false>), grid, dim3(256), 0, s, (const bf16_t*)qkv,
+                         (bf16_t*)out, lse, L, H, p, seed, offset);
+    return;
+  }
   if (causal)
-    hipLaunchKernelGGL((attn_fwd_kernel<D, true>), grid, dim3(256), 0, s, (const bf16_t*)qkv,
+    hipLaunchKernelGGL((attn_fwd_online_kernel<D, true>), grid, dim3(256), 0, s, (const bf16_t*)qkv,
                        (bf16_t*)out, lse, L, H, p, seed, offset);
   else
-    hipLaunchKernelGGL((attn_fwd_kernel<D, false>), grid, dim3(256), 0, s, (const bf16_t*)qkv,
+    hipLaunchKernelGGL((attn_fwd_online_kernel<D, false>), grid, dim3(256), 0, s, (const bf16_t*)qkv,
                        (bf16_t*)out, lse, L, H, p, seed, offset);
 }
 
