@@ -62,3 +62,25 @@ def test_allreduce_sweep_tool_runs_on_gloo_ranks():
     rows = [json.loads(l) for l in out.stdout.splitlines() if l.startswith("{")]
     assert [r["size_mb"] for r in rows] == [0.25, 1.0]
     assert all(r["world"] == 2 and r["algbw_GBps"] > 0 for r in rows)
+
+
+def test_bench_contract_two_ranks_gloo():
+    """bench.py under torch.distributed.run exactly as the round driver launches it
+    (tiny config on CPU ranks): rank 0 prints ONE JSON line with the whole-job value."""
+    import json
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ, OMP_NUM_THREADS="2")
+    out = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+                          "--master-addr", "127.0.0.1", "--master-port", str(find_free_port()),
+                          os.path.join(root, "bench.py"), "--gpus", "2", "--steps", "2", "--warmup", "1",
+                          "--config-name", "tiny", "--batch-size", "8", "--microbatch", "4", "--seq-len", "64",
+                          "--data-workers", "0"],
+                         capture_output=True, text=True, timeout=300, env=env, cwd=root)
+    assert out.returncode == 0, out.stderr[-3000:]
+    lines = [l for l in out.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1, out.stdout
+    d = json.loads(lines[0])
+    assert d["n_gpus"] == 2 and d["steps"] == 2 and d["warmup"] == 1 and d["scaling"] == "weak"
+    assert d["config"]["parallelism"] == "dp2" and d["config"]["global_batch"] == 16
+    assert abs(d["value"] - 2 * d["optimizer_steps_per_sec"]) < 1e-3 * d["value"]
+    assert abs(d["ms_per_step"] - 1e3 / d["optimizer_steps_per_sec"]) < 1e-2 * d["ms_per_step"]
