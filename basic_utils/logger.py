@@ -308,6 +308,19 @@ def profile(n):
 # Backend
 # ============================================================================
 
+# Callables ``hook(logger)`` run at the start of every ``Logger.dumpkvs`` (of any
+# logger, including one configured later), so code that accumulates metrics on
+# the device can publish them at log cadence without patching a logger instance.
+_DUMP_HOOKS = []
+
+
+def add_dump_hook(fn):
+    """Register ``fn(logger)`` to run before each dump; idempotent per function."""
+    if fn not in _DUMP_HOOKS:
+        _DUMP_HOOKS.append(fn)
+    return fn
+
+
 def get_current():
     if Logger.CURRENT is None:
         _configure_default_logger()
@@ -425,6 +438,8 @@ class Logger(object):
         return mpi_weighted_mean(self.comm, {k: (v, self.name2cnt.get(k, 1)) for k, v in d.items()})
 
     def dumpkvs(self):
+        for hook in list(_DUMP_HOOKS):  # late-bound keys (e.g. device-side accumulators)
+            hook(self)
         d = self._cross_rank_mean(self._collect())
         out = d.copy()
         if _global_rank() == 0:

@@ -37,6 +37,58 @@ __device__ __forceinline__ float dgelu_f(float z) {
   return fmaf(z * 0.39894228040143268f, e, c);
 }
 
+// Two-lane forms for the GEMM epilogues: the polynomial part runs on packed fp32
+// (v_pk_fma_f32 / v_pk_mul_f32, two elements per instruction); the exp and rcp
+// stay per element.  Same math as phi_cdf.
+__device__ __forceinline__ f32x2 phi_cdf2(f32x2 z, f32x2& e) {
+  const f32x2 x = f32x2{fabsf(z.x), fabsf(z.y)} * 0.70710678118654752f;
+  const f32x2 nx2 = -(x * x) * 1.4426950408889634f;
+  e = f32x2{__builtin_amdgcn_exp2f(nx2.x), __builtin_amdgcn_exp2f(nx2.y)};
+  const f32x2 d = x * 0.3275911f + 1.f;
+  const f32x2 t = {__builtin_amdgcn_rcpf(d.x), __builtin_amdgcn_rcpf(d.y)};
+  f32x2 p = t * 1.061405429f - 1.453152027f;
+  p = p * t + 1.421413741f;
+  p = p * t - 0.284496736f;
+  p = p * t + 0.254829592f;
+  p = p * t;
+  const f32x2 ea = 1.f - p * e;
+  const f32x2 sg = {copysignf(ea.x, z.x), copysignf(ea.y, z.y)};
+  return sg * 0.5f + 0.5f;
+}
+
+template <int ACT>
+__device__ __forceinline__ f32x2 act2(f32x2 z) {
+  if constexpr (ACT == 1) {
+    f32x2 e;
+    return z * phi_cdf2(z, e);
+  } else if constexpr (ACT == 2) {
+    return f32x2{tanhf(z.x), tanhf(z.y)};
+  } else if constexpr (ACT == 3) {
+    const f32x2 d = {1.f + fexp(-z.x), 1.f + fexp(-z.y)};
+    return z * f32x2{__builtin_amdgcn_rcpf(d.x), __builtin_amdgcn_rcpf(d.y)};
+  } else {
+    return z;
+  }
+}
+
+// d act / dz given aux = z (gelu, silu) or y = tanh(z) (tanh), two lanes
+template <int ACT>
+__device__ __forceinline__ f32x2 dact2(f32x2 a) {
+  if constexpr (ACT == 1) {
+    f32x2 e;
+    const f32x2 c = phi_cdf2(a, e);
+    return a * 0.39894228040143268f * e + c;
+  } else if constexpr (ACT == 2) {
+    return 1.f - a * a;
+  } else if constexpr (ACT == 3) {
+    const f32x2 d = {1.f + fexp(-a.x), 1.f + fexp(-a.y)};
+    const f32x2 sg = {__builtin_amdgcn_rcpf(d.x), __builtin_amdgcn_rcpf(d.y)};
+    return sg * (a * (1.f - sg) + 1.f);
+  } else {
+    return f32x2{1.f, 1.f};
+  }
+}
+
 __device__ __forceinline__ float act_apply(float z, int act) {
   switch (act) {
     case 1: return gelu_f(z);

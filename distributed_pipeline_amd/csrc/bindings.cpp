@@ -328,21 +328,39 @@ static at::Tensor gemm_nn(const at::Tensor& dy, const at::Tensor& W) {
   return dx;
 }
 
-// dz = (dy . W) * act'(aux); returns an undefined tensor when the shape does not
-// tile for the fused kernel (caller falls back to dgrad + separate act backward).
-static at::Tensor gemm_nn_dact(const at::Tensor& dy, const at::Tensor& W, const at::Tensor& aux,
-                               int64_t act) {
+// dx += dy . W in place (the residual-branch gradient accumulated by the dgrad GEMM);
+// false when the shape does not tile (caller adds separately).
+static bool gemm_nn_acc_(const at::Tensor& dy, const at::Tensor& W, at::Tensor& dx) {
+  CHECK_DEV(dy); CHECK_BF16(dy); CHECK_BF16(W); CHECK_BF16(dx);
+  CHECK_CONTIG(dy); CHECK_CONTIG(W); CHECK_CONTIG(dx);
+  const int T = (int)dy.size(0), N = (int)dy.size(1), K = (int)W.size(1);
+  TORCH_CHECK(W.size(0) == N && dx.size(0) == T && dx.size(1) == K, "gemm_nn_acc_ shapes");
+  const c10::DeviceGuard guard(dy.device());
+  return dpa::launch_gemmp_nn_acc(bf_ptr(dy), bf_ptr(W), reinterpret_cast<uint16_t*>(dx.data_ptr()), T, N, K,
+                                  dpa::device_cu_count(), cur_stream());
+}
+
+// dz = (dy . W) * act'(aux) [, db = colsum(dz) fp32 when want_db]; returns undefined
+// tensors when the shape does not tile for a fused kernel (caller falls back to dgrad +
+// separate act backward).  The persistent kernel writes per-tile column partials that
+// one reduction turns into db (no second pass over dz).
+static std::vector<at::Tensor> gemm_nn_dact(const at::Tensor& dy, const at::Tensor& W,
+                                            const at::Tensor& aux, int64_t act, bool want_db) {
   CHECK_DEV(dy); CHECK_BF16(dy); CHECK_BF16(W); CHECK_BF16(aux);
   CHECK_CONTIG(dy); CHECK_CONTIG(W); CHECK_CONTIG(aux);
   const int T = (int)dy.size(0), N = (int)dy.size(1), K = (int)W.size(1);
   TORCH_CHECK(W.size(0) == N && aux.size(0) == T && aux.size(1) == K, "gemm_nn_dact shapes");
   const c10::DeviceGuard guard(dy.device());
   at::Tensor dz = at::empty({T, K}, dy.options());
-  if (!dpa::launch_gemm256_nn_dact(bf_ptr(dy), bf_ptr(W), bf_ptr(aux),
-                                   reinterpret_cast<uint16_t*>(dz.data_ptr()), T, N, K, (int)act,
-                                   cur_stream()))
-    return at::Tensor();
-  return dz;
+  uint16_t* dzp = reinterpret_cast<uint16_t*>(dz.data_ptr());
+  at::Tensor part;
+  if (want_db && T % 256 == 0) part = at::empty({(int64_t)(T / 256) * 2, K}, dy.options().dtype(at::kFloat));
+  if (dpa::launch_gemmp_nn(bf_ptr(dy), bf_ptr(W), dzp, bf_ptr(aux), (int)act, T, N, K, dpa::device_cu_count(),
+                           cur_stream(), part.defined() ? part.data_ptr<float>() : nullptr))
+    return {dz, part.defined() ? part.sum(0) : at::Tensor()};
+  if (dpa::launch_gemm256_nn_dact(bf_ptr(dy), bf_ptr(W), bf_ptr(aux), dzp, T, N, K, (int)act, cur_stream()))
+    return {dz, at::Tensor()};
+  return {at::Tensor(), at::Tensor()};
 }
 
 static void gemm_wgrad(const at::Tensor& dy, const at::Tensor& x, at::Tensor& dW,
@@ -561,7 +579,10 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("causal"), py::arg("seed"), py::arg("offset"), py::arg("want_db") = false);
   m.def("gemm_nt", &gemm_nt, "y = act(x W^T + b) (bf16 MFMA) -> (y, z_preact)");
   m.def("gemm_nn", &gemm_nn, "dx = dy W (bf16 MFMA)");
-  m.def("gemm_nn_dact", &gemm_nn_dact, "dz = (dy W) * act'(aux) (bf16 MFMA, fused act backward)");
+  m.def("gemm_nn_dact", &gemm_nn_dact,
+        "dz = (dy W) * act'(aux) (bf16 MFMA, fused act backward) -> (dz, colsum(dz) fp32 or None)",
+        py::arg("dy"), py::arg("W"), py::arg("aux"), py::arg("act"), py::arg("want_db") = false);
+  m.def("gemm_nn_acc_", &gemm_nn_acc_, "dx += dy W in place (bf16 MFMA); False if the shape does not tile");
   m.def("gemm_wgrad", &gemm_wgrad, "dW += dy^T x, db += colsum(dy) (fp32 atomics, split-K)");
   m.def("gemm_supported", &gemm_supported, "shape check for the native GEMMs");
   m.def("set_gemm256", &dpa::set_gemm256, "enable/disable the 256x256 8-phase GEMM path");

@@ -265,8 +265,23 @@ __global__ void __launch_bounds__(256) gemm_kernel(
 
 static bool gemm_shape_ok(int M, int N, int K) { return M % 128 == 0 && N % 128 == 0 && K % 64 == 0; }
 
+// Compute units of the current device (cached per device id): the persistent GEMMs
+// launch one workgroup per CU.
+int device_cu_count() {
+  static int cache[64] = {0};
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return 256;
+  if (cache[dev] <= 0) {
+    int n = 0;
+    if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0) n = 256;
+    cache[dev] = n;
+  }
+  return cache[dev];
+}
+
 bool launch_gemm_nt(const uint16_t* x, const uint16_t* W, const uint16_t* bias, uint16_t* y,
                     uint16_t* z, int T, int N, int K, int act, hipStream_t s) {
+  if (launch_gemmp_nt(x, W, bias, y, z, T, N, K, act, device_cu_count(), s)) return true;
   if (launch_gemm256_nt(x, W, bias, y, z, T, N, K, act, s)) return true;
   if (!gemm_shape_ok(T, N, K)) return false;
   const int blocks = (T / 128) * (N / 128);
@@ -279,6 +294,7 @@ bool launch_gemm_nt(const uint16_t* x, const uint16_t* W, const uint16_t* bias, 
 bool launch_gemm_nn(const uint16_t* dy, const uint16_t* W, uint16_t* dx, int T, int N, int K,
                     hipStream_t s) {
   // dx[T][K] = dy[T][N] . W[N][K]: M = T, N' = K, reduction = N
+  if (launch_gemmp_nn(dy, W, dx, nullptr, 0, T, N, K, device_cu_count(), s, nullptr)) return true;
   if (launch_gemm256_nn(dy, W, dx, T, N, K, s)) return true;
   if (!gemm_shape_ok(T, K, N)) return false;
   const int blocks = (T / 128) * (K / 128);

@@ -52,7 +52,8 @@ __host__ __device__ constexpr int img_off(int buf, int h) { return buf * 2 * HAL
 
 // EPI_DACT: dgrad with the previous layer's activation backward fused in:
 // C = (A.B) * act'(aux), aux = pre-activation z (gelu, silu) or output y (tanh).
-enum { EPI_BF16 = 0, EPI_BIAS_ACT = 1, EPI_ATOMIC_F32 = 2, EPI_DACT = 3 };
+// EPI_NONE: no store (accumulators kept live) - timing probe of the main loop only.
+enum { EPI_BF16 = 0, EPI_BIAS_ACT = 1, EPI_ATOMIC_F32 = 2, EPI_DACT = 3, EPI_NONE = 4 };
 
 __device__ __forceinline__ f32x4 mfma16(const bf16x8& a, const bf16x8& b, const f32x4& c) {
   return __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8_v, a),
@@ -80,23 +81,34 @@ struct Operand {
   uint32_t off[2];     // byte offsets of this thread's two DMA pieces within a half image
                        // (unsigned 32-bit: the DMA uses SGPR base + VGPR offset addressing)
   uint32_t rd[4];      // LDS read byte offsets (relative to a half image)
+  int wv;              // wave id (wave-uniform)
+  int hstep;           // rows (row form) / columns (TR form) between the two half images
 
   // row0: first row (row form) / column (TR form) of the 256-wide tile; this
   // wave's sub-block starts at row/col wsub * wrows of a half; region: LDS byte
   // address of this operand's images.
+  // remap (B operand of the persistent kernel): half image h holds the 4 x 32 rows /
+  // columns {64 c + 32 h + (0..31) : c = 0..3} of the 256-wide tile instead of rows
+  // 128 h .. 128 h + 127, so the wave owning image block c of both halves owns 64
+  // CONTIGUOUS output columns (full 128-B lines in its epilogue stores).
   __device__ __forceinline__ void init(const bf16_t* p, int64_t ld_, int row0, int w, int lane,
-                                       int wsub, int wrows, uint32_t region) {
+                                       int wsub, int wrows, uint32_t region, bool remap = false) {
     ld = ld_;
+    wv = w;
+    hstep = remap ? 32 : 128;
     base = TR ? p + row0 : p + (int64_t)row0 * ld_;
 #pragma unroll
     for (int j = 0; j < 2; ++j) {
       const int piece = w * 2 + j;
       if constexpr (TR) {
         const int k = piece * 4 + (lane >> 4), phys = lane & 15;
-        off[j] = (uint32_t)(k * (int)ld_ + ((phys ^ tr_x(k)) << 3)) * 2u;
+        const int lc = phys ^ tr_x(k);                              // 16-B chunk of the image row
+        const int gc = remap ? lc * 8 + ((lc >> 2) << 5) : lc * 8;  // its first tile column
+        off[j] = (uint32_t)(k * (int)ld_ + gc) * 2u;
       } else {
         const int r = piece * 8 + (lane >> 3), phys = lane & 7;
-        off[j] = (uint32_t)(r * (int)ld_ + ((phys ^ ((r >> 1) & 7)) << 3)) * 2u;
+        const int rg = remap ? r + ((r >> 5) << 5) : r;             // tile row of image row r
+        off[j] = (uint32_t)(rg * (int)ld_ + ((phys ^ ((r >> 1) & 7)) << 3)) * 2u;
       }
     }
     const int g = lane >> 4, li = lane & 15;
@@ -118,15 +130,17 @@ struct Operand {
     }
   }
 
-  // DMA one half image (h = 0/1) of K-tile t into LDS at `img`.
+  // DMA one half image (h = 0/1) of K-tile t into LDS at `img`: buffer_load ... lds
+  // with a wave-uniform descriptor at the half image's origin and the 32-bit per-lane
+  // offsets (no 64-bit per-lane addresses to keep live across the main loop).
   __device__ __forceinline__ void stage(char* img, int h, int t) const {
-    const char* src = reinterpret_cast<const char*>(TR ? base + (int64_t)t * 64 * ld + h * 128
-                                                       : base + (int64_t)h * 128 * ld + t * 64);
-    const int w = threadIdx.x >> 6;
+    const bf16_t* src = TR ? base + (int64_t)t * 64 * ld + h * hstep : base + (int64_t)h * hstep * ld + t * 64;
+    const auto rs = __builtin_amdgcn_make_buffer_rsrc(const_cast<bf16_t*>(src), (short)0, 0x7fffffff,
+                                                      0x00020000);
 #pragma unroll
     for (int j = 0; j < 2; ++j)
-      __builtin_amdgcn_global_load_lds((glob_void*)(src + off[j]),
-                                       (lds_void*)(img + (w * 2 + j) * 1024), 16, 0, 0);
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (lds_void*)(img + (wv * 2 + j) * 1024), 16, off[j], 0, 0,
+                                               0);
   }
 
   // Fragment of 16-row (row form) / 16-column (TR form) block I, k-step KK, of
@@ -176,7 +190,10 @@ __device__ __forceinline__ void colsum_read(float& cs, const uint32_t (&csa)[2])
   }
 }
 
-template <int QA, int QB>
+// SWAP: B.A^T instead of A.B^T - the accumulator then holds C transposed (lane =
+// row of C, registers = 4 consecutive columns), the layout of the persistent
+// kernel's register-direct epilogue.
+template <int QA, int QB, bool SWAP = false>
 __device__ __forceinline__ void mfma_quadrant(f32x4 (&acc)[2][2][4][2], const bf16x8 (&fa)[4][2],
                                               const bf16x8 (&fb)[2][2]) {
   __builtin_amdgcn_s_setprio(1);
@@ -185,17 +202,49 @@ __device__ __forceinline__ void mfma_quadrant(f32x4 (&acc)[2][2][4][2], const bf
 #pragma unroll
     for (int i = 0; i < 4; ++i)
 #pragma unroll
-      for (int j = 0; j < 2; ++j) acc[QA][QB][i][j] = mfma16(fa[i][kk], fb[j][kk], acc[QA][QB][i][j]);
+      for (int j = 0; j < 2; ++j) {
+        if constexpr (SWAP) acc[QA][QB][i][j] = mfma16(fb[j][kk], fa[i][kk], acc[QA][QB][i][j]);
+        else acc[QA][QB][i][j] = mfma16(fa[i][kk], fb[j][kk], acc[QA][QB][i][j]);
+      }
   __builtin_amdgcn_s_setprio(0);
 }
 
+template <int N>
+__device__ __forceinline__ void wait_vm() { asm volatile("s_waitcnt vmcnt(%0)" ::"i"(N) : "memory"); }
+
+// Sum over the 16 lanes of a DPP row (every lane gets the row total): four DPP adds
+// (quad xor 1, quad xor 2, half-row mirror, row rotate by 8) - no LDS, no address VGPRs.
+__device__ __forceinline__ float row16_sum(float x) {
+  x += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(x), 0xB1, 0xF, 0xF, true));
+  x += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(x), 0x4E, 0xF, 0xF, true));
+  x += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(x), 0x141, 0xF, 0xF, true));
+  x += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(x), 0x128, 0xF, 0xF, true));
+  return x;
+}
+
+// Lane id recomputed from the EXEC mask (no VGPR has to stay live for it).
+__device__ __forceinline__ int lane_id() {
+  return (int)__builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u));
+}
+
+// A copy of x the compiler cannot see through (keeps loop-invariant lane
+// arithmetic from being hoisted across a long-lived register-heavy loop).
+__device__ __forceinline__ int opaque(int x) {
+  int y;
+  asm volatile("v_mov_b32 %0, %1" : "=v"(y) : "v"(x));
+  return y;
+}
+
 // One phase P (0..7) of a 2-K-tile iteration; te = even K-tile of the iteration.
-template <int P, bool A_TR, bool B_TR, bool CS>
+// XS / extra (persistent kernel): `extra` = XS stores of the previous tile were
+// issued between this tile's prologue DMA and its first iteration, so the waits
+// of phases 0-3 of that iteration leave them in flight.
+template <int P, bool A_TR, bool B_TR, bool CS, bool SWAP = false, int XS = 0>
 __device__ __forceinline__ void phase(f32x4 (&acc)[2][2][4][2], bf16x8 (&fa)[4][2],
                                       bf16x8 (&fb0)[2][2], bf16x8 (&fb1)[2][2], float& cs,
                                       const Operand<A_TR>& opA, const Operand<B_TR>& opB,
                                       char* smem, const uint32_t (&csa)[2], int te, bool more, bool do_cs,
-                                      int grp) {
+                                      int grp, bool extra = false) {
   constexpr int q = P & 3;
   constexpr int bf = P < 4 ? 0 : 1;
   char* const smB = smem + B_REGION;
@@ -223,16 +272,24 @@ __device__ __forceinline__ void phase(f32x4 (&acc)[2][2][4][2], bf16x8 (&fa)[4][
   if constexpr (P == 5) { if (more) opA.stage(smem + img_off(0, 1), 1, te + 2); }
   if constexpr (P == 6) { if (more) opA.stage(smem + img_off(1, 0), 0, te + 3); }
   if constexpr (P == 7) { if (more) opB.stage(smB + img_off(1, 0), 0, te + 3); }
-  if (more) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
-  else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  if (more) {
+    if constexpr (XS > 0 && P < 4) {
+      if (extra) wait_vm<8 + XS>();
+      else wait_vm<8>();
+    } else {
+      wait_vm<8>();
+    }
+  } else {
+    wait_vm<0>();
+  }
   // 3. barrier, retire reads, 16 MFMAs on one quadrant, barrier
   barrier();
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
   __builtin_amdgcn_sched_barrier(0);
-  if constexpr (q == 0) mfma_quadrant<0, 0>(acc, fa, fb0);
-  if constexpr (q == 1) mfma_quadrant<0, 1>(acc, fa, fb1);
-  if constexpr (q == 2) mfma_quadrant<1, 1>(acc, fa, fb1);
-  if constexpr (q == 3) mfma_quadrant<1, 0>(acc, fa, fb0);
+  if constexpr (q == 0) mfma_quadrant<0, 0, SWAP>(acc, fa, fb0);
+  if constexpr (q == 1) mfma_quadrant<0, 1, SWAP>(acc, fa, fb1);
+  if constexpr (q == 2) mfma_quadrant<1, 1, SWAP>(acc, fa, fb1);
+  if constexpr (q == 3) mfma_quadrant<1, 0, SWAP>(acc, fa, fb0);
   __builtin_amdgcn_sched_barrier(0);
   barrier();
 }
@@ -319,7 +376,16 @@ __global__ void __launch_bounds__(512) gemm256_kernel(
   // ---- epilogue: acc[qa][qb][i][j] reg r -> row qa*128 + wm*64 + i*16 + 4*(lane>>4) + r,
   //                                           col qb*128 + wn*32 + j*16 + (lane&15)
   const int g4 = (lane >> 4) * 4, li = lane & 15;
-  if constexpr (EPI == EPI_ATOMIC_F32) {
+  if constexpr (EPI == EPI_NONE) {
+#pragma unroll
+    for (int qa = 0; qa < 2; ++qa)
+#pragma unroll
+      for (int qb = 0; qb < 2; ++qb)
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+          for (int j = 0; j < 2; ++j) asm volatile("" ::"v"(acc[qa][qb][i][j]));
+  } else if constexpr (EPI == EPI_ATOMIC_F32) {
     if (do_cs) {
       float* red = reinterpret_cast<float*>(smem);  // [2 row halves][256 cols]
       const int t = tid & 255;
@@ -428,6 +494,326 @@ __global__ void __launch_bounds__(512) gemm256_kernel(
   }
 }
 
+
+// ---- persistent variant (forward / data-gradient GEMMs) ----------------------
+//
+// One workgroup per CU walks tiles tile = first, first + G, ... (G = grid).  What it
+// fixes (measured in tools/gemm_lab, profiles/gemm_lab_r2.txt): the non-persistent
+// kernel's 128 KiB output tile per CU costs ~25% of a K = 768 GEMM, because
+//  (a) a store instruction that covers 16 rows x 64 B (the MFMA accumulator layout,
+//      half cache lines) drains at ~33 GB/s per CU, while 8 rows x 128 B (full lines)
+//      drains at ~111 GB/s per CU - the epilogue is store-issue bound, and
+//  (b) the next tile's first loads queue behind those stores.
+// So:
+//  * the MFMAs run transposed (SWAP): a lane holds 4 consecutive columns of one row,
+//    and v_permlane16_swap pairs two such 16-column blocks into 16 contiguous bytes;
+//  * the B operand is remapped (Operand::init remap) so each wave owns 64 CONTIGUOUS
+//    output columns; each wave transposes its 16-row x 64-column blocks through a
+//    private 2 KiB LDS slot (no workgroup barrier) and stores full 128-B lines;
+//  * the NEXT tile's prologue DMA is issued before the epilogue, and the waits of the
+//    first half of its first K-iteration leave the XS epilogue ops in flight;
+//  * the bias of each tile comes into a double-buffered 512-B LDS slot by one DMA per
+//    wave in the prologue (uniform op counts per wave).
+// EPI: 0 plain (+bias), 1 act(x+bias) (y only), 2 y = act(z), z = x+bias (both stored),
+// 3 x * act'(aux) (data gradient fused with the previous layer's activation backward;
+// aux = pre-activation z for gelu/silu, the output y for tanh), 5 x + aux (a residual-
+// branch gradient accumulated by the GEMM; aux may alias C), 4 = 3 plus the column
+// sums of the result (that layer's bias gradient) as per-(tile, 128-row half) partials
+// colpart[(M/256)*2][N] (reduced by the caller).  ACT: act.h code.  Activations are
+// applied to the bf16-rounded value, exactly as a separate elementwise pass would.
+constexpr int P_BIAS_OFF = 2 * B_REGION;         // 2 x 512 B bias slots after the operand images
+constexpr int P_STAGE_OFF = 2 * B_REGION + 1024;  // 8 waves x 2 KiB epilogue transpose slots
+constexpr int P_LDS = P_STAGE_OFF + 8 * 2048;
+
+template <int EPI>
+struct PEpi {
+  // VMEM ops each lane issues after the next tile's prologue DMA: 16 stores (8 rounds x 2),
+  // EPI 2 a second 16 (z and y), EPI 3/4 the 12 aux loads of rounds 2..7, EPI 4 two partial stores
+  static constexpr int XS = EPI == 2 ? 32 : (EPI == 3 || EPI == 5) ? 28 : EPI == 4 ? 30 : 16;
+};
+
+template <int ACT>
+__device__ __forceinline__ float act_t(float z) { return act_apply(z, ACT); }
+template <int ACT>
+__device__ __forceinline__ float dact_t(float a) { return act_deriv(a, ACT); }
+
+typedef __attribute__((ext_vector_type(4))) unsigned u32x4_v;
+__device__ __forceinline__ void lds_write_b128(uint32_t addr, const uint4& v) {
+  const u32x4_v x = {v.x, v.y, v.z, v.w};
+  asm volatile("ds_write_b128 %0, %1" ::"v"(addr), "v"(x) : "memory");
+}
+__device__ __forceinline__ uint4 lds_read_b128_sync(uint32_t addr) {
+  u32x4_v v;
+  asm volatile("ds_read_b128 %0, %1\n\ts_waitcnt lgkmcnt(0)" : "=v"(v) : "v"(addr) : "memory");
+  return make_uint4(v[0], v[1], v[2], v[3]);
+}
+
+// 8 bf16 (one uint4) -> act on packed float pairs -> 8 bf16
+template <int ACT>
+__device__ __forceinline__ uint4 act8(const uint4& u) {
+  const uint32_t w[4] = {u.x, u.y, u.z, u.w};
+  uint32_t o[4];
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const f32x2 y = act2<ACT>(f32x2{__uint_as_float(w[q] << 16), __uint_as_float(w[q] & 0xffff0000u)});
+    o[q] = pack_bf2(y.x, y.y);
+  }
+  return make_uint4(o[0], o[1], o[2], o[3]);
+}
+
+__device__ __forceinline__ float bf_lo(uint32_t w) { return __uint_as_float(w << 16); }
+__device__ __forceinline__ float bf_hi(uint32_t w) { return __uint_as_float(w & 0xffff0000u); }
+
+template <bool B_TR, int EPI, int ACT>
+__global__ void __launch_bounds__(512) gemmp_kernel(const bf16_t* __restrict__ A, int64_t lda,
+                                                    const bf16_t* __restrict__ B, int64_t ldb, int M, int N,
+                                                    int nk, bf16_t* __restrict__ C, int64_t ldc,
+                                                    const bf16_t* __restrict__ bias,
+                                                    bf16_t* __restrict__ Zout, float* __restrict__ colpart) {
+  __shared__ __attribute__((aligned(1024))) char smem[P_LDS];
+  constexpr int XS = PEpi<EPI>::XS;
+  constexpr bool DACT = EPI == 3 || EPI == 4 || EPI == 5;  // epilogues that read aux
+  // wave id in an SGPR, lane id re-derived from EXEC wherever needed: nothing
+  // lane-dependent has to stay live across the register-full main loop
+  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int wm = (w >> 2) & 1, wn = w & 3;
+  const int grp = w >> 2;
+  const int NT = N / 256, ntiles = (M / 256) * NT;
+  const int G = gridDim.x;
+  const uint32_t sbase = lds_u32(smem);
+  char* const smB = smem + B_REGION;
+  const int niter = nk >> 1;
+  const bool has_bias = bias != nullptr;
+
+  Operand<false> opA;
+  Operand<B_TR> opB;
+  f32x4 acc[2][2][4][2];
+  bf16x8 fa[4][2], fb0[2][2], fb1[2][2];
+  float cs = 0.f;
+  const uint32_t csa[2] = {0u, 0u};
+
+  auto prologue = [&](int t, int slot) {
+    const int mt = t / NT, nt = t % NT;
+    const int lane = lane_id();
+    opA.init(A, lda, mt * 256, w, lane, wm, 64, sbase);
+    opB.init(B, ldb, nt * 256, w, lane, wn, 32, sbase + B_REGION, /*remap=*/true);
+    // bias slot: the tile's 256 bf16 = 2 x (64 lanes x 4 B); every wave issues one such
+    // DMA (waves of equal parity write identical bytes) so the vmcnt counts stay uniform
+    const int bh = (w & 1) * 256;
+    const char* bsrc = (has_bias ? reinterpret_cast<const char*>(bias + nt * 256)
+                                 : reinterpret_cast<const char*>(A)) + bh + lane * 4;
+    __builtin_amdgcn_global_load_lds((glob_void*)bsrc, (lds_void*)(smem + P_BIAS_OFF + slot * 512 + bh),
+                                     4, 0, 0);
+    opA.stage(smem + img_off(0, 0), 0, 0);
+    opB.stage(smB + img_off(0, 0), 0, 0);
+    opB.stage(smB + img_off(0, 1), 1, 0);
+    opA.stage(smem + img_off(0, 1), 1, 0);
+    opA.stage(smem + img_off(1, 0), 0, 1);
+    opB.stage(smB + img_off(1, 0), 0, 1);
+  };
+
+  // Epilogue rounds ro = qa*4 + i (0..7): this wave's rows qa*128 + wm*64 + i*16 + (0..15) of
+  // the tile, its 64 columns wn*64 + (0..63).  In the row-major domain (after the LDS
+  // transpose) lane l handles rows 8k + (l >> 3) (k = 0, 1) of the round, columns 8 (l & 7) .. +7.
+  auto row_off = [&](int t, int ro, int k, int ln) -> int64_t {
+    const int mt = t / NT, nt = t % NT;
+    const int qa = ro >> 2, i = ro & 3;
+    return ((int64_t)mt * 256 + qa * 128 + wm * 64 + i * 16 + k * 8 + (ln >> 3)) * ldc + nt * 256 + wn * 64 +
+           (ln & 7) * 8;
+  };
+
+  auto epilogue = [&](int t, int slot, uint4 (&aux)[2][2], bool has_next) {
+    // lane-derived addressing recomputed here from an opaque lane id: hoisted out of
+    // the tile loop it would be live across the main loop and spill
+    const int ln = opaque(lane_id());
+    const int R = ln >> 4, li = ln & 15;
+    const int cofs = ((R & 1) << 4) | ((R >> 1) << 3);  // after the permlane16 swap
+    const uint32_t bslot = sbase + P_BIAS_OFF + slot * 512;
+    const uint32_t stg = sbase + P_STAGE_OFF + w * 2048;
+    const int rr = ln >> 3, ch = ln & 7;
+    float csum[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    float bv[2][2][4];
+#pragma unroll
+    for (int qb = 0; qb < 2; ++qb)
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        if (!DACT && has_bias) {
+          // asm read: a compiler-visible LDS read here would be ordered behind the
+          // next tile's in-flight DMA (vmcnt(0)); the bias slot was retired long ago
+          uint2 b2;
+          asm volatile("ds_read_b64 %0, %1\n\ts_waitcnt lgkmcnt(0)"
+                       : "=v"(b2) : "v"(bslot + (uint32_t)(wn * 64 + qb * 32 + j * 16 + 4 * R) * 2));
+          bv[qb][j][0] = bf_lo(b2.x); bv[qb][j][1] = bf_hi(b2.x);
+          bv[qb][j][2] = bf_lo(b2.y); bv[qb][j][3] = bf_hi(b2.y);
+        } else {
+          bv[qb][j][0] = bv[qb][j][1] = bv[qb][j][2] = bv[qb][j][3] = 0.f;
+        }
+      }
+#pragma unroll
+    for (int ro = 0; ro < 8; ++ro) {
+      const int qa = ro >> 2, i = ro & 3;
+      // stage: pack (+bias), permlane16 swap, one 16-B row segment per qb
+#pragma unroll
+      for (int qb = 0; qb < 2; ++qb) {
+        float v[2][4];
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) v[j][r] = acc[qa][qb][i][j][r] + bv[qb][j][r];
+        uint32_t x0 = pack_bf2(v[0][0], v[0][1]), x1 = pack_bf2(v[0][2], v[0][3]);
+        uint32_t y0 = pack_bf2(v[1][0], v[1][1]), y1 = pack_bf2(v[1][2], v[1][3]);
+        auto s0 = __builtin_amdgcn_permlane16_swap(x0, y0, false, false);
+        auto s1 = __builtin_amdgcn_permlane16_swap(x1, y1, false, false);
+        const int lchunk = qb * 4 + (cofs >> 3);
+        lds_write_b128(stg + li * 128 + ((lchunk ^ (li & 7)) << 4), make_uint4(s0[0], s1[0], s0[1], s1[1]));
+      }
+      // read back row-major (the wave's own LDS ops complete in order) and store full lines
+      uint4 val[2];
+#pragma unroll
+      for (int k = 0; k < 2; ++k) {
+        const int row = k * 8 + rr;
+        val[k] = lds_read_b128_sync(stg + row * 128 + ((ch ^ (row & 7)) << 4));
+      }
+      if constexpr (DACT) {
+        // wait for this round's aux.  Issue order: aux(0) aux(1) [DMA: 13] | r0: wait aux(2)
+        // st(0) | r1: wait aux(3) st(1) | ... | r5: wait aux(7) st(5) | r6: wait st(6) | r7: wait
+        // st(7); the ops younger than aux(ro) at its wait (2 each; the DMA only when there is
+        // a next tile):  ro 0: aux1 DMA;  ro 1: DMA aux2 st0;  ro 2..6: st(ro-2) aux(ro+1)
+        // st(ro-1);  ro 7: st5 st6
+        if (ro == 0) {
+          if (has_next) wait_vm<15>(); else wait_vm<2>();
+        } else if (ro == 1) {
+          if (has_next) wait_vm<17>(); else wait_vm<4>();
+        } else if (ro < 7) {
+          wait_vm<6>();
+        } else {
+          wait_vm<4>();
+        }
+#pragma unroll
+        for (int k = 0; k < 2; ++k) {
+          const uint4 a = aux[ro & 1][k];
+          const uint32_t aw[4] = {a.x, a.y, a.z, a.w};
+          const uint32_t vw[4] = {val[k].x, val[k].y, val[k].z, val[k].w};
+          uint32_t o[4];
+#pragma unroll
+          for (int q = 0; q < 4; ++q) {
+            const f32x2 x = f32x2{bf_lo(vw[q]), bf_hi(vw[q])}, a = f32x2{bf_lo(aw[q]), bf_hi(aw[q])};
+            const f32x2 d = EPI == 5 ? x + a : x * dact2<ACT>(a);
+            o[q] = pack_bf2(d.x, d.y);
+            if constexpr (EPI == 4) {
+              csum[2 * q] += bf_lo(o[q]);
+              csum[2 * q + 1] += bf_hi(o[q]);
+            }
+          }
+          val[k] = make_uint4(o[0], o[1], o[2], o[3]);
+        }
+        // this round's aux slot is consumed: prefetch round ro + 2 into it
+        if (ro + 2 < 8) {
+#pragma unroll
+          for (int k = 0; k < 2; ++k)
+            aux[ro & 1][k] = *reinterpret_cast<const uint4*>(Zout + row_off(t, ro + 2, k, ln));
+        }
+      }
+#pragma unroll
+      for (int k = 0; k < 2; ++k) {
+        const int64_t o = row_off(t, ro, k, ln);
+        if constexpr (EPI == 2) *reinterpret_cast<uint4*>(Zout + o) = val[k];
+        if constexpr (EPI == 1 || EPI == 2) val[k] = act8<ACT>(val[k]);
+        *reinterpret_cast<uint4*>(C + o) = val[k];
+      }
+    }
+    if constexpr (EPI == 4) {
+      // column sums over this wave's 128 rows: reduce over the 8 lanes sharing a column
+      // chunk (lane bits 3, 4, 5), then lanes 0-7 store their 8 columns
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        float x = csum[e];
+        x += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(x), 0x128, 0xF, 0xF, true));
+        x += __int_as_float(__builtin_amdgcn_permlane16_swap(__float_as_int(x), __float_as_int(x), false, false)[0]);
+        x += __int_as_float(__builtin_amdgcn_permlane32_swap(__float_as_int(x), __float_as_int(x), false, false)[0]);
+        csum[e] = x;
+      }
+      const int mt = t / NT, nt = t % NT;
+      float* dst = colpart + ((int64_t)mt * 2 + wm) * (int64_t)(NT * 256) + nt * 256 + wn * 64 + ch * 8;
+      if (ln < 8) {
+        *reinterpret_cast<float4*>(dst) = make_float4(csum[0], csum[1], csum[2], csum[3]);
+        *reinterpret_cast<float4*>(dst + 4) = make_float4(csum[4], csum[5], csum[6], csum[7]);
+      }
+    }
+  };
+
+  auto zero_acc = [&]() {
+#pragma unroll
+    for (int a = 0; a < 2; ++a)
+#pragma unroll
+      for (int b = 0; b < 2; ++b)
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+          for (int j = 0; j < 2; ++j) acc[a][b][i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  };
+
+  int tile = xcd_remap(blockIdx.x, G);
+  if (tile >= ntiles) return;
+  int slot = 0;
+  bool extra = false;
+  zero_acc();
+  prologue(tile, slot);
+  wait_vm<8>();  // K-tile 0 halves A0, B0 (and the bias slot) landed
+  barrier();
+  if (grp == 1) barrier();
+
+  while (true) {
+    // first iteration: the previous tile's XS epilogue ops may still be in flight
+    {
+      const bool more = 1 < niter;
+      phase<0, false, B_TR, false, true, XS>(acc, fa, fb0, fb1, cs, opA, opB, smem, csa, 0, more, false, grp, extra);
+      phase<1, false, B_TR, false, true, XS>(acc, fa, fb0, fb1, cs, opA, opB, smem, csa, 0, more, false, grp, extra);
+      phase<2, false, B_TR, false, true, XS>(acc, fa, fb0, fb1, cs, opA, opB, smem, csa, 0, more, false, grp, extra);
+      phase<3, false, B_TR, false, true, XS>(acc, fa, fb0, fb1, cs, opA, opB, smem, csa, 0, more, false, grp, extra);
+      phase<4, false, B_TR, false, true>(acc, fa, fb0, fb1, cs, opA, opB, smem, csa, 0, more, false, grp);
+      phase<5, false, B_TR, false, true>(acc, fa, fb0, fb1, cs, opA, opB, smem, csa, 0, more, false, grp);
+      phase<6, false, B_TR, false, true>(acc, fa, fb0, fb1, cs, opA, opB, smem, csa, 0, more, false, grp);
+      phase<7, false, B_TR, false, true>(acc, fa, fb0, fb1, cs, opA, opB, smem, csa, 0, more, false, grp);
+    }
+    for (int it = 1; it < niter; ++it) {
+      const int te = 2 * it;
+      const bool more = it + 1 < niter;
+      phase<0, false, B_TR, false, true>(acc, fa, fb0, fb1, cs, opA, opB, smem, csa, te, more, false, grp);
+      phase<1, false, B_TR, false, true>(acc, fa, fb0, fb1, cs, opA, opB, smem, csa, te, more, false, grp);
+      phase<2, false, B_TR, false, true>(acc, fa, fb0, fb1, cs, opA, opB, smem, csa, te, more, false, grp);
+      phase<3, false, B_TR, false, true>(acc, fa, fb0, fb1, cs, opA, opB, smem, csa, te, more, false, grp);
+      phase<4, false, B_TR, false, true>(acc, fa, fb0, fb1, cs, opA, opB, smem, csa, te, more, false, grp);
+      phase<5, false, B_TR, false, true>(acc, fa, fb0, fb1, cs, opA, opB, smem, csa, te, more, false, grp);
+      phase<6, false, B_TR, false, true>(acc, fa, fb0, fb1, cs, opA, opB, smem, csa, te, more, false, grp);
+      phase<7, false, B_TR, false, true>(acc, fa, fb0, fb1, cs, opA, opB, smem, csa, te, more, false, grp);
+    }
+    if (grp == 0) barrier();  // re-align the groups: every wave's LDS reads are retired
+    const int next = tile + G;
+    const bool has_next = next < ntiles;
+    uint4 aux[2][2];
+    if constexpr (DACT) {
+      // activation-backward operand of rounds 0 and 1 (row-major, full lines), issued
+      // before the next tile's prologue DMA so that waiting for it leaves the DMA in flight
+      const int ln = opaque(lane_id());
+#pragma unroll
+      for (int ro = 0; ro < 2; ++ro)
+#pragma unroll
+        for (int k = 0; k < 2; ++k) aux[ro][k] = *reinterpret_cast<const uint4*>(Zout + row_off(tile, ro, k, ln));
+    }
+    if (has_next) prologue(next, slot ^ 1);
+    epilogue(tile, slot, aux, has_next);
+    if (!has_next) break;
+    zero_acc();
+    wait_vm<8 + XS>();  // next tile's K-tile 0 halves landed; this tile's epilogue ops may fly
+    barrier();
+    if (grp == 1) barrier();
+    tile = next;
+    slot ^= 1;
+    extra = true;
+  }
+}
+
 }  // namespace g256
 
 // Default on; DPA_GEMM256=0 or set_gemm256(false) routes every shape to gemm.hip.
@@ -470,6 +856,65 @@ bool launch_gemm256_nn_dact(const uint16_t* dy, const uint16_t* W, const uint16_
                      dim3((T / 256) * (K / 256)), dim3(512), 0, s, (const bf16_t*)dy, (int64_t)N,
                      (const bf16_t*)W, (int64_t)K, T, K, N / 64, N / 64, 1, (bf16_t*)dz, (int64_t)K,
                      nullptr, nullptr, act, (bf16_t*)aux, nullptr);
+  return true;
+}
+
+// ---- persistent forward / data-gradient launchers ---------------------------
+static int persistent_grid(int tiles, int ncu) { return tiles < ncu ? tiles : ncu; }
+
+template <bool B_TR, int EPI, int ACT>
+static void gemmp_go(const uint16_t* a, int64_t lda, const uint16_t* b, int64_t ldb, int M, int N, int K,
+                     uint16_t* c, const uint16_t* bias, uint16_t* z, int ncu, hipStream_t s,
+                     float* colpart = nullptr) {
+  const int tiles = (M / 256) * (N / 256);
+  hipLaunchKernelGGL((g256::gemmp_kernel<B_TR, EPI, ACT>), dim3(persistent_grid(tiles, ncu)), dim3(512), 0,
+                     s, (const bf16_t*)a, lda, (const bf16_t*)b, ldb, M, N, K / 64, (bf16_t*)c, (int64_t)N,
+                     (const bf16_t*)bias, (bf16_t*)z, colpart);
+}
+
+// y[T][N] = act(x[T][K] . W[N][K]^T + bias); z (nullable, act != 0) = the pre-activation.
+bool launch_gemmp_nt(const uint16_t* x, const uint16_t* W, const uint16_t* bias, uint16_t* y,
+                     uint16_t* z, int T, int N, int K, int act, int ncu, hipStream_t s) {
+  if (!g256_enabled() || T % 256 || N % 256 || K % 128 || K < 128 || act < 0 || act > 3) return false;
+  if (act == 0) gemmp_go<false, 0, 0>(x, K, W, K, T, N, K, y, bias, nullptr, ncu, s);
+  else if (z == nullptr) {
+    if (act == 1) gemmp_go<false, 1, 1>(x, K, W, K, T, N, K, y, bias, nullptr, ncu, s);
+    else if (act == 2) gemmp_go<false, 1, 2>(x, K, W, K, T, N, K, y, bias, nullptr, ncu, s);
+    else gemmp_go<false, 1, 3>(x, K, W, K, T, N, K, y, bias, nullptr, ncu, s);
+  } else {
+    if (act == 1) gemmp_go<false, 2, 1>(x, K, W, K, T, N, K, y, bias, z, ncu, s);
+    else if (act == 2) gemmp_go<false, 2, 2>(x, K, W, K, T, N, K, y, bias, z, ncu, s);
+    else gemmp_go<false, 2, 3>(x, K, W, K, T, N, K, y, bias, z, ncu, s);
+  }
+  return true;
+}
+
+// dx[T][K] = dy[T][N] . W[N][K]  (act != 0: times act'(aux[T][K]); colpart != nullptr:
+// also the per-tile column-sum partials [(T/256)*2][K] of the result)
+// dx[T][K] = dy[T][N] . W[N][K] + dx[T][K]  (in place, bf16)
+bool launch_gemmp_nn_acc(const uint16_t* dy, const uint16_t* W, uint16_t* dx, int T, int N, int K, int ncu,
+                         hipStream_t s) {
+  if (!g256_enabled() || T % 256 || K % 256 || N % 128 || N < 128) return false;
+  gemmp_go<true, 5, 0>(dy, N, W, K, T, K, N, dx, nullptr, dx, ncu, s);
+  return true;
+}
+
+bool launch_gemmp_nn(const uint16_t* dy, const uint16_t* W, uint16_t* dx, const uint16_t* aux, int act,
+                     int T, int N, int K, int ncu, hipStream_t s, float* colpart) {
+  if (!g256_enabled() || T % 256 || K % 256 || N % 128 || N < 128 || act < 0 || act > 3) return false;
+  uint16_t* ax = const_cast<uint16_t*>(aux);
+  if (act == 0 || aux == nullptr) {
+    if (colpart) return false;
+    gemmp_go<true, 0, 0>(dy, N, W, K, T, K, N, dx, nullptr, nullptr, ncu, s);
+  } else if (colpart) {
+    if (act == 1) gemmp_go<true, 4, 1>(dy, N, W, K, T, K, N, dx, nullptr, ax, ncu, s, colpart);
+    else if (act == 2) gemmp_go<true, 4, 2>(dy, N, W, K, T, K, N, dx, nullptr, ax, ncu, s, colpart);
+    else gemmp_go<true, 4, 3>(dy, N, W, K, T, K, N, dx, nullptr, ax, ncu, s, colpart);
+  } else {
+    if (act == 1) gemmp_go<true, 3, 1>(dy, N, W, K, T, K, N, dx, nullptr, ax, ncu, s);
+    else if (act == 2) gemmp_go<true, 3, 2>(dy, N, W, K, T, K, N, dx, nullptr, ax, ncu, s);
+    else gemmp_go<true, 3, 3>(dy, N, W, K, T, K, N, dx, nullptr, ax, ncu, s);
+  }
   return true;
 }
 

@@ -116,5 +116,17 @@ bool launch_gemm256_nn_dact(const uint16_t* dy, const uint16_t* W, const uint16_
                             uint16_t* dz, int T, int N, int K, int act, hipStream_t s);
 bool launch_gemm256_wgrad(const uint16_t* dy, const uint16_t* x, float* dW, float* db, int T,
                           int N, int K, hipStream_t s);
+// gemm256.hip persistent forward / data-gradient kernels with fused epilogues (false when
+// the shape does not tile).  ncu: compute units (grid = min(tiles, ncu)).
+//   nt: y[T][N] = act(x[T][K] W[N][K]^T + bias); z (nullable) = pre-activation
+//   nn: dx[T][K] = dy[T][N] W[N][K] (* act'(aux[T][K]) when aux); colpart (nullable, needs
+//       aux): per-tile column-sum partials [(T/256)*2][K] of dx (the bias gradient)
+bool launch_gemmp_nt(const uint16_t* x, const uint16_t* W, const uint16_t* bias, uint16_t* y,
+                     uint16_t* z, int T, int N, int K, int act, int ncu, hipStream_t s);
+bool launch_gemmp_nn(const uint16_t* dy, const uint16_t* W, uint16_t* dx, const uint16_t* aux, int act,
+                     int T, int N, int K, int ncu, hipStream_t s, float* colpart);
+bool launch_gemmp_nn_acc(const uint16_t* dy, const uint16_t* W, uint16_t* dx, int T, int N, int K, int ncu,
+                         hipStream_t s);
+int device_cu_count();
 
 }  // namespace dpa

