@@ -729,8 +729,10 @@ __global__ void __launch_bounds__(512) gemmp_kernel(const bf16_t* __restrict__ A
       for (int e = 0; e < 8; ++e) {
         float x = csum[e];
         x += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(x), 0x128, 0xF, 0xF, true));
-        x += __int_as_float(__builtin_amdgcn_permlane16_swap(__float_as_int(x), __float_as_int(x), false, false)[0]);
-        x += __int_as_float(__builtin_amdgcn_permlane32_swap(__float_as_int(x), __float_as_int(x), false, false)[0]);
+        // (a permlane swap of a register with itself is ambiguous under register
+        // allocation: cross-row steps go through ds_bpermute)
+        x += __shfl_xor(x, 16, 64);
+        x += __shfl_xor(x, 32, 64);
         csum[e] = x;
       }
       const int mt = t / NT, nt = t % NT;
