@@ -120,9 +120,9 @@ class PerfSettings(S):
     use_hip_kernels: bool \
         = _(True, "Use the hand-written gfx950 kernels (required on GPU).")
     exec_microbatch: int \
-        = _(0, "Samples per executed forward/backward (multiple of microbatch; 0 = microbatch). Gradients are identical.")
-    hip_graphs: bool \
-        = _(False, "Capture the micro-batch forward/backward in a HIP graph (launch-bound configs).")
+        = _(0, "Samples per executed forward/backward, a multiple of microbatch: 0 = auto (the whole "
+               "per-rank batch, halved on out-of-memory), -1 = microbatch (the reference schedule). "
+               "Gradients equal the reference's sum over micro-batches.")
     shard_data: bool \
         = _(False, "Give each rank a disjoint shard of the data (DistributedSampler-style).")
     log_cross_rank_mean: bool \

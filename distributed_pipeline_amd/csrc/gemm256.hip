@@ -926,11 +926,28 @@ bool launch_gemm256_wgrad(const uint16_t* dy, const uint16_t* x, float* dW, floa
   if (!g256_enabled() || N % 256 || K % 256 || T % 128 || T < 128) return false;
   const int tiles = (N / 256) * (K / 256);
   const int ktot = T / 64;
-  // One 128 KiB workgroup per CU: size the grid to whole rounds of 256 CUs
-  // (floor, never a nearly-empty extra round; ~2 rounds for load balance).
-  int splits = 512 / tiles;
-  if (splits > ktot / 2) splits = ktot / 2;
-  if (splits < 1) splits = 1;
+  // Split-K factor from a cost model (one 128 KiB workgroup per CU): rounds of
+  // workgroups x (K-tiles per split x ~1.5 us + ~4 us fixed) against the fp32
+  // atomic epilogue traffic (256 KiB per workgroup at ~1.3 TB/s chip-wide, ~0.35 us
+  // each under contention).  The old rule (fill two rounds regardless of T) split a
+  // 8192-token micro-batch 32 ways: 54x atomic amplification, 107 us per call.
+  const int ncu = device_cu_count();
+  int splits = 1;
+  double best = 1e30;
+  const int smax = ktot / 2 < 1 ? 1 : ktot / 2;
+  for (int sp = 1; sp <= smax; ++sp) {
+    int kps = (ktot + sp - 1) / sp;
+    kps += kps & 1;
+    const int s_eff = (ktot + kps - 1) / kps;
+    const int wgs = tiles * s_eff;
+    const int rounds = (wgs + ncu - 1) / ncu;
+    const double t = fmax(rounds * (kps * 1.5 + 4.0), wgs * 0.35);
+    if (t < best * 0.98) {
+      best = t;
+      splits = s_eff;
+    }
+    if (wgs > 4 * ncu) break;
+  }
   int kps = (ktot + splits - 1) / splits;
   kps += kps & 1;
   splits = (ktot + kps - 1) / kps;

@@ -14,15 +14,24 @@ def compute_dtype_for(precision):
 
 def build_model(*, model="diffuseq", precision="bf16", vocab_size=30522, hidden_dim=128,
                 hidden_t_dim=128, seq_len=128, config_name="bert-base-uncased", hidden_size=0,
-                num_layers=0, num_heads=0, intermediate_size=0, dropout=0.1, **_):
+                num_layers=0, num_heads=0, intermediate_size=0, dropout=0.1, use_hip_kernels=True,
+                use_plm_init="no", emb_scale_factor=1.0, **_):
+    from ..ops import _ext
+    _ext.set_native_enabled(use_hip_kernels)
     dt = compute_dtype_for(precision)
     if model == "diffuseq":
-        return TransformerNetModel(vocab_size=vocab_size, input_dims=hidden_dim,
-                                   hidden_t_dim=hidden_t_dim, seq_len=seq_len,
-                                   config_name=config_name, hidden_size=hidden_size,
-                                   num_layers=num_layers, num_heads=num_heads,
-                                   intermediate_size=intermediate_size, dropout=dropout,
-                                   compute_dtype=dt)
+        m = TransformerNetModel(vocab_size=vocab_size, input_dims=hidden_dim,
+                                hidden_t_dim=hidden_t_dim, seq_len=seq_len,
+                                config_name=config_name, hidden_size=hidden_size,
+                                num_layers=num_layers, num_heads=num_heads,
+                                intermediate_size=intermediate_size, dropout=dropout,
+                                compute_dtype=dt, emb_scale_factor=emb_scale_factor)
+        if use_plm_init == "bert":
+            from .plm_init import load_bert_init
+            load_bert_init(m, config_name)
+        return m
+    if use_plm_init != "no":
+        raise ValueError(f"use_plm_init={use_plm_init!r} is only defined for the diffuseq model")
     if model == "mlp_diffusion":
         return MLPDiffusionModel(vocab_size=vocab_size, input_dims=hidden_dim,
                                  hidden_t_dim=hidden_t_dim, hidden_size=hidden_size, compute_dtype=dt)

@@ -26,7 +26,8 @@ from .layers import MLP, BertEncoder, Embedding, LayerNorm, Linear
 class TransformerNetModel(nn.Module):
     def __init__(self, *, vocab_size=30522, input_dims=128, hidden_t_dim=128, seq_len=128,
                  config_name="bert-base-uncased", hidden_size=0, num_layers=0, num_heads=0,
-                 intermediate_size=0, dropout=0.1, compute_dtype=torch.bfloat16, **_):
+                 intermediate_size=0, dropout=0.1, compute_dtype=torch.bfloat16, emb_scale_factor=1.0,
+                 **_):
         super().__init__()
         cfg = presets.resolve(config_name, hidden_size=hidden_size, num_layers=num_layers,
                               num_heads=num_heads, intermediate_size=intermediate_size,
@@ -37,6 +38,9 @@ class TransformerNetModel(nn.Module):
         self.dropout = dropout
         self.compute_dtype = compute_dtype
         self.seq_len = seq_len
+        # DiffuSeq's --emb_scale_factor: the diffusion space is the word embedding times
+        # this factor (1.0 = DiffuSeq default; != 1 takes the PyTorch diffusion path)
+        self.emb_scale_factor = float(emb_scale_factor)
         assert seq_len <= cfg["max_position_embeddings"]
 
         self.word_embedding = Embedding(cfg["vocab_size"], input_dims)
@@ -58,8 +62,9 @@ class TransformerNetModel(nn.Module):
 
     # -- DiffuSeq API -------------------------------------------------------
     def get_embeds(self, input_ids):
-        """Word embeddings in fp32 (diffusion space stays fp32)."""
-        return ops.embedding(input_ids, self.word_embedding.weight, torch.float32)
+        """Word embeddings in fp32 (diffusion space stays fp32), times emb_scale_factor."""
+        e = ops.embedding(input_ids, self.word_embedding.weight, torch.float32)
+        return e if self.emb_scale_factor == 1.0 else e * self.emb_scale_factor
 
     def get_logits(self, hidden_repr):
         """Materialised rounding logits (API parity; training uses :meth:`token_nll`)."""

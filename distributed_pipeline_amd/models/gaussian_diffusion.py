@@ -61,9 +61,16 @@ def mean_flat(x):
 class GaussianDiffusion:
     """Noise schedule tables (kept on device) + the seq2seq training loss."""
 
-    def __init__(self, betas, predict_xstart=True, rescale_timesteps=True, learn_sigma=False):
+    def __init__(self, betas, predict_xstart=True, rescale_timesteps=True, learn_sigma=False,
+                 sigma_small=False, rescale_learned_sigmas=False):
         if learn_sigma:
             raise NotImplementedError("learn_sigma=True is not supported (DiffuSeq default is False)")
+        if rescale_learned_sigmas:
+            # guided-diffusion's RESCALED_MSE only rescales the learned-variance (vb) term
+            raise ValueError("rescale_learned_sigmas=True needs learn_sigma=True (unsupported)")
+        # reverse-process variance of p_sample (DiffuSeq: FIXED_SMALL if sigma_small
+        # else FIXED_LARGE); training losses do not depend on it
+        self.model_var_type = "fixed_small" if sigma_small else "fixed_large"
         self.predict_xstart = predict_xstart
         self.rescale_timesteps = rescale_timesteps
         betas = np.asarray(betas, dtype=np.float64)
@@ -75,6 +82,13 @@ class GaussianDiffusion:
         self.sqrt_alphas_cumprod = np.sqrt(self.alphas_cumprod)
         self.sqrt_one_minus_alphas_cumprod = np.sqrt(1.0 - self.alphas_cumprod)
         self.posterior_variance = betas * (1.0 - self.alphas_cumprod_prev) / (1.0 - self.alphas_cumprod)
+        self.posterior_log_variance_clipped = np.log(np.append(self.posterior_variance[1],
+                                                               self.posterior_variance[1:]))
+        self.posterior_mean_coef1 = betas * np.sqrt(self.alphas_cumprod_prev) / (1.0 - self.alphas_cumprod)
+        self.posterior_mean_coef2 = ((1.0 - self.alphas_cumprod_prev) * np.sqrt(alphas)
+                                     / (1.0 - self.alphas_cumprod))
+        # FIXED_LARGE uses betas (with the posterior variance at t = 0)
+        self.large_log_variance = np.log(np.append(self.posterior_variance[1], betas[1:]))
         self._dev_tables = {}
 
     # -- device tables ------------------------------------------------------
@@ -103,6 +117,49 @@ class GaussianDiffusion:
             return x_t
         return torch.where(mask.unsqueeze(-1) == 0, x_start, x_t)
 
+    # -- reverse process (sampling; DiffuSeq p_sample / p_sample_loop) -------
+    def q_posterior_mean(self, x_start, x_t, t):
+        return (self._extract("posterior_mean_coef1", t, x_t.dim()) * x_start
+                + self._extract("posterior_mean_coef2", t, x_t.dim()) * x_t)
+
+    @torch.no_grad()
+    def p_mean_variance(self, model, x, t, clip_denoised=False, denoised_fn=None):
+        """(mean, log variance, predicted x_0) of p(x_{t-1} | x_t) for an x_0-predicting model."""
+        out = model(x, self.scale_timesteps(t)).float()
+        if not self.predict_xstart:
+            raise NotImplementedError("p_mean_variance: eps-prediction models are not supported")
+        pred_x0 = out
+        if denoised_fn is not None:
+            pred_x0 = denoised_fn(pred_x0, t)
+        if clip_denoised:
+            pred_x0 = pred_x0.clamp(-1, 1)
+        name = "posterior_log_variance_clipped" if self.model_var_type == "fixed_small" else "large_log_variance"
+        return self.q_posterior_mean(pred_x0, x, t), self._extract(name, t, x.dim()), pred_x0
+
+    @torch.no_grad()
+    def p_sample(self, model, x, t, mask=None, x_start=None, clip_denoised=False, denoised_fn=None):
+        """One ancestral step x_t -> x_{t-1}; positions with mask == 0 (the source
+        sequence) are kept at x_start (DiffuSeq partial noising)."""
+        mean, logvar, pred_x0 = self.p_mean_variance(model, x, t, clip_denoised, denoised_fn)
+        noise = torch.randn_like(x)
+        nonzero = (t != 0).float().view(-1, *([1] * (x.dim() - 1)))
+        sample = mean + nonzero * torch.exp(0.5 * logvar) * noise
+        if mask is not None and x_start is not None:
+            sample = torch.where(mask.unsqueeze(-1) == 0, x_start, sample)
+        return sample, pred_x0
+
+    @torch.no_grad()
+    def p_sample_loop(self, model, shape, noise=None, mask=None, x_start=None, clip_denoised=False,
+                      denoised_fn=None, device=None):
+        """Sample x_0 from T steps of the reverse process (returns the final sample)."""
+        x = torch.randn(*shape, device=device) if noise is None else noise
+        if mask is not None and x_start is not None:
+            x = torch.where(mask.unsqueeze(-1) == 0, x_start, x)
+        for i in reversed(range(self.num_timesteps)):
+            t = torch.full((shape[0],), i, dtype=torch.long, device=x.device)
+            x, _ = self.p_sample(model, x, t, mask, x_start, clip_denoised, denoised_fn)
+        return x
+
     # -- loss ---------------------------------------------------------------
     def training_losses(self, model, *args, **kwargs):
         return self.training_losses_seq2seq(model, *args, **kwargs)
@@ -116,6 +173,8 @@ class GaussianDiffusion:
             return False
         emb = getattr(net, "word_embedding", None)
         if emb is None or getattr(net, "compute_dtype", None) != torch.bfloat16:
+            return False
+        if getattr(net, "emb_scale_factor", 1.0) != 1.0:
             return False
         from ..ops import diffusion as dops
         return dops.available(emb.weight)
@@ -185,7 +244,9 @@ class GaussianDiffusion:
 
 
 def create_gaussian_diffusion(steps=2000, noise_schedule="sqrt", predict_xstart=True,
-                              rescale_timesteps=True, learn_sigma=False, **_):
+                              rescale_timesteps=True, learn_sigma=False, sigma_small=False,
+                              rescale_learned_sigmas=False, **_):
     betas = get_named_beta_schedule(noise_schedule, steps)
     return GaussianDiffusion(betas, predict_xstart=predict_xstart,
-                             rescale_timesteps=rescale_timesteps, learn_sigma=learn_sigma)
+                             rescale_timesteps=rescale_timesteps, learn_sigma=learn_sigma,
+                             sigma_small=sigma_small, rescale_learned_sigmas=rescale_learned_sigmas)

@@ -19,11 +19,32 @@ PRESETS = {
 }
 
 
+def _from_hf_dir(path):
+    """Architecture of a local transformers BERT/GPT-2 checkpoint directory (config.json)."""
+    import json
+    import os
+    with open(os.path.join(path, "config.json")) as f:
+        c = json.load(f)
+    H = c.get("hidden_size", c.get("n_embd"))
+    return dict(hidden_size=H, num_layers=c.get("num_hidden_layers", c.get("n_layer")),
+                num_heads=c.get("num_attention_heads", c.get("n_head")),
+                intermediate_size=c.get("intermediate_size") or c.get("n_inner") or 4 * H,
+                max_position_embeddings=c.get("max_position_embeddings", c.get("n_positions", 512)),
+                vocab_size=c.get("vocab_size", 30522),
+                layer_norm_eps=c.get("layer_norm_eps", c.get("layer_norm_epsilon", 1e-12)))
+
+
 def resolve(config_name, **overrides):
-    """Preset merged with non-zero overrides (0 means "take the preset")."""
-    if config_name not in PRESETS:
-        raise ValueError(f"unknown config_name {config_name!r}; known: {sorted(PRESETS)}")
-    cfg = dict(PRESETS[config_name])
+    """Preset (or a local transformers checkpoint directory, e.g. for use_plm_init) merged
+    with non-zero overrides (0 means "take the preset")."""
+    import os
+    if config_name in PRESETS:
+        cfg = dict(PRESETS[config_name])
+    elif os.path.isfile(os.path.join(str(config_name), "config.json")):
+        cfg = _from_hf_dir(config_name)
+    else:
+        raise ValueError(f"unknown config_name {config_name!r}; known: {sorted(PRESETS)} "
+                         "or a local checkpoint directory")
     for k, v in overrides.items():
         if v:
             cfg[k] = v

@@ -56,6 +56,17 @@ class _SyncChecked:
         return checked
 
 
+_NATIVE_ENABLED = True
+
+
+def set_native_enabled(flag):
+    """``use_hip_kernels`` setting: False routes every op to its PyTorch reference path
+    (the eager ATen / hipBLASLt implementation) even on a GPU - an A/B and debugging
+    switch, never the default."""
+    global _NATIVE_ENABLED
+    _NATIVE_ENABLED = bool(flag)
+
+
 def gpu_present():
     return torch.cuda.is_available()
 
@@ -63,6 +74,8 @@ def gpu_present():
 def get_ext(required=None):
     """Return the ``_C`` module.  ``required`` defaults to "a GPU is present"."""
     global _EXT, _ERR
+    if not _NATIVE_ENABLED and not required:
+        return None
     if _EXT is None and _ERR is None:
         try:
             # DPA_EXT selects an alternative build of the same sources, e.g. the

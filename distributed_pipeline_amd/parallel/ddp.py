@@ -208,6 +208,13 @@ class DDPEngine(nn.Module):
                 self._next_launch = 0
         return self.module(*args, **kwargs)
 
+    def disarm(self):
+        """Abandon a partially run backward (e.g. an out-of-memory retry): no bucket of
+        it may be reduced, and the next forward re-arms."""
+        if self._native is not None:
+            self._native.disarm()
+        self._armed = False
+
     @contextlib.contextmanager
     def no_sync(self):
         prev = self._sync_enabled

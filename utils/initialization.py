@@ -37,9 +37,11 @@ def create_model_from_config(*, model="diffuseq", **settings):
 
 def create_diffusion_from_config(*, diffusion_steps=2000, noise_schedule="sqrt", predict_xstart=True,
                                  rescale_timesteps=True, learn_sigma=False, schedule_sampler="uniform",
-                                 **_):
+                                 sigma_small=False, rescale_learned_sigmas=False, **_):
     from distributed_pipeline_amd.models import create_gaussian_diffusion, create_named_schedule_sampler
     diffusion = create_gaussian_diffusion(steps=diffusion_steps, noise_schedule=noise_schedule,
                                           predict_xstart=predict_xstart,
-                                          rescale_timesteps=rescale_timesteps, learn_sigma=learn_sigma)
+                                          rescale_timesteps=rescale_timesteps, learn_sigma=learn_sigma,
+                                          sigma_small=sigma_small,
+                                          rescale_learned_sigmas=rescale_learned_sigmas)
     return diffusion, create_named_schedule_sampler(schedule_sampler, diffusion)

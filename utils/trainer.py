@@ -126,7 +126,6 @@ class TrainLoop:
             grad_reduce_dtype="fp32",
             shard_optimizer=False,
             exec_microbatch=0,
-            hip_graphs=False,
             log_cross_rank_mean=False,
             # ---- observability / robustness (all optional) ----
             nan_guard="off",
@@ -156,16 +155,22 @@ class TrainLoop:
         self.engine_kind = ddp_engine
         self.precision = precision
         self.shard_optimizer = bool(shard_optimizer)
-        self.hip_graphs = bool(hip_graphs)
 
         # Executed micro-batch: a multiple of the semantic one; the loss of a
         # fused micro-batch is scaled so gradients equal the sum over semantic
-        # micro-batches (bitwise-different only in fp rounding).
-        emb = int(exec_microbatch) if exec_microbatch else self.microbatch
+        # micro-batches (bitwise-different only in fp rounding).  0 = auto: the
+        # whole per-rank batch in one forward/backward (sized for 288 GB of HBM),
+        # halved on an out-of-memory error until it fits (down to `microbatch`).
+        # -1 = the reference schedule (one forward/backward per micro-batch).
+        self._exec_auto = int(exec_microbatch or 0) == 0
+        emb = self.microbatch if int(exec_microbatch or 0) < 0 else int(exec_microbatch or 0)
+        if self._exec_auto:
+            emb = self.batch_size if torch.cuda.is_available() else self.microbatch
         emb = max(self.microbatch, min(emb, self.batch_size))
         emb = (emb // self.microbatch) * self.microbatch
         if not getattr(self, "supports_microbatch_fusion", False):
             emb = self.microbatch
+            self._exec_auto = False
         self.exec_microbatch = emb
         self.loss_scale = emb / self.microbatch
 
@@ -421,6 +426,24 @@ class TrainLoop:
         self.model.train(was_training)
 
     def forward_backward(self, batch):
+        if not self._exec_auto or self.exec_microbatch <= self.microbatch:
+            return self._forward_backward(batch)
+        while True:
+            try:
+                return self._forward_backward(batch)
+            except torch.cuda.OutOfMemoryError:
+                # auto executed micro-batch: retry the whole step at half the size (the
+                # gradient buffer is zeroed again, so nothing of the failed try remains)
+                smaller = max(self.microbatch, (self.exec_microbatch // 2) // self.microbatch * self.microbatch)
+                if smaller == self.exec_microbatch:
+                    raise
+                logger.log(f"exec_microbatch {self.exec_microbatch} does not fit: retrying with {smaller}")
+                self.exec_microbatch = smaller
+                if self.use_ddp and hasattr(self.ddp_model, "disarm"):
+                    self.ddp_model.disarm()
+                torch.cuda.empty_cache()
+
+    def _forward_backward(self, batch):
         self._zero_grad()
         if self._tokens_per_sample is None and isinstance(batch, dict):
             v = next(iter(batch.values()))
