@@ -68,6 +68,31 @@ def parse():
     return ap.parse_args()
 
 
+def topology():
+    """xGMI topology of the node (recorded with every measurement):
+    `amd-smi topology --json` link types / hop counts between the visible GPUs,
+    compacted; None when the tool is unavailable."""
+    import subprocess
+    try:
+        r = subprocess.run(["amd-smi", "topology", "--json"], capture_output=True, text=True, timeout=20)
+        data = json.loads(r.stdout) if r.returncode == 0 and r.stdout.strip() else None
+    except Exception:  # noqa: BLE001
+        return None
+    if not data:
+        return None
+    rows = data if isinstance(data, list) else data.get("topology", [data])
+    out = []
+    for row in rows:
+        if not isinstance(row, dict):
+            continue
+        gpu = row.get("gpu")
+        links = row.get("links") or []
+        kinds = sorted({str(l.get("link_type")) for l in links if isinstance(l, dict) and l.get("link_type")})
+        hops = [l.get("num_hops") for l in links if isinstance(l, dict) and "num_hops" in l]
+        out.append({"gpu": gpu, "link_types": kinds, "peers": len(links), "max_hops": max(hops) if hops else None})
+    return out or None
+
+
 def main():
     a = parse()
     import torch
@@ -214,6 +239,12 @@ def main():
     }
     if engine == "native":
         out["config"]["bucket_mb"] = loop.ddp_model.bucket_sizes_mb()
+        nat = getattr(loop.ddp_model, "_native", None)
+        out["config"]["comm"] = ("reducer-owned RCCL communicator, priority %d stream" % nat.stream_priority()
+                                 if nat is not None and nat.direct() else
+                                 ("c10d process group" if world > 1 else "none (world 1)"))
+    if rank == 0:
+        out["topology"] = topology()
     if rank == 0:
         line = json.dumps(out)
         print(line, flush=True)

@@ -111,7 +111,7 @@ def build(force=False, jobs=None, debug=False, verbose=True):
     if force or not up_to_date:
         cmd = [_hipcc(), "-shared", "-fPIC", "--offload-arch=" + ARCH, "-o", target] + objects + [
             "-L" + tlib, "-lc10", "-lc10_hip", "-ltorch", "-ltorch_cpu", "-ltorch_hip",
-            "-ltorch_python", "-Wl,-rpath," + tlib]
+            "-ltorch_python", "-lrccl", "-Wl,-rpath," + tlib]  # torch's own librccl: one RCCL per process
         _run(cmd)
         with open(stamp, "w") as f:
             f.write(link_key)

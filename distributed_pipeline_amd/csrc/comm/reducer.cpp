@@ -1,6 +1,6 @@
 // Native bucket reducer of the DDP engine (SURVEY N-1: the role of torch's C++
-// DDP Reducer, reference utils/trainer.py:115-128), designed around the flat
-// gradient buffer instead of per-parameter copies:
+// DDP Reducer, reference utils/trainer.py:115-128; SURVEY N-2: its data plane),
+// designed around the flat gradient buffer instead of per-parameter copies:
 //
 // * Buckets are contiguous [begin, end) slices of ONE flat fp32 gradient buffer
 //   (the parameters' .grad are views into it), so a bucket is reduced in place:
@@ -19,25 +19,56 @@
 //   instead: this rank's summed chunk of bucket b lands at shard_offsets[b] of
 //   the compact shard buffer (bucket lengths are multiples of the world size).
 //
-// The collectives are issued through the c10d ProcessGroup object the Python
-// side created (RCCL "nccl" on ROCm, gloo on CPU), so stream ordering follows
-// the backend: RCCL work is enqueued after the producing kernels of the
-// current stream and completion is awaited in finalize().
+// Two data planes:
+// * direct (default on RCCL): the reducer owns an RCCL communicator (unique id
+//   handed out by rank 0 over the c10d store) and a HIGHEST-priority HIP stream.
+//   A bucket launch records an event on the producing (compute) stream at the
+//   grad-ready point, the comm stream waits on it, packs (bf16 wire) and runs
+//   ncclAllReduce / ncclReduceScatter; finalize() makes the compute stream wait on
+//   the comm stream's completion event - nothing blocks the host, and the
+//   all-reduce kernels get the CUs first when they contend with backward GEMMs.
+// * process group (gloo, fake PG, or DPA_REDUCER_COMM=pg): collectives through the
+//   c10d ProcessGroup the Python side created; ordering follows the backend.
 #include <torch/extension.h>
+#include <ATen/hip/impl/HIPStreamMasqueradingAsCUDA.h>
 #include <torch/csrc/distributed/c10d/ProcessGroup.hpp>
 #include <torch/csrc/distributed/c10d/Work.hpp>
+#include <rccl/rccl.h>
 
+#include <cstring>
 #include <mutex>
 #include <stdexcept>
+#include <string>
 #include <vector>
 
+#include "../launchers.h"
+
+#define DPA_RCCL_CHECK(cmd)                                                                  \
+  do {                                                                                       \
+    ncclResult_t r_ = (cmd);                                                                 \
+    TORCH_CHECK(r_ == ncclSuccess, "RCCL error '", ncclGetErrorString(r_), "' in ", #cmd);   \
+  } while (0)
+#define DPA_HIP_CHECK(cmd)                                                                   \
+  do {                                                                                       \
+    hipError_t e_ = (cmd);                                                                   \
+    TORCH_CHECK(e_ == hipSuccess, "HIP error '", hipGetErrorString(e_), "' in ", #cmd);      \
+  } while (0)
+
 namespace dpa {
+
+// 128 opaque bytes for ncclCommInitRank, created by one rank and shared by all.
+static pybind11::bytes rccl_unique_id() {
+  ncclUniqueId id;
+  DPA_RCCL_CHECK(ncclGetUniqueId(&id));
+  return pybind11::bytes(id.internal, NCCL_UNIQUE_ID_BYTES);
+}
 
 class BucketReducer {
  public:
   BucketReducer(c10::intrusive_ptr<c10d::ProcessGroup> pg, at::Tensor grad_flat,
                 std::vector<int64_t> bounds, std::vector<int64_t> param_bucket, bool bf16_wire,
-                c10::optional<at::Tensor> shard_out, std::vector<int64_t> shard_offsets)
+                c10::optional<at::Tensor> shard_out, std::vector<int64_t> shard_offsets,
+                std::string rccl_uid, int64_t rank, int64_t world)
       : pg_(std::move(pg)), grad_(std::move(grad_flat)), bounds_(std::move(bounds)),
         bucket_of_(std::move(param_bucket)), bf16_(bf16_wire) {
     TORCH_CHECK(grad_.is_contiguous() && grad_.dim() == 1, "grad_flat must be a 1-D contiguous tensor");
@@ -53,12 +84,12 @@ class BucketReducer {
     pending_ = size_;
     work_.resize(nb);
     launched_.assign(nb, false);
+    world_ = pg_ ? pg_->getSize() : world;
     if (bf16_) comm_ = at::empty({grad_.numel()}, grad_.options().dtype(at::kBFloat16));
     if (shard_out.has_value() && shard_out->defined()) {
       rs_ = true;
       shard_ = *shard_out;
       shard_off_ = std::move(shard_offsets);
-      world_ = pg_->getSize();
       TORCH_CHECK(shard_.is_contiguous() && shard_.scalar_type() == grad_.scalar_type(),
                   "shard buffer must be contiguous and of the gradient dtype");
       TORCH_CHECK((int)shard_off_.size() == nb, "one shard offset per bucket");
@@ -70,6 +101,15 @@ class BucketReducer {
       }
       if (bf16_) comm_out_ = at::empty({shard_.numel()}, grad_.options().dtype(at::kBFloat16));
     }
+    if (!rccl_uid.empty()) init_direct(rccl_uid, (int)rank, (int)world);
+  }
+
+  ~BucketReducer() {
+    // abort (not destroy): never blocks on peers that already left at shutdown
+    if (rcomm_) ncclCommAbort(rcomm_);
+    for (hipEvent_t e : ready_) if (e) (void)hipEventDestroy(e);
+    if (done_) (void)hipEventDestroy(done_);
+    if (cs_) (void)hipStreamDestroy(cs_);
   }
 
   // Called at forward time when gradient synchronisation is enabled (torch-DDP
@@ -89,6 +129,7 @@ class BucketReducer {
   }
 
   bool armed() const { return armed_; }
+  bool direct() const { return rcomm_ != nullptr; }
 
   void mark_ready(int64_t param_index) {
     std::lock_guard<std::mutex> g(mu_);
@@ -100,20 +141,38 @@ class BucketReducer {
   }
 
   // Launch whatever has not been launched (e.g. unused parameters, or graph
-  // replays without hooks), wait for every bucket, unpack the bf16 wire.
+  // replays without hooks), then order the reduced gradients before the current
+  // stream's next work (direct: a stream-side event wait, no host block; process
+  // group: wait on the Work handles), unpacking the bf16 wire.
   void finalize() {
     std::lock_guard<std::mutex> g(mu_);
     if (!armed_) return;
     const int nb = (int)launched_.size();
     for (int b = next_; b < nb; ++b) launch(b);
     next_ = nb;
-    for (int b = 0; b < nb; ++b) {
-      if (work_[b]) {
-        work_[b]->wait();
-        work_[b].reset();
-        if (bf16_) {
-          if (rs_) chunk(shard_, b).copy_(chunk(comm_out_, b));
-          else slice(grad_, b).copy_(slice(comm_, b));
+    if (rcomm_) {
+      if (bf16_) {
+        for (int b = 0; b < nb; ++b) {
+          if (rs_) {
+            const int64_t c = (bounds_[b + 1] - bounds_[b]) / world_;
+            launch_cast_f32(bf_ptr(comm_out_) + shard_off_[b], shard_.data_ptr<float>() + shard_off_[b], c, cs_);
+          } else {
+            launch_cast_f32(bf_ptr(comm_) + bounds_[b], grad_.data_ptr<float>() + bounds_[b],
+                            bounds_[b + 1] - bounds_[b], cs_);
+          }
+        }
+      }
+      DPA_HIP_CHECK(hipEventRecord(done_, cs_));
+      DPA_HIP_CHECK(hipStreamWaitEvent(compute_stream(), done_, 0));
+    } else {
+      for (int b = 0; b < nb; ++b) {
+        if (work_[b]) {
+          work_[b]->wait();
+          work_[b].reset();
+          if (bf16_) {
+            if (rs_) chunk(shard_, b).copy_(chunk(comm_out_, b));
+            else slice(grad_, b).copy_(slice(comm_, b));
+          }
         }
       }
     }
@@ -131,8 +190,33 @@ class BucketReducer {
   std::vector<int64_t> pending() const {
     return std::vector<int64_t>(pending_.begin(), pending_.end());
   }
+  // priority of the reducer's comm stream (direct mode; lower = higher priority)
+  int64_t stream_priority() const {
+    int p = 0;
+    if (cs_) (void)hipStreamGetPriority(cs_, &p);
+    return p;
+  }
 
  private:
+  static hipStream_t compute_stream() { return c10::hip::getCurrentHIPStreamMasqueradingAsCUDA().stream(); }
+  static uint16_t* bf_ptr(const at::Tensor& t) { return reinterpret_cast<uint16_t*>(t.data_ptr()); }
+
+  void init_direct(const std::string& uid, int rank, int world) {
+    TORCH_CHECK(grad_.is_cuda(), "the direct RCCL data plane needs device gradients");
+    TORCH_CHECK(uid.size() == NCCL_UNIQUE_ID_BYTES, "RCCL unique id must be ", NCCL_UNIQUE_ID_BYTES, " bytes");
+    TORCH_CHECK(world == world_, "direct communicator size differs from the process group's");
+    const c10::DeviceGuard guard(grad_.device());
+    ncclUniqueId id;
+    std::memcpy(id.internal, uid.data(), NCCL_UNIQUE_ID_BYTES);
+    DPA_RCCL_CHECK(ncclCommInitRank(&rcomm_, world, id, rank));
+    int least = 0, greatest = 0;
+    DPA_HIP_CHECK(hipDeviceGetStreamPriorityRange(&least, &greatest));
+    DPA_HIP_CHECK(hipStreamCreateWithPriority(&cs_, hipStreamNonBlocking, greatest));
+    ready_.assign(launched_.size(), nullptr);
+    for (auto& e : ready_) DPA_HIP_CHECK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+    DPA_HIP_CHECK(hipEventCreateWithFlags(&done_, hipEventDisableTiming));
+  }
+
   at::Tensor slice(const at::Tensor& t, int b) const { return t.slice(0, bounds_[b], bounds_[b + 1]); }
   // this rank's reduce-scatter output for bucket b inside a compact shard buffer
   at::Tensor chunk(const at::Tensor& t, int b) const {
@@ -146,6 +230,34 @@ class BucketReducer {
 
   void launch(int b) {
     if (launched_[b]) return;
+    if (rcomm_) launch_direct(b);
+    else launch_pg(b);
+    launched_[b] = true;
+  }
+
+  void launch_direct(int b) {
+    const int64_t n = bounds_[b + 1] - bounds_[b];
+    // the grad-ready point: everything the compute stream queued so far
+    DPA_HIP_CHECK(hipEventRecord(ready_[b], compute_stream()));
+    DPA_HIP_CHECK(hipStreamWaitEvent(cs_, ready_[b], 0));
+    float* g = grad_.data_ptr<float>() + bounds_[b];
+    void* buf = g;
+    ncclDataType_t dt = ncclFloat32;
+    if (bf16_) {
+      uint16_t* w = bf_ptr(comm_) + bounds_[b];
+      launch_cast_bf16(g, w, n, cs_);
+      buf = w;
+      dt = ncclBfloat16;
+    }
+    if (rs_) {
+      void* out = bf16_ ? (void*)(bf_ptr(comm_out_) + shard_off_[b]) : (void*)(shard_.data_ptr<float>() + shard_off_[b]);
+      DPA_RCCL_CHECK(ncclReduceScatter(buf, out, (size_t)(n / world_), dt, ncclSum, rcomm_, cs_));
+    } else {
+      DPA_RCCL_CHECK(ncclAllReduce(buf, buf, (size_t)n, dt, ncclSum, rcomm_, cs_));
+    }
+  }
+
+  void launch_pg(int b) {
     at::Tensor view = slice(grad_, b);
     if (bf16_) {
       at::Tensor wire = slice(comm_, b);
@@ -159,7 +271,6 @@ class BucketReducer {
       std::vector<at::Tensor> ts{view};
       work_[b] = pg_->allreduce(ts);
     }
-    launched_[b] = true;
   }
 
   c10::intrusive_ptr<c10d::ProcessGroup> pg_;
@@ -175,21 +286,30 @@ class BucketReducer {
   int next_ = 0;
   bool armed_ = false;
   bool bf16_;
+  // direct data plane
+  ncclComm_t rcomm_ = nullptr;
+  hipStream_t cs_ = nullptr;
+  std::vector<hipEvent_t> ready_;
+  hipEvent_t done_ = nullptr;
   std::mutex mu_;
 };
 
 void register_comm(pybind11::module& m) {
+  m.def("rccl_unique_id", &rccl_unique_id, "new RCCL unique id (bytes) for the reducer's communicator");
   pybind11::class_<BucketReducer>(m, "BucketReducer")
       .def(pybind11::init<c10::intrusive_ptr<c10d::ProcessGroup>, at::Tensor, std::vector<int64_t>,
-                          std::vector<int64_t>, bool, c10::optional<at::Tensor>,
-                          std::vector<int64_t>>(),
+                          std::vector<int64_t>, bool, c10::optional<at::Tensor>, std::vector<int64_t>,
+                          std::string, int64_t, int64_t>(),
            pybind11::arg("process_group"), pybind11::arg("grad_flat"), pybind11::arg("bounds"),
            pybind11::arg("param_bucket"), pybind11::arg("bf16_wire") = false,
            pybind11::arg("shard_out") = pybind11::none(),
-           pybind11::arg("shard_offsets") = std::vector<int64_t>())
+           pybind11::arg("shard_offsets") = std::vector<int64_t>(),
+           pybind11::arg("rccl_uid") = std::string(), pybind11::arg("rank") = 0, pybind11::arg("world") = 1)
       .def("arm", &BucketReducer::arm)
       .def("disarm", &BucketReducer::disarm)
       .def("armed", &BucketReducer::armed)
+      .def("direct", &BucketReducer::direct)
+      .def("stream_priority", &BucketReducer::stream_priority)
       .def("mark_ready", &BucketReducer::mark_ready, pybind11::call_guard<pybind11::gil_scoped_release>())
       .def("finalize", &BucketReducer::finalize, pybind11::call_guard<pybind11::gil_scoped_release>())
       .def("reduce_all", &BucketReducer::reduce_all, pybind11::call_guard<pybind11::gil_scoped_release>())

@@ -16,6 +16,7 @@ void launch_adamw_ema(float* p, const void* g, bool g_bf16, float* m, float* v, 
                       const float* clip, hipStream_t s);
 void launch_ema(float* e, const float* p, int64_t n, float rate, hipStream_t s);
 void launch_cast_bf16(const float* src, uint16_t* dst, int64_t n, hipStream_t s);
+void launch_cast_f32(const uint16_t* src, float* dst, int64_t n, hipStream_t s);  // n % 4 == 0
 
 // ---- xent.hip (fused linear + cross-entropy) ----------------------------------
 int64_t lxent_workspace_floats(int N, int V);

@@ -161,6 +161,17 @@ __global__ void __launch_bounds__(256) cast_bf16_kernel(const float* __restrict_
   }
 }
 
+// bf16 -> fp32 flat copy (unpacking a bf16-wire gradient bucket).
+__global__ void __launch_bounds__(256) cast_f32_kernel(const bf16_t* __restrict__ src,
+                                                      float* __restrict__ dst, int64_t n) {
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x * 4;
+  for (int64_t i = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) * 4; i < n; i += stride) {
+    const uint2 u = *reinterpret_cast<const uint2*>(src + i);
+    *reinterpret_cast<f32x4*>(dst + i) = f32x4{__uint_as_float(u.x << 16), __uint_as_float(u.x & 0xffff0000u),
+                                              __uint_as_float(u.y << 16), __uint_as_float(u.y & 0xffff0000u)};
+  }
+}
+
 static inline int grid_for(int64_t n, int per_thread, int block, int cap) {
   int64_t g = (n / per_thread + block - 1) / block;
   if (g < 1) g = 1;
@@ -215,6 +226,11 @@ void launch_adamw_ema(float* p, const void* g, bool g_bf16, float* m, float* v, 
 
 void launch_ema(float* e, const float* p, int64_t n, float rate, hipStream_t s) {
   hipLaunchKernelGGL(ema_kernel, dim3(grid_for(n, 4, 256, 2048)), dim3(256), 0, s, e, p, n, rate);
+}
+
+void launch_cast_f32(const uint16_t* src, float* dst, int64_t n, hipStream_t s) {
+  hipLaunchKernelGGL(cast_f32_kernel, dim3(grid_for(n, 4, 256, 2048)), dim3(256), 0, s, (const bf16_t*)src,
+                     dst, n);
 }
 
 void launch_cast_bf16(const float* src, uint16_t* dst, int64_t n, hipStream_t s) {

@@ -18,10 +18,12 @@ implements the same protocol for the single-GPU multi-rank test transport.
 * Readiness: a post-accumulate-grad hook per parameter decrements its bucket's
   pending counter (autograd runs it once per backward per leaf, after all uses,
   even when a fused wgrad GEMM accumulated the gradient in place and returned
-  None); the bucket whose counter hits zero is all-reduced
-  asynchronously (RCCL on its own internal stream, ordered after the
-  gradient-producing kernels of the current stream).  Buckets are launched in
-  order so every rank issues collectives in the same sequence.
+  None); the bucket whose counter hits zero is all-reduced asynchronously.  On
+  RCCL the C++ reducer owns its communicator and a highest-priority HIP stream:
+  an event recorded on the compute stream at the grad-ready point orders the
+  bucket's all-reduce after its gradient kernels, and finalize() makes the
+  compute stream wait on the comm stream (no host synchronisation).  Buckets are
+  launched in order so every rank issues collectives in the same sequence.
 * ``no_sync()`` has torch-DDP semantics: the decision is taken at *forward*
   time, so gradient accumulation over micro-batches issues exactly one
   reduction per optimizer step (SURVEY P-GA).
@@ -102,7 +104,8 @@ class DDPEngine(nn.Module):
         self.distributed = dist.is_available() and dist.is_initialized()
         self.world_size = dist.get_world_size(self.pg) if self.distributed else 1
         self.rank = dist.get_rank(self.pg) if self.distributed else 0
-        self.sharded = bool(shard_optimizer) and self.distributed and self.world_size > 1
+        # (world 1 keeps the sharded machinery - one shard - so it can be exercised alone)
+        self.sharded = bool(shard_optimizer) and self.distributed
         if space is None:
             kw = {}
             if self.sharded:
@@ -156,10 +159,20 @@ class DDPEngine(nn.Module):
                 pg = self.pg or dist.distributed_c10d._get_default_group()
                 bounds = [b.start for b in self.buckets] + [self.buckets[-1].end]
                 param_bucket = [self._bucket_of[id(p)].index for p in self.space.layout]
+                # SURVEY N-2: on RCCL the reducer owns its communicator + a highest-
+                # priority comm stream (DPA_REDUCER_COMM=pg: collectives through the c10d PG)
+                uid = ""
+                if (self._backend == "nccl" and self.space.device.type == "cuda"
+                        and os.environ.get("DPA_REDUCER_COMM", "direct") == "direct"
+                        and hasattr(ext, "rccl_unique_id")):
+                    box = [ext.rccl_unique_id() if self.rank == 0 else None]
+                    dist.broadcast_object_list(box, src=dist.get_global_rank(pg, 0), group=self.pg)
+                    uid = box[0]
                 self._native = ext.BucketReducer(pg, self.space.grad_flat, bounds, param_bucket,
                                                  self.reduce_dtype == torch.bfloat16,
                                                  self.grad_shard if self.sharded else None,
-                                                 [c[2] for c in self.shard_chunks])
+                                                 [c[2] for c in self.shard_chunks], uid, self.rank,
+                                                 self.world_size)
         if self.distributed:
             self._verify_shapes()
             if broadcast_from_rank0:

@@ -67,12 +67,15 @@ def _worker(rank, world, port, q, fused=False, native="1", wire="fp32"):
             with ctx:
                 loss = torch.nn.functional.mse_loss(eng(x), y)
             loss.backward()
+        # overlap: every bucket was launched from the grad-ready hooks DURING backward,
+        # none is left for finalize() (also for weights accumulated in place by a fused op)
+        launched = eng._native.next_bucket() if eng._native is not None else eng._next_launch
         eng.finalize()
         eng.average_gradients()
         # numpy copies travel by value (tensor storages are shared via fds, which
         # races with the worker exiting)
         q.put((rank, eng.space.param_flat.numpy().copy(), eng.space.grad_flat.numpy().copy(),
-               len(eng.buckets)))
+               len(eng.buckets), launched))
     finally:
         dist.destroy_process_group()
 
@@ -107,9 +110,10 @@ def test_ddp_engine_matches_single_process(world, fused, native, wire):
             loss.backward()
     space = FlatParamSpace(model.parameters())
     ref_grad = space.grad_flat
-    for rank, pflat, gflat, nb in res:
+    for rank, pflat, gflat, nb, launched in res:
         pflat, gflat = torch.from_numpy(pflat), torch.from_numpy(gflat)
         assert nb > 1, "test must exercise several buckets"
+        assert launched == nb, f"rank {rank}: only {launched}/{nb} buckets launched before finalize()"
         torch.testing.assert_close(pflat, space.param_flat)            # broadcast from rank 0
         tol = dict(rtol=1e-5, atol=1e-6) if wire == "fp32" else dict(rtol=2e-2, atol=2e-3)
         torch.testing.assert_close(gflat, ref_grad, **tol)

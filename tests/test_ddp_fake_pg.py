@@ -53,5 +53,8 @@ def test_fake_pg_world8_bucket_launch_order_and_no_sync(fake_world, monkeypatch,
     eng(x).square().mean().backward()
     if native == "0":
         assert launched == list(range(len(eng.buckets)))
+    else:  # the C++ reducer launched every bucket from the hooks, none left for finalize
+        assert eng._native.next_bucket() == eng._native.num_buckets() == len(eng.buckets)
+        assert list(eng._native.pending()) == [0] * len(eng.buckets)
     eng.finalize()
     torch.testing.assert_close(eng.space.grad_flat, 2 * g_local)

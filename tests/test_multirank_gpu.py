@@ -95,12 +95,16 @@ def _rccl_worker(port, wire, q):
             with (torch.enable_grad() if sync else eng.no_sync()):
                 terms = diff.training_losses(eng, None, t, dict(input_ids=ids, input_mask=mask))
             terms["loss"].mean().backward()
+            launched = eng._native.next_bucket() if native else -1
             eng.finalize()
-            return eng.space.grad_flat.clone()
+            return eng.space.grad_flat.clone(), launched
 
-        local = run(sync=False)   # no collective
-        reduced = run(sync=True)  # RCCL all-reduce of every bucket (world 1: identity)
-        q.put((native, len(eng.buckets), local.cpu().numpy(), reduced.cpu().numpy()))
+        local, _ = run(sync=False)   # no collective
+        reduced, launched = run(sync=True)  # RCCL all-reduce of every bucket (world 1: identity)
+        direct = bool(native and eng._native.direct())
+        prio = eng._native.stream_priority() if native else 0
+        q.put((native, len(eng.buckets), local.cpu().numpy(), reduced.cpu().numpy(), launched, direct,
+               prio))
     finally:
         dist.destroy_process_group()
 
@@ -114,11 +118,15 @@ def test_native_reducer_over_rccl_single_rank(wire):
     q = ctx.Queue()
     p = ctx.Process(target=_rccl_worker, args=(find_free_port(), wire, q))
     p.start()
-    native, nb, local, reduced = q.get(timeout=300)
+    native, nb, local, reduced, launched, direct, prio = q.get(timeout=300)
     p.join(timeout=60)
     assert p.exitcode == 0
     assert native, "native BucketReducer not used with the RCCL process group"
     assert nb > 3
+    # the reducer-owned RCCL communicator on a highest-priority comm stream (SURVEY N-2),
+    # every bucket launched from the grad-ready hooks while backward ran (overlap)
+    assert direct and prio < 0, (direct, prio)
+    assert launched == nb, f"{launched}/{nb} buckets launched before finalize()"
     local, reduced = torch.from_numpy(local), torch.from_numpy(reduced)
     assert local.abs().sum() > 0
     # split-K wgrad accumulates with fp32 atomics, so two backwards differ in rounding
@@ -128,3 +136,51 @@ def test_native_reducer_over_rccl_single_rank(wire):
     # 99.9% of elements agree to bf16 rounding
     close = torch.isclose(reduced, local, rtol=1e-2, atol=1e-6 * local.abs().max().item())
     assert close.float().mean() > 0.999
+
+
+def _zero_rccl_worker(port, wire, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    torch.cuda.set_device(0)
+    dist.init_process_group("nccl", rank=0, world_size=1, device_id=torch.device("cuda:0"))
+    try:
+        from distributed_pipeline_amd.parallel.ddp import DDPEngine
+        from distributed_pipeline_amd.parallel.optimizer import FusedAdamW
+        from distributed_pipeline_amd.parallel.zero import ZeroFusedAdamW
+        rd = torch.bfloat16 if wire == "bf16" else torch.float32
+        out = []
+        for sharded in (False, True):
+            torch.manual_seed(5)
+            model = torch.nn.Sequential(*[torch.nn.Linear(256, 256) for _ in range(4)]).cuda()
+            eng = DDPEngine(model, bucket_cap_mb=0.25, first_bucket_mb=0.1, shard_optimizer=sharded,
+                            reduce_dtype=rd)
+            assert eng.sharded == sharded
+            kw = dict(lr=1e-2, weight_decay=0.01, ema_rates=[0.9])
+            opt = ZeroFusedAdamW(eng, **kw) if sharded else FusedAdamW(eng.space, **kw)
+            torch.manual_seed(6)
+            for _ in range(3):
+                eng.zero_grad()
+                x = torch.randn(64, 256, device="cuda")
+                eng(x).square().mean().backward()
+                eng.finalize()
+                opt.step()
+                if sharded:
+                    eng.gather_params()
+            out.append(eng.space.param_flat.detach().cpu().numpy().copy())
+        q.put(out)
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("wire", ["fp32", "bf16"])
+def test_zero1_reduce_scatter_over_rccl_single_rank(wire):
+    """ZeRO-1 on a real RCCL communicator: buckets REDUCE-SCATTERED by the reducer's
+    own communicator into the shard buffer, sharded AdamW, all-gather of the updated
+    chunks - must match the unsharded engine step for step (world 1)."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    p = ctx.Process(target=_zero_rccl_worker, args=(find_free_port(), wire, q))
+    p.start()
+    plain, sharded = q.get(timeout=300)
+    p.join(timeout=60)
+    assert p.exitcode == 0
+    torch.testing.assert_close(torch.from_numpy(sharded), torch.from_numpy(plain), rtol=1e-6, atol=1e-7)
