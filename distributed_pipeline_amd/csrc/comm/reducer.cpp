@@ -29,12 +29,17 @@
 //   all-reduce kernels get the CUs first when they contend with backward GEMMs.
 // * process group (gloo, fake PG, or DPA_REDUCER_COMM=pg): collectives through the
 //   c10d ProcessGroup the Python side created; ordering follows the backend.
+// * opt-in on top of direct (DPA_IPC_ALLREDUCE=1, fp32 all-reduce buckets): peers map
+//   each other's staging buffers (hipIpc handles exchanged once) and the buckets are
+//   reduced by csrc/ipc_allreduce.hip on the same comm stream - all 7 xGMI links of a
+//   GPU carry traffic at once instead of one ring neighbour's link.
 #include <torch/extension.h>
 #include <ATen/hip/impl/HIPStreamMasqueradingAsCUDA.h>
 #include <torch/csrc/distributed/c10d/ProcessGroup.hpp>
 #include <torch/csrc/distributed/c10d/Work.hpp>
 #include <rccl/rccl.h>
 
+#include <algorithm>
 #include <cstring>
 #include <mutex>
 #include <stdexcept>
@@ -55,6 +60,41 @@
   } while (0)
 
 namespace dpa {
+
+// Single-device test of the IPC all-reduce protocol: the W tensors play W ranks in
+// ONE launch (csrc/ipc_allreduce.hip, gridDim.y = W); every call replaces each
+// tensor by the sum of all W.  mode: 0 one-shot, 1 two-shot, 2 alternate per call
+// (flag slots reused across the two modes' block counts).  Returns the kernel's error
+// word (0 = ok, 1 = a bounded spin timed out).
+static int64_t ipc_allreduce_sim(std::vector<at::Tensor> ts, int64_t mode, int64_t calls) {
+  const int W = (int)ts.size();
+  TORCH_CHECK(W >= 1 && W <= IPC_MAXW, "1..8 simulated ranks");
+  const int64_t n = ts[0].numel();
+  for (auto& t : ts)
+    TORCH_CHECK(t.is_cuda() && t.scalar_type() == at::kFloat && t.is_contiguous() && t.numel() == n,
+                "equal-size contiguous fp32 device tensors");
+  const c10::DeviceGuard guard(ts[0].device());
+  auto opt = ts[0].options();
+  at::Tensor stage = at::zeros({W, 2 * n}, opt);
+  at::Tensor flags = at::zeros({W, IPC_FLAG_WORDS}, opt.dtype(at::kInt));
+  at::Tensor err = at::zeros({1}, opt.dtype(at::kInt));
+  IpcPeers peers{};
+  IpcData data{};
+  for (int r = 0; r < W; ++r) {
+    peers.stage[r] = stage[r].data_ptr<float>();
+    peers.flags[r] = reinterpret_cast<uint32_t*>(flags[r].data_ptr<int>());
+    data.p[r] = ts[r].data_ptr<float>();
+  }
+  // all W x blocks must be co-resident (the simulated ranks spin on each other)
+  TORCH_CHECK(mode >= 0 && mode <= 2, "mode: 0 one-shot, 1 two-shot, 2 alternate");
+  TORCH_CHECK((int64_t)ipc_allreduce_blocks(n, W, true) * W <= 1024, "ipc_allreduce_sim: n too large");
+  hipStream_t s = c10::hip::getCurrentHIPStreamMasqueradingAsCUDA().stream();
+  for (int64_t c = 0; c < calls; ++c)
+    TORCH_CHECK(launch_ipc_allreduce(peers, data, W, 0, W, n, n, (uint32_t)(c + 1),
+                                     mode == 2 ? (c & 1) != 0 : mode == 1,
+                                     err.data_ptr<int>(), s), "ipc_allreduce_sim: bad arguments");
+  return err.item<int>();
+}
 
 // 128 opaque bytes for ncclCommInitRank, created by one rank and shared by all.
 static pybind11::bytes rccl_unique_id() {
@@ -107,6 +147,14 @@ class BucketReducer {
   ~BucketReducer() {
     // abort (not destroy): never blocks on peers that already left at shutdown
     if (rcomm_) ncclCommAbort(rcomm_);
+    for (int r = 0; r < world_; ++r)
+      if (r != rank_ && peers_.stage[r]) {
+        (void)hipIpcCloseMemHandle(peers_.stage[r]);
+        (void)hipIpcCloseMemHandle(peers_.flags[r]);
+      }
+    if (ipc_stage_) (void)hipFree(ipc_stage_);
+    if (ipc_flags_) (void)hipFree(ipc_flags_);
+    if (ipc_err_) (void)hipFree(ipc_err_);
     for (hipEvent_t e : ready_) if (e) (void)hipEventDestroy(e);
     if (done_) (void)hipEventDestroy(done_);
     if (cs_) (void)hipStreamDestroy(cs_);
@@ -190,6 +238,59 @@ class BucketReducer {
   std::vector<int64_t> pending() const {
     return std::vector<int64_t>(pending_.begin(), pending_.end());
   }
+  // ---- opt-in direct xGMI all-reduce over IPC-mapped buffers (DPA_IPC_ALLREDUCE=1) ----
+  // Phase 1: allocate this rank's staging buffer (two parity halves of the largest
+  // bucket) and flag words with hipMalloc and export their IPC handles.
+  pybind11::bytes ipc_export() {
+    TORCH_CHECK(rcomm_ != nullptr, "the IPC data plane rides on the direct mode's comm stream");
+    TORCH_CHECK(!rs_ && !bf16_, "IPC all-reduce: fp32 all-reduce buckets only");
+    const c10::DeviceGuard guard(grad_.device());
+    ipc_cap_ = 0;
+    for (size_t b = 0; b + 1 < bounds_.size(); ++b) ipc_cap_ = std::max(ipc_cap_, bounds_[b + 1] - bounds_[b]);
+    DPA_HIP_CHECK(hipMalloc(&ipc_stage_, 2 * ipc_cap_ * sizeof(float)));
+    DPA_HIP_CHECK(hipMalloc(&ipc_flags_, IPC_FLAG_WORDS * sizeof(uint32_t)));
+    DPA_HIP_CHECK(hipMemset(ipc_flags_, 0, IPC_FLAG_WORDS * sizeof(uint32_t)));
+    DPA_HIP_CHECK(hipMalloc(&ipc_err_, sizeof(int)));
+    DPA_HIP_CHECK(hipMemset(ipc_err_, 0, sizeof(int)));
+    DPA_HIP_CHECK(hipDeviceSynchronize());
+    hipIpcMemHandle_t h[2];
+    DPA_HIP_CHECK(hipIpcGetMemHandle(&h[0], ipc_stage_));
+    DPA_HIP_CHECK(hipIpcGetMemHandle(&h[1], ipc_flags_));
+    return pybind11::bytes(reinterpret_cast<const char*>(h), sizeof(h));
+  }
+
+  // Phase 2: map every peer's buffers (handles gathered from all ranks, rank order).
+  void ipc_open(std::vector<std::string> handles) {
+    TORCH_CHECK((int)handles.size() == world_ && world_ <= IPC_MAXW, "one handle blob per rank, <= 8 ranks");
+    const c10::DeviceGuard guard(grad_.device());
+    for (int r = 0; r < world_; ++r) {
+      if (r == rank_) {
+        peers_.stage[r] = ipc_stage_;
+        peers_.flags[r] = ipc_flags_;
+        continue;
+      }
+      TORCH_CHECK(handles[r].size() == 2 * sizeof(hipIpcMemHandle_t), "bad IPC handle blob");
+      hipIpcMemHandle_t h[2];
+      std::memcpy(h, handles[r].data(), sizeof(h));
+      void *st = nullptr, *fl = nullptr;
+      DPA_HIP_CHECK(hipIpcOpenMemHandle(&st, h[0], hipIpcMemLazyEnablePeerAccess));
+      DPA_HIP_CHECK(hipIpcOpenMemHandle(&fl, h[1], hipIpcMemLazyEnablePeerAccess));
+      peers_.stage[r] = static_cast<float*>(st);
+      peers_.flags[r] = static_cast<uint32_t*>(fl);
+    }
+    ipc_ready_ = true;
+  }
+
+  bool ipc_ready() const { return ipc_ready_; }
+  // the kernels' timeout word (host sync; debugging / tests only)
+  int64_t ipc_error() const {
+    if (!ipc_err_) return 0;
+    int e = 0;
+    DPA_HIP_CHECK(hipStreamSynchronize(cs_));
+    DPA_HIP_CHECK(hipMemcpy(&e, ipc_err_, sizeof(int), hipMemcpyDeviceToHost));
+    return e;
+  }
+
   // priority of the reducer's comm stream (direct mode; lower = higher priority)
   int64_t stream_priority() const {
     int p = 0;
@@ -208,6 +309,7 @@ class BucketReducer {
     const c10::DeviceGuard guard(grad_.device());
     ncclUniqueId id;
     std::memcpy(id.internal, uid.data(), NCCL_UNIQUE_ID_BYTES);
+    rank_ = rank;
     DPA_RCCL_CHECK(ncclCommInitRank(&rcomm_, world, id, rank));
     int least = 0, greatest = 0;
     DPA_HIP_CHECK(hipDeviceGetStreamPriorityRange(&least, &greatest));
@@ -249,6 +351,18 @@ class BucketReducer {
       buf = w;
       dt = ncclBfloat16;
     }
+    if (ipc_ready_) {
+      // one-shot below 256 KiB (latency), two-shot above (bandwidth: (W-1)/W n reads twice)
+      IpcData d{};
+      d.p[rank_] = g;
+      // (a bucket the kernel cannot take - length % 4, 16-byte alignment - goes through
+      // RCCL instead; the layout is identical on every rank, so all ranks agree)
+      if (launch_ipc_allreduce(peers_, d, (int)world_, rank_, 1, n, ipc_cap_, ipc_epoch_ + 1,
+                               n * 4 > (256 << 10), ipc_err_, cs_)) {
+        ++ipc_epoch_;
+        return;
+      }
+    }
     if (rs_) {
       void* out = bf16_ ? (void*)(bf_ptr(comm_out_) + shard_off_[b]) : (void*)(shard_.data_ptr<float>() + shard_off_[b]);
       DPA_RCCL_CHECK(ncclReduceScatter(buf, out, (size_t)(n / world_), dt, ncclSum, rcomm_, cs_));
@@ -288,6 +402,15 @@ class BucketReducer {
   bool bf16_;
   // direct data plane
   ncclComm_t rcomm_ = nullptr;
+  int rank_ = 0;
+  // IPC data plane
+  bool ipc_ready_ = false;
+  float* ipc_stage_ = nullptr;
+  uint32_t* ipc_flags_ = nullptr;
+  int* ipc_err_ = nullptr;
+  int64_t ipc_cap_ = 0;
+  uint32_t ipc_epoch_ = 0;
+  IpcPeers peers_{};
   hipStream_t cs_ = nullptr;
   std::vector<hipEvent_t> ready_;
   hipEvent_t done_ = nullptr;
@@ -296,6 +419,8 @@ class BucketReducer {
 
 void register_comm(pybind11::module& m) {
   m.def("rccl_unique_id", &rccl_unique_id, "new RCCL unique id (bytes) for the reducer's communicator");
+  m.def("ipc_allreduce_sim", &ipc_allreduce_sim,
+        "single-device test of the IPC all-reduce: the W tensors play W ranks -> error word");
   pybind11::class_<BucketReducer>(m, "BucketReducer")
       .def(pybind11::init<c10::intrusive_ptr<c10d::ProcessGroup>, at::Tensor, std::vector<int64_t>,
                           std::vector<int64_t>, bool, c10::optional<at::Tensor>, std::vector<int64_t>,
@@ -310,6 +435,10 @@ void register_comm(pybind11::module& m) {
       .def("armed", &BucketReducer::armed)
       .def("direct", &BucketReducer::direct)
       .def("stream_priority", &BucketReducer::stream_priority)
+      .def("ipc_export", &BucketReducer::ipc_export)
+      .def("ipc_open", &BucketReducer::ipc_open)
+      .def("ipc_ready", &BucketReducer::ipc_ready)
+      .def("ipc_error", &BucketReducer::ipc_error)
       .def("mark_ready", &BucketReducer::mark_ready, pybind11::call_guard<pybind11::gil_scoped_release>())
       .def("finalize", &BucketReducer::finalize, pybind11::call_guard<pybind11::gil_scoped_release>())
       .def("reduce_all", &BucketReducer::reduce_all, pybind11::call_guard<pybind11::gil_scoped_release>())

@@ -7,6 +7,21 @@
 
 namespace dpa {
 
+// ---- ipc_allreduce.hip: direct xGMI all-reduce over IPC-mapped peer buffers ----
+constexpr int IPC_MAXW = 8;
+struct IpcPeers {            // per rank: staging buffer (2 parity halves of `cap` floats) and flags
+  float* stage[IPC_MAXW];
+  uint32_t* flags[IPC_MAXW];
+};
+struct IpcData {             // in/out buffer of each (simulated) rank; real runs use p[rank]
+  float* p[IPC_MAXW];
+};
+constexpr int64_t IPC_FLAG_WORDS = 4 * 1024;  // [2 parity][2 phase][IPC_NBMAX]
+int ipc_allreduce_blocks(int64_t n, int W, bool two_shot);
+// sim_ranks == W: one launch plays all W ranks on one device (tests); 1: this rank only.
+bool launch_ipc_allreduce(const IpcPeers& peers, const IpcData& data, int W, int rank, int sim_ranks,
+                          int64_t n, int64_t cap, uint32_t epoch, bool two_shot, int* err, hipStream_t s);
+
 // ---- optim.hip -------------------------------------------------------------
 void launch_sqnorm(const void* g, bool g_bf16, int64_t n, float* partial, int nparts, float scale,
                    float max_norm, float* out, hipStream_t s);

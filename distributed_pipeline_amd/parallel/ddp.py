@@ -173,6 +173,13 @@ class DDPEngine(nn.Module):
                                                  self.grad_shard if self.sharded else None,
                                                  [c[2] for c in self.shard_chunks], uid, self.rank,
                                                  self.world_size)
+                # opt-in: the direct xGMI all-reduce over IPC-mapped peer buffers (fp32
+                # all-reduce buckets; csrc/ipc_allreduce.hip) instead of RCCL rings
+                if (uid and os.environ.get("DPA_IPC_ALLREDUCE", "0") == "1" and not self.sharded
+                        and self.reduce_dtype == torch.float32 and 1 < self.world_size <= 8):
+                    blobs = [None] * self.world_size
+                    dist.all_gather_object(blobs, self._native.ipc_export(), group=self.pg)
+                    self._native.ipc_open(blobs)
         if self.distributed:
             self._verify_shapes()
             if broadcast_from_rank0:
