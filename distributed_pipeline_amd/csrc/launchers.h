@@ -81,14 +81,6 @@ bool launch_attn_bwd(const uint16_t* qkv, const uint16_t* out, const uint16_t* d
                      int L, int H, int D, float p, bool causal, uint32_t seed, uint32_t offset,
                      hipStream_t s);
 
-// ---- xent2.hip: E = 128 LDS-DMA pipelined fused linear-CE (used by xent.hip) ----
-bool launch_lxent2_fwd(const uint16_t* x, const uint16_t* W, const uint16_t* b, const int64_t* tgt,
-                       int N, int V, int E, int splits, int vps, float* loss, float* lse,
-                       float* part_m, float* part_s, float* tgt_logit, hipStream_t s);
-bool launch_lxent2_dx(const uint16_t* x, const uint16_t* W, const uint16_t* b, const int64_t* tgt,
-                      const float* lse, const float* dloss, int N, int V, int E, int splits, int vps,
-                      uint16_t* dx, float* dx_acc, hipStream_t s);
-
 // ---- xent_rows.hip: row softmax-CE over materialised logits (wide-E chunked path) ----
 bool launch_xent_rows_fwd(const uint16_t* lg, int64_t ld, int V, const int64_t* tgt, int64_t R,
                           float* loss, float* lse, hipStream_t s);

@@ -412,10 +412,8 @@ static void fwd_impl(const bf16_t* x, const bf16_t* W, const bf16_t* b, const in
   float* pm = ws;
   float* ps = ws + (int64_t)Sx * N;
   float* tl = ws + 2 * (int64_t)Sx * N;
-  if (!launch_lxent2_fwd((const uint16_t*)x, (const uint16_t*)W, (const uint16_t*)b, tgt, N, V, E, Sx,
-                         vps, loss, lse, pm, ps, tl, st))
-    hipLaunchKernelGGL(lxent_fwd_kernel<E>, dim3(tb, Sx), dim3(256), 0, st, x, W, b, tgt, N, V, vps,
-                       loss, lse, pm, ps, tl);
+  hipLaunchKernelGGL(lxent_fwd_kernel<E>, dim3(tb, Sx), dim3(256), 0, st, x, W, b, tgt, N, V, vps, loss,
+                     lse, pm, ps, tl);
   if (Sx > 1)
     hipLaunchKernelGGL(lxent_combine_kernel, dim3((N + 255) / 256), dim3(256), 0, st, pm, ps, tl,
                        tgt, N, V, Sx, loss, lse);
@@ -445,10 +443,8 @@ static void dx_impl(const bf16_t* x, const bf16_t* W, const bf16_t* b, const int
   const int S = dx_acc ? pick_splits(tb, vchunks, 1024) : 1;
   const int vps = ((vchunks + S - 1) / S) * 64;
   const int Sx = (V + vps - 1) / vps;
-  if (!launch_lxent2_dx((const uint16_t*)x, (const uint16_t*)W, (const uint16_t*)b, tgt, lse, dl, N,
-                        V, E, Sx, vps, dx, Sx > 1 ? dx_acc : nullptr, st))
-    hipLaunchKernelGGL(lxent_dx_kernel<E>, dim3(tb, Sx), dim3(256), 0, st, x, W, b, tgt, lse, dl, N,
-                       V, vps, (bf16_t*)dx, Sx > 1 ? dx_acc : nullptr);
+  hipLaunchKernelGGL(lxent_dx_kernel<E>, dim3(tb, Sx), dim3(256), 0, st, x, W, b, tgt, lse, dl, N, V,
+                     vps, (bf16_t*)dx, Sx > 1 ? dx_acc : nullptr);
   if (Sx > 1) {
     const int64_t n = (int64_t)N * E;
     hipLaunchKernelGGL(f32_to_bf16_kernel, dim3((unsigned)((n / 4 + 255) / 256 + 1)), dim3(256), 0,

@@ -216,3 +216,60 @@ def test_fault_injection_marker(tmp_path, monkeypatch):
     tr._maybe_inject_fault(1, str(tmp_path))
     tr._maybe_inject_fault(1, str(tmp_path))
     assert exits == [17]
+
+
+def test_native_engine_rejects_frozen_parameters(tmp_path):
+    """the fused optimizer/EMA state covers trainable parameters only, while
+    opt_*.pt / ema_*.pt index model.parameters(): a frozen parameter is refused up front."""
+    logger.configure(dir=str(tmp_path), format_strs=["log"])
+    model = create_model_from_config(**SETTINGS)
+    next(model.parameters()).requires_grad_(False)
+    data = load_data_from_args("train", "x", 8, deterministic=True, loop=True, num_loader_proc=0,
+                               dataset="synthetic", seq_len=16, vocab_size=512, seed=0)
+    diffusion, sampler = create_diffusion_from_config(diffusion_steps=50)
+    with pytest.raises(ValueError, match="frozen"):
+        DiffusionTrainLoop(diffusion=diffusion, schedule_sampler=sampler, model=model, data=data,
+                           batch_size=8, microbatch=4, lr=1e-2, ema_rate="0.9", log_interval=1,
+                           save_interval=100, resume_checkpoint="", learning_steps=1,
+                           checkpoint_path=str(tmp_path), ddp_engine="native", precision="fp32")
+
+
+def _sharded_callback_worker(rank, world, port, tmpdir, q):
+    import torch.distributed as dist
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        seen = []
+
+        def callback(trainer):  # reference-style sampling callback: reads the EMA on rank 0 only
+            seen.append(float(sum(p.double().sum() for p in trainer.ema_params[0])))
+
+        eval_data = load_data_from_args("valid", "x", 8, deterministic=True, loop=True,
+                                        num_loader_proc=0, dataset="synthetic", seq_len=16,
+                                        vocab_size=512, seed=1)
+        loop = _loop(os.path.join(tmpdir, str(rank)), "native", steps=3, save_interval=100,
+                     shard_optimizer=True, eval_data=eval_data, eval_interval=1,
+                     eval_callbacks=[callback])
+        loop.run_loop()
+        q.put((rank, len(seen)))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_sharded_ema_readable_from_rank0_callback(tmp_path):
+    """with shard_optimizer the EMA views are a collective; a rank-0-only eval
+    callback reading trainer.ema_params must not hang the other ranks (world 2, gloo)."""
+    import torch.multiprocessing as mp
+    from basic_utils.dist_util import find_free_port
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = find_free_port()
+    procs = [ctx.Process(target=_sharded_callback_worker, args=(r, 2, port, str(tmp_path), q))
+             for r in range(2)]
+    for p in procs:
+        p.start()
+    res = dict(q.get(timeout=240) for _ in range(2))
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    assert res[0] == 3 and res[1] == 0   # the callback ran on rank 0 at every eval step

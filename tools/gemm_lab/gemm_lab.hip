@@ -17,6 +17,14 @@
 
 #include "gemm256.hip"
 
+namespace dpa {
+int device_cu_count() {
+  int n = 0;
+  (void)hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, 0);
+  return n;
+}
+}  // namespace dpa
+
 
 #define CK(x)                                                                      \
   do {                                                                             \
@@ -195,9 +203,12 @@ int main(int argc, char** argv) {
   CK(hipMalloc(&C, maxC * 2));
   CK(hipMalloc(&Z, maxC * 2));
   CK(hipMalloc(&bias, 4096 * 2));
+  float* DW;
+  CK(hipMalloc(&DW, 3072LL * 3072 * 4));
   hipLaunchKernelGGL(fill_rand, dim3(4096), dim3(256), 0, 0, A, maxA, 1u, 1.f);
   hipLaunchKernelGGL(fill_rand, dim3(4096), dim3(256), 0, 0, B, maxB, 2u, 0.05f);
   hipLaunchKernelGGL(fill_rand, dim3(16), dim3(256), 0, 0, bias, (int64_t)4096, 3u, 0.1f);
+  hipLaunchKernelGGL(fill_rand, dim3(4096), dim3(256), 0, 0, Z, maxC, 4u, 1.f);
   CK(hipDeviceSynchronize());
 
   std::vector<Variant> vs;
@@ -244,6 +255,78 @@ int main(int argc, char** argv) {
                       dpa::launch_gemmp_nn(A, B, C, Z, 1, T, N, K, ncu, st, CP);
                     }, fl, {}});
     }
+  }
+  // epilogue cost split: ldc = 0 makes every row of a column band hit the same L2 lines
+  // (stores still issue, the HBM drain is ~gone) - issue/VALU cost vs drain cost
+  {
+    const int K = 768, N = 3072;
+    const double fl = 2.0 * T * K * N;
+    const int grid = std::min((T / 256) * (N / 256), ncu);
+    vs.push_back({"ffn_in/fwd_gp_ldc0", [=](hipStream_t st) {
+                    hipLaunchKernelGGL((dpa::g256::gemmp_kernel<false, 0, 0>), dim3(grid), dim3(512), 0, st,
+                                       (const dpa::bf16_t*)A, (int64_t)K, (const dpa::bf16_t*)B, (int64_t)K, T, N,
+                                       K / 64, (dpa::bf16_t*)C, (int64_t)0, (const dpa::bf16_t*)bias,
+                                       (dpa::bf16_t*)nullptr, (float*)nullptr);
+                  }, fl, {}});
+    vs.push_back({"ffn_in/fwd_gelu_z_gp_ldc0", [=](hipStream_t st) {
+                    hipLaunchKernelGGL((dpa::g256::gemmp_kernel<false, 2, 1>), dim3(grid), dim3(512), 0, st,
+                                       (const dpa::bf16_t*)A, (int64_t)K, (const dpa::bf16_t*)B, (int64_t)K, T, N,
+                                       K / 64, (dpa::bf16_t*)C, (int64_t)0, (const dpa::bf16_t*)bias,
+                                       (dpa::bf16_t*)Z, (float*)nullptr);
+                  }, fl, {}});
+    vs.push_back({"ffn_in/fwd_z_noact_gp_ldc0", [=](hipStream_t st) {
+                    hipLaunchKernelGGL((dpa::g256::gemmp_kernel<false, 2, 0>), dim3(grid), dim3(512), 0, st,
+                                       (const dpa::bf16_t*)A, (int64_t)K, (const dpa::bf16_t*)B, (int64_t)K, T, N,
+                                       K / 64, (dpa::bf16_t*)C, (int64_t)0, (const dpa::bf16_t*)bias,
+                                       (dpa::bf16_t*)Z, (float*)nullptr);
+                  }, fl, {}});
+    vs.push_back({"ffn_in/fwd_z_noact_gp", [=](hipStream_t st) {
+                    hipLaunchKernelGGL((dpa::g256::gemmp_kernel<false, 2, 0>), dim3(grid), dim3(512), 0, st,
+                                       (const dpa::bf16_t*)A, (int64_t)K, (const dpa::bf16_t*)B, (int64_t)K, T, N,
+                                       K / 64, (dpa::bf16_t*)C, (int64_t)N, (const dpa::bf16_t*)bias,
+                                       (dpa::bf16_t*)Z, (float*)nullptr);
+                  }, fl, {}});
+    vs.push_back({"ffn_out/dgrad_dact_noact_gp_ldc0", [=](hipStream_t st) {
+                    hipLaunchKernelGGL((dpa::g256::gemmp_kernel<true, 3, 0>), dim3(grid), dim3(512), 0, st,
+                                       (const dpa::bf16_t*)A, (int64_t)768, (const dpa::bf16_t*)B, (int64_t)3072, T,
+                                       3072, 768 / 64, (dpa::bf16_t*)C, (int64_t)0, (const dpa::bf16_t*)nullptr,
+                                       (dpa::bf16_t*)Z, (float*)nullptr);
+                  }, fl, {}});
+    // dgrad of ffn_out with dgelu: dh[T][3072] = dy[T][768] . W2[768][3072] * gelu'(z)
+    vs.push_back({"ffn_out/dgrad_dgelu_gp_ldc0", [=](hipStream_t st) {
+                    hipLaunchKernelGGL((dpa::g256::gemmp_kernel<true, 3, 1>), dim3(grid), dim3(512), 0, st,
+                                       (const dpa::bf16_t*)A, (int64_t)768, (const dpa::bf16_t*)B, (int64_t)3072, T,
+                                       3072, 768 / 64, (dpa::bf16_t*)C, (int64_t)0, (const dpa::bf16_t*)nullptr,
+                                       (dpa::bf16_t*)Z, (float*)nullptr);
+                  }, fl, {}});
+    vs.push_back({"ffn_out/dgrad_nostore_g256", [=](hipStream_t st) {
+                    hipLaunchKernelGGL((dpa::g256::gemm256_kernel<false, true, dpa::g256::EPI_NONE>),
+                                       dim3((T / 256) * (3072 / 256)), dim3(512), 0, st, (const dpa::bf16_t*)A,
+                                       (int64_t)768, (const dpa::bf16_t*)B, (int64_t)3072, T, 3072, 768 / 64,
+                                       768 / 64, 1, (dpa::bf16_t*)C, (int64_t)3072, nullptr, nullptr, 0, nullptr,
+                                       nullptr);
+                  }, fl, {}});
+  }
+  // weight gradients dW[N][K] += dy[T][N]^T . x[T][K] (split-K, fp32 atomics) and the
+  // same grid without the atomic epilogue (main loop with both operands transposed)
+  for (const Shape& sh : shapes) {
+    const int K = sh.K, N = sh.N;
+    const double fl = 2.0 * T * K * N;
+    const std::string nm = sh.name;
+    vs.push_back({nm + "/wgrad", [=](hipStream_t st) {
+                    dpa::launch_gemm256_wgrad(A, Z, DW, nullptr, T, N, K, st);
+                  }, fl, {}});
+    vs.push_back({nm + "/wgrad_nostore", [=](hipStream_t st) {
+                    const int tiles = (N / 256) * (K / 256), ktot = T / 64;
+                    const int splits = std::max(1, (2 * ncu + tiles - 1) / tiles);
+                    int kps = (ktot + splits - 1) / splits;
+                    kps += kps & 1;
+                    const int sp = (ktot + kps - 1) / kps;
+                    hipLaunchKernelGGL((dpa::g256::gemm256_kernel<true, true, dpa::g256::EPI_NONE>),
+                                       dim3(tiles * sp), dim3(512), 0, st, (const dpa::bf16_t*)A, (int64_t)N,
+                                       (const dpa::bf16_t*)Z, (int64_t)K, N, K, ktot, kps, sp, nullptr, (int64_t)K,
+                                       DW, nullptr, 0, nullptr, nullptr);
+                  }, fl, {}});
   }
   {  // per-CU store rate vs number of storing CUs (each WG writes 36 tiles of 128 KiB)
     const int N = 2304;

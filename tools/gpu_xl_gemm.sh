@@ -5,4 +5,3 @@ cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT" &&
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d /tmp/prof_xl -o run -- python3 bench.py --steps 1 --warmup 1 \
   --config-name diffuseq-xl --batch-size 2048 --microbatch 64 --exec-microbatch 512 > gpurun_out/xl/prof.log 2>&1 &&
 python tools/prof_summary.py /tmp/prof_xl/run_results.db 30 2 > gpurun_out/xl/prof_summary.txt &&
-DPA_XENT2=1 timeout -k 10 300 python bench.py --steps 10 --warmup 2 > gpurun_out/xl/bench_xent2.log 2>&1

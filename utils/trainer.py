@@ -210,6 +210,12 @@ class TrainLoop:
         from distributed_pipeline_amd.parallel.optimizer import FusedAdamW
         from distributed_pipeline_amd.parallel.zero import ZeroFusedAdamW
         shadow = torch.bfloat16 if self.precision == "bf16" else None
+        frozen = [n for n, p in self.model.named_parameters() if not p.requires_grad]
+        if frozen:
+            # the fused optimizer / EMA state is laid out over the trainable parameters,
+            # while opt_*.pt / ema_*.pt index the full model.parameters() list
+            raise ValueError(f"ddp_engine='native' needs every parameter trainable (frozen: "
+                             f"{frozen[:4]}{'...' if len(frozen) > 4 else ''}); use ddp_engine='torch'")
         self.ddp_model = DDPEngine(
             self.model, device=self.device, bucket_cap_mb=bucket_cap_mb,
             first_bucket_mb=first_bucket_mb, shadow_dtype=shadow,
@@ -234,9 +240,15 @@ class TrainLoop:
         """Per-rate lists of EMA tensors (model.parameters() order).  Native engine:
         views of the fused optimizer's flat EMA buffers; with ``shard_optimizer`` each
         access gathers the shards (a collective: call it on every rank)."""
+        if getattr(self, "_ema_snapshot", None) is not None:
+            return self._ema_snapshot
         if self.engine_kind == "native" and getattr(self, "opt", None) is not None:
             return [self.opt.ema_params(i) for i in range(len(self.ema_rate))]
         return self._ema_params
+
+    def _ema_is_collective(self):
+        return (self.engine_kind == "native" and getattr(self, "ddp_model", None) is not None
+                and getattr(self.ddp_model, "sharded", False))
 
     @ema_params.setter
     def ema_params(self, value):
@@ -323,9 +335,18 @@ class TrainLoop:
                 self.forward_only(cond_eval)
                 print('eval on validation set')
                 logger.dumpkvs()
-                if dist_util.get_rank() == 0:
-                    for callback in self.eval_callbacks:
-                        callback(self)
+                if self.eval_callbacks:
+                    # With shard_optimizer the EMA views are gathered by a collective:
+                    # take them on EVERY rank here, so a reference-style callback that
+                    # reads trainer.ema_params on rank 0 alone cannot hang the others.
+                    snap = self.ema_params if self._ema_is_collective() else None
+                    if dist_util.get_rank() == 0:
+                        self._ema_snapshot = snap
+                        try:
+                            for callback in self.eval_callbacks:
+                                callback(self)
+                        finally:
+                            self._ema_snapshot = None
             if self.step > 0 and self.step % self.save_interval == 0:
                 self.save()
             self.step += 1
