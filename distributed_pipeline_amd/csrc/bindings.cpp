@@ -159,7 +159,9 @@ static std::vector<at::Tensor> lxent_bwd(const at::Tensor& dloss, const at::Tens
 // ---- fused dropout + residual + LayerNorm ------------------------------------------
 static std::vector<at::Tensor> add_ln_fwd(const at::Tensor& y, c10::optional<at::Tensor> res,
                                           const at::Tensor& g, const at::Tensor& b, double p,
-                                          double eps, int64_t seed, int64_t offset) {
+                                          double eps, int64_t seed, int64_t offset,
+                                          c10::optional<at::Tensor> pos, c10::optional<at::Tensor> temb,
+                                          int64_t L, bool post) {
   CHECK_DEV(y); CHECK_BF16(y); CHECK_CONTIG(y); CHECK_BF16(g); CHECK_BF16(b);
   TORCH_CHECK(y.dim() == 2, "y must be [R, D]");
   const int64_t R = y.size(0);
@@ -171,6 +173,19 @@ static std::vector<at::Tensor> add_ln_fwd(const at::Tensor& y, c10::optional<at:
     TORCH_CHECK(res->sizes() == y.sizes(), "residual shape");
     rp = bf_ptr(*res);
   }
+  // row-broadcast terms: pos [L, D] (row % L), temb [R / L, D] (row / L)
+  const uint16_t* pp = nullptr;
+  const uint16_t* tp = nullptr;
+  if (pos.has_value() && pos->defined()) {
+    CHECK_BF16((*pos)); CHECK_CONTIG((*pos));
+    TORCH_CHECK(L > 0 && R % L == 0 && pos->numel() == L * D, "pos must be [L, D] with R % L == 0");
+    pp = bf_ptr(*pos);
+  }
+  if (temb.has_value() && temb->defined()) {
+    CHECK_BF16((*temb)); CHECK_CONTIG((*temb));
+    TORCH_CHECK(L > 0 && R % L == 0 && temb->numel() == (R / L) * D, "temb must be [R / L, D]");
+    tp = bf_ptr(*temb);
+  }
   const c10::DeviceGuard guard(y.device());
   at::Tensor out = at::empty_like(y), hs = at::empty_like(y);
   auto f32 = y.options().dtype(at::kFloat);
@@ -179,7 +194,7 @@ static std::vector<at::Tensor> add_ln_fwd(const at::Tensor& y, c10::optional<at:
                                    reinterpret_cast<uint16_t*>(out.data_ptr()),
                                    reinterpret_cast<uint16_t*>(hs.data_ptr()), mean.data_ptr<float>(),
                                    rstd.data_ptr<float>(), R, D, (float)p, (float)eps,
-                                   (uint32_t)seed, (uint32_t)offset, cur_stream());
+                                   (uint32_t)seed, (uint32_t)offset, cur_stream(), pp, tp, (int)L, post);
   TORCH_CHECK(ok, "add_ln_fwd: unsupported hidden size ", D);
   return {out, hs, mean, rstd};
 }
@@ -188,8 +203,14 @@ static std::vector<at::Tensor> add_ln_bwd(const at::Tensor& dout, const at::Tens
                                           const at::Tensor& mean, const at::Tensor& rstd,
                                           const at::Tensor& g, double p, int64_t seed,
                                           int64_t offset, bool need_dres, bool need_dy,
-                                          bool want_dyb) {
+                                          bool want_dyb, c10::optional<at::Tensor> dh_in, bool post) {
   CHECK_DEV(dout); CHECK_BF16(dout); CHECK_CONTIG(dout); CHECK_BF16(hs); CHECK_CONTIG(hs);
+  const uint16_t* dhp = nullptr;
+  if (dh_in.has_value() && dh_in->defined()) {
+    CHECK_BF16((*dh_in)); CHECK_CONTIG((*dh_in));
+    TORCH_CHECK(dh_in->sizes() == dout.sizes(), "dh_in shape");
+    dhp = bf_ptr(*dh_in);
+  }
   const int64_t R = dout.size(0);
   const int D = (int)dout.size(1);
   const c10::DeviceGuard guard(dout.device());
@@ -208,7 +229,7 @@ static std::vector<at::Tensor> add_ln_bwd(const at::Tensor& dout, const at::Tens
       need_dy ? reinterpret_cast<uint16_t*>(dy.data_ptr()) : nullptr,
       dyb.defined() ? dyb.data_ptr<float>() : nullptr,
       dg.data_ptr<float>(), db.data_ptr<float>(), R, D, (float)p, (uint32_t)seed, (uint32_t)offset,
-      cur_stream());
+      cur_stream(), dhp, post);
   TORCH_CHECK(ok, "add_ln_bwd: unsupported hidden size ", D);
   return {dres, dy, dg, db, dyb};
 }
@@ -566,11 +587,15 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("adamw_ema", &adamw_ema, "fused AdamW + EMA + bf16 shadow refresh");
   m.def("ema_update", &ema_update, "flat EMA update");
   m.def("cast_bf16", &cast_bf16, "flat fp32->bf16");
-  m.def("add_ln_fwd", &add_ln_fwd, "LN(dropout(y)+res) -> (out, hsave, mean, rstd)");
+  m.def("add_ln_fwd", &add_ln_fwd,
+        "LN(dropout(y [+pos] [+temb]) + res) (post: dropout(LN(...))) -> (out, hsave, mean, rstd)",
+        py::arg("y"), py::arg("res"), py::arg("gamma"), py::arg("beta"), py::arg("p"), py::arg("eps"),
+        py::arg("seed"), py::arg("offset"), py::arg("pos") = py::none(), py::arg("temb") = py::none(),
+        py::arg("L") = 1, py::arg("post") = false);
   m.def("add_ln_bwd", &add_ln_bwd, "backward of add_ln_fwd -> (dres, dy, dgamma, dbeta, colsum(dy))",
         py::arg("dout"), py::arg("hsave"), py::arg("mean"), py::arg("rstd"), py::arg("gamma"),
         py::arg("p"), py::arg("seed"), py::arg("offset"), py::arg("need_dres"), py::arg("need_dy"),
-        py::arg("want_dy_colsum") = false);
+        py::arg("want_dy_colsum") = false, py::arg("dh_in") = py::none(), py::arg("post") = false);
   m.def("bias_act_fwd", &bias_act_fwd, "z += bias (in place); y = act(z) -> (z, y)");
   m.def("bias_act_bwd", &bias_act_bwd, "dz = dy*act'(zy); db = colsum(dz) -> (dz, db)");
   m.def("attn_fwd", &attn_fwd, "fused attention forward (head_dim 64/128) -> (out, lse)");

@@ -48,13 +48,15 @@ void launch_lxent_dw(const uint16_t* x, const uint16_t* W, const uint16_t* b, co
 // ---- norm.hip (fused dropout + residual + LayerNorm) ---------------------------
 bool launch_add_ln_fwd(const uint16_t* y, const uint16_t* res, const uint16_t* g, const uint16_t* b,
                        uint16_t* out, uint16_t* hsave, float* mean, float* rstd, int64_t R, int D,
-                       float p, float eps, uint32_t seed, uint32_t off, hipStream_t s);
+                       float p, float eps, uint32_t seed, uint32_t off, hipStream_t s,
+                       const uint16_t* pos = nullptr, const uint16_t* temb = nullptr, int L = 1,
+                       bool post = false);
 int ln_bwd_blocks(int64_t R);
 // dyb (nullable): column sums of dy (the bias gradient of the layer producing y)
 bool launch_add_ln_bwd(const uint16_t* dout, const uint16_t* hsave, const float* mean,
                        const float* rstd, const uint16_t* g, uint16_t* dres, uint16_t* dy, float* dyb,
                        float* dg, float* db, int64_t R, int D, float p, uint32_t seed, uint32_t off,
-                       hipStream_t s);
+                       hipStream_t s, const uint16_t* dh_in = nullptr, bool post = false);
 
 // ---- elementwise.hip (bias + activation epilogues) -------------------------------
 void launch_bias_act_fwd(uint16_t* z, const uint16_t* bias, uint16_t* y, int64_t R, int N, int act,

@@ -1,9 +1,15 @@
-// Fused post-LN residual block epilogue (SURVEY K-M6/K-M9/K-M10):
+// Fused residual / embedding-sum + LayerNorm (SURVEY K-M6/K-M9/K-M10):
 //
-//   h   = dropout_p(y) + residual          (either term optional)
-//   out = LayerNorm(h) * gamma + beta      -> bf16; saves h (bf16), mean, rstd
+//   s   = y + pos[row % L] + temb[row / L]   (pos, temb optional row-broadcast terms)
+//   h   = dropout_p(s) + residual            (pre-dropout; residual optional)
+//   out = LayerNorm(h) * gamma + beta        -> bf16; saves h (bf16), mean, rstd
+//   post mode: h = s + residual, out = dropout_p(LayerNorm(h) * gamma + beta)
 //
-// and its backward (dy, dresidual, dgamma, dbeta) in one pass per row.  One
+// Uses: BERT post-LN sublayers (y = branch output, residual = x); the DiffuSeq input
+// block (y = up-proj, pos, temb = time embedding, post dropout: reference model's
+// Dropout(LayerNorm(...))); GPT-2 pre-LN residual streams (h is the new residual
+// stream, out the next sublayer's LN input; the backward adds h's own incoming
+// gradient dh_in).  Backward (dy, dresidual, dgamma, dbeta) in one pass per row.  One
 // wave64 owns a row: D/64 contiguous elements per lane (D = 768 -> 12), loaded
 // as 8-byte vectors, so a row is one fully coalesced 1.5 KiB transaction and
 // both reductions are a single wave-wide shuffle tree (no LDS, no barriers).
@@ -72,7 +78,8 @@ __global__ void __launch_bounds__(256) add_ln_fwd_kernel(
     const bf16_t* __restrict__ y, const bf16_t* __restrict__ res, const bf16_t* __restrict__ gamma,
     const bf16_t* __restrict__ beta, bf16_t* __restrict__ out, bf16_t* __restrict__ hsave,
     float* __restrict__ mean_out, float* __restrict__ rstd_out, int64_t R, float p, float eps,
-    uint32_t seed, uint32_t offset) {
+    uint32_t seed, uint32_t offset, const bf16_t* __restrict__ pos, const bf16_t* __restrict__ temb,
+    int L, int post) {
   constexpr int D = VEC * 64;
   const int lane = threadIdx.x & 63;
   const int64_t row = (int64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
@@ -80,7 +87,19 @@ __global__ void __launch_bounds__(256) add_ln_fwd_kernel(
   const int col0 = lane * VEC;
   float h[VEC];
   RowIO<VEC>::load(y + row * D + col0, h);
-  if (p > 0.f) {
+  if (pos) {
+    float t[VEC];
+    RowIO<VEC>::load(pos + (row % L) * D + col0, t);
+#pragma unroll
+    for (int i = 0; i < VEC; ++i) h[i] += t[i];
+  }
+  if (temb) {
+    float t[VEC];
+    RowIO<VEC>::load(temb + (row / L) * D + col0, t);
+#pragma unroll
+    for (int i = 0; i < VEC; ++i) h[i] += t[i];
+  }
+  if (p > 0.f && !post) {
     bool keep[VEC];
     dropout_keep<VEC>(seed, offset, row, col0, p, keep);
     const float sc = 1.f / (1.f - p);
@@ -110,6 +129,13 @@ __global__ void __launch_bounds__(256) add_ln_fwd_kernel(
   RowIO<VEC>::load(beta + col0, b);
 #pragma unroll
   for (int i = 0; i < VEC; ++i) o[i] = (h[i] - mean) * rstd * g[i] + b[i];
+  if (p > 0.f && post) {
+    bool keep[VEC];
+    dropout_keep<VEC>(seed, offset, row, col0, p, keep);
+    const float sc = 1.f / (1.f - p);
+#pragma unroll
+    for (int i = 0; i < VEC; ++i) o[i] = keep[i] ? o[i] * sc : 0.f;
+  }
   RowIO<VEC>::store(out + row * D + col0, o);
   if (lane == 0) {
     mean_out[row] = mean;
@@ -124,7 +150,7 @@ __global__ void __launch_bounds__(256) add_ln_bwd_kernel(
     const float* __restrict__ mean_in, const float* __restrict__ rstd_in,
     const bf16_t* __restrict__ gamma, bf16_t* __restrict__ dres, bf16_t* __restrict__ dy,
     float* __restrict__ dyb, float* __restrict__ part_dg, float* __restrict__ part_db, int64_t R,
-    float p, uint32_t seed, uint32_t offset) {
+    float p, uint32_t seed, uint32_t offset, const bf16_t* __restrict__ dh_in, int post) {
   constexpr int D = VEC * 64;
   __shared__ float red[3][4][D];
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
@@ -138,6 +164,12 @@ __global__ void __launch_bounds__(256) add_ln_bwd_kernel(
     float h[VEC], d[VEC];
     RowIO<VEC>::load(hsave + row * D + col0, h);
     RowIO<VEC>::load(dout + row * D + col0, d);
+    if (p > 0.f && post) {
+      bool keep[VEC];
+      dropout_keep<VEC>(seed, offset, row, col0, p, keep);
+#pragma unroll
+      for (int i = 0; i < VEC; ++i) d[i] = keep[i] ? d[i] * sc : 0.f;
+    }
     const float mean = mean_in[row], rstd = rstd_in[row];
     float s1 = 0.f, s2 = 0.f;
 #pragma unroll
@@ -155,9 +187,15 @@ __global__ void __launch_bounds__(256) add_ln_bwd_kernel(
     s2 = wave_sum(s2) * (1.f / D);
 #pragma unroll
     for (int i = 0; i < VEC; ++i) d[i] = rstd * (d[i] - s1 - h[i] * s2);
+    if (dh_in) {
+      float e[VEC];
+      RowIO<VEC>::load(dh_in + row * D + col0, e);
+#pragma unroll
+      for (int i = 0; i < VEC; ++i) d[i] += e[i];
+    }
     if (dres) RowIO<VEC>::store(dres + row * D + col0, d);
     if (dy) {
-      if (p > 0.f) {
+      if (p > 0.f && !post) {
         bool keep[VEC];
         dropout_keep<VEC>(seed, offset, row, col0, p, keep);
 #pragma unroll
@@ -202,17 +240,22 @@ __global__ void __launch_bounds__(256) add_ln_bwd_kernel(
 template <int VEC>
 static void ln_fwd_impl(const uint16_t* y, const uint16_t* res, const uint16_t* g, const uint16_t* b,
                         uint16_t* out, uint16_t* hsave, float* mean, float* rstd, int64_t R, float p,
-                        float eps, uint32_t seed, uint32_t off, hipStream_t s) {
+                        float eps, uint32_t seed, uint32_t off, const uint16_t* pos, const uint16_t* temb,
+                        int L, bool post, hipStream_t s) {
   const unsigned grid = (unsigned)((R + 3) / 4);
   hipLaunchKernelGGL(add_ln_fwd_kernel<VEC>, dim3(grid), dim3(256), 0, s, (const bf16_t*)y,
                      (const bf16_t*)res, (const bf16_t*)g, (const bf16_t*)b, (bf16_t*)out,
-                     (bf16_t*)hsave, mean, rstd, R, p, eps, seed, off);
+                     (bf16_t*)hsave, mean, rstd, R, p, eps, seed, off, (const bf16_t*)pos,
+                     (const bf16_t*)temb, L < 1 ? 1 : L, post ? 1 : 0);
 }
 
 bool launch_add_ln_fwd(const uint16_t* y, const uint16_t* res, const uint16_t* g, const uint16_t* b,
                        uint16_t* out, uint16_t* hsave, float* mean, float* rstd, int64_t R, int D,
-                       float p, float eps, uint32_t seed, uint32_t off, hipStream_t s) {
-  DPA_LN_DISPATCH(D, ln_fwd_impl, y, res, g, b, out, hsave, mean, rstd, R, p, eps, seed, off, s)
+                       float p, float eps, uint32_t seed, uint32_t off, hipStream_t s, const uint16_t* pos,
+                       const uint16_t* temb, int L, bool post) {
+  if ((pos || temb) && (L < 1 || R % L)) return false;
+  DPA_LN_DISPATCH(D, ln_fwd_impl, y, res, g, b, out, hsave, mean, rstd, R, p, eps, seed, off, pos, temb, L,
+                  post, s)
   return true;
 }
 
@@ -225,7 +268,7 @@ template <int VEC>
 static void ln_bwd_impl(const uint16_t* dout, const uint16_t* hsave, const float* mean,
                         const float* rstd, const uint16_t* g, uint16_t* dres, uint16_t* dy,
                         float* dyb, float* dg, float* db, int64_t R, float p, uint32_t seed,
-                        uint32_t off, hipStream_t s) {
+                        uint32_t off, const uint16_t* dh_in, bool post, hipStream_t s) {
   constexpr int D = VEC * 64;
   const int nb = ln_bwd_blocks(R);
   hipMemsetAsync(dg, 0, sizeof(float) * D, s);
@@ -233,15 +276,15 @@ static void ln_bwd_impl(const uint16_t* dout, const uint16_t* hsave, const float
   if (dyb) hipMemsetAsync(dyb, 0, sizeof(float) * D, s);
   hipLaunchKernelGGL(add_ln_bwd_kernel<VEC>, dim3(nb), dim3(256), 0, s, (const bf16_t*)dout,
                      (const bf16_t*)hsave, mean, rstd, (const bf16_t*)g, (bf16_t*)dres, (bf16_t*)dy,
-                     dy ? dyb : nullptr, dg, db, R, p, seed, off);
+                     dy ? dyb : nullptr, dg, db, R, p, seed, off, (const bf16_t*)dh_in, post ? 1 : 0);
 }
 
 bool launch_add_ln_bwd(const uint16_t* dout, const uint16_t* hsave, const float* mean,
                        const float* rstd, const uint16_t* g, uint16_t* dres, uint16_t* dy, float* dyb,
                        float* dg, float* db, int64_t R, int D, float p, uint32_t seed, uint32_t off,
-                       hipStream_t s) {
+                       hipStream_t s, const uint16_t* dh_in, bool post) {
   DPA_LN_DISPATCH(D, ln_bwd_impl, dout, hsave, mean, rstd, g, dres, dy, dyb, dg, db, R, p, seed,
-                  off, s)
+                  off, dh_in, post, s)
   return true;
 }
 

@@ -15,7 +15,6 @@ Parameter names follow DiffuSeq where the structure is the same
 encoder packs Q/K/V into ``input_transformers.layer.N.attn.qkv``.
 """
 import torch
-import torch.nn.functional as F
 from torch import nn
 
 from ..ops import nn as ops
@@ -83,10 +82,9 @@ class TransformerNetModel(nn.Module):
         emb_t = self.time_embed(temb)                                        # [B, H]
         emb_x = self.input_up_proj(x.to(dt))                                 # [B, L, H]
         pos = self.position_embeddings(self.position_ids[:, :L], dt)         # [1, L, H]
-        h = emb_x + pos + emb_t.unsqueeze(1)
-        h = self.LayerNorm(h)
-        if self.training and self.dropout > 0:
-            h = F.dropout(h, self.dropout, True)
+        # Dropout(LayerNorm(emb_x + pos + emb_t)) as one kernel (ops.embed_layernorm)
+        h = ops.embed_layernorm(emb_x, pos, emb_t, self.LayerNorm.weight, self.LayerNorm.bias,
+                                self.dropout, self.LayerNorm.eps, self.training)
         h = self.input_transformers(h)
         return self.output_down_proj(h)
 

@@ -33,12 +33,17 @@ class GPT2LMModel(nn.Module):
     def hidden_states(self, input_ids):
         dt = self.compute_dtype
         B, L = input_ids.shape
-        h = self.wte(input_ids, dt) + self.wpe(self.position_ids[:, :L], dt)
-        if self.training and self.dropout > 0:
-            h = torch.nn.functional.dropout(h, self.dropout, True)
-        for blk in self.h:
-            h = blk(h)
-        return self.ln_f(h)
+        # every residual add (and the embedding sum + dropout) runs fused with the
+        # LayerNorm that reads it: x = x + dropout(branch), a = LN_next(x) in one kernel
+        lns = [blk.ln_1 for blk in self.h] + [self.ln_f]
+        x, a = ops.residual_layernorm(self.wte(input_ids, dt), None, lns[0].weight, lns[0].bias,
+                                      self.dropout, lns[0].eps, self.training,
+                                      pos=self.wpe(self.position_ids[:, :L], dt))
+        for i, blk in enumerate(self.h):
+            x, h = blk(x, a)
+            x, a = ops.residual_layernorm(h, x, lns[i + 1].weight, lns[i + 1].bias, self.dropout,
+                                          lns[i + 1].eps, self.training)
+        return a
 
     def forward(self, input_ids, labels=None):
         """Returns per-token CE [B, L-1] when ``labels`` (shifted internally) are given."""

@@ -144,14 +144,11 @@ class GPT2Block(nn.Module):
         self.mlp_fc = Linear(hidden, 4 * hidden, act="gelu", init_std=init_std)
         self.mlp_proj = Linear(4 * hidden, hidden, init_std=init_std / math.sqrt(2 * n_layers))
 
-    def forward(self, x):
-        h = self.attn_proj(self.attn(self.ln_1(x)))
-        x = _residual_dropout(h, x, self.dropout, self.training)
-        h = ops.mlp(self.ln_2(x), self.mlp_fc, self.mlp_proj)
-        return _residual_dropout(h, x, self.dropout, self.training)
-
-
-def _residual_dropout(h, x, p, training):
-    if training and p > 0:
-        h = torch.nn.functional.dropout(h, p, True)
-    return x + h
+    def forward(self, x, a):
+        """x: residual stream, a = ln_1(x) (produced by the previous fused residual
+        step) -> (x + dropout(attn), MLP branch output); the caller adds that branch
+        fused with the next LayerNorm (ops.residual_layernorm)."""
+        h = self.attn_proj(self.attn(a))
+        x, a = ops.residual_layernorm(h, x, self.ln_2.weight, self.ln_2.bias, self.dropout,
+                                      self.ln_2.eps, self.training)
+        return x, ops.mlp(a, self.mlp_fc, self.mlp_proj)

@@ -531,6 +531,88 @@ class _AddLNFn(torch.autograd.Function):
         return dy, (dres if has_res else None), dw, db, None, None, None, None, None, None
 
 
+class _AddLNExFn(torch.autograd.Function):
+    """(out, h) with h = dropout(y [+ pos] [+ temb]) + residual and out = LN(h) (post:
+    h = y + pos + temb + residual, out = dropout(LN(h))) in one kernel; h is an
+    output of its own (the pre-LN residual stream), whose incoming gradient the
+    backward kernel adds to the LN gradient.  pos: [L, H] broadcast over the batch,
+    temb: [B, H] broadcast over the sequence (their gradients are the batch / sequence
+    sums of dy, reduced in fp32)."""
+
+    @staticmethod
+    def forward(ctx, y, residual, pos, temb, w, b, w16, b16, p, eps, seed, offset, post, L):
+        out, hsave, mean, rstd = get_ext().add_ln_fwd(y, residual, w16, b16, float(p), float(eps), seed,
+                                                      offset, pos, temb, int(L), bool(post))
+        ctx.save_for_backward(hsave, mean, rstd, w16)
+        ctx.cfg = (p, seed, offset, residual is not None, pos is not None, temb is not None, post, L)
+        ctx.set_materialize_grads(False)  # an unused h (last layer, input block) costs nothing
+        return out, hsave
+
+    @staticmethod
+    def backward(ctx, dout, dh):
+        hsave, mean, rstd, w16 = ctx.saved_tensors
+        p, seed, offset, has_res, has_pos, has_temb, post, L = ctx.cfg
+        ng = ctx.needs_input_grad
+        need_dy = ng[0] or (has_pos and ng[2]) or (has_temb and ng[3])
+        if dout is None:
+            dout = torch.zeros_like(hsave)
+        dres, dy, dw, db, _ = get_ext().add_ln_bwd(
+            dout.contiguous(), hsave, mean, rstd, w16, float(p), seed, offset, has_res and ng[1], need_dy,
+            False, dh_in=None if dh is None else dh.contiguous(), post=bool(post))
+        dpos = dtemb = None
+        if need_dy:
+            H = dy.shape[-1]
+            d3 = dy.view(-1, L, H)
+            if has_pos and ng[2]:
+                dpos = torch.sum(d3, 0, dtype=torch.float32).to(dy.dtype)
+            if has_temb and ng[3]:
+                dtemb = torch.sum(d3, 1, dtype=torch.float32).to(dy.dtype)
+        return ((dy if ng[0] else None), (dres if has_res else None), dpos, dtemb, dw, db,
+                None, None, None, None, None, None, None, None)
+
+
+def _add_ln_ex(y, residual, pos, temb, weight, bias, p, eps, training, post):
+    """Shared front of :func:`embed_layernorm` / :func:`residual_layernorm` -> (out, h)."""
+    p = p if training else 0.0
+    B, L, H = y.shape
+    if (y.dtype == torch.bfloat16 and native_ok(y, kernel="add_ln_fwd") and H % 64 == 0 and H <= 2048):
+        seed, off = RNG.next()
+        out, h = _AddLNExFn.apply(
+            y.reshape(-1, H).contiguous(),
+            None if residual is None else residual.reshape(-1, H).contiguous(),
+            None if pos is None else pos.reshape(L, H).to(y.dtype).contiguous(),
+            None if temb is None else temb.reshape(B, H).to(y.dtype).contiguous(),
+            weight, bias, shadow(weight, y.dtype), shadow(bias, y.dtype), p, eps, seed, off, post, L)
+        return out.view(B, L, H), h.view(B, L, H)
+    s_ = y
+    if pos is not None:
+        s_ = s_ + pos.reshape(1, L, H).to(y.dtype)
+    if temb is not None:
+        s_ = s_ + temb.reshape(B, 1, H).to(y.dtype)
+    h = F.dropout(s_, p, True) if (p > 0 and not post) else s_
+    if residual is not None:
+        h = h + residual
+    out = (F.layer_norm(h, (H,), weight, bias, eps) if h.dtype == torch.float32
+           else _LNTorchFn.apply(h, weight, bias, eps))
+    if p > 0 and post:
+        out = F.dropout(out, p, True)
+    return out, h
+
+
+def embed_layernorm(y, pos, temb, weight, bias, p=0.0, eps=1e-12, training=True):
+    """dropout(LN(y + pos + temb)): the DiffuSeq input block (reference model:
+    ``Dropout(LayerNorm(up_proj(x) + pos_emb + time_emb))``) in one kernel.
+    y: [B, L, H]; pos: [1, L, H] / [L, H]; temb: [B, H]."""
+    return _add_ln_ex(y, None, pos, temb, weight, bias, p, eps, training, post=True)[0]
+
+
+def residual_layernorm(h, x, weight, bias, p=0.0, eps=1e-5, training=True, pos=None):
+    """Pre-LN residual step -> (x_new, LN(x_new)) with x_new = x + dropout(h [+ pos])
+    (x may be None: the GPT-2 input, h = token + position embeddings)."""
+    ln, xn = _add_ln_ex(h, x, pos, None, weight, bias, p, eps, training, post=False)
+    return xn, ln
+
+
 class RNG:
     """Device-resident (seed, offset) for the in-kernel Philox streams.
 

@@ -86,3 +86,27 @@ def test_fused_sublayers_match_composed_ops_with_dropout(monkeypatch):
     for n in g_c:
         scale = g_c[n].abs().max().item() + 1e-6
         assert (g_f[n] - g_c[n]).abs().max().item() / scale < 3e-2, n
+
+
+def test_gpt2_native_bf16_matches_fp32():
+    """GPT-2 (pre-LN) with every residual add fused into the next LayerNorm
+    (ops.residual_layernorm, VERDICT r1 #6) against the same weights in fp32 torch ops."""
+    torch.manual_seed(0)
+    cfg = dict(model="gpt2", config_name="tiny", hidden_size=256, num_layers=2, num_heads=4,
+               vocab_size=3000, seq_len=256, dropout=0.0)
+    ref = build_model(precision="fp32", **cfg).cuda()
+    nat = build_model(precision="bf16", **cfg).cuda()
+    nat.load_state_dict(ref.state_dict())
+    eng = DDPEngine(nat, shadow_dtype=torch.bfloat16)
+    ids = torch.randint(1000, 3000, (4, 256), device="cuda")
+    lr = ref(ids, labels=ids).float()
+    lr.mean().backward()
+    ln = eng(ids, labels=ids).float()
+    ln.mean().backward()
+    torch.testing.assert_close(ln.mean(), lr.mean(), rtol=2e-2, atol=2e-2)
+    gr, gn = _grads(ref), _grads(nat)
+    assert set(gr) == set(gn)
+    for n in gr:
+        scale = gr[n].abs().max().item() + 1e-6
+        err = (gn[n] - gr[n]).abs().max().item() / scale
+        assert err < 6e-2, (n, err)

@@ -78,3 +78,81 @@ def test_linear_bias_act_autograd(act):
     torch.testing.assert_close(x.grad.float(), xr.grad, rtol=3e-2, atol=3e-2 * xr.grad.abs().max().item())
     torch.testing.assert_close(w.grad, wr.grad, rtol=3e-2, atol=3e-2 * wr.grad.abs().max().item())
     torch.testing.assert_close(b.grad, br.grad, rtol=3e-2, atol=3e-2 * br.grad.abs().max().item())
+
+
+def _ln_params(D):
+    w = torch.nn.Parameter(1 + 0.1 * torch.randn(D, device="cuda"))
+    b = torch.nn.Parameter(0.1 * torch.randn(D, device="cuda"))
+    return w, b
+
+
+@pytest.mark.parametrize("p", [0.0, 0.1])
+def test_embed_layernorm_matches_torch(p):
+    """DiffuSeq input block dropout(LN(y + pos + temb)) in one kernel vs fp32 torch (the
+    dropout mask is read off the kernel's output zeros and applied to the reference)."""
+    torch.manual_seed(0)
+    B, L, D = 16, 128, 768
+    y = torch.randn(B, L, D, device="cuda").bfloat16().requires_grad_(True)
+    pos = (0.5 * torch.randn(1, L, D, device="cuda")).bfloat16().requires_grad_(True)
+    temb = (0.5 * torch.randn(B, D, device="cuda")).bfloat16().requires_grad_(True)
+    w, b = _ln_params(D)
+    out = ops.embed_layernorm(y, pos, temb, w, b, p, 1e-12, True)
+    keep = (out != 0).float()
+    if p > 0:
+        assert abs(keep.mean().item() - (1 - p)) < 0.01
+    yr, pr, tr = (t.detach().float().requires_grad_(True) for t in (y, pos, temb))
+    wr, br = (t.detach().clone().requires_grad_(True) for t in (w, b))
+    h = (yr + pr + tr[:, None]).bfloat16().float()  # the kernel rounds h to bf16
+    ref = torch.nn.functional.layer_norm(h, (D,), wr, br, 1e-12) * keep / (1 - p)
+    torch.testing.assert_close(out.float(), ref, rtol=2e-2, atol=3e-2)
+    g = torch.randn_like(ref)
+    out.backward(g.bfloat16())
+    ref.backward(g.bfloat16().float())
+    torch.testing.assert_close(y.grad.float(), yr.grad, rtol=2e-2, atol=2e-2)
+    torch.testing.assert_close(pos.grad.float(), pr.grad, rtol=2e-2, atol=2e-2 * pr.grad.abs().max().item())
+    torch.testing.assert_close(temb.grad.float(), tr.grad, rtol=2e-2, atol=2e-2 * tr.grad.abs().max().item())
+    torch.testing.assert_close(w.grad, wr.grad, rtol=1e-2, atol=1e-2 * wr.grad.abs().max().item())
+    torch.testing.assert_close(b.grad, br.grad, rtol=1e-2, atol=1e-2 * br.grad.abs().max().item())
+
+
+def test_residual_layernorm_two_outputs():
+    """Pre-LN step (x_new, LN(x_new)), x_new = x + h: both outputs carry gradient (the
+    kernel adds x_new's own incoming gradient to the LN backward), vs fp32 torch."""
+    torch.manual_seed(0)
+    B, L, D = 8, 256, 768
+    h = torch.randn(B, L, D, device="cuda").bfloat16().requires_grad_(True)
+    x = torch.randn(B, L, D, device="cuda").bfloat16().requires_grad_(True)
+    w, b = _ln_params(D)
+    xn, a = ops.residual_layernorm(h, x, w, b, 0.0, 1e-5, True)
+    hr, xr = h.detach().float().requires_grad_(True), x.detach().float().requires_grad_(True)
+    wr, br = (t.detach().clone().requires_grad_(True) for t in (w, b))
+    xnr = (xr + hr).bfloat16().float()
+    xnr.retain_grad()
+    ar = torch.nn.functional.layer_norm(xnr, (D,), wr, br, 1e-5)
+    torch.testing.assert_close(xn.float(), xnr, rtol=0, atol=0)
+    torch.testing.assert_close(a.float(), ar, rtol=2e-2, atol=2e-2)
+    ga, gx = torch.randn_like(ar).bfloat16(), torch.randn_like(ar).bfloat16()
+    ((a.float() * ga.float()).sum() + (xn.float() * gx.float()).sum()).backward()
+    ((ar * ga.float()).sum() + (xnr * gx.float()).sum()).backward()
+    torch.testing.assert_close(h.grad.float(), hr.grad, rtol=2e-2, atol=3e-2)
+    torch.testing.assert_close(x.grad.float(), xr.grad, rtol=2e-2, atol=3e-2)
+    torch.testing.assert_close(w.grad, wr.grad, rtol=1e-2, atol=1e-2 * wr.grad.abs().max().item())
+
+
+def test_gpt2_input_embedding_dropout_then_ln():
+    """GPT-2 input: x = dropout(wte + wpe) (pre-LN dropout of the SUM), a = ln_1(x)."""
+    torch.manual_seed(0)
+    B, L, D, p = 4, 512, 768, 0.1
+    # strictly positive sum, so x == 0 exactly where dropped (the mask is read off x)
+    e = (torch.randn(B, L, D, device="cuda").abs() + 0.5).bfloat16().requires_grad_(True)
+    pos = (0.1 * torch.rand(1, L, D, device="cuda")).bfloat16()
+    w, b = _ln_params(D)
+    x, a = ops.residual_layernorm(e, None, w, b, p, 1e-5, True, pos=pos)
+    keep = (x != 0).float()
+    assert abs(keep.mean().item() - (1 - p)) < 0.01
+    ref_x = ((e.float() + pos.float()) * keep / (1 - p)).bfloat16().float()
+    torch.testing.assert_close(x.float(), ref_x, rtol=1e-2, atol=1e-2)
+    torch.testing.assert_close(a.float(), torch.nn.functional.layer_norm(x.float(), (D,), w, b, 1e-5),
+                               rtol=2e-2, atol=2e-2)
+    x.float().sum().backward()
+    torch.testing.assert_close(e.grad.float(), keep / (1 - p), rtol=1e-2, atol=1e-2)
