@@ -144,13 +144,15 @@ __global__ void __launch_bounds__(256) add_ln_fwd_kernel(
 }
 
 // grid-stride over rows; block = 4 waves; partial dgamma/dbeta per block.
-template <int VEC>
-__global__ void __launch_bounds__(256) add_ln_bwd_kernel(
+// POST at compile time (the two dropout placements share no loop body) and <= 128 VGPRs
+// (4 waves per SIMD: the LDS reduction buffer allows 4 blocks per CU)
+template <int VEC, bool POST>
+__global__ void __launch_bounds__(256, 4) add_ln_bwd_kernel(
     const bf16_t* __restrict__ dout, const bf16_t* __restrict__ hsave,
     const float* __restrict__ mean_in, const float* __restrict__ rstd_in,
     const bf16_t* __restrict__ gamma, bf16_t* __restrict__ dres, bf16_t* __restrict__ dy,
     float* __restrict__ dyb, float* __restrict__ part_dg, float* __restrict__ part_db, int64_t R,
-    float p, uint32_t seed, uint32_t offset, const bf16_t* __restrict__ dh_in, int post) {
+    float p, uint32_t seed, uint32_t offset, const bf16_t* __restrict__ dh_in) {
   constexpr int D = VEC * 64;
   __shared__ float red[3][4][D];
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
@@ -164,7 +166,7 @@ __global__ void __launch_bounds__(256) add_ln_bwd_kernel(
     float h[VEC], d[VEC];
     RowIO<VEC>::load(hsave + row * D + col0, h);
     RowIO<VEC>::load(dout + row * D + col0, d);
-    if (p > 0.f && post) {
+    if (POST && p > 0.f) {
       bool keep[VEC];
       dropout_keep<VEC>(seed, offset, row, col0, p, keep);
 #pragma unroll
@@ -195,7 +197,7 @@ __global__ void __launch_bounds__(256) add_ln_bwd_kernel(
     }
     if (dres) RowIO<VEC>::store(dres + row * D + col0, d);
     if (dy) {
-      if (p > 0.f && !post) {
+      if (!POST && p > 0.f) {
         bool keep[VEC];
         dropout_keep<VEC>(seed, offset, row, col0, p, keep);
 #pragma unroll
@@ -274,9 +276,14 @@ static void ln_bwd_impl(const uint16_t* dout, const uint16_t* hsave, const float
   hipMemsetAsync(dg, 0, sizeof(float) * D, s);
   hipMemsetAsync(db, 0, sizeof(float) * D, s);
   if (dyb) hipMemsetAsync(dyb, 0, sizeof(float) * D, s);
-  hipLaunchKernelGGL(add_ln_bwd_kernel<VEC>, dim3(nb), dim3(256), 0, s, (const bf16_t*)dout,
-                     (const bf16_t*)hsave, mean, rstd, (const bf16_t*)g, (bf16_t*)dres, (bf16_t*)dy,
-                     dy ? dyb : nullptr, dg, db, R, p, seed, off, (const bf16_t*)dh_in, post ? 1 : 0);
+  if (post)
+    hipLaunchKernelGGL((add_ln_bwd_kernel<VEC, true>), dim3(nb), dim3(256), 0, s, (const bf16_t*)dout,
+                       (const bf16_t*)hsave, mean, rstd, (const bf16_t*)g, (bf16_t*)dres, (bf16_t*)dy,
+                       dy ? dyb : nullptr, dg, db, R, p, seed, off, (const bf16_t*)dh_in);
+  else
+    hipLaunchKernelGGL((add_ln_bwd_kernel<VEC, false>), dim3(nb), dim3(256), 0, s, (const bf16_t*)dout,
+                       (const bf16_t*)hsave, mean, rstd, (const bf16_t*)g, (bf16_t*)dres, (bf16_t*)dy,
+                       dy ? dyb : nullptr, dg, db, R, p, seed, off, (const bf16_t*)dh_in);
 }
 
 bool launch_add_ln_bwd(const uint16_t* dout, const uint16_t* hsave, const float* mean,

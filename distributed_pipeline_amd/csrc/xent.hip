@@ -310,25 +310,44 @@ __global__ void __launch_bounds__(512) lxent_dw_kernel(
 
   const int tbeg = blockIdx.y * t_per_split;
   const int tend = min(N, tbeg + t_per_split);
-  for (int t0 = tbeg; t0 < tend; t0 += 64) {
-    // stage x tile [64 tokens][E] + per-token scalars
-    for (int c = tid; c < 64 * CH; c += 512) {
-      const int row = c / CH, ch = c % CH;
-      const int t = t0 + row;
-      uint4 val = make_uint4(0, 0, 0, 0);
-      if (t < tend) val = *reinterpret_cast<const uint4*>(x + (int64_t)t * E + ch * 8);
-      *reinterpret_cast<uint4*>(xt + swz<ROWB>(row, ch)) = val;
+  // x tile [64 tokens][E] + per-token scalars, register-staged one tile ahead so the
+  // global loads of tile i+1 fly behind the MFMAs of tile i
+  constexpr int PER = 64 * CH / 512;
+  uint4 xr[PER];
+  float r_lse = 0.f, r_g = 0.f;
+  int r_tg = -1;
+  auto load_tile = [&](int t0) {
+#pragma unroll
+    for (int i = 0; i < PER; ++i) {
+      const int c = tid + i * 512;
+      const int t = t0 + c / CH;
+      xr[i] = t < tend ? *reinterpret_cast<const uint4*>(x + (int64_t)t * E + (c % CH) * 8)
+                       : make_uint4(0, 0, 0, 0);
     }
     if (tid < 64) {
       const int t = t0 + tid;
       const bool ok = t < tend;
       const int64_t tg = ok ? target[t] : -1;
       const bool valid = ok && tg >= 0 && tg < V;
-      s_lse[tid] = ok ? lse[t] * LOG2E : 0.f;
-      s_g[tid] = valid ? dloss[t] : 0.f;
-      s_tg[tid] = valid ? (int)tg : -1;
+      r_lse = ok ? lse[t] * LOG2E : 0.f;
+      r_g = valid ? dloss[t] : 0.f;
+      r_tg = valid ? (int)tg : -1;
+    }
+  };
+  if (tbeg < tend) load_tile(tbeg);
+  for (int t0 = tbeg; t0 < tend; t0 += 64) {
+#pragma unroll
+    for (int i = 0; i < PER; ++i) {
+      const int c = tid + i * 512;
+      *reinterpret_cast<uint4*>(xt + swz<ROWB>(c / CH, c % CH)) = xr[i];
+    }
+    if (tid < 64) {
+      s_lse[tid] = r_lse;
+      s_g[tid] = r_g;
+      s_tg[tid] = r_tg;
     }
     __syncthreads();
+    if (t0 + 64 < tend) load_tile(t0 + 64);
 #pragma unroll
     for (int tt = 0; tt < 2; ++tt) {
       f32x16 acc;  // S'[t][v]: rows = tokens, cols = vocab (lane); starts at the bias

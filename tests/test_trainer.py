@@ -273,3 +273,30 @@ def test_sharded_ema_readable_from_rank0_callback(tmp_path):
         p.join(timeout=60)
         assert p.exitcode == 0
     assert res[0] == 3 and res[1] == 0   # the callback ran on rank 0 at every eval step
+
+
+def test_device_prefetcher_passthrough_cpu():
+    from data.prefetch import DevicePrefetcher
+    src = [{"input_ids": torch.full((2, 3), i)} for i in range(3)]
+    got = list(DevicePrefetcher(src, "cpu"))
+    assert [int(b["input_ids"][0, 0]) for b in got] == [0, 1, 2]
+
+
+@pytest.mark.gpu
+def test_device_prefetcher_stages_next_batch_on_side_stream():
+    """SURVEY K-2: batch k+1 is already on the device (copied on the prefetch stream)
+    when batch k is handed out; values survive the compute stream's later allocations."""
+    from data.prefetch import DevicePrefetcher
+    src = [{"input_ids": torch.arange(4096).view(32, 128) + i, "input_mask": torch.ones(32, 128)}
+           for i in range(4)]
+    pf = DevicePrefetcher(src, "cuda")
+    for i in range(4):
+        b = next(pf)
+        assert b["input_ids"].is_cuda and b["input_mask"].is_cuda
+        if i < 3:
+            assert pf._next[0]["input_ids"].is_cuda   # next batch already staged
+        junk = torch.randn(1 << 20, device="cuda")     # allocator churn on the compute stream
+        assert torch.equal(b["input_ids"].cpu(), src[i]["input_ids"]), i
+        del junk
+    with pytest.raises(StopIteration):
+        next(pf)

@@ -118,6 +118,7 @@ class TrainLoop:
             eval_data=None,
             eval_interval=-1,
             eval_callbacks=(),
+            device_prefetch=True,
             # ---- MI355X engine options (all optional) ----
             ddp_engine="native",
             precision="bf16",
@@ -197,6 +198,9 @@ class TrainLoop:
 
         self._load_and_sync_parameters()
         self.device = next(self.model.parameters()).device
+        if device_prefetch and self.device.type == "cuda" and self.data is not None:
+            from data.prefetch import DevicePrefetcher
+            self.data = DevicePrefetcher(self.data, self.device)  # SURVEY K-2
 
         if self.engine_kind == "native":
             self._build_native(bucket_cap_mb, first_bucket_mb, grad_reduce_dtype)
