@@ -20,6 +20,8 @@
 //         (token splits), two 128-B row segments per wave instruction.
 //
 // Out-of-range targets (< 0 or >= V) are ignored (loss 0, no gradient).
+#include <cstdlib>
+
 #include "common.h"
 #include "launchers.h"
 #include "mfma.h"
@@ -76,14 +78,20 @@ __global__ void __launch_bounds__(256) lxent_fwd_kernel(
     const bf16_t* __restrict__ x, const bf16_t* __restrict__ W, const bf16_t* __restrict__ bias,
     const int64_t* __restrict__ target, int N, int V, int v_per_split, float* __restrict__ loss,
     float* __restrict__ lse_out, float* __restrict__ part_m, float* __restrict__ part_s,
-    float* __restrict__ tgt_logit) {
+    float* __restrict__ tgt_logit, int xsplit) {
   constexpr int KS = E / 16, ROWB = E * 2;
   __shared__ __attribute__((aligned(16))) char smem[64 * ROWB + 64 * 4];
   char* wt = smem;
   float* bt = reinterpret_cast<float*>(smem + 64 * ROWB);
 
+  // xsplit > 1: vocabulary split s = blockIdx.x % xsplit, i.e. (with the round-robin
+  // workgroup -> XCD dispatch) every XCD sweeps only its 1/8 of W, which then stays
+  // resident in that XCD's L2 instead of streaming all of W from the MALL per workgroup
+  const int split = xsplit > 1 ? (int)(blockIdx.x % xsplit) : (int)blockIdx.y;
+  const int tblk = xsplit > 1 ? (int)(blockIdx.x / xsplit) : (int)blockIdx.x;
+  const int nsplit = xsplit > 1 ? xsplit : (int)gridDim.y;
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, h = lane >> 5;
-  const int t = blockIdx.x * 128 + w * 32 + (lane & 31);
+  const int t = tblk * 128 + w * 32 + (lane & 31);
   const bool tok_ok = t < N;
   bf16x8 xf[KS];
 #pragma unroll
@@ -93,7 +101,7 @@ __global__ void __launch_bounds__(256) lxent_fwd_kernel(
   }
   const int64_t tg = tok_ok ? target[t] : -1;
 
-  const int vbeg = blockIdx.y * v_per_split;
+  const int vbeg = split * v_per_split;
   const int vend = min(V, vbeg + v_per_split);
   float m = -1e30f, ssum = 0.f, tl = -INFINITY;
 
@@ -153,14 +161,14 @@ __global__ void __launch_bounds__(256) lxent_fwd_kernel(
   const float S = ssum * fexp2(m - M) + s2 * fexp2(m2 - M);
   tl = fmaxf(tl, tl2);
   if (h == 0 && tok_ok) {
-    if (gridDim.y == 1) {
+    if (nsplit == 1) {
       const bool valid = tg >= 0 && tg < V;
       const float lse = (M + log2f(S)) * LN2;
       loss[t] = valid ? lse - tl : 0.f;
       lse_out[t] = lse;
     } else {
-      part_m[(int64_t)blockIdx.y * N + t] = M;
-      part_s[(int64_t)blockIdx.y * N + t] = S;
+      part_m[(int64_t)split * N + t] = M;
+      part_s[(int64_t)split * N + t] = S;
       if (tl > -INFINITY) tgt_logit[t] = tl;
     }
   }
@@ -420,28 +428,46 @@ static int pick_splits(int blocks, int chunks, int target_wgs) {
   return s;
 }
 
+// vocabulary splits of the forward: at least 8 (one per XCD, see the kernel) once the
+// vocabulary has 8 x 64 rows, more when there are too few token blocks to fill the chip
+static int fwd_splits(int N, int V) {
+  const int tb = (N + 127) / 128;
+  const int vchunks = (V + 63) / 64;
+  int S = pick_splits(tb, vchunks, 1024);
+  static int xs = -1;
+  if (xs < 0) {
+    const char* e = std::getenv("DPA_XENT_XSPLIT");
+    xs = e ? std::atoi(e) : 8;
+  }
+  if (xs > 1 && vchunks >= xs) S = (S + xs - 1) / xs * xs;
+  return S;
+}
+
 template <int E>
 static void fwd_impl(const bf16_t* x, const bf16_t* W, const bf16_t* b, const int64_t* tgt, int N,
                      int V, float* loss, float* lse, float* ws, hipStream_t st) {
   const int tb = (N + 127) / 128;
   const int vchunks = (V + 63) / 64;
-  const int S = pick_splits(tb, vchunks, 1024);
+  const int S = fwd_splits(N, V);
   const int vps = ((vchunks + S - 1) / S) * 64;
   const int Sx = (V + vps - 1) / vps;
   float* pm = ws;
   float* ps = ws + (int64_t)Sx * N;
   float* tl = ws + 2 * (int64_t)Sx * N;
-  hipLaunchKernelGGL(lxent_fwd_kernel<E>, dim3(tb, Sx), dim3(256), 0, st, x, W, b, tgt, N, V, vps, loss,
-                     lse, pm, ps, tl);
+  if (Sx == 8)  // one split per XCD: 1-D grid, split = blockIdx % 8
+    hipLaunchKernelGGL(lxent_fwd_kernel<E>, dim3(tb * 8), dim3(256), 0, st, x, W, b, tgt, N, V, vps, loss,
+                       lse, pm, ps, tl, 8);
+  else
+    hipLaunchKernelGGL(lxent_fwd_kernel<E>, dim3(tb, Sx), dim3(256), 0, st, x, W, b, tgt, N, V, vps, loss,
+                       lse, pm, ps, tl, 0);
   if (Sx > 1)
     hipLaunchKernelGGL(lxent_combine_kernel, dim3((N + 255) / 256), dim3(256), 0, st, pm, ps, tl,
                        tgt, N, V, Sx, loss, lse);
 }
 
 int64_t lxent_workspace_floats(int N, int V) {
-  const int tb = (N + 127) / 128;
   const int vchunks = (V + 63) / 64;
-  const int S = pick_splits(tb, vchunks, 1024);
+  const int S = fwd_splits(N, V);
   const int vps = ((vchunks + S - 1) / S) * 64;
   const int Sx = (V + vps - 1) / vps;
   return (2 * (int64_t)Sx + 1) * N + 64;
