@@ -241,7 +241,7 @@ __global__ void __launch_bounds__(256) attn_fwd_kernel(const bf16_t* __restrict_
 // register's factor is fetched from the lane that owns that query (one
 // ds_bpermute per register per tile).  K is read once instead of twice.
 template <int D, bool CAUSAL>
-__global__ void __launch_bounds__(256) attn_fwd_online_kernel(const bf16_t* __restrict__ qkv,
+__global__ void __launch_bounds__(256, D == 64 ? 2 : 1) attn_fwd_online_kernel(const bf16_t* __restrict__ qkv,
                                                              bf16_t* __restrict__ out,
                                                              float* __restrict__ lse, int L, int H,
                                                              float p, uint32_t seed, uint32_t offset) {
@@ -284,55 +284,71 @@ __global__ void __launch_bounds__(256) attn_fwd_online_kernel(const bf16_t* __re
       tile_load<D>(kr, kb, ld, kv0 + 64, L, tid);
       tile_load<D>(vr, vb, ld, kv0 + 64, L, tid);
     }
+    // wave-uniform: 32-key subtiles past this wave's last query are skipped outright
+    // (causal), and the element mask runs only on tiles that cross the diagonal or L
+    const int nsub = CAUSAL ? min(2, max(0, (qbase + 31 - kv0) / 32 + 1)) : 2;
+    const bool masked = (CAUSAL && kv0 + 63 > qbase) || kv0 + 64 > L;
     f32x16 acc[2];
     float tmax = -1e30f;
 #pragma unroll
     for (int t = 0; t < 2; ++t) {
       acc[t] = zero16();
+      if (t >= nsub) continue;
 #pragma unroll
       for (int s = 0; s < D / 16; ++s)
         acc[t] = mfma32(lds_frag<2 * D>(kt_lds, t * 32 + (lane & 31), 2 * s + hf), qf[s], acc[t]);
+      if (masked) {
 #pragma unroll
-      for (int i = 0; i < 16; ++i) {
-        const int key = kv0 + t * 32 + acc_row(i, hf);
-        float y = acc[t][i] * att_c<D>();
-        if ((CAUSAL && key > q) || key >= L) y = -INFINITY;
-        acc[t][i] = y;
-        tmax = fmaxf(tmax, y);
+        for (int i = 0; i < 16; ++i) {
+          const int key = kv0 + t * 32 + acc_row(i, hf);
+          if ((CAUSAL && key > q) || key >= L) acc[t][i] = -INFINITY;
+        }
+      }
+#pragma unroll
+      for (int i = 0; i < 16; ++i) tmax = fmaxf(tmax, acc[t][i]);
+    }
+    if (nsub > 0) {
+      // running max in the scaled (exp2) domain; O and l are rescaled only when some
+      // query's max grew by more than 2^8 (lazy rescale: p <= 256 otherwise, exact
+      // in fp32 and bf16), which after the first tiles is almost never
+      tmax = fmaxf(tmax, __shfl_xor(tmax, 32, 64)) * att_c<D>();
+      if (__any(tmax > m + 8.f)) {
+        const float mn = fmaxf(m, tmax);
+        const float alpha = fexp2(m - mn);
+        m = mn;
+        l *= alpha;
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+          const float f = __shfl(alpha, src[i] + 32 * hf, 64);
+#pragma unroll
+          for (int dt = 0; dt < D / 32; ++dt) o[dt][i] *= f;
+        }
+      }
+      float add = 0.f;
+#pragma unroll
+      for (int t = 0; t < 2; ++t) {
+        if (t >= nsub) continue;
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+          float pr = fexp2(fmaf(acc[t][i], att_c<D>(), -m));
+          add += pr;
+          if (dc.on) pr = keep_bit(dc, q, kv0 + t * 32 + acc_row(i, hf)) ? pr * dc.scale : 0.f;
+          acc[t][i] = pr;
+        }
+      }
+      l += add;
+#pragma unroll
+      for (int t = 0; t < 2; ++t) {
+        if (t >= nsub) continue;
+#pragma unroll
+        for (int s = 0; s < 2; ++s) {
+          const bf16x8 af = acc_to_frag(acc[t], s);
+#pragma unroll
+          for (int dt = 0; dt < D / 32; ++dt)
+            o[dt] = mfma32(af, lds_tr_frag<2 * D>(vt_lds, t * 32 + 16 * s, dt * 32, lane), o[dt]);
+        }
       }
     }
-    tmax = fmaxf(tmax, __shfl_xor(tmax, 32, 64));
-    const float mn = fmaxf(m, tmax);
-    const float alpha = fexp2(m - mn);
-    m = mn;
-    float add = 0.f;
-#pragma unroll
-    for (int t = 0; t < 2; ++t)
-#pragma unroll
-      for (int i = 0; i < 16; ++i) {
-        const int key = kv0 + t * 32 + acc_row(i, hf);
-        float pr = fexp2(acc[t][i] - mn);
-        add += pr;
-        if (dc.on) pr = keep_bit(dc, q, key) ? pr * dc.scale : 0.f;
-        acc[t][i] = pr;
-      }
-    l = l * alpha + add;
-    // rescale O rows by their query's alpha
-#pragma unroll
-    for (int i = 0; i < 16; ++i) {
-      const float f = __shfl(alpha, src[i] + 32 * hf, 64);
-#pragma unroll
-      for (int dt = 0; dt < D / 32; ++dt) o[dt][i] *= f;
-    }
-#pragma unroll
-    for (int t = 0; t < 2; ++t)
-#pragma unroll
-      for (int s = 0; s < 2; ++s) {
-        const bf16x8 af = acc_to_frag(acc[t], s);
-#pragma unroll
-        for (int dt = 0; dt < D / 32; ++dt)
-          o[dt] = mfma32(af, lds_tr_frag<2 * D>(vt_lds, t * 32 + 16 * s, dt * 32, lane), o[dt]);
-      }
     __syncthreads();
   }
   l += __shfl_xor(l, 32, 64);
@@ -480,7 +496,7 @@ __global__ void __launch_bounds__(256) attn_delta_kernel(const bf16_t* __restric
 // both straight from the accumulators (dO / Q read transposed from LDS).
 // ---------------------------------------------------------------------------
 template <int D, bool CAUSAL>
-__global__ void __launch_bounds__(256) attn_bwd_kv_kernel(
+__global__ void __launch_bounds__(256, D == 64 ? 2 : 1) attn_bwd_kv_kernel(
     const bf16_t* __restrict__ qkv, const bf16_t* __restrict__ dout, const float* __restrict__ lse,
     const float* __restrict__ delta, bf16_t* __restrict__ dqkv, int L, int H, float p,
     uint32_t seed, uint32_t offset) {
@@ -533,6 +549,11 @@ __global__ void __launch_bounds__(256) attn_bwd_kv_kernel(
     }
 #pragma unroll 1
     for (int qt = 0; qt < 2; ++qt) {
+      const int qs = q0 + qt * 32;
+      // wave-uniform: causal subtiles whose queries all precede this wave's keys are
+      // skipped; the element mask runs only across the diagonal / past L
+      if (CAUSAL && qs + 31 < kbase) continue;
+      const bool masked = (CAUSAL && qs < kbase + 31) || qs + 32 > L || kbase + 32 > L;
       f32x16 sacc = zero16(), dpacc = zero16();
 #pragma unroll
       for (int s = 0; s < D / 16; ++s) {
@@ -543,8 +564,8 @@ __global__ void __launch_bounds__(256) attn_bwd_kv_kernel(
       for (int i = 0; i < 16; ++i) {
         const int r = qt * 32 + acc_row(i, hf);
         const int qq = q0 + r;
-        float pr = fexp2(sacc[i] * att_c<D>() - s_lse[r]);
-        if ((CAUSAL && key > qq) || !k_ok || qq >= L) pr = 0.f;
+        float pr = fexp2(fmaf(sacc[i], att_c<D>(), -s_lse[r]));
+        if (masked && ((CAUSAL && key > qq) || !k_ok || qq >= L)) pr = 0.f;
         float pd = pr, dpd = dpacc[i];
         if (dc.on) {
           const bool kp = keep_bit(dc, qq, key);
@@ -588,7 +609,7 @@ __global__ void __launch_bounds__(256) attn_bwd_kv_kernel(
 // No atomics: each workgroup owns its queries' dQ rows completely.
 // ---------------------------------------------------------------------------
 template <int D, bool CAUSAL>
-__global__ void __launch_bounds__(256) attn_bwd_q_kernel(
+__global__ void __launch_bounds__(256, D == 64 ? 2 : 1) attn_bwd_q_kernel(
     const bf16_t* __restrict__ qkv, const bf16_t* __restrict__ dout, const float* __restrict__ lse,
     const float* __restrict__ delta, bf16_t* __restrict__ dqkv, int L, int H, float p,
     uint32_t seed, uint32_t offset) {
@@ -636,6 +657,10 @@ __global__ void __launch_bounds__(256) attn_bwd_q_kernel(
     }
 #pragma unroll 1
     for (int t = 0; t < 2; ++t) {
+      const int ks = kv0 + t * 32;
+      // wave-uniform subtile skip (all keys after this wave's queries) and diagonal-only mask
+      if (CAUSAL && ks > qbase + 31) continue;
+      const bool masked = (CAUSAL && ks + 31 > qbase) || ks + 32 > L || qbase + 32 > L;
       f32x16 sacc = zero16(), dpacc = zero16();
 #pragma unroll
       for (int s = 0; s < D / 16; ++s) {
@@ -645,8 +670,8 @@ __global__ void __launch_bounds__(256) attn_bwd_q_kernel(
 #pragma unroll
       for (int i = 0; i < 16; ++i) {
         const int kk = kv0 + t * 32 + acc_row(i, hf);
-        float pr = fexp2(sacc[i] * att_c<D>() - lse2);
-        if ((CAUSAL && kk > q) || !q_ok || kk >= L) pr = 0.f;
+        float pr = fexp2(fmaf(sacc[i], att_c<D>(), -lse2));
+        if (masked && ((CAUSAL && kk > q) || !q_ok || kk >= L)) pr = 0.f;
         float dpd = dpacc[i];
         if (dc.on) dpd = keep_bit(dc, q, kk) ? dpd * dc.scale : 0.f;
         sacc[i] = pr * (dpd - dlt);
