@@ -48,7 +48,7 @@ __device__ __forceinline__ DropCfg make_drop(float p, uint32_t seed, uint32_t of
 }
 
 __device__ __forceinline__ bool keep_bit(const DropCfg& d, int q, int key) {
-  const uint32_t h = lowbias32(d.seedmix ^ ((uint32_t)q * 0x9E3779B1u) ^ ((uint32_t)(key >> 1) * 0x85EBCA77u));
+  const uint32_t h = mix32(d.seedmix ^ ((uint32_t)q * 0x9E3779B1u) ^ ((uint32_t)(key >> 1) * 0x85EBCA77u));
   const uint32_t r = (key & 1) ? (h >> 16) : (h & 0xffffu);
   return r >= d.thr16;
 }

@@ -497,10 +497,17 @@ static void emb_qsample_bwd(const at::Tensor& ids, const at::Tensor& mask, const
     else { CHECK_F32((*d_xt)); p_xt32 = d_xt->data_ptr<float>(); }
   }
   const c10::DeviceGuard guard(dW.device());
-  if (n > 0)
+  if (n > 0) {
+    // device sort of the token ids -> runs of equal ids summed in registers (one atomic
+    // per run and column instead of per token and column)
+    at::Tensor sorted, perm;
+    if (E == 128 || E == 256) std::tie(sorted, perm) = at::sort(ids.reshape({-1}));
     dpa::launch_emb_qsample_bwd(ids.data_ptr<int64_t>(), mask.data_ptr<int64_t>(), t.data_ptr<int64_t>(),
                                 sa.data_ptr<float>(), p_xs, p_xs16, p_xt16, p_xt32, B * L, (int)L, (int)E,
-                                (int)dW.size(0), dW.data_ptr<float>(), cur_stream());
+                                (int)dW.size(0), dW.data_ptr<float>(), cur_stream(),
+                                sorted.defined() ? sorted.data_ptr<int64_t>() : nullptr,
+                                perm.defined() ? perm.data_ptr<int64_t>() : nullptr);
+  };
 }
 
 static void check_loss_inputs(const at::Tensor& xs, const at::Tensor& out, const at::Tensor& ids,

@@ -97,7 +97,8 @@ bool launch_emb_qsample_fwd(const int64_t* ids, const int64_t* mask, const int64
 bool launch_emb_qsample_bwd(const int64_t* ids, const int64_t* mask, const int64_t* t, const float* sa,
                             const float* d_xs, const uint16_t* d_xs16, const uint16_t* d_xt16,
                             const float* d_xt32, int64_t NT, int L, int E, int V, float* dW,
-                            hipStream_t s);
+                            hipStream_t s, const int64_t* sorted_ids = nullptr,
+                            const int64_t* perm = nullptr);
 bool launch_diff_loss_fwd(const float* x_start, const void* out, bool out_bf16, const int64_t* ids,
                           const int64_t* t, const float* W, int B, int L, int E, int V, float sa_last,
                           float* mse, float* tT, hipStream_t s);
