@@ -47,10 +47,15 @@ __device__ __forceinline__ DropCfg make_drop(float p, uint32_t seed, uint32_t of
   return d;
 }
 
-__device__ __forceinline__ bool keep_bit(const DropCfg& d, int q, int key) {
-  const uint32_t h = mix32(d.seedmix ^ ((uint32_t)q * 0x9E3779B1u) ^ ((uint32_t)(key >> 1) * 0x85EBCA77u));
+__device__ __forceinline__ uint32_t drop_hash(const DropCfg& d, int q, int key) {
+  return mix32(d.seedmix ^ ((uint32_t)q * 0x9E3779B1u) ^ ((uint32_t)(key >> 1) * 0x85EBCA77u));
+}
+__device__ __forceinline__ bool keep_from(const DropCfg& d, uint32_t h, int key) {
   const uint32_t r = (key & 1) ? (h >> 16) : (h & 0xffffu);
   return r >= d.thr16;
+}
+__device__ __forceinline__ bool keep_bit(const DropCfg& d, int q, int key) {
+  return keep_from(d, drop_hash(d, q, key), key);
 }
 
 // softmax scale in the exp2 domain and the 1/sqrt(D) gradient scale
@@ -560,6 +565,21 @@ __global__ void __launch_bounds__(256, D == 64 ? 2 : 1) attn_bwd_kv_kernel(
         sacc = mfma32(lds_frag<2 * D>(qt_lds, qt * 32 + (lane & 31), 2 * s + hf), kf[s], sacc);
         dpacc = mfma32(lds_frag<2 * D>(dot_lds, qt * 32 + (lane & 31), 2 * s + hf), vf[s], dpacc);
       }
+      // dropout hashes: lanes key and key^1 need the same (query, key pair) hashes, so
+      // each lane of an adjacent pair computes every other one and takes the rest from
+      // its neighbour (DPP quad_perm [1,0,3,2]) - half the quarter-rate multiplies
+      uint32_t hh[16];
+      if (dc.on) {
+        const int par = lane & 1;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const int qa = q0 + qt * 32 + acc_row(2 * j, hf), qb2 = q0 + qt * 32 + acc_row(2 * j + 1, hf);
+          const uint32_t mine = drop_hash(dc, par ? qb2 : qa, key);
+          const uint32_t other = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)mine, 0xB1, 0xF, 0xF, true);
+          hh[2 * j] = par ? other : mine;
+          hh[2 * j + 1] = par ? mine : other;
+        }
+      }
 #pragma unroll
       for (int i = 0; i < 16; ++i) {
         const int r = qt * 32 + acc_row(i, hf);
@@ -568,7 +588,7 @@ __global__ void __launch_bounds__(256, D == 64 ? 2 : 1) attn_bwd_kv_kernel(
         if (masked && ((CAUSAL && key > qq) || !k_ok || qq >= L)) pr = 0.f;
         float pd = pr, dpd = dpacc[i];
         if (dc.on) {
-          const bool kp = keep_bit(dc, qq, key);
+          const bool kp = keep_from(dc, hh[i], key);
           pd = kp ? pr * dc.scale : 0.f;
           dpd = kp ? dpd * dc.scale : 0.f;
         }

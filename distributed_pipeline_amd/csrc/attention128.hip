@@ -54,10 +54,15 @@ __device__ __forceinline__ DropCfg make_drop(float p, uint32_t seed, uint32_t of
   d.seedmix = lowbias32(seed ^ lowbias32(offset * 0xC2B2AE3Du ^ (bh * 0x27D4EB2Fu)));
   return d;
 }
-__device__ __forceinline__ bool keep_bit(const DropCfg& d, int q, int key) {
-  const uint32_t h = mix32(d.seedmix ^ ((uint32_t)q * 0x9E3779B1u) ^ ((uint32_t)(key >> 1) * 0x85EBCA77u));
+__device__ __forceinline__ uint32_t drop_hash(const DropCfg& d, int q, int key) {
+  return mix32(d.seedmix ^ ((uint32_t)q * 0x9E3779B1u) ^ ((uint32_t)(key >> 1) * 0x85EBCA77u));
+}
+__device__ __forceinline__ bool keep_from(const DropCfg& d, uint32_t h, int key) {
   const uint32_t r = (key & 1) ? (h >> 16) : (h & 0xffffu);
   return r >= d.thr16;
+}
+__device__ __forceinline__ bool keep_bit(const DropCfg& d, int q, int key) {
+  return keep_from(d, drop_hash(d, q, key), key);
 }
 
 // ---- LDS access (inline asm) ------------------------------------------------
@@ -404,13 +409,26 @@ __device__ __forceinline__ void bwd_pds(f32x16& sacc, f32x16& dpacc, uint32_t ba
   const f32x4 lv = rdf4o<T * 128 + G * 32>(base + B.stat);
   const f32x4 dl = rdf4o<T * 128 + G * 32 + 512>(base + B.stat);
   lgkm0();
+  // keys key and key^1 sit on adjacent lanes and need the same (query, key pair)
+  // hashes: each lane computes two of the four and swaps for the rest (DPP)
+  uint32_t hh[4];
+  if (dc.on) {
+    const int par = key & 1;
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const uint32_t mine = drop_hash(dc, T * 32 + 8 * G + 4 * hf + 2 * j + par, key);
+      const uint32_t other = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)mine, 0xB1, 0xF, 0xF, true);
+      hh[2 * j] = par ? other : mine;
+      hh[2 * j + 1] = par ? mine : other;
+    }
+  }
 #pragma unroll
   for (int r = 0; r < 4; ++r) {
     const int i = 4 * G + r;
-    const float pr = fexp2(sacc[i] * ATT_C - lv[r]);
+    const float pr = fexp2(fmaf(sacc[i], ATT_C, -lv[r]));
     float pd = pr, dpd = dpacc[i];
     if (dc.on) {
-      const bool kp = keep_bit(dc, T * 32 + 8 * G + 4 * hf + r, key);
+      const bool kp = keep_from(dc, hh[r], key);
       pd = kp ? pr * dc.scale : 0.f;
       dpd = kp ? dpd * dc.scale : 0.f;
     }

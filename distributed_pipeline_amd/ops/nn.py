@@ -756,21 +756,11 @@ def _pad_vocab(w16, b16, mult=256):
 
 
 def _chunk_logits(xc, wp, bp):
-    """[chunk, Vp] logits of one token chunk: the native persistent GEMM when the chunk
-    tiles (Vp is a multiple of 256 by construction), else hipBLASLt."""
-    ext = get_ext(required=False)
-    if ext is not None and xc.shape[0] % 128 == 0 and xc.shape[1] % 128 == 0:
-        return ext.gemm_nt(xc.contiguous(), wp, bp, 0)[0]
+    """[chunk, Vp] logits of one token chunk.  hipBLASLt on purpose: a K = 768 GEMM
+    writing 0.5 GB of bf16 logits per chunk is store-bound, where the persistent
+    kernel's non-overlapped epilogue loses (measured r2: 21 vs 13 ms per GPT-2 step),
+    and the chunk's dx GEMM (output 768 wide, K = Vp) needs split-K."""
     return torch.addmm(bp, xc, wp.t()) if bp is not None else xc @ wp.t()
-
-
-def _chunk_dx(dlg, wp, out):
-    """out = dlogits . W (the chunk's input gradient), native when the chunk tiles."""
-    ext = get_ext(required=False)
-    if ext is not None and dlg.shape[0] % 128 == 0 and wp.shape[1] % 256 == 0:
-        out.copy_(ext.gemm_nn(dlg, wp))
-    else:
-        torch.mm(dlg, wp, out=out)
 
 
 class _ChunkedLinearXentFn(torch.autograd.Function):
@@ -818,7 +808,7 @@ class _ChunkedLinearXentFn(torch.autograd.Function):
             dlg = _chunk_logits(x[s:e], wp, bp)
             ext.xent_rows_bwd_(dlg, V, target[s:e], lse[s:e], dloss[s:e])
             if need_dx:
-                _chunk_dx(dlg, wp, dx[s:e])
+                torch.mm(dlg, wp, out=dx[s:e])
             if need_dw:
                 if native_wgrad and (e - s) % 128 == 0:
                     ext.gemm_wgrad(dlg, x[s:e], dwp, None)   # split-K MFMA, fp32 accumulate
