@@ -777,12 +777,19 @@ class _ChunkedLinearXentFn(torch.autograd.Function):
         wp, bp = _pad_vocab(w16, b16)
         loss = torch.empty(N, dtype=torch.float32, device=x.device)
         lse = torch.empty(N, dtype=torch.float32, device=x.device)
+        # 288 GB of HBM: keep the bf16 logit chunks for the backward (which turns them
+        # into dlogits in place) instead of recomputing them, when they fit the budget
+        keep = any(ctx.needs_input_grad[:3]) and N * wp.shape[0] * 2 <= _XENT_KEEP_BYTES
+        kept = []
         for s in range(0, N, chunk):
             e = min(N, s + chunk)
             lg = _chunk_logits(x[s:e], wp, bp)
             l_c, lse_c = ext.xent_rows_fwd(lg, V, target[s:e])
             loss[s:e].copy_(l_c)
             lse[s:e].copy_(lse_c)
+            if keep:
+                kept.append(lg)
+        ctx.kept = kept if keep else None
         ctx.save_for_backward(x, w16, b16, target, lse)
         ctx.params = (w, b)
         ctx.chunk = chunk
@@ -803,9 +810,12 @@ class _ChunkedLinearXentFn(torch.autograd.Function):
         dwp = torch.zeros(Vp, E, dtype=torch.float32, device=x.device) if need_dw else None
         db = torch.zeros(V, dtype=torch.float32, device=x.device) if need_db else None
         native_wgrad = need_dw and Vp % 256 == 0 and E % 256 == 0 and hasattr(ext, "gemm_wgrad")
-        for s in range(0, N, ctx.chunk):
+        kept, ctx.kept = ctx.kept, None
+        for ci, s in enumerate(range(0, N, ctx.chunk)):
             e = min(N, s + ctx.chunk)
-            dlg = _chunk_logits(x[s:e], wp, bp)
+            dlg = kept[ci] if kept is not None else _chunk_logits(x[s:e], wp, bp)
+            if kept is not None:
+                kept[ci] = None  # freed as soon as its gradient GEMMs are queued
             ext.xent_rows_bwd_(dlg, V, target[s:e], lse[s:e], dloss[s:e])
             if need_dx:
                 torch.mm(dlg, wp, out=dx[s:e])
@@ -822,6 +832,9 @@ class _ChunkedLinearXentFn(torch.autograd.Function):
 
 # tokens per logits chunk of the wide-E path: about 0.5 GiB of bf16 logits
 _XENT_CHUNK_BYTES = int(os.environ.get("DPA_XENT_CHUNK_MB", "512")) << 20
+# logits kept from the forward for the backward (bytes; GPT-2 small at 128 x 1024 tokens
+# needs 13 GB): above this the backward recomputes each chunk
+_XENT_KEEP_BYTES = int(os.environ.get("DPA_XENT_KEEP_GB", "24")) << 30
 
 
 def linear_cross_entropy(x, weight, bias, target):

@@ -60,12 +60,16 @@ def test_linear_cross_entropy_autograd_matches_torch():
     torch.testing.assert_close(x.grad.float(), xr.grad, rtol=2e-2, atol=2e-2 * xr.grad.abs().max().item())
 
 
-@pytest.mark.parametrize("N,V,E,with_bias,chunk_mb", [(1000, 50257, 768, False, 16),
-                                                      (300, 1000, 512, True, 1)])
-def test_chunked_linear_cross_entropy_wide_E(N, V, E, with_bias, chunk_mb, monkeypatch):
+@pytest.mark.parametrize("N,V,E,with_bias,chunk_mb,keep", [(1000, 50257, 768, False, 16, True),
+                                                           (1000, 50257, 768, False, 16, False),
+                                                           (300, 1000, 512, True, 1, True)])
+def test_chunked_linear_cross_entropy_wide_E(N, V, E, with_bias, chunk_mb, keep, monkeypatch):
     """Wide-E path (GPT-2 LM head): hipBLASLt chunk logits + csrc/xent_rows.hip row
-    kernels, several chunks (incl. a ragged last one), ignored targets, padding columns."""
+    kernels, several chunks (incl. a ragged last one), ignored targets, padding columns;
+    logits kept from the forward (keep) or recomputed in the backward."""
     monkeypatch.setattr(ops, "_XENT_CHUNK_BYTES", chunk_mb << 20)
+    if not keep:
+        monkeypatch.setattr(ops, "_XENT_KEEP_BYTES", 0)
     torch.manual_seed(2)
     x = (torch.randn(N, E, device="cuda") * 0.05).bfloat16().requires_grad_(True)
     W = torch.nn.Parameter(torch.randn(V, E, device="cuda") * 0.5)
