@@ -4,7 +4,9 @@
 // Abramowitz-Stegun 7.1.26 rational approximation of erf (|error| < 1.5e-7,
 // far below bf16 resolution): one v_exp_f32 and one v_rcp_f32 instead of the
 // libm erff, and the same exp(-z^2/2) term serves the derivative's pdf.
-// Codes: 0 none, 1 gelu, 2 tanh, 3 silu.
+// Codes: 0 none, 1 gelu, 2 tanh, 3 silu; 4 = "the saved operand already IS act'(z)"
+// (forward epilogues that store the derivative instead of the pre-activation, so the
+// backward epilogue is one multiply instead of a second erf/exp evaluation).
 #pragma once
 #include <hip/hip_runtime.h>
 
@@ -71,10 +73,35 @@ __device__ __forceinline__ f32x2 act2(f32x2 z) {
   }
 }
 
+// act(z) and act'(z) together (the shared erf/exp work done once), two lanes
+template <int ACT>
+__device__ __forceinline__ f32x2 act_dact2(f32x2 z, f32x2& d) {
+  if constexpr (ACT == 1) {
+    f32x2 e;
+    const f32x2 c = phi_cdf2(z, e);
+    d = z * 0.39894228040143268f * e + c;
+    return z * c;
+  } else if constexpr (ACT == 2) {
+    const f32x2 y = {tanhf(z.x), tanhf(z.y)};
+    d = 1.f - y * y;
+    return y;
+  } else if constexpr (ACT == 3) {
+    const f32x2 den = {1.f + fexp(-z.x), 1.f + fexp(-z.y)};
+    const f32x2 sg = {__builtin_amdgcn_rcpf(den.x), __builtin_amdgcn_rcpf(den.y)};
+    d = sg * (z * (1.f - sg) + 1.f);
+    return z * sg;
+  } else {
+    d = f32x2{1.f, 1.f};
+    return z;
+  }
+}
+
 // d act / dz given aux = z (gelu, silu) or y = tanh(z) (tanh), two lanes
 template <int ACT>
 __device__ __forceinline__ f32x2 dact2(f32x2 a) {
-  if constexpr (ACT == 1) {
+  if constexpr (ACT == 4) {
+    return a;
+  } else if constexpr (ACT == 1) {
     f32x2 e;
     const f32x2 c = phi_cdf2(a, e);
     return a * 0.39894228040143268f * e + c;
@@ -107,6 +134,7 @@ __device__ __forceinline__ float act_deriv(float a, int act) {
       const float sg = __builtin_amdgcn_rcpf(1.f + fexp(-a));
       return sg * fmaf(a, 1.f - sg, 1.f);
     }
+    case 4: return a;
     default: return 1.f;
   }
 }

@@ -320,8 +320,9 @@ static std::vector<at::Tensor> attn_bwd(const at::Tensor& dout, const at::Tensor
 }
 
 // ---- GEMMs ---------------------------------------------------------------------------
-static std::vector<at::Tensor> gemm_nt(const at::Tensor& x, const at::Tensor& W,
-                                       c10::optional<at::Tensor> b, int64_t act) {
+static std::tuple<at::Tensor, at::Tensor, bool> gemm_nt(const at::Tensor& x, const at::Tensor& W,
+                                                        c10::optional<at::Tensor> b, int64_t act,
+                                                        bool want_deriv) {
   CHECK_DEV(x); CHECK_BF16(x); CHECK_BF16(W); CHECK_CONTIG(x); CHECK_CONTIG(W);
   const int T = (int)x.size(0), K = (int)x.size(1), N = (int)W.size(0);
   TORCH_CHECK(W.size(1) == K, "gemm_nt: W [N, K]");
@@ -329,12 +330,13 @@ static std::vector<at::Tensor> gemm_nt(const at::Tensor& x, const at::Tensor& W,
   at::Tensor y = at::empty({T, N}, x.options());
   at::Tensor z;
   if (act == 1 || act == 3) z = at::empty({T, N}, x.options());
+  bool deriv = want_deriv && z.defined();
   bool ok = dpa::launch_gemm_nt(bf_ptr(x), bf_ptr(W), opt_bf_ptr(b),
                                 reinterpret_cast<uint16_t*>(y.data_ptr()),
                                 z.defined() ? reinterpret_cast<uint16_t*>(z.data_ptr()) : nullptr, T, N,
-                                K, (int)act, cur_stream());
+                                K, (int)act, cur_stream(), &deriv);
   TORCH_CHECK(ok, "gemm_nt: unsupported shape T=", T, " N=", N, " K=", K);
-  return {y, z};
+  return {y, z, deriv};
 }
 
 static at::Tensor gemm_nn(const at::Tensor& dy, const at::Tensor& W) {
@@ -609,7 +611,10 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("attn_bwd", &attn_bwd, "fused attention backward -> (dqkv, colsum(dqkv) or None)",
         py::arg("dout"), py::arg("qkv"), py::arg("out"), py::arg("lse"), py::arg("heads"), py::arg("p"),
         py::arg("causal"), py::arg("seed"), py::arg("offset"), py::arg("want_db") = false);
-  m.def("gemm_nt", &gemm_nt, "y = act(x W^T + b) (bf16 MFMA) -> (y, z_preact)");
+  m.def("gemm_nt", &gemm_nt,
+        "y = act(x W^T + b) (bf16 MFMA) -> (y, z, z_is_derivative): z is the pre-activation, or "
+        "act'(pre-activation) when want_deriv and the persistent kernel ran (backward act code 4)",
+        py::arg("x"), py::arg("W"), py::arg("b"), py::arg("act"), py::arg("want_deriv") = false);
   m.def("gemm_nn", &gemm_nn, "dx = dy W (bf16 MFMA)");
   m.def("gemm_nn_dact", &gemm_nn_dact,
         "dz = (dy W) * act'(aux) (bf16 MFMA, fused act backward) -> (dz, colsum(dz) fp32 or None)",

@@ -279,9 +279,13 @@ int device_cu_count() {
   return cache[dev];
 }
 
+// zderiv (in/out, nullable): requests act'(pre-activation) in z instead of the
+// pre-activation; reset to false when the kernel that ran stored the pre-activation.
 bool launch_gemm_nt(const uint16_t* x, const uint16_t* W, const uint16_t* bias, uint16_t* y,
-                    uint16_t* z, int T, int N, int K, int act, hipStream_t s) {
-  if (launch_gemmp_nt(x, W, bias, y, z, T, N, K, act, device_cu_count(), s)) return true;
+                    uint16_t* z, int T, int N, int K, int act, hipStream_t s, bool* zderiv) {
+  const bool want_d = zderiv && *zderiv;
+  if (launch_gemmp_nt(x, W, bias, y, z, T, N, K, act, device_cu_count(), s, want_d)) return true;
+  if (zderiv) *zderiv = false;
   if (launch_gemm256_nt(x, W, bias, y, z, T, N, K, act, s)) return true;
   if (!gemm_shape_ok(T, N, K)) return false;
   const int blocks = (T / 128) * (N / 128);

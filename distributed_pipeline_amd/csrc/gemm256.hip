@@ -529,7 +529,7 @@ template <int EPI>
 struct PEpi {
   // VMEM ops each lane issues after the next tile's prologue DMA: 16 stores (8 rounds x 2),
   // EPI 2 a second 16 (z and y), EPI 3/4 the 12 aux loads of rounds 2..7, EPI 4 two partial stores
-  static constexpr int XS = EPI == 2 ? 32 : (EPI == 3 || EPI == 5) ? 28 : EPI == 4 ? 30 : 16;
+  static constexpr int XS = (EPI == 2 || EPI == 6) ? 32 : (EPI == 3 || EPI == 5) ? 28 : EPI == 4 ? 30 : 16;
 };
 
 template <int ACT>
@@ -546,6 +546,22 @@ __device__ __forceinline__ uint4 lds_read_b128_sync(uint32_t addr) {
   u32x4_v v;
   asm volatile("ds_read_b128 %0, %1\n\ts_waitcnt lgkmcnt(0)" : "=v"(v) : "v"(addr) : "memory");
   return make_uint4(v[0], v[1], v[2], v[3]);
+}
+
+// 8 bf16 (one uint4) -> act(z) (returned) and act'(z) (d), on packed float pairs
+template <int ACT>
+__device__ __forceinline__ uint4 act_dact8(const uint4& u, uint4& dv) {
+  const uint32_t w[4] = {u.x, u.y, u.z, u.w};
+  uint32_t o[4], g[4];
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    f32x2 d;
+    const f32x2 y = act_dact2<ACT>(f32x2{__uint_as_float(w[q] << 16), __uint_as_float(w[q] & 0xffff0000u)}, d);
+    o[q] = pack_bf2(y.x, y.y);
+    g[q] = pack_bf2(d.x, d.y);
+  }
+  dv = make_uint4(g[0], g[1], g[2], g[3]);
+  return make_uint4(o[0], o[1], o[2], o[3]);
 }
 
 // 8 bf16 (one uint4) -> act on packed float pairs -> 8 bf16
@@ -719,6 +735,11 @@ __global__ void __launch_bounds__(512) gemmp_kernel(const bf16_t* __restrict__ A
         const int64_t o = row_off(t, ro, k, ln);
         if constexpr (EPI == 2) *reinterpret_cast<uint4*>(Zout + o) = val[k];
         if constexpr (EPI == 1 || EPI == 2) val[k] = act8<ACT>(val[k]);
+        if constexpr (EPI == 6) {
+          uint4 dv;
+          val[k] = act_dact8<ACT>(val[k], dv);
+          *reinterpret_cast<uint4*>(Zout + o) = dv;
+        }
         *reinterpret_cast<uint4*>(C + o) = val[k];
       }
     }
@@ -874,12 +895,17 @@ static void gemmp_go(const uint16_t* a, int64_t lda, const uint16_t* b, int64_t 
                      (const bf16_t*)bias, (bf16_t*)z, colpart);
 }
 
-// y[T][N] = act(x[T][K] . W[N][K]^T + bias); z (nullable, act != 0) = the pre-activation.
+// y[T][N] = act(x[T][K] . W[N][K]^T + bias); z (nullable, act != 0) = the pre-activation,
+// or act'(pre-activation) when zderiv (the backward then multiplies: act code 4).
 bool launch_gemmp_nt(const uint16_t* x, const uint16_t* W, const uint16_t* bias, uint16_t* y,
-                     uint16_t* z, int T, int N, int K, int act, int ncu, hipStream_t s) {
+                     uint16_t* z, int T, int N, int K, int act, int ncu, hipStream_t s, bool zderiv) {
   if (!g256_enabled() || T % 256 || N % 256 || K % 128 || K < 128 || act < 0 || act > 3) return false;
   if (act == 0) gemmp_go<false, 0, 0>(x, K, W, K, T, N, K, y, bias, nullptr, ncu, s);
-  else if (z == nullptr) {
+  else if (z != nullptr && zderiv) {
+    if (act == 1) gemmp_go<false, 6, 1>(x, K, W, K, T, N, K, y, bias, z, ncu, s);
+    else if (act == 2) gemmp_go<false, 6, 2>(x, K, W, K, T, N, K, y, bias, z, ncu, s);
+    else gemmp_go<false, 6, 3>(x, K, W, K, T, N, K, y, bias, z, ncu, s);
+  } else if (z == nullptr) {
     if (act == 1) gemmp_go<false, 1, 1>(x, K, W, K, T, N, K, y, bias, nullptr, ncu, s);
     else if (act == 2) gemmp_go<false, 1, 2>(x, K, W, K, T, N, K, y, bias, nullptr, ncu, s);
     else gemmp_go<false, 1, 3>(x, K, W, K, T, N, K, y, bias, nullptr, ncu, s);
@@ -903,7 +929,7 @@ bool launch_gemmp_nn_acc(const uint16_t* dy, const uint16_t* W, uint16_t* dx, in
 
 bool launch_gemmp_nn(const uint16_t* dy, const uint16_t* W, uint16_t* dx, const uint16_t* aux, int act,
                      int T, int N, int K, int ncu, hipStream_t s, float* colpart) {
-  if (!g256_enabled() || T % 256 || K % 256 || N % 128 || N < 128 || act < 0 || act > 3) return false;
+  if (!g256_enabled() || T % 256 || K % 256 || N % 128 || N < 128 || act < 0 || act > 4) return false;
   uint16_t* ax = const_cast<uint16_t*>(aux);
   if (act == 0 || aux == nullptr) {
     if (colpart) return false;
@@ -911,11 +937,13 @@ bool launch_gemmp_nn(const uint16_t* dy, const uint16_t* W, uint16_t* dx, const 
   } else if (colpart) {
     if (act == 1) gemmp_go<true, 4, 1>(dy, N, W, K, T, K, N, dx, nullptr, ax, ncu, s, colpart);
     else if (act == 2) gemmp_go<true, 4, 2>(dy, N, W, K, T, K, N, dx, nullptr, ax, ncu, s, colpart);
-    else gemmp_go<true, 4, 3>(dy, N, W, K, T, K, N, dx, nullptr, ax, ncu, s, colpart);
+    else if (act == 3) gemmp_go<true, 4, 3>(dy, N, W, K, T, K, N, dx, nullptr, ax, ncu, s, colpart);
+    else gemmp_go<true, 4, 4>(dy, N, W, K, T, K, N, dx, nullptr, ax, ncu, s, colpart);
   } else {
     if (act == 1) gemmp_go<true, 3, 1>(dy, N, W, K, T, K, N, dx, nullptr, ax, ncu, s);
     else if (act == 2) gemmp_go<true, 3, 2>(dy, N, W, K, T, K, N, dx, nullptr, ax, ncu, s);
-    else gemmp_go<true, 3, 3>(dy, N, W, K, T, K, N, dx, nullptr, ax, ncu, s);
+    else if (act == 3) gemmp_go<true, 3, 3>(dy, N, W, K, T, K, N, dx, nullptr, ax, ncu, s);
+    else gemmp_go<true, 3, 4>(dy, N, W, K, T, K, N, dx, nullptr, ax, ncu, s);
   }
   return true;
 }

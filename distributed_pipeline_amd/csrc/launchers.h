@@ -111,7 +111,8 @@ void launch_timestep_emb(const float* ts, int B, int dim, float max_period, uint
 
 // ---- gemm.hip (bf16 MFMA GEMMs of Linear layers) ----------------------------------
 bool launch_gemm_nt(const uint16_t* x, const uint16_t* W, const uint16_t* bias, uint16_t* y,
-                    uint16_t* z, int T, int N, int K, int act, hipStream_t s);
+                    uint16_t* z, int T, int N, int K, int act, hipStream_t s,
+                    bool* zderiv = nullptr);
 bool launch_gemm_nn(const uint16_t* dy, const uint16_t* W, uint16_t* dx, int T, int N, int K,
                     hipStream_t s);
 bool launch_gemm_wgrad(const uint16_t* dy, const uint16_t* x, float* dW, float* db, int T, int N,
@@ -129,11 +130,13 @@ bool launch_gemm256_wgrad(const uint16_t* dy, const uint16_t* x, float* dW, floa
                           int N, int K, hipStream_t s);
 // gemm256.hip persistent forward / data-gradient kernels with fused epilogues (false when
 // the shape does not tile).  ncu: compute units (grid = min(tiles, ncu)).
-//   nt: y[T][N] = act(x[T][K] W[N][K]^T + bias); z (nullable) = pre-activation
-//   nn: dx[T][K] = dy[T][N] W[N][K] (* act'(aux[T][K]) when aux); colpart (nullable, needs
+//   nt: y[T][N] = act(x[T][K] W[N][K]^T + bias); z (nullable) = pre-activation, or act'(it)
+//       when zderiv (backward act code 4 multiplies by it)
+//   nn: dx[T][K] = dy[T][N] W[N][K] (* act'(aux[T][K]) when aux; act 4: * aux); colpart (nullable, needs
 //       aux): per-tile column-sum partials [(T/256)*2][K] of dx (the bias gradient)
 bool launch_gemmp_nt(const uint16_t* x, const uint16_t* W, const uint16_t* bias, uint16_t* y,
-                     uint16_t* z, int T, int N, int K, int act, int ncu, hipStream_t s);
+                     uint16_t* z, int T, int N, int K, int act, int ncu, hipStream_t s,
+                     bool zderiv = false);
 bool launch_gemmp_nn(const uint16_t* dy, const uint16_t* W, uint16_t* dx, const uint16_t* aux, int act,
                      int T, int N, int K, int ncu, hipStream_t s, float* colpart);
 bool launch_gemmp_nn_acc(const uint16_t* dy, const uint16_t* W, uint16_t* dx, int T, int N, int K, int ncu,

@@ -62,7 +62,8 @@ def _mm_fp32(a, b):
 # Linear (+ optional fused activation)
 # --------------------------------------------------------------------------- #
 
-_ACTS = ("none", "gelu", "tanh", "silu")
+# index = kernel act code; "deriv" (4): the saved operand is already act'(z)
+_ACTS = ("none", "gelu", "tanh", "silu", "deriv")
 
 
 def _act_fwd(z, act):
@@ -82,6 +83,8 @@ def _act_bwd(dy, z, y, act):
     if act == "none":
         return dy
     dyf = dy.float()
+    if act == "deriv":  # z holds act'(pre-activation), saved by the forward epilogue
+        return (dyf * z.float()).to(dy.dtype)
     if act == "tanh":
         yf = y.float()
         return (dyf * (1.0 - yf * yf)).to(dy.dtype)
@@ -125,6 +128,8 @@ def _bias_act_bwd(dy2d, z, y, act, want_db):
 #   "blas"   - every Linear GEMM on hipBLASLt (plus separate epilogue kernels), the
 #            A/B reference.
 GEMM_MODE = os.environ.get("DPA_GEMM", "auto")
+# forward GEMM epilogues store act'(z) instead of z for the backward (DPA_SAVE_ACT_DERIV=0: z)
+_SAVE_ACT_DERIV = os.environ.get("DPA_SAVE_ACT_DERIV", "1") != "0"
 
 
 def _gemm_shape_ok(x2, n_out):
@@ -163,12 +168,18 @@ def _accumulate_wgrad(p, dz, x2, bias):
 
 
 def _lin_fwd(x2, w16, b16, act, route):
-    """Forward GEMM (+bias, +activation) of one Linear -> (y, z).
+    """Forward GEMM (+bias, +activation) of one Linear -> (y, z, zact).
 
-    z is the pre-activation, returned only when the activation backward needs it
-    (gelu/silu); tanh's backward uses y."""
+    z is what the activation backward needs (gelu/silu; tanh's backward uses y):
+    on the persistent kernel act'(pre-activation), computed in the forward epilogue
+    together with act (the erf/exp work is shared, and the backward epilogue becomes
+    one multiply), else the pre-activation.  zact names the backward rule for z:
+    "deriv" or ``act``."""
     if route[0]:
-        y, z = get_ext().gemm_nt(x2, w16, b16, _ACTS.index(act))
+        y, z, is_d = get_ext().gemm_nt(x2, w16, b16, _ACTS.index(act),
+                                       _SAVE_ACT_DERIV and act in ("gelu", "silu"))
+        if act in ("gelu", "silu"):
+            return y, z, ("deriv" if is_d else act)
     else:
         if b16 is not None and x2.is_cuda:
             z = torch.addmm(b16, x2, w16.t())  # hipBLASLt bias epilogue
@@ -180,7 +191,7 @@ def _lin_fwd(x2, w16, b16, act, route):
             z, y = _bias_act_fwd(z, b16_epi, act)
         else:
             y = z
-    return y, (z if act in ("gelu", "silu") else None)
+    return y, (z if act in ("gelu", "silu") else None), act
 
 
 # Bias-gradient hand-off.  The kernel that produces a Linear's output gradient
@@ -246,10 +257,10 @@ class _LinearFn(torch.autograd.Function):
         shp = x.shape
         x2 = x.reshape(-1, shp[-1])
         route = _route(x2, w16.shape[0], act)
-        y, z = _lin_fwd(x2, w16, b16, act, route)
+        y, z, zact = _lin_fwd(x2, w16, b16, act, route)
         ctx.save_for_backward(x2, w16, z, y if act == "tanh" else None)
         ctx.params = (w, b)
-        ctx.act = act
+        ctx.act = zact
         ctx.route = route
         ctx.shp = shp
         return y.reshape(*shp[:-1], w16.shape[0])
@@ -293,10 +304,10 @@ def _dgrad_acc(dz, w16, native, dx_acc):
 
 def _mlp_fwd(x2, w1_16, b1_16, w2_16, b2_16, act):
     r1 = _route(x2, w1_16.shape[0], act)
-    h, z1 = _lin_fwd(x2, w1_16, b1_16, act, r1)
+    h, z1, zact = _lin_fwd(x2, w1_16, b1_16, act, r1)
     r2 = _route(h, w2_16.shape[0], "none")
-    y, _ = _lin_fwd(h, w2_16, b2_16, "none", r2)
-    return y, h, z1, (act, r1, r2)
+    y, _, _ = _lin_fwd(h, w2_16, b2_16, "none", r2)
+    return y, h, z1, (zact, r1, r2)
 
 
 def _mlp_bwd(dy2, x2, w1_16, w2_16, h, z1, params, cfg, need_dx, db2=None, dx_acc=None):
@@ -412,12 +423,12 @@ class _AttnLNFn(torch.autograd.Function):
         B, L, D = shp
         x2 = x.reshape(-1, D)
         rq = _route(x2, wq16.shape[0], "none")
-        qkv, _ = _lin_fwd(x2, wq16, bq16, "none", rq)
+        qkv, _, _ = _lin_fwd(x2, wq16, bq16, "none", rq)
         qkv3 = qkv.view(B, L, wq16.shape[0])
         o, lse = get_ext().attn_fwd(qkv3, heads, float(p_attn), False, seed_a, off_a)
         o2 = o.view(-1, o.shape[-1])
         ro = _route(o2, wo16.shape[0], "none")
-        y, _ = _lin_fwd(o2, wo16, bo16, "none", ro)
+        y, _, _ = _lin_fwd(o2, wo16, bo16, "none", ro)
         out, hsave, mean, rstd = get_ext().add_ln_fwd(y, x2, lw16, lb16, float(p), float(eps), seed_l,
                                                       off_l)
         ctx.save_for_backward(x2, qkv3, o, lse, wq16, wo16, hsave, mean, rstd, lw16)

@@ -32,7 +32,7 @@ def test_gemm_nt_bias_act(T, K, N, act, tile):
     x = torch.randn(T, K, device="cuda").bfloat16()
     W = (torch.randn(N, K, device="cuda") * 0.05).bfloat16()
     b = torch.randn(N, device="cuda").bfloat16()
-    y, z = _ext().gemm_nt(x, W, b, act)
+    y, z, _ = _ext().gemm_nt(x, W, b, act)
     zr = x.float() @ W.float().t() + b.float()
     yr = {0: zr, 1: torch.nn.functional.gelu(zr), 2: torch.tanh(zr), 3: torch.nn.functional.silu(zr)}[act]
     _close(y, yr)
@@ -101,7 +101,7 @@ def test_gemm_persistent_forward_many_tiles(T, K, N, act):
     x = torch.randn(T, K, device="cuda").bfloat16()
     W = (torch.randn(N, K, device="cuda") * 0.05).bfloat16()
     b = torch.randn(N, device="cuda").bfloat16()
-    y, z = _ext().gemm_nt(x, W, b, act)
+    y, z, _ = _ext().gemm_nt(x, W, b, act)
     zr = (x.float() @ W.float().t() + b.float()).bfloat16().float()
     yr = {0: zr, 1: torch.nn.functional.gelu(zr), 2: torch.tanh(zr), 3: torch.nn.functional.silu(zr)}[act]
     _close(y, yr)
@@ -167,3 +167,35 @@ def test_fused_mlp_matches_reference():
         _close(xg, x.grad)
         for a, p in zip(grads, m.parameters()):
             _close(a, p.grad)
+
+
+def _dact_ref(a, act):
+    if act == 1:
+        return 0.5 * (1 + torch.erf(a / 2 ** 0.5)) + a * torch.exp(-0.5 * a * a) / (2 * torch.pi) ** 0.5
+    if act == 2:
+        return 1 - torch.tanh(a) ** 2
+    s = torch.sigmoid(a)
+    return s * (1 + a * (1 - s))
+
+
+@pytest.mark.parametrize("T,K,N,act", [(32768, 768, 3072, 1), (16384, 768, 1024, 3), (768, 768, 3072, 1)])
+def test_gemm_forward_saves_activation_derivative(T, K, N, act):
+    """want_deriv: the persistent forward epilogue stores act'(pre-activation) next to
+    act(pre-activation); backward code 4 then multiplies (dz = (dy W) * z)."""
+    torch.manual_seed(3)
+    x = torch.randn(T, K, device="cuda").bfloat16()
+    W = (torch.randn(N, K, device="cuda") * 0.05).bfloat16()
+    b = torch.randn(N, device="cuda").bfloat16()
+    y, g, is_d = _ext().gemm_nt(x, W, b, act, True)
+    assert is_d  # these shapes tile for the persistent kernel
+    zr = (x.float() @ W.float().t() + b.float()).bfloat16().float()
+    yr = {1: torch.nn.functional.gelu(zr), 3: torch.nn.functional.silu(zr)}[act]
+    _close(y, yr)
+    _close(g, _dact_ref(zr, act))
+    # backward with the saved derivative: code 4 in the fused dgrad epilogue
+    dy = torch.randn(T, 512, device="cuda").bfloat16()
+    W2 = (torch.randn(512, N, device="cuda") * 0.05).bfloat16()
+    dz, db = _ext().gemm_nn_dact(dy, W2, g, 4, True)
+    ref = (dy.float() @ W2.float()).bfloat16().float() * g.float()
+    _close(dz, ref)
+    torch.testing.assert_close(db, dz.float().sum(0), rtol=1e-2, atol=1e-2 * db.abs().max().item())
