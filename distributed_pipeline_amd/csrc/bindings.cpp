@@ -623,6 +623,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("gemm_wgrad", &gemm_wgrad, "dW += dy^T x, db += colsum(dy) (fp32 atomics, split-K)");
   m.def("gemm_supported", &gemm_supported, "shape check for the native GEMMs");
   m.def("set_gemm256", &dpa::set_gemm256, "enable/disable the 256x256 8-phase GEMM path");
+  m.def("set_gemmp_dynamic", &dpa::set_gemmp_dynamic,
+        "dynamic per-XCD tile queues for the persistent GEMMs (on for world > 1; env DPA_GEMMP_DYNAMIC wins)");
   m.def("lxent_fwd", &lxent_fwd, "fused linear + cross-entropy forward -> (loss, lse)");
   m.def("lxent_bwd", &lxent_bwd, "fused linear + cross-entropy backward -> (dx, dW fp32, db fp32)");
   m.def("xent_rows_fwd", &xent_rows_fwd, "row softmax-CE over bf16 logits [R, ld] -> (loss, lse)");

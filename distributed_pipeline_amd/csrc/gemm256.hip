@@ -523,7 +523,8 @@ __global__ void __launch_bounds__(512) gemm256_kernel(
 // applied to the bf16-rounded value, exactly as a separate elementwise pass would.
 constexpr int P_BIAS_OFF = 2 * B_REGION;         // 2 x 512 B bias slots after the operand images
 constexpr int P_STAGE_OFF = 2 * B_REGION + 1024;  // 8 waves x 2 KiB epilogue transpose slots
-constexpr int P_LDS = P_STAGE_OFF + 8 * 2048;
+constexpr int P_NEXT_OFF = P_STAGE_OFF + 8 * 2048;  // dynamic schedule: next tile index
+constexpr int P_LDS = P_NEXT_OFF + 16;
 
 template <int EPI>
 struct PEpi {
@@ -577,6 +578,15 @@ __device__ __forceinline__ uint4 act8(const uint4& u) {
   return make_uint4(o[0], o[1], o[2], o[3]);
 }
 
+__device__ __forceinline__ void lds_write_b32(uint32_t addr, int v) {
+  asm volatile("ds_write_b32 %0, %1\n\ts_waitcnt lgkmcnt(0)" ::"v"(addr), "v"(v) : "memory");
+}
+__device__ __forceinline__ int lds_read_b32_sync(uint32_t addr) {
+  int v;
+  asm volatile("ds_read_b32 %0, %1\n\ts_waitcnt lgkmcnt(0)" : "=v"(v) : "v"(addr) : "memory");
+  return v;
+}
+
 __device__ __forceinline__ float bf_lo(uint32_t w) { return __uint_as_float(w << 16); }
 __device__ __forceinline__ float bf_hi(uint32_t w) { return __uint_as_float(w & 0xffff0000u); }
 
@@ -585,7 +595,8 @@ __global__ void __launch_bounds__(512) gemmp_kernel(const bf16_t* __restrict__ A
                                                     const bf16_t* __restrict__ B, int64_t ldb, int M, int N,
                                                     int nk, bf16_t* __restrict__ C, int64_t ldc,
                                                     const bf16_t* __restrict__ bias,
-                                                    bf16_t* __restrict__ Zout, float* __restrict__ colpart) {
+                                                    bf16_t* __restrict__ Zout, float* __restrict__ colpart,
+                                                    int* __restrict__ tile_ctr) {
   __shared__ __attribute__((aligned(1024))) char smem[P_LDS];
   constexpr int XS = PEpi<EPI>::XS;
   constexpr bool DACT = EPI == 3 || EPI == 4 || EPI == 5;  // epilogues that read aux
@@ -778,6 +789,22 @@ __global__ void __launch_bounds__(512) gemmp_kernel(const bf16_t* __restrict__ A
 
   int tile = xcd_remap(blockIdx.x, G);
   if (tile >= ntiles) return;
+  // Dynamic schedule (tile_ctr != nullptr, G >= 8): the first tile is static; later ones
+  // are claimed from a per-XCD queue (blockIdx % 8, the round-robin dispatch xcd_remap
+  // assumes for locality only), item i of queue x = tile (1 + i / |J_x|) G + J_x[i % |J_x|]
+  // with J_x the XCD's static column range - the static schedule's tile set, but a
+  // workgroup that starts late (its CU held by a concurrent RCCL kernel) just takes fewer
+  // tiles instead of finishing last.  Claimed items form a prefix, so the first claim past
+  // ntiles ends the workgroup.
+  const bool dyn = tile_ctr != nullptr && G >= 8;
+  int qbase = 0, qsize = 1;
+  int* qctr = nullptr;
+  if (dyn) {
+    const int qg = G >> 3, rg = G & 7, x = blockIdx.x & 7;
+    qbase = x < rg ? x * (qg + 1) : rg * (qg + 1) + (x - rg) * qg;
+    qsize = x < rg ? qg + 1 : qg;
+    qctr = tile_ctr + x * 16;  // one 64-byte line per queue
+  }
   int slot = 0;
   bool extra = false;
   zero_acc();
@@ -787,6 +814,10 @@ __global__ void __launch_bounds__(512) gemmp_kernel(const bf16_t* __restrict__ A
   if (grp == 1) barrier();
 
   while (true) {
+    // claim the next tile now (wave 0, lane 0); the result is consumed after the main
+    // loop, whose counted waits at most over-wait by this one extra VMEM op
+    int claimed = 0;
+    if (dyn && w == 0 && lane_id() == 0) claimed = atomicAdd(qctr, 1);
     // first iteration: the previous tile's XS epilogue ops may still be in flight
     {
       const bool more = 1 < niter;
@@ -811,8 +842,13 @@ __global__ void __launch_bounds__(512) gemmp_kernel(const bf16_t* __restrict__ A
       phase<6, false, B_TR, false, true>(acc, fa, fb0, fb1, cs, opA, opB, smem, csa, te, more, false, grp);
       phase<7, false, B_TR, false, true>(acc, fa, fb0, fb1, cs, opA, opB, smem, csa, te, more, false, grp);
     }
+    if (dyn && w == 0) {
+      // every wave's main loop ended in vmcnt(0): the claim has landed
+      const int i = __builtin_amdgcn_readfirstlane(claimed);
+      if (lane_id() == 0) lds_write_b32(sbase + P_NEXT_OFF, (1 + i / qsize) * G + qbase + i % qsize);
+    }
     if (grp == 0) barrier();  // re-align the groups: every wave's LDS reads are retired
-    const int next = tile + G;
+    const int next = dyn ? __builtin_amdgcn_readfirstlane(lds_read_b32_sync(sbase + P_NEXT_OFF)) : tile + G;
     const bool has_next = next < ntiles;
     uint4 aux[2][2];
     if constexpr (DACT) {
@@ -885,14 +921,40 @@ bool launch_gemm256_nn_dact(const uint16_t* dy, const uint16_t* W, const uint16_
 // ---- persistent forward / data-gradient launchers ---------------------------
 static int persistent_grid(int tiles, int ncu) { return tiles < ncu ? tiles : ncu; }
 
+// Dynamic tile schedule of the persistent kernels (see gemmp_kernel): on when the
+// compute stream shares the chip with collectives (the DDP engine turns it on for
+// world > 1; DPA_GEMMP_DYNAMIC=0/1 overrides).  Queue counters: one small device buffer
+// per device, zeroed on the stream before each launch (the GEMMs of a rank run on one
+// stream, so launches never overlap on it).
+static int g_gemmp_dynamic = -1;
+void set_gemmp_dynamic(bool on) {
+  const char* e = std::getenv("DPA_GEMMP_DYNAMIC");
+  g_gemmp_dynamic = e ? (e[0] == '1' ? 1 : 0) : (on ? 1 : 0);
+}
+static int* gemmp_queue(hipStream_t s) {
+  if (g_gemmp_dynamic < 0) set_gemmp_dynamic(false);
+  if (!g_gemmp_dynamic) return nullptr;
+  static int* bufs[64] = {nullptr};
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return nullptr;
+  if (!bufs[dev] && hipMalloc(&bufs[dev], 8 * 16 * sizeof(int)) != hipSuccess) {
+    bufs[dev] = nullptr;
+    return nullptr;
+  }
+  if (hipMemsetAsync(bufs[dev], 0, 8 * 16 * sizeof(int), s) != hipSuccess) return nullptr;
+  return bufs[dev];
+}
+
 template <bool B_TR, int EPI, int ACT>
 static void gemmp_go(const uint16_t* a, int64_t lda, const uint16_t* b, int64_t ldb, int M, int N, int K,
                      uint16_t* c, const uint16_t* bias, uint16_t* z, int ncu, hipStream_t s,
                      float* colpart = nullptr) {
   const int tiles = (M / 256) * (N / 256);
-  hipLaunchKernelGGL((g256::gemmp_kernel<B_TR, EPI, ACT>), dim3(persistent_grid(tiles, ncu)), dim3(512), 0,
-                     s, (const bf16_t*)a, lda, (const bf16_t*)b, ldb, M, N, K / 64, (bf16_t*)c, (int64_t)N,
-                     (const bf16_t*)bias, (bf16_t*)z, colpart);
+  const int grid = persistent_grid(tiles, ncu);
+  int* q = (tiles > grid && grid >= 8) ? gemmp_queue(s) : nullptr;
+  hipLaunchKernelGGL((g256::gemmp_kernel<B_TR, EPI, ACT>), dim3(grid), dim3(512), 0, s, (const bf16_t*)a,
+                     lda, (const bf16_t*)b, ldb, M, N, K / 64, (bf16_t*)c, (int64_t)N, (const bf16_t*)bias,
+                     (bf16_t*)z, colpart, q);
 }
 
 // y[T][N] = act(x[T][K] . W[N][K]^T + bias); z (nullable, act != 0) = the pre-activation,

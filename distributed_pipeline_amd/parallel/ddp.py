@@ -180,6 +180,12 @@ class DDPEngine(nn.Module):
                     blobs = [None] * self.world_size
                     dist.all_gather_object(blobs, self._native.ipc_export(), group=self.pg)
                     self._native.ipc_open(blobs)
+        if self.distributed and self.world_size > 1 and self.space.device.type == "cuda":
+            # collectives share the CUs with the persistent GEMMs: let late-starting GEMM
+            # workgroups take fewer tiles instead of finishing last (csrc/gemm256.hip)
+            ext = get_ext(required=False)
+            if ext is not None and hasattr(ext, "set_gemmp_dynamic"):
+                ext.set_gemmp_dynamic(True)
         if self.distributed:
             self._verify_shapes()
             if broadcast_from_rank0:

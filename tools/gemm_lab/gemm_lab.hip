@@ -266,38 +266,38 @@ int main(int argc, char** argv) {
                     hipLaunchKernelGGL((dpa::g256::gemmp_kernel<false, 0, 0>), dim3(grid), dim3(512), 0, st,
                                        (const dpa::bf16_t*)A, (int64_t)K, (const dpa::bf16_t*)B, (int64_t)K, T, N,
                                        K / 64, (dpa::bf16_t*)C, (int64_t)0, (const dpa::bf16_t*)bias,
-                                       (dpa::bf16_t*)nullptr, (float*)nullptr);
+                                       (dpa::bf16_t*)nullptr, (float*)nullptr, (int*)nullptr);
                   }, fl, {}});
     vs.push_back({"ffn_in/fwd_gelu_z_gp_ldc0", [=](hipStream_t st) {
                     hipLaunchKernelGGL((dpa::g256::gemmp_kernel<false, 2, 1>), dim3(grid), dim3(512), 0, st,
                                        (const dpa::bf16_t*)A, (int64_t)K, (const dpa::bf16_t*)B, (int64_t)K, T, N,
                                        K / 64, (dpa::bf16_t*)C, (int64_t)0, (const dpa::bf16_t*)bias,
-                                       (dpa::bf16_t*)Z, (float*)nullptr);
+                                       (dpa::bf16_t*)Z, (float*)nullptr, (int*)nullptr);
                   }, fl, {}});
     vs.push_back({"ffn_in/fwd_z_noact_gp_ldc0", [=](hipStream_t st) {
                     hipLaunchKernelGGL((dpa::g256::gemmp_kernel<false, 2, 0>), dim3(grid), dim3(512), 0, st,
                                        (const dpa::bf16_t*)A, (int64_t)K, (const dpa::bf16_t*)B, (int64_t)K, T, N,
                                        K / 64, (dpa::bf16_t*)C, (int64_t)0, (const dpa::bf16_t*)bias,
-                                       (dpa::bf16_t*)Z, (float*)nullptr);
+                                       (dpa::bf16_t*)Z, (float*)nullptr, (int*)nullptr);
                   }, fl, {}});
     vs.push_back({"ffn_in/fwd_z_noact_gp", [=](hipStream_t st) {
                     hipLaunchKernelGGL((dpa::g256::gemmp_kernel<false, 2, 0>), dim3(grid), dim3(512), 0, st,
                                        (const dpa::bf16_t*)A, (int64_t)K, (const dpa::bf16_t*)B, (int64_t)K, T, N,
                                        K / 64, (dpa::bf16_t*)C, (int64_t)N, (const dpa::bf16_t*)bias,
-                                       (dpa::bf16_t*)Z, (float*)nullptr);
+                                       (dpa::bf16_t*)Z, (float*)nullptr, (int*)nullptr);
                   }, fl, {}});
     vs.push_back({"ffn_out/dgrad_dact_noact_gp_ldc0", [=](hipStream_t st) {
                     hipLaunchKernelGGL((dpa::g256::gemmp_kernel<true, 3, 0>), dim3(grid), dim3(512), 0, st,
                                        (const dpa::bf16_t*)A, (int64_t)768, (const dpa::bf16_t*)B, (int64_t)3072, T,
                                        3072, 768 / 64, (dpa::bf16_t*)C, (int64_t)0, (const dpa::bf16_t*)nullptr,
-                                       (dpa::bf16_t*)Z, (float*)nullptr);
+                                       (dpa::bf16_t*)Z, (float*)nullptr, (int*)nullptr);
                   }, fl, {}});
     // dgrad of ffn_out with dgelu: dh[T][3072] = dy[T][768] . W2[768][3072] * gelu'(z)
     vs.push_back({"ffn_out/dgrad_dgelu_gp_ldc0", [=](hipStream_t st) {
                     hipLaunchKernelGGL((dpa::g256::gemmp_kernel<true, 3, 1>), dim3(grid), dim3(512), 0, st,
                                        (const dpa::bf16_t*)A, (int64_t)768, (const dpa::bf16_t*)B, (int64_t)3072, T,
                                        3072, 768 / 64, (dpa::bf16_t*)C, (int64_t)0, (const dpa::bf16_t*)nullptr,
-                                       (dpa::bf16_t*)Z, (float*)nullptr);
+                                       (dpa::bf16_t*)Z, (float*)nullptr, (int*)nullptr);
                   }, fl, {}});
     vs.push_back({"ffn_out/dgrad_nostore_g256", [=](hipStream_t st) {
                     hipLaunchKernelGGL((dpa::g256::gemm256_kernel<false, true, dpa::g256::EPI_NONE>),
