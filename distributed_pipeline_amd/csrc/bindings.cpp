@@ -123,6 +123,19 @@ static std::vector<at::Tensor> lxent_fwd(const at::Tensor& x, const at::Tensor& 
   return {loss, lse};
 }
 
+static std::vector<at::Tensor> lxent_fwd_dx(const at::Tensor& x, const at::Tensor& W,
+                                            c10::optional<at::Tensor> b, const at::Tensor& tgt) {
+  check_lxent(x, W, b, tgt);
+  const c10::DeviceGuard guard(x.device());
+  const int N = (int)x.size(0), V = (int)W.size(0), E = (int)x.size(1);
+  auto f32 = x.options().dtype(at::kFloat);
+  at::Tensor loss = at::empty({N}, f32), lse = at::empty({N}, f32), dxu = at::empty({N, E}, f32);
+  if (N > 0)
+    dpa::launch_lxent_fwd_dx(bf_ptr(x), bf_ptr(W), opt_bf_ptr(b), tgt.data_ptr<int64_t>(), N, V, E,
+                             loss.data_ptr<float>(), lse.data_ptr<float>(), dxu.data_ptr<float>(), cur_stream());
+  return {loss, lse, dxu};
+}
+
 static std::vector<at::Tensor> lxent_bwd(const at::Tensor& dloss, const at::Tensor& x,
                                          const at::Tensor& W, c10::optional<at::Tensor> b,
                                          const at::Tensor& tgt, const at::Tensor& lse, bool need_dx,
@@ -626,6 +639,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("set_gemmp_dynamic", &dpa::set_gemmp_dynamic,
         "dynamic per-XCD tile queues for the persistent GEMMs (on for world > 1; env DPA_GEMMP_DYNAMIC wins)");
   m.def("lxent_fwd", &lxent_fwd, "fused linear + cross-entropy forward -> (loss, lse)");
+  m.def("lxent_fwd_dx", &lxent_fwd_dx,
+        "fused linear-CE forward + unscaled input gradient -> (loss, lse, dxu fp32 [N, E])");
   m.def("lxent_bwd", &lxent_bwd, "fused linear + cross-entropy backward -> (dx, dW fp32, db fp32)");
   m.def("xent_rows_fwd", &xent_rows_fwd, "row softmax-CE over bf16 logits [R, ld] -> (loss, lse)");
   m.def("xent_rows_bwd_", &xent_rows_bwd_, "in place: logits -> dloss * (softmax - onehot)");

@@ -284,6 +284,133 @@ __global__ void __launch_bounds__(256) lxent_dx_kernel(
 }
 
 // ---------------------------------------------------------------------------
+// Forward + input gradient in one vocabulary sweep (training): the loss of token t
+// is lse_t - s_t[target], and its gradient w.r.t. x_t does not depend on the upstream
+// scalar g_t except as a factor:  dx_t = g_t (sum_v p_tv W_v - W_target).  So the
+// forward accumulates  u_t = sum_v exp(s_tv - m_t) W_v  with an online max m_t (the
+// flash-attention recurrence; lazy rescale, |growth| <= 2^8 between rescales) and
+// writes dxu_t = u_t / l_t - W_target in fp32; the backward only multiplies by g_t.
+// Versus lxent_fwd + lxent_dx this removes one full recompute of the logits and their
+// exponentials (the dx kernel's S = W x^T pass).
+// ---------------------------------------------------------------------------
+template <int E>
+__global__ void __launch_bounds__(256, E == 128 ? 2 : 1) lxent_fwd_dx_kernel(
+    const bf16_t* __restrict__ x, const bf16_t* __restrict__ W, const bf16_t* __restrict__ bias,
+    const int64_t* __restrict__ target, int N, int V, float* __restrict__ loss,
+    float* __restrict__ lse_out, float* __restrict__ dxu) {
+  constexpr int KS = E / 16, ROWB = E * 2, KT = E / 32;
+  __shared__ __attribute__((aligned(16))) char smem[64 * ROWB + 64 * 4];
+  char* wt = smem;
+  float* bt = reinterpret_cast<float*>(smem + 64 * ROWB);
+
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, h = lane >> 5;
+  const int t = blockIdx.x * 128 + w * 32 + (lane & 31);
+  const bool tok_ok = t < N;
+  bf16x8 xf[KS];
+#pragma unroll
+  for (int s = 0; s < KS; ++s) {
+    if (tok_ok) xf[s] = ld_frag(x + (int64_t)t * E + 16 * s + 8 * h);
+    else for (int j = 0; j < 8; ++j) xf[s][j] = 0;
+  }
+  const int64_t tg = tok_ok ? target[t] : -1;
+  f32x16 dacc[KT];
+#pragma unroll
+  for (int k = 0; k < KT; ++k) dacc[k] = zero16();
+  float m = -1e30f, l = 0.f, tl = -INFINITY;  // m in the log2 domain
+
+  WTile<E, 256> stage;
+  stage.load(W, 0, V, tid);
+  for (int v0 = 0; v0 < V; v0 += 64) {
+    stage.store(wt, tid);
+    if (tid < 64) {
+      const int v = v0 + tid;
+      bt[tid] = (v < V) ? (bias ? bf2f(bias[v]) : 0.f) : -INFINITY;
+    }
+    __syncthreads();
+    if (v0 + 64 < V) stage.load(W, v0 + 64, V, tid);  // prefetch behind the MFMAs
+
+    // one 32-row vocabulary subtile at a time (a single live logit accumulator keeps
+    // the kernel at 2 waves / SIMD); each subtile is one online-softmax step
+#pragma unroll
+    for (int vt = 0; vt < 2; ++vt) {
+      f32x16 acc;
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        const f32x4 bv = *reinterpret_cast<const f32x4*>(bt + vt * 32 + 8 * g + 4 * h);
+#pragma unroll
+        for (int r = 0; r < 4; ++r) acc[4 * g + r] = bv[r];
+      }
+#pragma unroll
+      for (int s = 0; s < KS; ++s)
+        acc = mfma32(lds_frag<ROWB>(wt, vt * 32 + (lane & 31), 2 * s + h), xf[s], acc);
+      // the target's logit, from whichever lane half holds its row
+      const int64_t r = tg - (v0 + vt * 32);
+      if (r >= 0 && r < 32 && ((((int)r >> 2) & 1) == h)) tl = sel16(acc, ((int)r & 3) + 4 * ((int)r >> 3));
+      // running max over both lane halves of the token (they feed the same dacc rows)
+      float tmax = -INFINITY;
+#pragma unroll
+      for (int i = 0; i < 16; ++i) tmax = fmaxf(tmax, acc[i]);
+      tmax = fmaxf(tmax, __shfl_xor(tmax, 32, 64)) * LOG2E;
+      if (__any(tmax > m + 8.f)) {
+        const float mn = fmaxf(m, tmax);
+        const float alpha = fexp2(m - mn);
+        m = mn;
+        l *= alpha;
+        // dacc rows are tokens (register i <-> token acc_row(i, h)): fetch their alpha
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+          const float f = __shfl(alpha, acc_row(i, h), 64);
+#pragma unroll
+          for (int kt = 0; kt < KT; ++kt) dacc[kt][i] *= f;
+        }
+      }
+#pragma unroll
+      for (int i = 0; i < 16; ++i) {
+        const float pr = fexp2(fmaf(acc[i], LOG2E, -m));
+        l += pr;
+        acc[i] = pr;
+      }
+      // u[t][k] += sum_v p[v][t] W[v][k]   (p as A operand, W read transposed)
+#pragma unroll
+      for (int s = 0; s < 2; ++s) {
+        const bf16x8 af = acc_to_frag(acc, s);
+#pragma unroll
+        for (int kt = 0; kt < KT; ++kt)
+          dacc[kt] = mfma32(af, lds_tr_frag<ROWB>(wt, vt * 32 + 16 * s, kt * 32, lane), dacc[kt]);
+      }
+    }
+    __syncthreads();
+  }
+  l += __shfl_xor(l, 32, 64);
+  tl = fmaxf(tl, __shfl_xor(tl, 32, 64));
+  const bool valid = tok_ok && tg >= 0 && tg < V;
+  const float lse = (m + log2f(l)) * LN2;
+  if (h == 0 && tok_ok) {
+    loss[t] = valid ? lse - tl : 0.f;
+    lse_out[t] = lse;
+  }
+  // dxu[t][k] = u[t][k] / l_t - W[target_t][k]   (0 for ignored targets)
+  const float inv_l = valid ? 1.f / l : 0.f;
+  const int tb = blockIdx.x * 128 + w * 32;
+#pragma unroll
+  for (int i = 0; i < 16; ++i) {
+    const int src = acc_row(i, h);
+    const float f = __shfl(inv_l, src, 64);
+    const int64_t tgi = __shfl(tg, src, 64);
+    const int tt = tb + src;
+    if (tt < N) {
+#pragma unroll
+      for (int kt = 0; kt < KT; ++kt) {
+        const int k = kt * 32 + (lane & 31);
+        float vv = 0.f;
+        if (f != 0.f) vv = dacc[kt][i] * f - bf2f(W[tgi * E + k]);
+        dxu[(int64_t)tt * E + k] = vv;
+      }
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
 // Backward: dW (+ db)
 // ---------------------------------------------------------------------------
 template <int E>
@@ -463,6 +590,17 @@ static void fwd_impl(const bf16_t* x, const bf16_t* W, const bf16_t* b, const in
   if (Sx > 1)
     hipLaunchKernelGGL(lxent_combine_kernel, dim3((N + 255) / 256), dim3(256), 0, st, pm, ps, tl,
                        tgt, N, V, Sx, loss, lse);
+}
+
+void launch_lxent_fwd_dx(const uint16_t* x, const uint16_t* W, const uint16_t* b, const int64_t* tgt,
+                         int N, int V, int E, float* loss, float* lse, float* dxu, hipStream_t s) {
+  const unsigned tb = (unsigned)((N + 127) / 128);
+  if (E == 128)
+    hipLaunchKernelGGL(lxent_fwd_dx_kernel<128>, dim3(tb), dim3(256), 0, s, (const bf16_t*)x, (const bf16_t*)W,
+                       (const bf16_t*)b, tgt, N, V, loss, lse, dxu);
+  else
+    hipLaunchKernelGGL(lxent_fwd_dx_kernel<256>, dim3(tb), dim3(256), 0, s, (const bf16_t*)x, (const bf16_t*)W,
+                       (const bf16_t*)b, tgt, N, V, loss, lse, dxu);
 }
 
 int64_t lxent_workspace_floats(int N, int V) {

@@ -733,9 +733,20 @@ def attention(qkv, n_heads, p=0.0, causal=False, training=True):
 # --------------------------------------------------------------------------- #
 
 class _LinearXentFn(torch.autograd.Function):
+    """Per-token CE of x @ W^T + b, logits never materialised (csrc/xent.hip).  When x
+    needs a gradient the forward also produces the unscaled input gradient
+    dxu = softmax . W - W[target] in the same vocabulary sweep (fp32, [N, E]), so the
+    backward's dx is one multiply by the upstream per-token gradient instead of a
+    second pass over all N x V logits."""
+
     @staticmethod
     def forward(ctx, x, w, b, w16, b16, target):
-        loss, lse = get_ext().lxent_fwd(x, w16, b16, target)
+        ext = get_ext()
+        ctx.dxu = None
+        if ctx.needs_input_grad[0] and _XENT_FUSED_DX and hasattr(ext, "lxent_fwd_dx"):
+            loss, lse, ctx.dxu = ext.lxent_fwd_dx(x, w16, b16, target)
+        else:
+            loss, lse = ext.lxent_fwd(x, w16, b16, target)
         ctx.save_for_backward(x, w16, b16, target, lse)
         ctx.has_b = b is not None
         return loss
@@ -743,9 +754,13 @@ class _LinearXentFn(torch.autograd.Function):
     @staticmethod
     def backward(ctx, dloss):
         x, w16, b16, target, lse = ctx.saved_tensors
-        dx, dw, db = get_ext().lxent_bwd(dloss.contiguous().float(), x, w16, b16, target, lse,
-                                         ctx.needs_input_grad[0], ctx.needs_input_grad[1],
+        dxu, ctx.dxu = ctx.dxu, None
+        g = dloss.contiguous().float()
+        need_dx = ctx.needs_input_grad[0] and dxu is None
+        dx, dw, db = get_ext().lxent_bwd(g, x, w16, b16, target, lse, need_dx, ctx.needs_input_grad[1],
                                          ctx.has_b and ctx.needs_input_grad[2])
+        if dxu is not None:
+            dx = dxu.mul_(g.unsqueeze(1)).to(x.dtype)
         return dx, dw, db, None, None, None
 
 
@@ -840,6 +855,9 @@ class _ChunkedLinearXentFn(torch.autograd.Function):
         dw = dwp[:V] if need_dw else None
         return dx, dw, db, None, None, None, None
 
+
+# fused CE: forward also emits the unscaled input gradient (DPA_XENT_FUSED_DX=0: separate dx pass)
+_XENT_FUSED_DX = os.environ.get("DPA_XENT_FUSED_DX", "1") != "0"
 
 # tokens per logits chunk of the wide-E path: about 2 GiB of bf16 logits (fewer, larger
 # GEMMs: GPT-2 bs128 171 -> 162 ms/step against 0.5 GiB chunks)

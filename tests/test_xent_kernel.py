@@ -36,6 +36,12 @@ def test_lxent_fwd_bwd(N, V, E, with_bias):
     ref_loss.backward(g)
     dx, dW, db = ext.lxent_bwd(g, x, W, b, tgt, lse, True, True, with_bias)
     torch.testing.assert_close(dx.float(), xr.grad, rtol=2e-2, atol=2e-2 * xr.grad.abs().max().item())
+    # fused forward + unscaled input gradient (training path): same loss / lse, and
+    # g * dxu is the input gradient
+    loss2, lse2, dxu = ext.lxent_fwd_dx(x, W, b, tgt)
+    torch.testing.assert_close(loss2, ref_loss, rtol=2e-3, atol=2e-3)
+    torch.testing.assert_close(lse2, lse, rtol=1e-4, atol=1e-4)
+    torch.testing.assert_close(dxu * g[:, None], xr.grad, rtol=2e-2, atol=2e-2 * xr.grad.abs().max().item())
     torch.testing.assert_close(dW, Wr.grad, rtol=2e-2, atol=1e-2 * Wr.grad.abs().max().item())
     if with_bias:
         torch.testing.assert_close(db, br.grad, rtol=2e-2, atol=1e-2 * br.grad.abs().max().item())

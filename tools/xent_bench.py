@@ -44,9 +44,11 @@ def main():
     bw = bench(lambda: ext.lxent_bwd(dl, x, W, b, tgt, lse, True, True, True))
     dxo = bench(lambda: ext.lxent_bwd(dl, x, W, b, tgt, lse, True, False, False))
     dwo = bench(lambda: ext.lxent_bwd(dl, x, W, b, tgt, lse, False, True, True))
+    fdx = bench(lambda: ext.lxent_fwd_dx(x, W, b, tgt)) if hasattr(ext, "lxent_fwd_dx") else None
     fl = 2.0 * N * V * E
     print(json.dumps({"N": N, "V": V, "E": E, "fwd_ms": round(f, 3), "fwd_logit_TF": round(fl / f / 1e9, 1),
-                      "bwd_ms": round(bw, 3), "dx_ms": round(dxo, 3), "dw_ms": round(dwo, 3)}))
+                      "bwd_ms": round(bw, 3), "dx_ms": round(dxo, 3), "dw_ms": round(dwo, 3),
+                      "fused_fwd_dx_ms": round(fdx, 3) if fdx else None}))
 
 
 if __name__ == "__main__":
