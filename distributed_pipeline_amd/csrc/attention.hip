@@ -57,6 +57,15 @@ __device__ __forceinline__ bool keep_from(const DropCfg& d, uint32_t h, int key)
 __device__ __forceinline__ bool keep_bit(const DropCfg& d, int q, int key) {
   return keep_from(d, drop_hash(d, q, key), key);
 }
+// The same hash from precomputed terms: qt = q * 0x9E3779B1, kt = (key >> 1) * 0x85EBCA77.
+// Inside a tile the per-register rows differ by compile-time constants, so the caller
+// forms both terms with adds instead of quarter-rate multiplies.
+__device__ __forceinline__ uint32_t drop_hash_t(const DropCfg& d, uint32_t qt, uint32_t kt) {
+  return mix32(d.seedmix ^ qt ^ kt);
+}
+constexpr uint32_t DROP_CQ = 0x9E3779B1u, DROP_CK = 0x85EBCA77u;
+// accumulator row offset of register i relative to acc_row(0, h) (even for even i)
+__host__ __device__ constexpr int acc_off(int i) { return (i & 3) + 8 * (i >> 2); }
 
 // softmax scale in the exp2 domain and the 1/sqrt(D) gradient scale
 template <int D>
@@ -269,6 +278,7 @@ __global__ void __launch_bounds__(256, D == 64 ? 2 : 1) attn_fwd_online_kernel(c
     else for (int j = 0; j < 8; ++j) qf[s][j] = 0;
   }
   const DropCfg dc = make_drop(p, seed, offset, (uint32_t)(b * H + hd));
+  const uint32_t qterm = (uint32_t)q * DROP_CQ;
   const int kv_end = CAUSAL ? min(L, (int)blockIdx.x * 128 + 128) : L;
   // source lane (in this half's numbering) of the query that register i of O belongs to
   int src[16];
@@ -333,11 +343,17 @@ __global__ void __launch_bounds__(256, D == 64 ? 2 : 1) attn_fwd_online_kernel(c
 #pragma unroll
       for (int t = 0; t < 2; ++t) {
         if (t >= nsub) continue;
+        // key pair of register i: (kv0 + 32 t + 4 hf + acc_off(i)) / 2, all terms even
+        const uint32_t kt0 = (uint32_t)((kv0 + t * 32 + 4 * hf) >> 1) * DROP_CK;
+        uint32_t hsh = 0;
 #pragma unroll
         for (int i = 0; i < 16; ++i) {
           float pr = fexp2(fmaf(acc[t][i], att_c<D>(), -m));
           add += pr;
-          if (dc.on) pr = keep_bit(dc, q, kv0 + t * 32 + acc_row(i, hf)) ? pr * dc.scale : 0.f;
+          if (dc.on) {
+            if ((i & 1) == 0) hsh = drop_hash_t(dc, qterm, kt0 + (uint32_t)(acc_off(i) >> 1) * DROP_CK);
+            pr = keep_from(dc, hsh, i & 1) ? pr * dc.scale : 0.f;
+          }
           acc[t][i] = pr;
         }
       }
@@ -571,10 +587,12 @@ __global__ void __launch_bounds__(256, D == 64 ? 2 : 1) attn_bwd_kv_kernel(
       uint32_t hh[16];
       if (dc.on) {
         const int par = lane & 1;
+        const uint32_t kt = (uint32_t)(key >> 1) * DROP_CK;
+        const uint32_t qt0 = (uint32_t)(q0 + qt * 32 + 4 * hf + par) * DROP_CQ;
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
-          const int qa = q0 + qt * 32 + acc_row(2 * j, hf), qb2 = q0 + qt * 32 + acc_row(2 * j + 1, hf);
-          const uint32_t mine = drop_hash(dc, par ? qb2 : qa, key);
+          // query of register 2j + par: q0 + 32 qt + 4 hf + acc_off(2j) + par
+          const uint32_t mine = drop_hash_t(dc, qt0 + (uint32_t)acc_off(2 * j) * DROP_CQ, kt);
           const uint32_t other = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)mine, 0xB1, 0xF, 0xF, true);
           hh[2 * j] = par ? other : mine;
           hh[2 * j + 1] = par ? mine : other;
@@ -660,6 +678,7 @@ __global__ void __launch_bounds__(256, D == 64 ? 2 : 1) attn_bwd_q_kernel(
   const float lse2 = q_ok ? lse[lrow + q] * 1.4426950408889634f : 0.f;
   const float dlt = q_ok ? delta[lrow + q] : 0.f;
   const DropCfg dc = make_drop(p, seed, offset, (uint32_t)(b * H + hd));
+  const uint32_t qterm = (uint32_t)q * DROP_CQ;
   f32x16 dq[D / 32];
 #pragma unroll
   for (int dt = 0; dt < D / 32; ++dt) dq[dt] = zero16();
@@ -687,13 +706,18 @@ __global__ void __launch_bounds__(256, D == 64 ? 2 : 1) attn_bwd_q_kernel(
         sacc = mfma32(lds_frag<2 * D>(kt_lds, t * 32 + (lane & 31), 2 * s + hf), qf[s], sacc);
         dpacc = mfma32(lds_frag<2 * D>(vt_lds, t * 32 + (lane & 31), 2 * s + hf), df[s], dpacc);
       }
+      const uint32_t kt0 = (uint32_t)((kv0 + t * 32 + 4 * hf) >> 1) * DROP_CK;
+      uint32_t hsh = 0;
 #pragma unroll
       for (int i = 0; i < 16; ++i) {
         const int kk = kv0 + t * 32 + acc_row(i, hf);
         float pr = fexp2(fmaf(sacc[i], att_c<D>(), -lse2));
         if (masked && ((CAUSAL && kk > q) || !q_ok || kk >= L)) pr = 0.f;
         float dpd = dpacc[i];
-        if (dc.on) dpd = keep_bit(dc, q, kk) ? dpd * dc.scale : 0.f;
+        if (dc.on) {
+          if ((i & 1) == 0) hsh = drop_hash_t(dc, qterm, kt0 + (uint32_t)(acc_off(i) >> 1) * DROP_CK);
+          dpd = keep_from(dc, hsh, i & 1) ? dpd * dc.scale : 0.f;
+        }
         sacc[i] = pr * (dpd - dlt);
       }
 #pragma unroll
