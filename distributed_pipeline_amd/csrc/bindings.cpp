@@ -233,9 +233,10 @@ static std::vector<at::Tensor> add_ln_bwd(const at::Tensor& dout, const at::Tens
   auto f32 = dout.options().dtype(at::kFloat);
   const int nb = dpa::ln_bwd_blocks(R);
   (void)nb;
-  at::Tensor dyb;
-  if (need_dy && want_dyb) dyb = at::empty({D}, f32);
-  at::Tensor dg = at::empty({D}, f32), db = at::empty({D}, f32);
+  // dgamma, dbeta and colsum(dy) as consecutive rows of one buffer: one memset zeroes all
+  at::Tensor acc3 = at::empty({3, D}, f32);
+  at::Tensor dg = acc3[0], db = acc3[1], dyb;
+  if (need_dy && want_dyb) dyb = acc3[2];
   bool ok = dpa::launch_add_ln_bwd(
       bf_ptr(dout), bf_ptr(hs), mean.data_ptr<float>(), rstd.data_ptr<float>(), bf_ptr(g),
       need_dres ? reinterpret_cast<uint16_t*>(dres.data_ptr()) : nullptr,

@@ -273,9 +273,15 @@ static void ln_bwd_impl(const uint16_t* dout, const uint16_t* hsave, const float
                         uint32_t off, const uint16_t* dh_in, bool post, hipStream_t s) {
   constexpr int D = VEC * 64;
   const int nb = ln_bwd_blocks(R);
-  hipMemsetAsync(dg, 0, sizeof(float) * D, s);
-  hipMemsetAsync(db, 0, sizeof(float) * D, s);
-  if (dyb) hipMemsetAsync(dyb, 0, sizeof(float) * D, s);
+  // one memset when the three accumulators are consecutive rows of one buffer (the binding
+  // allocates them so), else one each
+  if (db == dg + D && (dyb == nullptr || dyb == dg + 2 * D)) {
+    (void)hipMemsetAsync(dg, 0, sizeof(float) * D * (dyb ? 3 : 2), s);
+  } else {
+    (void)hipMemsetAsync(dg, 0, sizeof(float) * D, s);
+    (void)hipMemsetAsync(db, 0, sizeof(float) * D, s);
+    if (dyb) (void)hipMemsetAsync(dyb, 0, sizeof(float) * D, s);
+  }
   if (post)
     hipLaunchKernelGGL((add_ln_bwd_kernel<VEC, true>), dim3(nb), dim3(256), 0, s, (const bf16_t*)dout,
                        (const bf16_t*)hsave, mean, rstd, (const bf16_t*)g, (bf16_t*)dres, (bf16_t*)dy,
