@@ -103,6 +103,20 @@ __global__ void __launch_bounds__(256) lxent_fwd_kernel(
 
   const int vbeg = split * v_per_split;
   const int vend = min(V, vbeg + v_per_split);
+  // a block of only ignored targets (e.g. the unmasked tokens of the logged nll, sorted
+  // to the end by the caller) skips the vocabulary sweep: loss 0, neutral statistics
+  if (!__syncthreads_or(tg >= 0 && tg < V)) {
+    if (h == 0 && tok_ok) {
+      if (nsplit == 1) {
+        loss[t] = 0.f;
+        lse_out[t] = 0.f;
+      } else {
+        part_m[(int64_t)split * N + t] = 0.f;
+        part_s[(int64_t)split * N + t] = 1.f;
+      }
+    }
+    return;
+  }
   float m = -1e30f, ssum = 0.f, tl = -INFINITY;
 
   WTile<E, 256> stage;

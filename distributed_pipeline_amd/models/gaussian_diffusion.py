@@ -236,7 +236,16 @@ class GaussianDiffusion:
     def token_discrete_loss(x, net, input_ids, mask=None):
         """Per-sample CE of the rounding head (DiffuSeq ``_token_discrete_loss``)."""
         B, L = input_ids.shape
-        per_tok = net.token_nll(x.reshape(B * L, -1), input_ids.reshape(-1)).view(B, L)
+        if mask is not None and not torch.is_grad_enabled() and x.is_cuda:
+            # only masked tokens count (the logged nll): sort them first and mark the rest
+            # ignored, so the fused CE kernel skips whole blocks of them (same values)
+            fm = mask.reshape(-1)
+            order = torch.argsort(fm, descending=True, stable=True)
+            ids_s = torch.where(fm[order] != 0, input_ids.reshape(-1)[order], -100)
+            per_s = net.token_nll(x.reshape(B * L, -1)[order], ids_s)
+            per_tok = torch.empty_like(per_s).scatter_(0, order, per_s).view(B, L)
+        else:
+            per_tok = net.token_nll(x.reshape(B * L, -1), input_ids.reshape(-1)).view(B, L)
         if mask is not None:
             m = mask.to(per_tok.dtype)
             return (per_tok * m).sum(-1) / m.sum(-1).clamp_min(1.0)
