@@ -11,7 +11,8 @@
 //   applies dropout and feeds them - still in registers - as the A operand of
 //   O = P^T V, with V read transposed from LDS (ds_read_b64_tr_b16).
 //   For L <= 128 a single pass holds the whole S^T column in registers.
-// Backward: two lean kernels, neither with atomics.  kv-kernel: 128 keys per
+// Backward: two lean kernels, neither with atomics (the q-kernel runs first and also
+//   forms delta = rowsum(dO * O) for its queries).  kv-kernel: 128 keys per
 //   workgroup (keys on the lane, K/V in registers), sweeps query tiles:
 //   dV += dropout(P)^T dO and dK += dS^T Q straight from the accumulators.
 //   q-kernel: 128 queries per workgroup (like the forward), sweeps key tiles:
@@ -482,32 +483,6 @@ __global__ void __launch_bounds__(256) attn_fwd_small_kernel(const bf16_t* __res
     }
 }
 
-// delta[b,h,q] = sum_d dO * O
-template <int D>
-__global__ void __launch_bounds__(256) attn_delta_kernel(const bf16_t* __restrict__ dout,
-                                                        const bf16_t* __restrict__ out,
-                                                        float* __restrict__ delta, int B, int L, int H) {
-  const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;  // (b, q, h)
-  if (idx >= (int64_t)B * L * H) return;
-  const int hd = (int)(idx % H);
-  const int64_t bq = idx / H;
-  const int q = (int)(bq % L), b = (int)(bq / L);
-  const bf16_t* d = dout + idx * D;
-  const bf16_t* o = out + idx * D;
-  float s = 0.f;
-#pragma unroll
-  for (int c = 0; c < D / 8; ++c) {
-    uint4 a = *reinterpret_cast<const uint4*>(d + c * 8);
-    uint4 bb = *reinterpret_cast<const uint4*>(o + c * 8);
-    const uint32_t aw[4] = {a.x, a.y, a.z, a.w}, bw[4] = {bb.x, bb.y, bb.z, bb.w};
-#pragma unroll
-    for (int k = 0; k < 4; ++k) {
-      s += __uint_as_float(aw[k] << 16) * __uint_as_float(bw[k] << 16);
-      s += __uint_as_float(aw[k] & 0xffff0000u) * __uint_as_float(bw[k] & 0xffff0000u);
-    }
-  }
-  delta[((int64_t)b * H + hd) * L + q] = s;
-}
 
 // ---------------------------------------------------------------------------
 // backward, part 1: dK, dV.  Workgroup = 128 keys (4 waves x 32, keys on the
@@ -649,8 +624,8 @@ __global__ void __launch_bounds__(256, D == 64 ? 2 : 1) attn_bwd_kv_kernel(
 template <int D, bool CAUSAL>
 __global__ void __launch_bounds__(256, D == 64 ? 2 : 1) attn_bwd_q_kernel(
     const bf16_t* __restrict__ qkv, const bf16_t* __restrict__ dout, const float* __restrict__ lse,
-    const float* __restrict__ delta, bf16_t* __restrict__ dqkv, int L, int H, float p,
-    uint32_t seed, uint32_t offset) {
+    float* __restrict__ delta, bf16_t* __restrict__ dqkv, int L, int H, float p,
+    uint32_t seed, uint32_t offset, const bf16_t* __restrict__ out) {
   __shared__ __attribute__((aligned(16))) char smem[2 * 64 * 2 * D];
   char* kt_lds = smem;
   char* vt_lds = smem + 64 * 2 * D;
@@ -676,7 +651,21 @@ __global__ void __launch_bounds__(256, D == 64 ? 2 : 1) attn_bwd_q_kernel(
   }
   const int64_t lrow = ((int64_t)b * H + hd) * L;
   const float lse2 = q_ok ? lse[lrow + q] * 1.4426950408889634f : 0.f;
-  const float dlt = q_ok ? delta[lrow + q] : 0.f;
+  // delta = rowsum(dO * O) of this lane's query, from the dO fragments already in
+  // registers and the matching O chunks (the two lane halves hold complementary
+  // columns); published for the dK/dV kernel, which runs after this one
+  float dlt = 0.f;
+  if (q_ok) {
+    const bf16_t* obq = out + ((int64_t)b * L + q) * ldo + (int64_t)hd * D;
+#pragma unroll
+    for (int s = 0; s < D / 16; ++s) {
+      const bf16x8 of = ld_frag(obq + 16 * s + 8 * hf);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) dlt += bf2f(df[s][j]) * bf2f(of[j]);
+    }
+  }
+  dlt += __shfl_xor(dlt, 32, 64);
+  if (q_ok && hf == 0) delta[lrow + q] = dlt;
   const DropCfg dc = make_drop(p, seed, offset, (uint32_t)(b * H + hd));
   const uint32_t qterm = (uint32_t)q * DROP_CQ;
   f32x16 dq[D / 32];
@@ -787,19 +776,20 @@ template <int D>
 static void attn_bwd_general(const uint16_t* qkv, const uint16_t* out, const uint16_t* dout,
                              const float* lse, float* delta, uint16_t* dqkv, int B, int L, int H,
                              float p, bool causal, uint32_t seed, uint32_t offset, hipStream_t s) {
-  const int64_t rows = (int64_t)B * L * H;
-  hipLaunchKernelGGL(attn_delta_kernel<D>, dim3((unsigned)((rows + 255) / 256)), dim3(256), 0, s,
-                     (const bf16_t*)dout, (const bf16_t*)out, delta, B, L, H);
+  // dQ kernel first: it forms delta = rowsum(dO * O) in-kernel and publishes it for the
+  // dK/dV kernel (no separate delta pass over O and dO)
   dim3 grid((L + 127) / 128, H, B);
   if (causal) {
+    hipLaunchKernelGGL((attn_bwd_q_kernel<D, true>), grid, dim3(256), 0, s, (const bf16_t*)qkv,
+                       (const bf16_t*)dout, lse, delta, (bf16_t*)dqkv, L, H, p, seed, offset,
+                       (const bf16_t*)out);
     hipLaunchKernelGGL((attn_bwd_kv_kernel<D, true>), grid, dim3(256), 0, s, (const bf16_t*)qkv,
                        (const bf16_t*)dout, lse, delta, (bf16_t*)dqkv, L, H, p, seed, offset);
-    hipLaunchKernelGGL((attn_bwd_q_kernel<D, true>), grid, dim3(256), 0, s, (const bf16_t*)qkv,
-                       (const bf16_t*)dout, lse, delta, (bf16_t*)dqkv, L, H, p, seed, offset);
   } else {
-    hipLaunchKernelGGL((attn_bwd_kv_kernel<D, false>), grid, dim3(256), 0, s, (const bf16_t*)qkv,
-                       (const bf16_t*)dout, lse, delta, (bf16_t*)dqkv, L, H, p, seed, offset);
     hipLaunchKernelGGL((attn_bwd_q_kernel<D, false>), grid, dim3(256), 0, s, (const bf16_t*)qkv,
+                       (const bf16_t*)dout, lse, delta, (bf16_t*)dqkv, L, H, p, seed, offset,
+                       (const bf16_t*)out);
+    hipLaunchKernelGGL((attn_bwd_kv_kernel<D, false>), grid, dim3(256), 0, s, (const bf16_t*)qkv,
                        (const bf16_t*)dout, lse, delta, (bf16_t*)dqkv, L, H, p, seed, offset);
   }
 }
