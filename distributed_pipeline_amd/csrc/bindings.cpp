@@ -216,7 +216,9 @@ static std::vector<at::Tensor> add_ln_bwd(const at::Tensor& dout, const at::Tens
                                           const at::Tensor& mean, const at::Tensor& rstd,
                                           const at::Tensor& g, double p, int64_t seed,
                                           int64_t offset, bool need_dres, bool need_dy,
-                                          bool want_dyb, c10::optional<at::Tensor> dh_in, bool post) {
+                                          bool want_dyb, c10::optional<at::Tensor> dh_in, bool post,
+                                          c10::optional<at::Tensor> dg_acc, c10::optional<at::Tensor> db_acc,
+                                          c10::optional<at::Tensor> dyb_acc) {
   CHECK_DEV(dout); CHECK_BF16(dout); CHECK_CONTIG(dout); CHECK_BF16(hs); CHECK_CONTIG(hs);
   const uint16_t* dhp = nullptr;
   if (dh_in.has_value() && dh_in->defined()) {
@@ -233,19 +235,30 @@ static std::vector<at::Tensor> add_ln_bwd(const at::Tensor& dout, const at::Tens
   auto f32 = dout.options().dtype(at::kFloat);
   const int nb = dpa::ln_bwd_blocks(R);
   (void)nb;
-  // dgamma, dbeta and colsum(dy) as consecutive rows of one buffer: one memset zeroes all
+  // dgamma, dbeta and colsum(dy) as consecutive rows of one scratch buffer (one memset),
+  // or accumulated straight onto given fp32 .grad buffers (returned undefined then: no
+  // autograd-side add and no memset)
+  auto acc_ok = [&](const c10::optional<at::Tensor>& t) {
+    return t.has_value() && t->defined() && t->scalar_type() == at::kFloat && t->is_contiguous() &&
+           t->numel() == D && t->device() == dout.device();
+  };
   at::Tensor acc3 = at::empty({3, D}, f32);
   at::Tensor dg = acc3[0], db = acc3[1], dyb;
   if (need_dy && want_dyb) dyb = acc3[2];
+  int zero_mask = 7;
+  const bool ext_g = acc_ok(dg_acc), ext_b = acc_ok(db_acc), ext_y = dyb.defined() && acc_ok(dyb_acc);
+  if (ext_g) { dg = *dg_acc; zero_mask &= ~1; }
+  if (ext_b) { db = *db_acc; zero_mask &= ~2; }
+  if (ext_y) { dyb = *dyb_acc; zero_mask &= ~4; }
   bool ok = dpa::launch_add_ln_bwd(
       bf_ptr(dout), bf_ptr(hs), mean.data_ptr<float>(), rstd.data_ptr<float>(), bf_ptr(g),
       need_dres ? reinterpret_cast<uint16_t*>(dres.data_ptr()) : nullptr,
       need_dy ? reinterpret_cast<uint16_t*>(dy.data_ptr()) : nullptr,
       dyb.defined() ? dyb.data_ptr<float>() : nullptr,
       dg.data_ptr<float>(), db.data_ptr<float>(), R, D, (float)p, (uint32_t)seed, (uint32_t)offset,
-      cur_stream(), dhp, post);
+      cur_stream(), dhp, post, zero_mask);
   TORCH_CHECK(ok, "add_ln_bwd: unsupported hidden size ", D);
-  return {dres, dy, dg, db, dyb};
+  return {dres, dy, ext_g ? at::Tensor() : dg, ext_b ? at::Tensor() : db, ext_y ? at::Tensor() : dyb};
 }
 
 // ---- bias + activation epilogues ------------------------------------------------------
@@ -618,7 +631,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("add_ln_bwd", &add_ln_bwd, "backward of add_ln_fwd -> (dres, dy, dgamma, dbeta, colsum(dy))",
         py::arg("dout"), py::arg("hsave"), py::arg("mean"), py::arg("rstd"), py::arg("gamma"),
         py::arg("p"), py::arg("seed"), py::arg("offset"), py::arg("need_dres"), py::arg("need_dy"),
-        py::arg("want_dy_colsum") = false, py::arg("dh_in") = py::none(), py::arg("post") = false);
+        py::arg("want_dy_colsum") = false, py::arg("dh_in") = py::none(), py::arg("post") = false,
+        py::arg("dg_acc") = py::none(), py::arg("db_acc") = py::none(), py::arg("dyb_acc") = py::none());
   m.def("bias_act_fwd", &bias_act_fwd, "z += bias (in place); y = act(z) -> (z, y)");
   m.def("bias_act_bwd", &bias_act_bwd, "dz = dy*act'(zy); db = colsum(dz) -> (dz, db)");
   m.def("attn_fwd", &attn_fwd, "fused attention forward (head_dim 64/128) -> (out, lse)");

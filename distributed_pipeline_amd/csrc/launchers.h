@@ -59,7 +59,8 @@ int ln_bwd_blocks(int64_t R);
 bool launch_add_ln_bwd(const uint16_t* dout, const uint16_t* hsave, const float* mean,
                        const float* rstd, const uint16_t* g, uint16_t* dres, uint16_t* dy, float* dyb,
                        float* dg, float* db, int64_t R, int D, float p, uint32_t seed, uint32_t off,
-                       hipStream_t s, const uint16_t* dh_in = nullptr, bool post = false);
+                       hipStream_t s, const uint16_t* dh_in = nullptr, bool post = false,
+                       int zero_mask = 7);
 
 // ---- elementwise.hip (bias + activation epilogues) -------------------------------
 void launch_bias_act_fwd(uint16_t* z, const uint16_t* bias, uint16_t* y, int64_t R, int N, int act,

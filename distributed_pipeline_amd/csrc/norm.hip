@@ -270,17 +270,19 @@ template <int VEC>
 static void ln_bwd_impl(const uint16_t* dout, const uint16_t* hsave, const float* mean,
                         const float* rstd, const uint16_t* g, uint16_t* dres, uint16_t* dy,
                         float* dyb, float* dg, float* db, int64_t R, float p, uint32_t seed,
-                        uint32_t off, const uint16_t* dh_in, bool post, hipStream_t s) {
+                        uint32_t off, const uint16_t* dh_in, bool post, int zero_mask, hipStream_t s) {
   constexpr int D = VEC * 64;
   const int nb = ln_bwd_blocks(R);
-  // one memset when the three accumulators are consecutive rows of one buffer (the binding
-  // allocates them so), else one each
-  if (db == dg + D && (dyb == nullptr || dyb == dg + 2 * D)) {
-    (void)hipMemsetAsync(dg, 0, sizeof(float) * D * (dyb ? 3 : 2), s);
+  // zero the accumulators that are scratch (zero_mask bits: 1 dg, 2 db, 4 dyb); the others
+  // are parameter .grad buffers the kernel accumulates onto.  One memset when the scratch
+  // ones are consecutive rows of one buffer (the binding allocates them so).
+  const bool zg = zero_mask & 1, zb = zero_mask & 2, zy = dyb && (zero_mask & 4);
+  if (zg && zb && db == dg + D && (!dyb || !zy || dyb == dg + 2 * D)) {
+    (void)hipMemsetAsync(dg, 0, sizeof(float) * D * (zy ? 3 : 2), s);
   } else {
-    (void)hipMemsetAsync(dg, 0, sizeof(float) * D, s);
-    (void)hipMemsetAsync(db, 0, sizeof(float) * D, s);
-    if (dyb) (void)hipMemsetAsync(dyb, 0, sizeof(float) * D, s);
+    if (zg) (void)hipMemsetAsync(dg, 0, sizeof(float) * D, s);
+    if (zb) (void)hipMemsetAsync(db, 0, sizeof(float) * D, s);
+    if (zy) (void)hipMemsetAsync(dyb, 0, sizeof(float) * D, s);
   }
   if (post)
     hipLaunchKernelGGL((add_ln_bwd_kernel<VEC, true>), dim3(nb), dim3(256), 0, s, (const bf16_t*)dout,
@@ -295,9 +297,9 @@ static void ln_bwd_impl(const uint16_t* dout, const uint16_t* hsave, const float
 bool launch_add_ln_bwd(const uint16_t* dout, const uint16_t* hsave, const float* mean,
                        const float* rstd, const uint16_t* g, uint16_t* dres, uint16_t* dy, float* dyb,
                        float* dg, float* db, int64_t R, int D, float p, uint32_t seed, uint32_t off,
-                       hipStream_t s, const uint16_t* dh_in, bool post) {
+                       hipStream_t s, const uint16_t* dh_in, bool post, int zero_mask) {
   DPA_LN_DISPATCH(D, ln_bwd_impl, dout, hsave, mean, rstd, g, dres, dy, dyb, dg, db, R, p, seed,
-                  off, dh_in, post, s)
+                  off, dh_in, post, zero_mask, s)
   return true;
 }
 

@@ -221,6 +221,25 @@ def _take_db(g):
     return None
 
 
+# marker for ``_lin_param_grads(..., db=_ACCUMULATED)``: the bias gradient was already
+# added onto ``b.grad`` in place by the kernel that produced it
+_ACCUMULATED = object()
+
+
+_GRAD_ACC = os.environ.get("DPA_LN_GRAD_ACC", "1") != "0"
+
+
+def _grad_acc(p):
+    """``p.grad`` when a kernel can accumulate onto it in place (the flat fp32 gradient
+    buffer views of the DDP engine), else None (the gradient is returned to autograd)."""
+    if p is None or not _GRAD_ACC:
+        return None
+    g = p.grad
+    if g is None or g.dtype != torch.float32 or not g.is_contiguous() or g.shape != p.shape:
+        return None
+    return g
+
+
 def _lin_param_grads(w, b, dz, x2, native, db=None):
     """(dW, db) of one Linear from its output-side gradient dz [T, N] and input x2.
 
@@ -228,6 +247,9 @@ def _lin_param_grads(w, b, dz, x2, native, db=None):
     has it) into the fp32 .grad buffers in place (returns None grads).
     Otherwise fp32-output GEMM; db is taken from ``db`` when the caller already
     reduced it, else summed here."""
+    if db is _ACCUMULATED:
+        dw = _accumulate_wgrad(w, dz, x2, None)[0] if native else _mm_fp32(dz.t(), x2)
+        return dw, None
     if native:
         if db is not None:
             dw, _ = _accumulate_wgrad(w, dz, x2, None)
@@ -387,6 +409,7 @@ class _MLPLNFn(torch.autograd.Function):
                                                       off)
         ctx.save_for_backward(x2, w1_16, w2_16, h, z1, hsave, mean, rstd, lw16)
         ctx.params = (w1, b1, w2, b2)
+        ctx.ln_params = (lw, lb)
         ctx.cfg = cfg
         ctx.ln = (p, seed, off)
         ctx.shp = shp
@@ -397,9 +420,14 @@ class _MLPLNFn(torch.autograd.Function):
         x2, w1_16, w2_16, h, z1, hsave, mean, rstd, lw16 = ctx.saved_tensors
         p, seed, off = ctx.ln
         need_dx = ctx.needs_input_grad[0]
+        lw, lb = ctx.ln_params
+        b2 = ctx.params[3]
+        gb2 = _grad_acc(b2)
         dres, dy, dlw, dlb, dyb = get_ext().add_ln_bwd(
             dout.reshape(-1, dout.shape[-1]).contiguous(), hsave, mean, rstd, lw16, float(p), seed,
-            off, need_dx, True, True)
+            off, need_dx, True, True, dg_acc=_grad_acc(lw), db_acc=_grad_acc(lb), dyb_acc=gb2)
+        if b2 is not None and dyb is None:
+            dyb = _ACCUMULATED  # fc2's bias gradient went onto b2.grad in the LN kernel
         dx, dw1, db1, dw2, db2 = _mlp_bwd(dy, x2, w1_16, w2_16, h, z1, ctx.params, ctx.cfg, need_dx,
                                           db2=dyb, dx_acc=dres)
         if dx is not None:
@@ -433,6 +461,7 @@ class _AttnLNFn(torch.autograd.Function):
                                                       off_l)
         ctx.save_for_backward(x2, qkv3, o, lse, wq16, wo16, hsave, mean, rstd, lw16)
         ctx.params = (wq, bq, wo, bo)
+        ctx.ln_params = (lw, lb)
         ctx.cfg = (heads, p_attn, seed_a, off_a, p, seed_l, off_l, rq, ro)
         ctx.shp = shp
         return out.reshape(shp)
@@ -444,9 +473,12 @@ class _AttnLNFn(torch.autograd.Function):
         heads, p_attn, seed_a, off_a, p, seed_l, off_l, rq, ro = ctx.cfg
         need_dx = ctx.needs_input_grad[0]
         ext = get_ext()
+        lw, lb = ctx.ln_params
         dres, dy, dlw, dlb, dyb = ext.add_ln_bwd(
             dout.reshape(-1, dout.shape[-1]).contiguous(), hsave, mean, rstd, lw16, float(p), seed_l,
-            off_l, need_dx, True, True)
+            off_l, need_dx, True, True, dg_acc=_grad_acc(lw), db_acc=_grad_acc(lb), dyb_acc=_grad_acc(bo))
+        if bo is not None and dyb is None:
+            dyb = _ACCUMULATED  # the out projection's bias gradient went onto bo.grad
         # out projection
         o2 = o.view(-1, o.shape[-1])
         do = _dgrad(dy, wo16, ro[1])
@@ -528,15 +560,18 @@ class _AddLNFn(torch.autograd.Function):
                                                       seed, offset)
         ctx.save_for_backward(hsave, mean, rstd, w16)
         ctx.cfg = (p, seed, offset, residual is not None)
+        ctx.wb = (w, b)
         return out
 
     @staticmethod
     def backward(ctx, dout):
         hsave, mean, rstd, w16 = ctx.saved_tensors
         p, seed, offset, has_res = ctx.cfg
+        w, b = ctx.wb
         dres, dy, dw, db, dyb = get_ext().add_ln_bwd(dout.contiguous(), hsave, mean, rstd, w16,
                                                      float(p), seed, offset, has_res,
-                                                     ctx.needs_input_grad[0], ctx.needs_input_grad[0])
+                                                     ctx.needs_input_grad[0], ctx.needs_input_grad[0],
+                                                     dg_acc=_grad_acc(w), db_acc=_grad_acc(b))
         if dy is not None:
             _offer_db(dy, dyb)
         return dy, (dres if has_res else None), dw, db, None, None, None, None, None, None
@@ -556,6 +591,7 @@ class _AddLNExFn(torch.autograd.Function):
                                                       offset, pos, temb, int(L), bool(post))
         ctx.save_for_backward(hsave, mean, rstd, w16)
         ctx.cfg = (p, seed, offset, residual is not None, pos is not None, temb is not None, post, L)
+        ctx.wb = (w, b)
         ctx.set_materialize_grads(False)  # an unused h (last layer, input block) costs nothing
         return out, hsave
 
@@ -567,9 +603,11 @@ class _AddLNExFn(torch.autograd.Function):
         need_dy = ng[0] or (has_pos and ng[2]) or (has_temb and ng[3])
         if dout is None:
             dout = torch.zeros_like(hsave)
+        w, b = ctx.wb
         dres, dy, dw, db, _ = get_ext().add_ln_bwd(
             dout.contiguous(), hsave, mean, rstd, w16, float(p), seed, offset, has_res and ng[1], need_dy,
-            False, dh_in=None if dh is None else dh.contiguous(), post=bool(post))
+            False, dh_in=None if dh is None else dh.contiguous(), post=bool(post),
+            dg_acc=_grad_acc(w), db_acc=_grad_acc(b))
         dpos = dtemb = None
         if need_dy:
             H = dy.shape[-1]

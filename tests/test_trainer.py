@@ -106,7 +106,9 @@ def test_microbatch_fusion_gives_same_gradients(tmp_path, monkeypatch):
     """exec_microbatch=8 (one fused fwd/bwd) == two semantic micro-batches of 4."""
     from distributed_pipeline_amd.models.resample import FixSampler
     monkeypatch.setattr(torch, "randn_like", lambda x: torch.zeros_like(x))  # deterministic noise
-    a = _loop(tmp_path / "a", "native", steps=1, save_interval=100)
+    # exec_microbatch=-1: execute the semantic micro-batches as they are (the auto default
+    # fuses them on a GPU)
+    a = _loop(tmp_path / "a", "native", steps=1, save_interval=100, exec_microbatch=-1)
     b = _loop(tmp_path / "b", "native", steps=1, save_interval=100, exec_microbatch=8)
     assert a.exec_microbatch == 4 and b.exec_microbatch == 8 and b.loss_scale == 2
     a.schedule_sampler = FixSampler(a.diffusion.num_timesteps)
@@ -125,7 +127,7 @@ def test_microbatch_fusion_uneven_chunks(tmp_path, monkeypatch, mb, exec_mb):
     the reference's per-micro-batch means do (per-chunk loss scale)."""
     from distributed_pipeline_amd.models.resample import FixSampler
     monkeypatch.setattr(torch, "randn_like", lambda x: torch.zeros_like(x))
-    a = _loop(tmp_path / "a", "native", steps=1, save_interval=100, microbatch=mb)
+    a = _loop(tmp_path / "a", "native", steps=1, save_interval=100, microbatch=mb, exec_microbatch=-1)
     b = _loop(tmp_path / "b", "native", steps=1, save_interval=100, microbatch=mb,
               exec_microbatch=exec_mb)
     assert a.exec_microbatch == mb and b.exec_microbatch == exec_mb
