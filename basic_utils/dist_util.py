@@ -152,7 +152,7 @@ def barrier(*args, **kwargs):
     if is_initialized():
         if (dist.get_backend() == "nccl" and _cuda_available()
                 and "device_ids" not in kwargs):
-            kwargs["device_ids"] = [get_local_rank()]
+            kwargs["device_ids"] = [dev().index]
         return dist.barrier(*args, **kwargs)
 
 
