@@ -137,6 +137,37 @@ __device__ __forceinline__ void stage64(char* lds, const bf16_t* __restrict__ sr
 // ---------------------------------------------------------------------------
 // forward
 // ---------------------------------------------------------------------------
+// Work item (row tile, head, batch) of a 1-D grid of NT x H x B blocks (NT = L/128 row
+// tiles).  Blocks are dealt round-robin over the 8 XCDs (MI355X_MICROARCH "Workgroup
+// dispatch"), so the plain 3-D grid (tile fastest, NT = 8 at L = 1024) put every block
+// of row tile k on one XCD: causal work per tile is 1..NT units, and the XCD holding the
+// heaviest tile finished last (~NT / ((NT + 1) / 2) = 1.8x the balanced time).  Here the
+// 8 consecutive blocks dealt to the 8 XCDs share a tile index and take 8 different
+// (b, h); the tile index advances every 8 blocks, so each XCD sees every tile of its
+// (b, h) items back to back (K/V panel reuse in that XCD's L2) and the same work mix as
+// the others.  HEAVY_HIGH: tile t costs t + 1 units (queries; fwd, dQ) - issued heaviest
+// first; else NT - t (keys; dK/dV).
+struct AttnItem { int t, hd, b; };
+template <bool HEAVY_HIGH>
+__device__ __forceinline__ AttnItem attn_item(int L, int H) {
+  const int NT = (L + 127) / 128;
+  const int i = blockIdx.x, BH = gridDim.x / NT;
+  int r, bh;
+  if ((BH & 7) == 0) {
+    const int j = i >> 3;
+    r = j % NT;
+    bh = (j / NT) * 8 + (i & 7);
+  } else {
+    r = i % NT;
+    bh = i / NT;
+  }
+  AttnItem it;
+  it.t = HEAVY_HIGH ? NT - 1 - r : r;
+  it.hd = bh % H;
+  it.b = bh / H;
+  return it;
+}
+
 template <int D, bool CAUSAL>
 __global__ void __launch_bounds__(256) attn_fwd_kernel(const bf16_t* __restrict__ qkv,
                                                       bf16_t* __restrict__ out, float* __restrict__ lse,
@@ -145,13 +176,14 @@ __global__ void __launch_bounds__(256) attn_fwd_kernel(const bf16_t* __restrict_
   __shared__ __attribute__((aligned(16))) char smem[2 * 64 * 2 * D];
   char* kt_lds = smem;
   char* vt_lds = smem + 64 * 2 * D;
-  const int b = blockIdx.z, hd = blockIdx.y;
+  const AttnItem it = attn_item<true>(L, H);
+  const int b = it.b, hd = it.hd;
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, hf = lane >> 5;
   const int64_t ld = 3LL * H * D;  // token stride
   const bf16_t* qb = qkv + (int64_t)b * L * ld + (int64_t)hd * D;
   const bf16_t* kb = qb + (int64_t)H * D;
   const bf16_t* vb = qb + 2LL * H * D;
-  const int qbase = blockIdx.x * 128 + w * 32;
+  const int qbase = it.t * 128 + w * 32;
   const int q = qbase + (lane & 31);
   const bool q_ok = q < L;
   bf16x8 qf[D / 16];
@@ -161,7 +193,7 @@ __global__ void __launch_bounds__(256) attn_fwd_kernel(const bf16_t* __restrict_
     else for (int j = 0; j < 8; ++j) qf[s][j] = 0;
   }
   const DropCfg dc = make_drop(p, seed, offset, (uint32_t)(b * H + hd));
-  const int kv_end = CAUSAL ? min(L, (int)blockIdx.x * 128 + 128) : L;
+  const int kv_end = CAUSAL ? min(L, it.t * 128 + 128) : L;
 
   // ---- pass 1: row statistics -------------------------------------------------
   float m = -1e30f, l = 0.f;
@@ -263,13 +295,14 @@ __global__ void __launch_bounds__(256, D == 64 ? 2 : 1) attn_fwd_online_kernel(c
   __shared__ __attribute__((aligned(16))) char smem[2 * 64 * 2 * D];
   char* kt_lds = smem;
   char* vt_lds = smem + 64 * 2 * D;
-  const int b = blockIdx.z, hd = blockIdx.y;
+  const AttnItem it = attn_item<true>(L, H);
+  const int b = it.b, hd = it.hd;
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, hf = lane >> 5;
   const int64_t ld = 3LL * H * D;
   const bf16_t* qb = qkv + (int64_t)b * L * ld + (int64_t)hd * D;
   const bf16_t* kb = qb + (int64_t)H * D;
   const bf16_t* vb = qb + 2LL * H * D;
-  const int qbase = blockIdx.x * 128 + w * 32;
+  const int qbase = it.t * 128 + w * 32;
   const int q = qbase + (lane & 31);
   const bool q_ok = q < L;
   bf16x8 qf[D / 16];
@@ -280,7 +313,7 @@ __global__ void __launch_bounds__(256, D == 64 ? 2 : 1) attn_fwd_online_kernel(c
   }
   const DropCfg dc = make_drop(p, seed, offset, (uint32_t)(b * H + hd));
   const uint32_t qterm = (uint32_t)q * DROP_CQ;
-  const int kv_end = CAUSAL ? min(L, (int)blockIdx.x * 128 + 128) : L;
+  const int kv_end = CAUSAL ? min(L, it.t * 128 + 128) : L;
   // source lane (in this half's numbering) of the query that register i of O belongs to
   int src[16];
 #pragma unroll
@@ -501,14 +534,15 @@ __global__ void __launch_bounds__(256, D == 64 ? 2 : 1) attn_bwd_kv_kernel(
   char* dot_lds = smem + 64 * 2 * D;
   float* s_lse = reinterpret_cast<float*>(smem + 2 * 64 * 2 * D);
   float* s_del = s_lse + 64;
-  const int b = blockIdx.z, hd = blockIdx.y;
+  const AttnItem it = attn_item<false>(L, H);
+  const int b = it.b, hd = it.hd;
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, hf = lane >> 5;
   const int64_t ld = 3LL * H * D, ldo = (int64_t)H * D;
   const bf16_t* qb = qkv + (int64_t)b * L * ld + (int64_t)hd * D;
   const bf16_t* kb = qb + (int64_t)H * D;
   const bf16_t* vb = qb + 2LL * H * D;
   const bf16_t* dob = dout + (int64_t)b * L * ldo + (int64_t)hd * D;
-  const int kbase = blockIdx.x * 128 + w * 32;
+  const int kbase = it.t * 128 + w * 32;
   const int key = kbase + (lane & 31);
   const bool k_ok = key < L;
   bf16x8 kf[D / 16], vf[D / 16];
@@ -526,7 +560,7 @@ __global__ void __launch_bounds__(256, D == 64 ? 2 : 1) attn_bwd_kv_kernel(
   f32x16 dk[D / 32], dv[D / 32];
 #pragma unroll
   for (int dt = 0; dt < D / 32; ++dt) { dk[dt] = zero16(); dv[dt] = zero16(); }
-  const int qbeg = CAUSAL ? (int)blockIdx.x * 128 : 0;
+  const int qbeg = CAUSAL ? it.t * 128 : 0;
   TileRegs<D> qr, dr;  // register prefetch of the next query tile (Q, dO)
   tile_load<D>(qr, qb, ld, qbeg, L, tid);
   tile_load<D>(dr, dob, ldo, qbeg, L, tid);
@@ -629,14 +663,15 @@ __global__ void __launch_bounds__(256, D == 64 ? 2 : 1) attn_bwd_q_kernel(
   __shared__ __attribute__((aligned(16))) char smem[2 * 64 * 2 * D];
   char* kt_lds = smem;
   char* vt_lds = smem + 64 * 2 * D;
-  const int b = blockIdx.z, hd = blockIdx.y;
+  const AttnItem it = attn_item<true>(L, H);
+  const int b = it.b, hd = it.hd;
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, hf = lane >> 5;
   const int64_t ld = 3LL * H * D, ldo = (int64_t)H * D;
   const bf16_t* qb = qkv + (int64_t)b * L * ld + (int64_t)hd * D;
   const bf16_t* kb = qb + (int64_t)H * D;
   const bf16_t* vb = qb + 2LL * H * D;
   const bf16_t* dob = dout + (int64_t)b * L * ldo + (int64_t)hd * D;
-  const int qbase = blockIdx.x * 128 + w * 32;
+  const int qbase = it.t * 128 + w * 32;
   const int q = qbase + (lane & 31);
   const bool q_ok = q < L;
   bf16x8 qf[D / 16], df[D / 16];
@@ -671,7 +706,7 @@ __global__ void __launch_bounds__(256, D == 64 ? 2 : 1) attn_bwd_q_kernel(
   f32x16 dq[D / 32];
 #pragma unroll
   for (int dt = 0; dt < D / 32; ++dt) dq[dt] = zero16();
-  const int kv_end = CAUSAL ? min(L, (int)blockIdx.x * 128 + 128) : L;
+  const int kv_end = CAUSAL ? min(L, it.t * 128 + 128) : L;
   TileRegs<D> kr, vr;  // register prefetch of the next key tile (K, V)
   tile_load<D>(kr, kb, ld, 0, L, tid);
   tile_load<D>(vr, vb, ld, 0, L, tid);
@@ -731,7 +766,7 @@ __global__ void __launch_bounds__(256, D == 64 ? 2 : 1) attn_bwd_q_kernel(
 template <int D>
 static void attn_fwd_general(const uint16_t* qkv, uint16_t* out, float* lse, int B, int L, int H,
                              float p, bool causal, uint32_t seed, uint32_t offset, hipStream_t s) {
-  dim3 grid((L + 127) / 128, H, B);
+  dim3 grid((unsigned)((L + 127) / 128 * H * B));  // attn_item() layout
   static const bool two_pass = [] {
     const char* e = getenv("DPA_ATTN_TWOPASS");
     return e != nullptr && e[0] == '1';
@@ -778,7 +813,7 @@ static void attn_bwd_general(const uint16_t* qkv, const uint16_t* out, const uin
                              float p, bool causal, uint32_t seed, uint32_t offset, hipStream_t s) {
   // dQ kernel first: it forms delta = rowsum(dO * O) in-kernel and publishes it for the
   // dK/dV kernel (no separate delta pass over O and dO)
-  dim3 grid((L + 127) / 128, H, B);
+  dim3 grid((unsigned)((L + 127) / 128 * H * B));  // attn_item() layout
   if (causal) {
     hipLaunchKernelGGL((attn_bwd_q_kernel<D, true>), grid, dim3(256), 0, s, (const bf16_t*)qkv,
                        (const bf16_t*)dout, lse, delta, (bf16_t*)dqkv, L, H, p, seed, offset,
