@@ -154,7 +154,7 @@ __global__ void __launch_bounds__(256, 4) add_ln_bwd_kernel(
     float* __restrict__ dyb, float* __restrict__ part_dg, float* __restrict__ part_db, int64_t R,
     float p, uint32_t seed, uint32_t offset, const bf16_t* __restrict__ dh_in) {
   constexpr int D = VEC * 64;
-  __shared__ float red[3][4][D];
+  __shared__ float red[4][D];  // reused for dgamma, dbeta, dyb in turn (D = 2048: 32 KiB)
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int col0 = lane * VEC;
   float g[VEC], adg[VEC], adb[VEC], ady[VEC];
@@ -211,18 +211,18 @@ __global__ void __launch_bounds__(256, 4) add_ln_bwd_kernel(
       }
     }
   }
+  // one fp32 atomic per column per block and accumulator (dg/db/dyb zeroed by the
+  // launcher or accumulated onto the parameter grads)
+  float* const dst[3] = {part_dg, part_db, dyb};
 #pragma unroll
-  for (int i = 0; i < VEC; ++i) {
-    red[0][w][col0 + i] = adg[i];
-    red[1][w][col0 + i] = adb[i];
-    red[2][w][col0 + i] = ady[i];
-  }
-  __syncthreads();
-  // one fp32 atomic per column per block (dg/db/dyb zeroed by the launcher)
-  for (int c = threadIdx.x; c < D; c += blockDim.x) {
-    atomicAdd(part_dg + c, red[0][0][c] + red[0][1][c] + red[0][2][c] + red[0][3][c]);
-    atomicAdd(part_db + c, red[1][0][c] + red[1][1][c] + red[1][2][c] + red[1][3][c]);
-    if (dyb) atomicAdd(dyb + c, red[2][0][c] + red[2][1][c] + red[2][2][c] + red[2][3][c]);
+  for (int a = 0; a < 3; ++a) {
+    if (a == 2 && !dyb) break;
+    if (a) __syncthreads();  // previous accumulator's columns have been read
+#pragma unroll
+    for (int i = 0; i < VEC; ++i) red[w][col0 + i] = a == 0 ? adg[i] : a == 1 ? adb[i] : ady[i];
+    __syncthreads();
+    for (int c = threadIdx.x; c < D; c += blockDim.x)
+      atomicAdd(dst[a] + c, red[0][c] + red[1][c] + red[2][c] + red[3][c]);
   }
 }
 

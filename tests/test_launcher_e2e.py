@@ -84,3 +84,5 @@ def test_bench_contract_two_ranks_gloo():
     assert d["config"]["parallelism"] == "dp2" and d["config"]["global_batch"] == 16
     assert abs(d["value"] - 2 * d["optimizer_steps_per_sec"]) < 1e-3 * d["value"]
     assert abs(d["ms_per_step"] - 1e3 / d["optimizer_steps_per_sec"]) < 1e-2 * d["ms_per_step"]
+    # the BASELINE metric / ratio belong to the headline config only
+    assert d["vs_baseline"] is None and "tiny" in d["metric"]
