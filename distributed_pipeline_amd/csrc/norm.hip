@@ -145,9 +145,11 @@ __global__ void __launch_bounds__(256) add_ln_fwd_kernel(
 
 // grid-stride over rows; block = 4 waves; partial dgamma/dbeta per block.
 // POST at compile time (the two dropout placements share no loop body) and <= 128 VGPRs
-// (4 waves per SIMD: the LDS reduction buffer allows 4 blocks per CU)
+// (4 waves per SIMD: the LDS reduction buffer allows 4 blocks per CU); D > 768 keeps
+// 6 x VEC live accumulator/row floats: 2 waves per SIMD up to D = 1536, 1 for D = 2048
+// (512 VGPRs) - no scratch spills at any width
 template <int VEC, bool POST>
-__global__ void __launch_bounds__(256, 4) add_ln_bwd_kernel(
+__global__ void __launch_bounds__(256, VEC <= 12 ? 4 : VEC <= 24 ? 2 : 1) add_ln_bwd_kernel(
     const bf16_t* __restrict__ dout, const bf16_t* __restrict__ hsave,
     const float* __restrict__ mean_in, const float* __restrict__ rstd_in,
     const bf16_t* __restrict__ gamma, bf16_t* __restrict__ dres, bf16_t* __restrict__ dy,
