@@ -247,6 +247,8 @@ def main():
         out["config"]["comm"] = ("reducer-owned RCCL communicator, priority %d stream" % nat.stream_priority()
                                  if nat is not None and nat.direct() else
                                  ("c10d process group" if world > 1 else "none (world 1)"))
+    if dev.type == "cuda":  # HBM headroom of the fused schedule (288 GB per MI355X)
+        out["peak_hbm_gb"] = round(torch.cuda.max_memory_allocated(dev) / 2**30, 1)
     if rank == 0:
         out["topology"] = topology()
     if rank == 0:

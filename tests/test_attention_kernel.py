@@ -29,7 +29,9 @@ def _ref(qkv, H, causal, keep=None, p=0.0):
 
 @pytest.mark.parametrize("B,L,H,causal", [(3, 128, 4, False), (2, 64, 2, False), (2, 256, 3, False),
                                             (2, 128, 2, True), (1, 512, 2, True),
-                                            (48, 128, 12, False)])  # > #CUs items: persistent loop
+                                            (48, 128, 12, False),  # > #CUs items: persistent loop
+                                            # B*H % 8 == 0: the XCD-interleaved tile order of attn_item()
+                                            (4, 384, 2, True), (2, 320, 4, False)])
 def test_attention_no_dropout(B, L, H, causal):
     torch.manual_seed(0)
     qkv = (torch.randn(B, L, 3 * H * 64, device="cuda") * 0.7).bfloat16()
@@ -84,6 +86,7 @@ def test_attention_dropout_consistent_with_mask():
 
 
 @pytest.mark.parametrize("B,L,H,causal", [(2, 128, 4, False), (2, 256, 2, False), (2, 192, 2, True),
+                                            (4, 256, 2, True),
                                             (1, 512, 2, True)])
 def test_attention_head_dim_128(B, L, H, causal):
     """DiffuSeq-XL heads (2048 / 16 = 128): the general two-pass kernels templated on D."""
