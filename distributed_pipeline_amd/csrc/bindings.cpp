@@ -130,9 +130,12 @@ static std::vector<at::Tensor> lxent_fwd_dx(const at::Tensor& x, const at::Tenso
   const int N = (int)x.size(0), V = (int)W.size(0), E = (int)x.size(1);
   auto f32 = x.options().dtype(at::kFloat);
   at::Tensor loss = at::empty({N}, f32), lse = at::empty({N}, f32), dxu = at::empty({N, E}, f32);
+  const int64_t wsn = N > 0 ? dpa::lxent_fwd_dx_workspace_floats(N, V, E) : 0;
+  at::Tensor ws = at::empty({wsn}, f32);
   if (N > 0)
     dpa::launch_lxent_fwd_dx(bf_ptr(x), bf_ptr(W), opt_bf_ptr(b), tgt.data_ptr<int64_t>(), N, V, E,
-                             loss.data_ptr<float>(), lse.data_ptr<float>(), dxu.data_ptr<float>(), cur_stream());
+                             loss.data_ptr<float>(), lse.data_ptr<float>(), dxu.data_ptr<float>(), cur_stream(),
+                             wsn ? ws.data_ptr<float>() : nullptr);
   return {loss, lse, dxu};
 }
 

@@ -37,7 +37,10 @@ void launch_cast_f32(const uint16_t* src, float* dst, int64_t n, hipStream_t s);
 int64_t lxent_workspace_floats(int N, int V);
 // forward + unscaled input gradient in one sweep: dxu[t] = softmax_t . W - W[target_t] (fp32)
 void launch_lxent_fwd_dx(const uint16_t* x, const uint16_t* W, const uint16_t* b, const int64_t* tgt,
-                         int N, int V, int E, float* loss, float* lse, float* dxu, hipStream_t s);
+                         int N, int V, int E, float* loss, float* lse, float* dxu, hipStream_t s,
+                         float* ws = nullptr);
+// fp32 workspace of the vocabulary-split fused forward (0: no split for this shape)
+int64_t lxent_fwd_dx_workspace_floats(int N, int V, int E);
 bool lxent_dx_needs_acc(int N);
 void launch_lxent_fwd(const uint16_t* x, const uint16_t* W, const uint16_t* b, const int64_t* tgt,
                       int N, int V, int E, float* loss, float* lse, float* ws, hipStream_t s);

@@ -311,9 +311,13 @@ template <int E>
 __global__ void __launch_bounds__(256, E == 128 ? 2 : 1) lxent_fwd_dx_kernel(
     const bf16_t* __restrict__ x, const bf16_t* __restrict__ W, const bf16_t* __restrict__ bias,
     const int64_t* __restrict__ target, int N, int V, float* __restrict__ loss,
-    float* __restrict__ lse_out, float* __restrict__ dxu) {
+    float* __restrict__ lse_out, float* __restrict__ dxu, int vps, float* __restrict__ part) {
   constexpr int KS = E / 16, ROWB = E * 2, KT = E / 32;
   __shared__ __attribute__((aligned(16))) char smem[64 * ROWB + 64 * 4];
+  // vocabulary split (part != nullptr, few token blocks): this block sweeps rows
+  // [v_lo, v_hi) and leaves (m, l, target logit, unnormalised u) for lxent_fwd_dx_combine
+  const int v_lo = part ? (int)blockIdx.y * vps : 0;
+  const int v_hi = part ? min(V, v_lo + vps) : V;
   char* wt = smem;
   float* bt = reinterpret_cast<float*>(smem + 64 * ROWB);
 
@@ -333,15 +337,15 @@ __global__ void __launch_bounds__(256, E == 128 ? 2 : 1) lxent_fwd_dx_kernel(
   float m = -1e30f, l = 0.f, tl = -INFINITY;  // m in the log2 domain
 
   WTile<E, 256> stage;
-  stage.load(W, 0, V, tid);
-  for (int v0 = 0; v0 < V; v0 += 64) {
+  stage.load(W, v_lo, V, tid);
+  for (int v0 = v_lo; v0 < v_hi; v0 += 64) {
     stage.store(wt, tid);
     if (tid < 64) {
       const int v = v0 + tid;
-      bt[tid] = (v < V) ? (bias ? bf2f(bias[v]) : 0.f) : -INFINITY;
+      bt[tid] = (v < v_hi) ? (bias ? bf2f(bias[v]) : 0.f) : -INFINITY;
     }
     __syncthreads();
-    if (v0 + 64 < V) stage.load(W, v0 + 64, V, tid);  // prefetch behind the MFMAs
+    if (v0 + 64 < v_hi) stage.load(W, v0 + 64, V, tid);  // prefetch behind the MFMAs
 
     // one 32-row vocabulary subtile at a time (a single live logit accumulator keeps
     // the kernel at 2 waves / SIMD); each subtile is one online-softmax step
@@ -397,6 +401,28 @@ __global__ void __launch_bounds__(256, E == 128 ? 2 : 1) lxent_fwd_dx_kernel(
   }
   l += __shfl_xor(l, 32, 64);
   tl = fmaxf(tl, __shfl_xor(tl, 32, 64));
+  if (part) {
+    const int S = gridDim.y, sp = blockIdx.y;
+    float* pm = part;
+    float* pl = pm + (int64_t)S * N;
+    float* pt = pl + (int64_t)S * N;
+    float* pu = pt + (int64_t)S * N;
+    if (h == 0 && tok_ok) {
+      pm[(int64_t)sp * N + t] = m;
+      pl[(int64_t)sp * N + t] = l;
+      pt[(int64_t)sp * N + t] = tl;
+    }
+    const int tb0 = blockIdx.x * 128 + w * 32;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+      const int tt = tb0 + acc_row(i, h);
+      if (tt < N) {
+#pragma unroll
+        for (int kt = 0; kt < KT; ++kt) pu[((int64_t)sp * N + tt) * E + kt * 32 + (lane & 31)] = dacc[kt][i];
+      }
+    }
+    return;
+  }
   const bool valid = tok_ok && tg >= 0 && tg < V;
   const float lse = (m + log2f(l)) * LN2;
   if (h == 0 && tok_ok) {
@@ -422,6 +448,41 @@ __global__ void __launch_bounds__(256, E == 128 ? 2 : 1) lxent_fwd_dx_kernel(
       }
     }
   }
+}
+
+// Merge of the vocabulary splits of lxent_fwd_dx_kernel: per token the split maxima
+// (log2 domain) give M, L = sum_s l_s 2^(m_s - M), lse = (M + log2 L) ln 2, and
+// dxu = sum_s 2^(m_s - M) u_s / L - W[target].  One thread per (token, column).
+template <int E>
+__global__ void __launch_bounds__(256) lxent_fwd_dx_combine_kernel(
+    const float* __restrict__ part, int S, const bf16_t* __restrict__ W, const int64_t* __restrict__ target,
+    int N, int V, float* __restrict__ loss, float* __restrict__ lse_out, float* __restrict__ dxu) {
+  const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (idx >= (int64_t)N * E) return;
+  const int t = (int)(idx / E), k = (int)(idx % E);
+  const float* pm = part;
+  const float* pl = pm + (int64_t)S * N;
+  const float* pt = pl + (int64_t)S * N;
+  const float* pu = pt + (int64_t)S * N;
+  float M = -1e30f, tl = -INFINITY;
+  for (int s = 0; s < S; ++s) {
+    M = fmaxf(M, pm[(int64_t)s * N + t]);
+    tl = fmaxf(tl, pt[(int64_t)s * N + t]);
+  }
+  float L = 0.f, u = 0.f;
+  for (int s = 0; s < S; ++s) {
+    const float f = fexp2(pm[(int64_t)s * N + t] - M);
+    L += pl[(int64_t)s * N + t] * f;
+    u += pu[((int64_t)s * N + t) * E + k] * f;
+  }
+  const int64_t tg = target[t];
+  const bool valid = tg >= 0 && tg < V;
+  const float lse = (M + log2f(L)) * LN2;
+  if (k == 0) {
+    loss[t] = valid ? lse - tl : 0.f;
+    lse_out[t] = lse;
+  }
+  dxu[(int64_t)t * E + k] = valid ? u / L - bf2f(W[tg * E + k]) : 0.f;
 }
 
 // ---------------------------------------------------------------------------
@@ -606,15 +667,51 @@ static void fwd_impl(const bf16_t* x, const bf16_t* W, const bf16_t* b, const in
                        tgt, N, V, Sx, loss, lse);
 }
 
-void launch_lxent_fwd_dx(const uint16_t* x, const uint16_t* W, const uint16_t* b, const int64_t* tgt,
-                         int N, int V, int E, float* loss, float* lse, float* dxu, hipStream_t s) {
+// Vocabulary splits of the fused forward + dx: one block per 128 tokens sweeps the whole
+// vocabulary, so below ~3 blocks per CU (a reference-schedule micro-batch: 8192 tokens =
+// 64 blocks for 256 CUs) the vocabulary is split over gridDim.y and merged afterwards.
+static void fwd_dx_plan(int N, int V, int& S, int& vps) {
+  const int tb = (N + 127) / 128, vchunks = (V + 63) / 64;
+  S = 1;
+  vps = vchunks * 64;
+  if (tb >= 768) return;
+  int want = (768 + tb - 1) / tb;
+  if (want > vchunks) want = vchunks;
+  if (want < 2) return;
+  vps = ((vchunks + want - 1) / want) * 64;
+  S = (V + vps - 1) / vps;
+}
+
+int64_t lxent_fwd_dx_workspace_floats(int N, int V, int E) {
+  int S, vps;
+  fwd_dx_plan(N, V, S, vps);
+  return S > 1 ? (int64_t)S * N * (3 + E) : 0;
+}
+
+template <int E>
+static void fwd_dx_impl(const bf16_t* x, const bf16_t* W, const bf16_t* b, const int64_t* tgt, int N, int V,
+                        float* loss, float* lse, float* dxu, float* ws, hipStream_t s) {
   const unsigned tb = (unsigned)((N + 127) / 128);
+  int S, vps;
+  fwd_dx_plan(N, V, S, vps);
+  if (S > 1 && ws != nullptr) {
+    hipLaunchKernelGGL(lxent_fwd_dx_kernel<E>, dim3(tb, S), dim3(256), 0, s, x, W, b, tgt, N, V, loss, lse,
+                       dxu, vps, ws);
+    const int64_t n = (int64_t)N * E;
+    hipLaunchKernelGGL(lxent_fwd_dx_combine_kernel<E>, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, ws,
+                       S, W, tgt, N, V, loss, lse, dxu);
+  } else {
+    hipLaunchKernelGGL(lxent_fwd_dx_kernel<E>, dim3(tb), dim3(256), 0, s, x, W, b, tgt, N, V, loss, lse, dxu,
+                       V, nullptr);
+  }
+}
+
+void launch_lxent_fwd_dx(const uint16_t* x, const uint16_t* W, const uint16_t* b, const int64_t* tgt,
+                         int N, int V, int E, float* loss, float* lse, float* dxu, hipStream_t s, float* ws) {
   if (E == 128)
-    hipLaunchKernelGGL(lxent_fwd_dx_kernel<128>, dim3(tb), dim3(256), 0, s, (const bf16_t*)x, (const bf16_t*)W,
-                       (const bf16_t*)b, tgt, N, V, loss, lse, dxu);
+    fwd_dx_impl<128>((const bf16_t*)x, (const bf16_t*)W, (const bf16_t*)b, tgt, N, V, loss, lse, dxu, ws, s);
   else
-    hipLaunchKernelGGL(lxent_fwd_dx_kernel<256>, dim3(tb), dim3(256), 0, s, (const bf16_t*)x, (const bf16_t*)W,
-                       (const bf16_t*)b, tgt, N, V, loss, lse, dxu);
+    fwd_dx_impl<256>((const bf16_t*)x, (const bf16_t*)W, (const bf16_t*)b, tgt, N, V, loss, lse, dxu, ws, s);
 }
 
 int64_t lxent_workspace_floats(int N, int V) {

@@ -16,8 +16,11 @@ def _ref(x, W, b, tgt):
     return loss, x, Wf, bf
 
 
+# N < 98304: lxent_fwd_dx splits the vocabulary over blocks and merges (m, l, u) partials;
+# 131072 tokens: one block per 128 tokens sweeps the whole vocabulary
 @pytest.mark.parametrize("N,V,E,with_bias", [(300, 1000, 128, True), (4096, 30522, 128, True),
-                                               (130, 517, 256, False), (70000, 2000, 128, True)])
+                                               (130, 517, 256, False), (70000, 2000, 128, True),
+                                               (131072, 1000, 128, True)])
 def test_lxent_fwd_bwd(N, V, E, with_bias):
     torch.manual_seed(0)
     dev = "cuda"
