@@ -428,8 +428,11 @@ static void gemm_wgrad(const at::Tensor& dy, const at::Tensor& x, at::Tensor& dW
     dbp = db->data_ptr<float>();
   }
   const c10::DeviceGuard guard(dy.device());
+  // split-K merge workspace (stream-ordered caching-allocator block, freed after the launch)
+  const int64_t wsn = dpa::gemm256_wgrad_workspace_floats(T, N, K);
+  at::Tensor ws = at::empty({wsn}, dW.options());
   bool ok = dpa::launch_gemm_wgrad(bf_ptr(dy), bf_ptr(x), dW.data_ptr<float>(), dbp, T, N, K,
-                                   cur_stream());
+                                   cur_stream(), wsn ? ws.data_ptr<float>() : nullptr);
   TORCH_CHECK(ok, "gemm_wgrad: unsupported shape");
 }
 

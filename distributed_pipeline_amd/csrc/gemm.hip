@@ -309,9 +309,9 @@ bool launch_gemm_nn(const uint16_t* dy, const uint16_t* W, uint16_t* dx, int T, 
 }
 
 bool launch_gemm_wgrad(const uint16_t* dy, const uint16_t* x, float* dW, float* db, int T, int N,
-                       int K, hipStream_t s) {
+                       int K, hipStream_t s, float* ws) {
   // dW[N][K] += dy[T][N]^T . x[T][K]: M = N, N' = K, reduction = T (split over workgroups)
-  if (launch_gemm256_wgrad(dy, x, dW, db, T, N, K, s)) return true;
+  if (launch_gemm256_wgrad(dy, x, dW, db, T, N, K, s, ws)) return true;
   if (!gemm_shape_ok(N, K, T)) return false;
   const int tiles = (N / 128) * (K / 128);
   int splits = (1024 + tiles - 1) / tiles;

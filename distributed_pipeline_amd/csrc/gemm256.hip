@@ -299,7 +299,7 @@ __global__ void __launch_bounds__(512) gemm256_kernel(
     const bf16_t* __restrict__ A, int64_t lda, const bf16_t* __restrict__ B, int64_t ldb, int M,
     int N, int ktiles_total, int ktiles_per_split, int splits, bf16_t* __restrict__ C, int64_t ldc,
     float* __restrict__ Cf, const bf16_t* __restrict__ bias, int act, bf16_t* __restrict__ Zout,
-    float* __restrict__ colsum) {
+    float* __restrict__ colsum, float* __restrict__ wsp = nullptr) {
   __shared__ __attribute__((aligned(1024))) char smem[2 * B_REGION];
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int wm = (w >> 2) & 1, wn = w & 3;  // 2 x 4 waves over a 128 x 128 quadrant
@@ -413,12 +413,25 @@ __global__ void __launch_bounds__(512) gemm256_kernel(
               ct[row * 256 + col] = acc[qa][qb][i][j][r];
             }
       __syncthreads();
-      float* dst = Cf + (int64_t)(m0 + qa * 128) * ldc + n0;
+      if (wsp) {
+        // split-K partial of split z into the workspace [splits][M][N] with plain 16-B
+        // stores (HBM rate); wgrad_reduce_kernel adds the splits into Cf afterwards
+        float* dst = wsp + ((int64_t)z * M + m0 + qa * 128) * N + n0;
 #pragma unroll 4
-      for (int c = 0; c < 64; ++c) {
-        const int idx = tid + c * 512;
-        const int row = idx >> 8, col = idx & 255;
-        atomicAdd(dst + (int64_t)row * ldc + col, ct[row * 256 + (col ^ ((row & 3) << 4))]);
+        for (int c = 0; c < 16; ++c) {
+          const int idx = tid + c * 512;
+          const int row = idx >> 6, col = (idx & 63) * 4;
+          const f32x4 v = *reinterpret_cast<const f32x4*>(ct + row * 256 + (col ^ ((row & 3) << 4)));
+          *reinterpret_cast<f32x4*>(dst + (int64_t)row * N + col) = v;
+        }
+      } else {
+        float* dst = Cf + (int64_t)(m0 + qa * 128) * ldc + n0;
+#pragma unroll 4
+        for (int c = 0; c < 64; ++c) {
+          const int idx = tid + c * 512;
+          const int row = idx >> 8, col = idx & 255;
+          atomicAdd(dst + (int64_t)row * ldc + col, ct[row * 256 + (col ^ ((row & 3) << 4))]);
+        }
       }
     }
   } else {
@@ -1010,41 +1023,85 @@ bool launch_gemmp_nn(const uint16_t* dy, const uint16_t* W, uint16_t* dx, const 
   return true;
 }
 
-bool launch_gemm256_wgrad(const uint16_t* dy, const uint16_t* x, float* dW, float* db, int T,
-                          int N, int K, hipStream_t s) {
-  // dW[N][K] += dy[T][N]^T . x[T][K]: M = N, N' = K, reduction = T split over workgroups
-  if (!g256_enabled() || N % 256 || K % 256 || T % 128 || T < 128) return false;
+// Split-K plan of the weight gradient (one 128 KiB workgroup per CU): rounds of
+// workgroups x (K-tiles per split x ~1.5 us + ~4 us fixed) plus the cost of merging the
+// splits.  Two merges: fp32 atomics straight into the gradient (~1.2 TB/s chip-wide: the
+// L2 does one 4-byte RMW per atomic) or plain 16-B stores of each split's partial into a
+// workspace plus one reduce pass over it ((2 s + 2) x the gradient bytes at HBM rate).
+// The old rule (fill two rounds regardless of T) split an 8192-token micro-batch 32
+// ways: 54x atomic amplification, 107 us per call.
+struct WgradPlan { int splits, kps; bool ws; };
+static WgradPlan wgrad_plan(int T, int N, int K) {
   const int tiles = (N / 256) * (K / 256);
   const int ktot = T / 64;
-  // Split-K factor from a cost model (one 128 KiB workgroup per CU): rounds of
-  // workgroups x (K-tiles per split x ~1.5 us + ~4 us fixed) against the fp32
-  // atomic epilogue traffic (256 KiB per workgroup at ~1.3 TB/s chip-wide, ~0.35 us
-  // each under contention).  The old rule (fill two rounds regardless of T) split a
-  // 8192-token micro-batch 32 ways: 54x atomic amplification, 107 us per call.
   const int ncu = device_cu_count();
-  int splits = 1;
+  const double mb = (double)N * K * 4.0 / 1e6;  // gradient bytes, MB
+  static int force_ws = -2, force_s = -2;
+  if (force_ws == -2) {
+    // default: merge through the workspace whenever K is split (measured faster at every
+    // encoder shape: 8192 tokens -17%, 262144 tokens -2..5%, tools/wgrad_bench.py)
+    const char* e = std::getenv("DPA_WGRAD_WS");
+    force_ws = e ? std::atoi(e) : 1;
+    const char* f = std::getenv("DPA_WGRAD_SPLITS");
+    force_s = f ? std::atoi(f) : -1;
+  }
+  WgradPlan best_p{1, ktot + (ktot & 1), false};
   double best = 1e30;
   const int smax = ktot / 2 < 1 ? 1 : ktot / 2;
   for (int sp = 1; sp <= smax; ++sp) {
+    if (force_s > 0 && sp != force_s) continue;
     int kps = (ktot + sp - 1) / sp;
     kps += kps & 1;
     const int s_eff = (ktot + kps - 1) / kps;
     const int wgs = tiles * s_eff;
     const int rounds = (wgs + ncu - 1) / ncu;
-    const double t = fmax(rounds * (kps * 1.5 + 4.0), wgs * 0.35);
-    if (t < best * 0.98) {
-      best = t;
-      splits = s_eff;
+    const double main = rounds * (kps * 1.5 + 4.0);
+    for (int w = 0; w < 2; ++w) {
+      if (w == 1 && s_eff < 2) continue;
+      if (force_ws >= 0 && w != force_ws && !(w == 0 && s_eff < 2)) continue;
+      const double t = w ? main + (2.0 * s_eff + 2.0) * mb / 4.0 : fmax(main, wgs * 0.35);
+      if (t < best * 0.98) {
+        best = t;
+        best_p = WgradPlan{s_eff, kps, w == 1};
+      }
     }
     if (wgs > 4 * ncu) break;
   }
-  int kps = (ktot + splits - 1) / splits;
-  kps += kps & 1;
-  splits = (ktot + kps - 1) / kps;
+  return best_p;
+}
+
+int64_t gemm256_wgrad_workspace_floats(int T, int N, int K) {
+  if (!g256_enabled() || N % 256 || K % 256 || T % 128 || T < 128) return 0;
+  const WgradPlan p = wgrad_plan(T, N, K);
+  return p.ws ? (int64_t)p.splits * N * K : 0;
+}
+
+__global__ void __launch_bounds__(256) wgrad_reduce_kernel(const float* __restrict__ ws, float* __restrict__ dW,
+                                                           int64_t n4, int splits) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n4) return;
+  f32x4 acc = reinterpret_cast<const f32x4*>(dW)[i];
+  for (int s = 0; s < splits; ++s) acc += reinterpret_cast<const f32x4*>(ws)[s * n4 + i];
+  reinterpret_cast<f32x4*>(dW)[i] = acc;
+}
+
+bool launch_gemm256_wgrad(const uint16_t* dy, const uint16_t* x, float* dW, float* db, int T,
+                          int N, int K, hipStream_t s, float* ws) {
+  // dW[N][K] += dy[T][N]^T . x[T][K]: M = N, N' = K, reduction = T split over workgroups
+  if (!g256_enabled() || N % 256 || K % 256 || T % 128 || T < 128) return false;
+  const int tiles = (N / 256) * (K / 256);
+  const int ktot = T / 64;
+  const WgradPlan p = wgrad_plan(T, N, K);
+  float* wsp = (p.ws && ws != nullptr) ? ws : nullptr;
   hipLaunchKernelGGL((g256::gemm256_kernel<true, true, g256::EPI_ATOMIC_F32>),
-                     dim3(tiles * splits), dim3(512), 0, s, (const bf16_t*)dy, (int64_t)N,
-                     (const bf16_t*)x, (int64_t)K, N, K, ktot, kps, splits, nullptr, (int64_t)K, dW,
-                     nullptr, 0, nullptr, db);
+                     dim3(tiles * p.splits), dim3(512), 0, s, (const bf16_t*)dy, (int64_t)N,
+                     (const bf16_t*)x, (int64_t)K, N, K, ktot, p.kps, p.splits, nullptr, (int64_t)K, dW,
+                     nullptr, 0, nullptr, db, wsp);
+  if (wsp) {
+    const int64_t n4 = (int64_t)N * K / 4;
+    hipLaunchKernelGGL(wgrad_reduce_kernel, dim3((unsigned)((n4 + 255) / 256)), dim3(256), 0, s, wsp, dW, n4,
+                       p.splits);
+  }
   return true;
 }
 

@@ -123,7 +123,7 @@ bool launch_gemm_nt(const uint16_t* x, const uint16_t* W, const uint16_t* bias, 
 bool launch_gemm_nn(const uint16_t* dy, const uint16_t* W, uint16_t* dx, int T, int N, int K,
                     hipStream_t s);
 bool launch_gemm_wgrad(const uint16_t* dy, const uint16_t* x, float* dW, float* db, int T, int N,
-                       int K, hipStream_t s);
+                       int K, hipStream_t s, float* ws = nullptr);
 // gemm256.hip: 256x256 8-phase variants (return false when the shape does not tile
 // or DPA_GEMM256=0); the launch_gemm_* entry points try them first.
 bool launch_gemm256_nt(const uint16_t* x, const uint16_t* W, const uint16_t* bias, uint16_t* y,
@@ -135,7 +135,9 @@ void set_gemmp_dynamic(bool on);  // dynamic tile schedule of the persistent GEM
 bool launch_gemm256_nn_dact(const uint16_t* dy, const uint16_t* W, const uint16_t* aux,
                             uint16_t* dz, int T, int N, int K, int act, hipStream_t s);
 bool launch_gemm256_wgrad(const uint16_t* dy, const uint16_t* x, float* dW, float* db, int T,
-                          int N, int K, hipStream_t s);
+                          int N, int K, hipStream_t s, float* ws = nullptr);
+// fp32 workspace the split-K weight gradient merges through (0: atomics / no split)
+int64_t gemm256_wgrad_workspace_floats(int T, int N, int K);
 // gemm256.hip persistent forward / data-gradient kernels with fused epilogues (false when
 // the shape does not tile).  ncu: compute units (grid = min(tiles, ncu)).
 //   nt: y[T][N] = act(x[T][K] W[N][K]^T + bias); z (nullable) = pre-activation, or act'(it)
