@@ -316,6 +316,9 @@ bool launch_gemm_wgrad(const uint16_t* dy, const uint16_t* x, float* dW, float* 
   const int tiles = (N / 128) * (K / 128);
   int splits = (1024 + tiles - 1) / tiles;
   const int ksteps = T / 64;
+  // at least 16 K-steps (1024 tokens) per split: an 8192-token micro-batch of the 128-wide
+  // up/down projections otherwise split 128 ways, 128 x the gradient in fp32 atomics
+  if (splits > ksteps / 16) splits = ksteps / 16;
   if (splits > ksteps) splits = ksteps;
   if (splits < 1) splits = 1;
   const int kps = ((ksteps + splits - 1) / splits) * 64;
