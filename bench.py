@@ -156,8 +156,11 @@ def main():
         dist_util.barrier()
 
     t_w = time.time()
-    for _ in range(a.warmup):
+    for i in range(a.warmup):
         one_step()
+        if rank == 0:  # progress (outside the timed region) for long or profiled runs
+            print(f"[bench] warmup step {i + 1}/{a.warmup} queued at {time.time() - t_w:.1f} s",
+                  file=sys.stderr, flush=True)
     sync()
     warm_s = time.time() - t_w
     sync()

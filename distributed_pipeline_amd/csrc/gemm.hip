@@ -51,7 +51,7 @@ struct Op {
       const int row = pc * RPP + lane / CHR;
       const int phys = lane % CHR;
       int logical;
-      if constexpr (TR) logical = phys ^ (row & 15);
+      if constexpr (TR) logical = phys ^ swz_x256<>(row);  // inverse of swz<256>
       else logical = phys ^ ((row >> 1) & 7);
       const bf16_t* src = g + (int64_t)row * ld + logical * 8;
       __builtin_amdgcn_global_load_lds((glob_void*)src, (lds_void*)(lds + pc * 1024), 16, 0, 0);

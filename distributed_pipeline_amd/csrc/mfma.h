@@ -46,10 +46,27 @@ __device__ __forceinline__ bf16x8 ld_frag(const bf16_t* p) {
   return *reinterpret_cast<const bf16x8*>(p);
 }
 
+// XOR applied to the 16-byte chunk index of row `row` in rows of >= 256 bytes (a bank
+// period).  Both read shapes on these tiles are conflict-free with it
+// (MI355X_MICROARCH LDS banking table):
+//  * ds_read_b128 of 32 consecutive rows at one chunk - lane groups {0-3,12-15,20-27}
+//    and {4-11,16-19,28-31} each get 16 distinct chunk positions;
+//  * ds_read_b64_tr_b16 (lds_tr_frag*): a 32-lane group reads rows 4m..4m+3 at 4 chunk
+//    offsets x 2 halves: (row & 3) in the high two bits keeps the 32 8-byte slots apart.
+// The previous XOR (row & 15) left the transposed reads 4-way conflicted
+// (PMC r2: 3.0 conflict cycles per LDS instruction in lxent_fwd_dx).
+// LEG selects the previous XOR (row & 15): same-box A/B (tools/gpu_r2cc.sh) had the fused CE
+// forward+dx and dx kernels 6-8% faster with the new XOR but lxent_dw 8% slower, so the dW
+// kernel's x tile keeps it.
+template <bool LEG = false>
+__host__ __device__ __forceinline__ constexpr int swz_x256(int row) {
+  return LEG ? (row & 15) : (((row & 3) << 2) | ((row >> 2) & 3));
+}
+
 // LDS byte offset of 16-byte chunk `ch` of row `row` for a [rows][ROWBYTES]
 // bf16 tile with XOR swizzle (conflict-free ds_read_b128 row reads and 8-byte
-// transposed reads).  ROWBYTES is a multiple of 256.
-template <int ROWBYTES>
+// transposed reads).  ROWBYTES is 64, 128 or a multiple of 256.
+template <int ROWBYTES, bool LEG = false>
 __device__ __forceinline__ int swz(int row, int ch) {
   if constexpr (ROWBYTES == 64) {
     return row * 64 + ((ch ^ ((row >> 2) & 3)) << 4);
@@ -57,7 +74,7 @@ __device__ __forceinline__ int swz(int row, int ch) {
     return row * 128 + ((ch ^ ((row >> 1) & 7)) << 4);
   } else {
     static_assert(ROWBYTES % 256 == 0, "row must be 64, 128 or a multiple of 256 bytes");
-    return row * ROWBYTES + ((ch ^ (row & 15)) << 4);
+    return row * ROWBYTES + ((ch ^ swz_x256<LEG>(row)) << 4);
   }
 }
 
@@ -70,9 +87,9 @@ __device__ __forceinline__ bf16x4 ds_read_tr16(const void* lds_ptr) {
 }
 
 // A/B fragment (8 bf16 of row `row`, 16-byte chunk `ch`) from a swizzled tile.
-template <int ROWB>
+template <int ROWB, bool LEG = false>
 __device__ __forceinline__ bf16x8 lds_frag(const char* lds, int row, int ch) {
-  return *reinterpret_cast<const bf16x8*>(lds + swz<ROWB>(row, ch));
+  return *reinterpret_cast<const bf16x8*>(lds + swz<ROWB, LEG>(row, ch));
 }
 
 __device__ __forceinline__ bf16x8 cat44(const bf16x4& a, const bf16x4& b) {
@@ -86,13 +103,13 @@ __device__ __forceinline__ bf16x8 cat44(const bf16x4& a, const bf16x4& b) {
 // the header comment): rows r0 + 4h + q and r0 + 8 + 4h + q (q = 0..3) of the
 // column block col0..col0+31 (this lane receives column col0 + (lane & 31)),
 // read transposed from a swizzled LDS tile.  EXEC must be all ones.
-template <int ROWB>
+template <int ROWB, bool LEG = false>
 __device__ __forceinline__ bf16x8 lds_tr_frag(const char* lds, int r0, int col0, int lane) {
   const int g = lane >> 4, li = lane & 15, q = li >> 2, p = li & 3, h = lane >> 5;
   const int col = col0 + 16 * (g & 1) + 4 * p;
   const int ra = r0 + 4 * h + q;
-  const char* pa = lds + swz<ROWB>(ra, col >> 3) + (col & 7) * 2;
-  const char* pb = lds + swz<ROWB>(ra + 8, col >> 3) + (col & 7) * 2;
+  const char* pa = lds + swz<ROWB, LEG>(ra, col >> 3) + (col & 7) * 2;
+  const char* pb = lds + swz<ROWB, LEG>(ra + 8, col >> 3) + (col & 7) * 2;
   return cat44(ds_read_tr16(pa), ds_read_tr16(pb));
 }
 

@@ -549,7 +549,7 @@ __global__ void __launch_bounds__(512) lxent_dw_kernel(
 #pragma unroll
     for (int i = 0; i < PER; ++i) {
       const int c = tid + i * 512;
-      *reinterpret_cast<uint4*>(xt + swz<ROWB>(c / CH, c % CH)) = xr[i];
+      *reinterpret_cast<uint4*>(xt + swz<ROWB, true>(c / CH, c % CH)) = xr[i];
     }
     if (tid < 64) {
       s_lse[tid] = r_lse;
@@ -565,7 +565,7 @@ __global__ void __launch_bounds__(512) lxent_dw_kernel(
       for (int i = 0; i < 16; ++i) acc[i] = bv;
 #pragma unroll
       for (int s = 0; s < KS; ++s)
-        acc = mfma32(lds_frag<ROWB>(xt, tt * 32 + (lane & 31), 2 * s + h), wf[s], acc);
+        acc = mfma32(lds_frag<ROWB, true>(xt, tt * 32 + (lane & 31), 2 * s + h), wf[s], acc);
 #pragma unroll
       for (int g4 = 0; g4 < 4; ++g4) {
         // per-token scalars of rows tt*32 + 8 g4 + 4 h + r, one 16-byte read each
@@ -588,7 +588,7 @@ __global__ void __launch_bounds__(512) lxent_dw_kernel(
         const bf16x8 af = acc_to_frag(acc, s);
 #pragma unroll
         for (int kt = 0; kt < KT; ++kt)
-          dacc[kt] = mfma32(af, lds_tr_frag<ROWB>(xt, tt * 32 + 16 * s, kt * 32, lane), dacc[kt]);
+          dacc[kt] = mfma32(af, lds_tr_frag<ROWB, true>(xt, tt * 32 + 16 * s, kt * 32, lane), dacc[kt]);
       }
     }
     __syncthreads();
