@@ -30,6 +30,8 @@ def main():
     ap.add_argument("--N", type=int, default=262144)
     ap.add_argument("--V", type=int, default=30522)
     ap.add_argument("--E", type=int, default=128)
+    ap.add_argument("--ignore-frac", type=float, default=0.0,
+                    help="fraction of targets set to -100, sorted last (the logged masked nll)")
     a = ap.parse_args()
     from distributed_pipeline_amd.ops._ext import get_ext
     ext = get_ext(required=True)
@@ -38,6 +40,8 @@ def main():
     W = (torch.randn(V, E, device="cuda") * 0.5).bfloat16()
     b = (torch.randn(V, device="cuda") * 0.1).bfloat16()
     tgt = torch.randint(0, V, (N,), device="cuda")
+    if a.ignore_frac > 0:
+        tgt[int(N * (1 - a.ignore_frac)):] = -100
     loss, lse = ext.lxent_fwd(x, W, b, tgt)
     dl = torch.rand(N, device="cuda")
     f = bench(lambda: ext.lxent_fwd(x, W, b, tgt))
@@ -46,7 +50,7 @@ def main():
     dwo = bench(lambda: ext.lxent_bwd(dl, x, W, b, tgt, lse, False, True, True))
     fdx = bench(lambda: ext.lxent_fwd_dx(x, W, b, tgt)) if hasattr(ext, "lxent_fwd_dx") else None
     fl = 2.0 * N * V * E
-    print(json.dumps({"N": N, "V": V, "E": E, "fwd_ms": round(f, 3), "fwd_logit_TF": round(fl / f / 1e9, 1),
+    print(json.dumps({"N": N, "V": V, "E": E, "ignore_frac": a.ignore_frac, "fwd_ms": round(f, 3), "fwd_logit_TF": round(fl / f / 1e9, 1),
                       "bwd_ms": round(bw, 3), "dx_ms": round(dxo, 3), "dw_ms": round(dwo, 3),
                       "fused_fwd_dx_ms": round(fdx, 3) if fdx else None}))
 
