@@ -456,6 +456,23 @@ static std::vector<at::Tensor> xent_rows_fwd(const at::Tensor& lg, int64_t V, co
   return {loss, lse};
 }
 
+// in place: logits -> softmax - onehot (unscaled); returns (loss, lse) (empty list if refused)
+static std::vector<at::Tensor> xent_rows_fwd_grad_(at::Tensor& lg, int64_t V, const at::Tensor& tgt) {
+  CHECK_DEV(lg); CHECK_BF16(lg); CHECK_CONTIG(lg); CHECK_ALIGNED(lg);
+  check_i64(tgt, "target");
+  TORCH_CHECK(lg.dim() == 2 && lg.size(1) % 8 == 0 && V > 0 && V <= lg.size(1),
+              "logits [R, ld] with ld % 8 == 0 and V <= ld");
+  TORCH_CHECK(tgt.numel() == lg.size(0), "target [R]");
+  const c10::DeviceGuard guard(lg.device());
+  auto f32 = lg.options().dtype(at::kFloat);
+  at::Tensor loss = at::empty({lg.size(0)}, f32), lse = at::empty({lg.size(0)}, f32);
+  if (!dpa::launch_xent_rows_fwd_grad(reinterpret_cast<uint16_t*>(lg.data_ptr()), lg.size(1), (int)V,
+                                      tgt.data_ptr<int64_t>(), lg.size(0), loss.data_ptr<float>(),
+                                      lse.data_ptr<float>(), cur_stream()))
+    return {};
+  return {loss, lse};
+}
+
 static void xent_rows_bwd_(at::Tensor& lg, int64_t V, const at::Tensor& tgt, const at::Tensor& lse,
                            const at::Tensor& dloss) {
   CHECK_DEV(lg); CHECK_BF16(lg); CHECK_CONTIG(lg); CHECK_ALIGNED(lg);
@@ -665,6 +682,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("lxent_bwd", &lxent_bwd, "fused linear + cross-entropy backward -> (dx, dW fp32, db fp32)");
   m.def("xent_rows_fwd", &xent_rows_fwd, "row softmax-CE over bf16 logits [R, ld] -> (loss, lse)");
   m.def("xent_rows_bwd_", &xent_rows_bwd_, "in place: logits -> dloss * (softmax - onehot)");
+  m.def("xent_rows_fwd_grad_", &xent_rows_fwd_grad_,
+        "in place: logits -> softmax - onehot (unscaled), returns (loss, lse) or [] if the row is too long");
   m.def("emb_qsample_fwd", &emb_qsample_fwd,
         "DiffuSeq embedding gather + x_start noise + masked q_sample -> (x_start, x_start bf16, x_t bf16)");
   m.def("emb_qsample_bwd", &emb_qsample_bwd, "scatter-add of the q_sample gradients into dW (fp32)");

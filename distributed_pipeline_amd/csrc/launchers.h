@@ -91,6 +91,9 @@ bool launch_attn_bwd(const uint16_t* qkv, const uint16_t* out, const uint16_t* d
                      hipStream_t s);
 
 // ---- xent_rows.hip: row softmax-CE over materialised logits (wide-E chunked path) ----
+// forward that leaves softmax - onehot (unscaled) in place of the logits (false: row too long)
+bool launch_xent_rows_fwd_grad(uint16_t* lg, int64_t ld, int V, const int64_t* tgt, int64_t R, float* loss,
+                               float* lse, hipStream_t s);
 bool launch_xent_rows_fwd(const uint16_t* lg, int64_t ld, int V, const int64_t* tgt, int64_t R,
                           float* loss, float* lse, hipStream_t s);
 bool launch_xent_rows_bwd(uint16_t* lg, int64_t ld, int V, const int64_t* tgt, const float* lse,

@@ -845,15 +845,24 @@ class _ChunkedLinearXentFn(torch.autograd.Function):
         # into dlogits in place) instead of recomputing them, when they fit the budget
         keep = any(ctx.needs_input_grad[:3]) and N * wp.shape[0] * 2 <= _XENT_KEEP_BYTES
         kept = []
+        # kept chunks: one row pass leaves softmax - onehot (unscaled) in place of the
+        # logits (xent_rows_fwd_grad_), so the backward needs no row pass of its own
+        kept_is_grad = keep and _XENT_ROWS_FUSED
         for s in range(0, N, chunk):
             e = min(N, s + chunk)
             lg = _chunk_logits(x[s:e], wp, bp)
-            l_c, lse_c = ext.xent_rows_fwd(lg, V, target[s:e])
+            if kept_is_grad:
+                res = ext.xent_rows_fwd_grad_(lg, V, target[s:e])
+                assert res, "xent_rows_fwd_grad_ refused the row length"
+                l_c, lse_c = res
+            else:
+                l_c, lse_c = ext.xent_rows_fwd(lg, V, target[s:e])
             loss[s:e].copy_(l_c)
             lse[s:e].copy_(lse_c)
             if keep:
                 kept.append(lg)
         ctx.kept = kept if keep else None
+        ctx.kept_is_grad = kept_is_grad
         ctx.save_for_backward(x, w16, b16, target, lse)
         ctx.params = (w, b)
         ctx.chunk = chunk
@@ -875,24 +884,41 @@ class _ChunkedLinearXentFn(torch.autograd.Function):
         db = torch.zeros(V, dtype=torch.float32, device=x.device) if need_db else None
         native_wgrad = need_dw and Vp % 256 == 0 and E % 256 == 0 and hasattr(ext, "gemm_wgrad")
         kept, ctx.kept = ctx.kept, None
+        unscaled = kept is not None and ctx.kept_is_grad
         for ci, s in enumerate(range(0, N, ctx.chunk)):
             e = min(N, s + ctx.chunk)
             dlg = kept[ci] if kept is not None else _chunk_logits(x[s:e], wp, bp)
             if kept is not None:
                 kept[ci] = None  # freed as soon as its gradient GEMMs are queued
-            ext.xent_rows_bwd_(dlg, V, target[s:e], lse[s:e], dloss[s:e])
+            if unscaled:
+                # dlg = softmax - onehot; the per-token upstream gradient g scales rows:
+                # dx = diag(g) (G W), dW = G^T (diag(g) x), db = G^T g
+                g = dloss[s:e]
+                xg = (x[s:e] * g[:, None]).to(x.dtype) if need_dw else None
+            else:
+                ext.xent_rows_bwd_(dlg, V, target[s:e], lse[s:e], dloss[s:e])
+                xg = x[s:e]
             if need_dx:
                 torch.mm(dlg, wp, out=dx[s:e])
+                if unscaled:
+                    dx[s:e].mul_(g[:, None])
             if need_dw:
                 if native_wgrad and (e - s) % 128 == 0:
-                    ext.gemm_wgrad(dlg, x[s:e], dwp, None)   # split-K MFMA, fp32 accumulate
+                    ext.gemm_wgrad(dlg, xg, dwp, None)   # split-K MFMA, fp32 accumulate
                 else:
-                    dwp.add_(_mm_fp32(dlg.t(), x[s:e]))
+                    dwp.add_(_mm_fp32(dlg.t(), xg))
             if need_db:
-                db.add_(dlg[:, :V].float().sum(0))
+                if unscaled:
+                    db.add_(g @ dlg[:, :V].float())
+                else:
+                    db.add_(dlg[:, :V].float().sum(0))
         dw = dwp[:V] if need_dw else None
         return dx, dw, db, None, None, None, None
 
+
+# wide-E CE: kept logit chunks become softmax - onehot in the forward's row pass
+# (DPA_XENT_ROWS_FUSED=0: forward statistics only, separate backward row pass)
+_XENT_ROWS_FUSED = os.environ.get("DPA_XENT_ROWS_FUSED", "1") != "0"
 
 # fused CE: forward also emits the unscaled input gradient (DPA_XENT_FUSED_DX=0: separate dx pass)
 _XENT_FUSED_DX = os.environ.get("DPA_XENT_FUSED_DX", "1") != "0"
