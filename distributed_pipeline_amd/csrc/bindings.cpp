@@ -236,8 +236,6 @@ static std::vector<at::Tensor> add_ln_bwd(const at::Tensor& dout, const at::Tens
   if (need_dres) dres = at::empty_like(dout);
   if (need_dy) dy = at::empty_like(dout);
   auto f32 = dout.options().dtype(at::kFloat);
-  const int nb = dpa::ln_bwd_blocks(R);
-  (void)nb;
   // dgamma, dbeta and colsum(dy) as consecutive rows of one scratch buffer (one memset),
   // or accumulated straight onto given fp32 .grad buffers (returned undefined then: no
   // autograd-side add and no memset)
