@@ -148,7 +148,6 @@ __device__ __forceinline__ void stage64(char* lds, const bf16_t* __restrict__ sr
 // (b, h) items back to back (K/V panel reuse in that XCD's L2) and the same work mix as
 // the others.  Causal: row tiles are paired (see below).
 struct AttnItem { int t, hd, b, npass; };
-template <bool HEAVY_HIGH>
 __device__ __forceinline__ AttnItem attn_item(int L, int H, bool causal) {
   const int NT = (L + 127) / 128;
   // causal: one block runs row tiles r and NT - 1 - r of its (b, h) one after the other,
@@ -167,7 +166,7 @@ __device__ __forceinline__ AttnItem attn_item(int L, int H, bool causal) {
     bh = i / NI;
   }
   AttnItem it;
-  it.t = causal ? r : (HEAVY_HIGH ? NT - 1 - r : r);
+  it.t = r;
   it.npass = causal && NT - 1 - r != r ? 2 : 1;
   it.hd = bh % H;
   it.b = bh / H;
@@ -193,7 +192,7 @@ __global__ void __launch_bounds__(256) attn_fwd_kernel(const bf16_t* __restrict_
   __shared__ __attribute__((aligned(16))) char smem[2 * 64 * 2 * D];
   char* kt_lds = smem;
   char* vt_lds = smem + 64 * 2 * D;
-  const AttnItem it0 = attn_item<true>(L, H, CAUSAL);
+  const AttnItem it0 = attn_item(L, H, CAUSAL);
   for (int pass = 0; pass < it0.npass; ++pass) {  // 2 row tiles per block when causal
   const AttnItem it = attn_pass(it0, pass, L);
   const int b = it.b, hd = it.hd;
@@ -316,7 +315,7 @@ __global__ void __launch_bounds__(256, D == 64 ? 2 : 1) attn_fwd_online_kernel(c
   __shared__ __attribute__((aligned(16))) char smem[2 * 64 * 2 * D];
   char* kt_lds = smem;
   char* vt_lds = smem + 64 * 2 * D;
-  const AttnItem it0 = attn_item<true>(L, H, CAUSAL);
+  const AttnItem it0 = attn_item(L, H, CAUSAL);
   for (int pass = 0; pass < it0.npass; ++pass) {  // 2 row tiles per block when causal
   const AttnItem it = attn_pass(it0, pass, L);
   const int b = it.b, hd = it.hd;
@@ -567,7 +566,7 @@ __global__ void __launch_bounds__(256, D == 64 ? 2 : 1) attn_bwd_kv_kernel(
   char* dot_lds = smem + 64 * 2 * D;
   float* s_lse = reinterpret_cast<float*>(smem + 2 * 64 * 2 * D);
   float* s_del = s_lse + 64;
-  const AttnItem it0 = attn_item<false>(L, H, CAUSAL);
+  const AttnItem it0 = attn_item(L, H, CAUSAL);
   for (int pass = 0; pass < it0.npass; ++pass) {  // 2 row tiles per block when causal
   const AttnItem it = attn_pass(it0, pass, L);
   const int b = it.b, hd = it.hd;
@@ -707,7 +706,7 @@ __global__ void __launch_bounds__(256, D == 64 ? 2 : 1) attn_bwd_q_kernel(
   __shared__ __attribute__((aligned(16))) char smem[2 * 64 * 2 * D];
   char* kt_lds = smem;
   char* vt_lds = smem + 64 * 2 * D;
-  const AttnItem it0 = attn_item<true>(L, H, CAUSAL);
+  const AttnItem it0 = attn_item(L, H, CAUSAL);
   for (int pass = 0; pass < it0.npass; ++pass) {  // 2 row tiles per block when causal
   const AttnItem it = attn_pass(it0, pass, L);
   const int b = it.b, hd = it.hd;
