@@ -846,11 +846,21 @@ class _ChunkedLinearXentFn(torch.autograd.Function):
         keep = any(ctx.needs_input_grad[:3]) and N * wp.shape[0] * 2 <= _XENT_KEEP_BYTES
         kept = []
         # kept chunks: one row pass leaves softmax - onehot (unscaled) in place of the
-        # logits (xent_rows_fwd_grad_), so the backward needs no row pass of its own
+        # logits (xent_rows_fwd_grad_), so the backward needs no row pass of its own;
+        # the chunks are row slices of ONE [N, Vp] buffer, so the backward's weight
+        # gradient is a single split-K GEMM over all N tokens
         kept_is_grad = keep and _XENT_ROWS_FUSED
+        allg = torch.empty(N, wp.shape[0], dtype=x.dtype, device=x.device) if kept_is_grad else None
         for s in range(0, N, chunk):
             e = min(N, s + chunk)
-            lg = _chunk_logits(x[s:e], wp, bp)
+            if allg is not None:
+                lg = allg[s:e]
+                if bp is not None:
+                    torch.addmm(bp, x[s:e], wp.t(), out=lg)
+                else:
+                    torch.mm(x[s:e], wp.t(), out=lg)
+            else:
+                lg = _chunk_logits(x[s:e], wp, bp)
             if kept_is_grad:
                 res = ext.xent_rows_fwd_grad_(lg, V, target[s:e])
                 assert res, "xent_rows_fwd_grad_ refused the row length"
@@ -863,6 +873,7 @@ class _ChunkedLinearXentFn(torch.autograd.Function):
                 kept.append(lg)
         ctx.kept = kept if keep else None
         ctx.kept_is_grad = kept_is_grad
+        ctx.allg = allg
         ctx.save_for_backward(x, w16, b16, target, lse)
         ctx.params = (w, b)
         ctx.chunk = chunk
@@ -884,7 +895,10 @@ class _ChunkedLinearXentFn(torch.autograd.Function):
         db = torch.zeros(V, dtype=torch.float32, device=x.device) if need_db else None
         native_wgrad = need_dw and Vp % 256 == 0 and E % 256 == 0 and hasattr(ext, "gemm_wgrad")
         kept, ctx.kept = ctx.kept, None
+        allg, ctx.allg = ctx.allg, None
         unscaled = kept is not None and ctx.kept_is_grad
+        # all chunks in one buffer: dW = G^T (diag(g) x) as one GEMM after the chunk loop
+        whole_wgrad = (unscaled and allg is not None and need_dw and native_wgrad and N % 128 == 0)
         for ci, s in enumerate(range(0, N, ctx.chunk)):
             e = min(N, s + ctx.chunk)
             dlg = kept[ci] if kept is not None else _chunk_logits(x[s:e], wp, bp)
@@ -894,7 +908,7 @@ class _ChunkedLinearXentFn(torch.autograd.Function):
                 # dlg = softmax - onehot; the per-token upstream gradient g scales rows:
                 # dx = diag(g) (G W), dW = G^T (diag(g) x), db = G^T g
                 g = dloss[s:e]
-                xg = (x[s:e] * g[:, None]).to(x.dtype) if need_dw else None
+                xg = (x[s:e] * g[:, None]).to(x.dtype) if need_dw and not whole_wgrad else None
             else:
                 ext.xent_rows_bwd_(dlg, V, target[s:e], lse[s:e], dloss[s:e])
                 xg = x[s:e]
@@ -902,7 +916,7 @@ class _ChunkedLinearXentFn(torch.autograd.Function):
                 torch.mm(dlg, wp, out=dx[s:e])
                 if unscaled:
                     dx[s:e].mul_(g[:, None])
-            if need_dw:
+            if need_dw and not whole_wgrad:
                 if native_wgrad and (e - s) % 128 == 0:
                     ext.gemm_wgrad(dlg, xg, dwp, None)   # split-K MFMA, fp32 accumulate
                 else:
@@ -912,6 +926,9 @@ class _ChunkedLinearXentFn(torch.autograd.Function):
                     db.add_(g @ dlg[:, :V].float())
                 else:
                     db.add_(dlg[:, :V].float().sum(0))
+        if whole_wgrad:
+            ext.gemm_wgrad(allg, (x * dloss[:, None]).to(x.dtype), dwp, None)
+        del allg
         dw = dwp[:V] if need_dw else None
         return dx, dw, db, None, None, None, None
 

@@ -71,7 +71,10 @@ def test_linear_cross_entropy_autograd_matches_torch():
 
 @pytest.mark.parametrize("N,V,E,with_bias,chunk_mb,keep", [(1000, 50257, 768, False, 16, True),
                                                            (1000, 50257, 768, False, 16, False),
-                                                           (300, 1000, 512, True, 1, True)])
+                                                           (300, 1000, 512, True, 1, True),
+                                                           # N % 128 == 0: one wgrad GEMM over all kept chunks
+                                                           (1024, 50257, 768, False, 16, True),
+                                                           (1024, 1000, 512, True, 1, True)])
 def test_chunked_linear_cross_entropy_wide_E(N, V, E, with_bias, chunk_mb, keep, monkeypatch):
     """Wide-E path (GPT-2 LM head): hipBLASLt chunk logits + csrc/xent_rows.hip row
     kernels, several chunks (incl. a ragged last one), ignored targets, padding columns;
