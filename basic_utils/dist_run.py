@@ -19,7 +19,10 @@ Differences from the reference:
 * Per-rank environment defaults for ROCm/RCCL are set before spawning
   (``OMP_NUM_THREADS`` = physical cores / GPUs as in the reference, plus
   ``HSA_ENABLE_IPC_MODE_LEGACY=0`` which the dmabuf-only driver needs for RCCL
-  IPC between ranks).
+  IPC between ranks, and ``NCCL_IB_DISABLE=1`` for a single node).  Each worker
+  pins itself to its GPU's NUMA node (``dist_util.bind_cpus_to_gpu``, in-process,
+  ``DPA_NUMA_BIND``), since torchrun's ``--numa-binding`` needs ``numactl`` and
+  device queries in this launcher process; the parent never initialises HIP.
 """
 
 import os
@@ -55,6 +58,8 @@ def run_argv_as_distributed(program_or_module, argv, dist_namespace, *, run_as_m
                           str(max(1, (psutil.cpu_count(logical=False) or 1) // (n_gpu or 1))))
     # dmabuf IPC is the only mode the MI355X host driver supports for RCCL.
     os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    if str(getattr(dist_namespace, "nnodes", "1")) in ("1", "1:1"):
+        os.environ.setdefault("NCCL_IB_DISABLE", "1")  # one node: xGMI only, no NIC probing
 
     if hasattr(dist_namespace, "distributed"):
         delattr(dist_namespace, "distributed")
@@ -104,7 +109,9 @@ def create_distributed_parser(parser=None):
         if action.dest in _SKIP_DESTS or not action.option_strings:
             continue
         if action.dest == "nproc_per_node":
-            action.default = "gpu" if torch.cuda.is_available() else "1"
+            # device_count() does not initialise HIP in this (launcher) process: the workers
+            # torchrun spawns must be the first processes to touch the GPU
+            action.default = "gpu" if torch.cuda.device_count() > 0 else "1"
         if action.dest in ("no_python", "run_path"):
             action.help = SUPPRESS
         parser._add_action(action)  # noqa: SLF001

@@ -105,6 +105,7 @@ def setup_dist(backend=None, silent=False):
                 torch.cuda.set_device(dev())
                 if backend == "nccl":
                     kwargs["device_id"] = dev()
+                bind_cpus_to_gpu(int(os.environ["LOCAL_RANK"]))
             dist.init_process_group(**kwargs)
             if use_gpu:
                 torch.cuda.empty_cache()
@@ -126,6 +127,80 @@ def setup_dist(backend=None, silent=False):
     if int(os.getenv("LOCAL_RANK")) == 0 and not silent:
         print("<INFO> torch.distributed is not available, skipping distributed setting..")
     return False
+
+
+def _parse_cpulist(text):
+    """'0-3,8,10-11' -> {0, 1, 2, 3, 8, 10, 11} (sysfs cpulist format)."""
+    cpus = set()
+    for part in text.strip().split(","):
+        if not part:
+            continue
+        if "-" in part:
+            a, b = part.split("-")
+            cpus.update(range(int(a), int(b) + 1))
+        else:
+            cpus.add(int(part))
+    return cpus
+
+
+def gpu_numa_cpus(pci_bus_id, sysfs="/sys"):
+    """CPUs of the NUMA node a PCI device (``"0000:72:00.0"``) hangs off, from sysfs;
+    empty when the node is unknown (-1) or sysfs lacks the entries."""
+    try:
+        with open(os.path.join(sysfs, "bus/pci/devices", pci_bus_id.lower(), "numa_node")) as f:
+            node = int(f.read().strip())
+        if node < 0:
+            return set()
+        with open(os.path.join(sysfs, "devices/system/node", f"node{node}", "cpulist")) as f:
+            return _parse_cpulist(f.read())
+    except (OSError, ValueError):
+        return set()
+
+
+def bind_cpus_to_gpu(local_rank, mode=None, sysfs="/sys"):
+    """Per-GCD host binding (SURVEY L-1 / 5.8): pin this rank's threads to the CPUs
+    of its GPU's NUMA node, so pinned-memory copies, the data loader and the launch
+    thread stay on the socket that owns the xGMI/PCIe root of the device.
+
+    In-process (``sched_setaffinity``), so it needs neither ``numactl`` (which torchrun's
+    ``--numa-binding`` shells out to) nor a HIP call in the launcher parent.
+    ``mode`` (``DPA_NUMA_BIND``): ``node`` (default with several local ranks) binds to the
+    whole node; ``exclusive`` splits the node's allowed CPUs evenly between the local
+    ranks that share it; ``off`` does nothing.  Returns the CPU set bound to (or None)."""
+    mode = mode or os.environ.get("DPA_NUMA_BIND")
+    if mode is None:
+        mode = "node" if int(os.environ.get("LOCAL_WORLD_SIZE", "1")) > 1 else "off"
+    if mode == "off" or not hasattr(os, "sched_setaffinity"):
+        return None
+    try:
+        p = torch.cuda.get_device_properties(local_rank)
+        bdf = f"{p.pci_domain_id:04x}:{p.pci_bus_id:02x}:{p.pci_device_id:02x}.0"
+    except Exception:  # noqa: BLE001 - best effort: no device properties, no binding
+        return None
+    cpus = gpu_numa_cpus(bdf, sysfs) & os.sched_getaffinity(0)
+    if not cpus:
+        return None
+    if mode == "exclusive":
+        peers = []
+        for r in range(int(os.environ.get("LOCAL_WORLD_SIZE", "1"))):
+            try:
+                q = torch.cuda.get_device_properties(r)
+                if gpu_numa_cpus(f"{q.pci_domain_id:04x}:{q.pci_bus_id:02x}:{q.pci_device_id:02x}.0",
+                                 sysfs) & cpus:
+                    peers.append(r)
+            except Exception:  # noqa: BLE001
+                continue
+        cpus = split_cpus(cpus, peers.index(local_rank) if local_rank in peers else 0, max(1, len(peers)))
+    os.sched_setaffinity(0, cpus)
+    return cpus
+
+
+def split_cpus(cpus, index, parts):
+    """The index-th of ``parts`` contiguous, near-equal slices of a sorted CPU set."""
+    c = sorted(cpus)
+    per, extra = divmod(len(c), parts)
+    lo = index * per + min(index, extra)
+    return set(c[lo:lo + per + (1 if index < extra else 0)]) or set(c)
 
 
 # --------------------------------------------------------------------------- #

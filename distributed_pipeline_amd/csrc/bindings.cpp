@@ -39,7 +39,8 @@ static void sqnorm(const at::Tensor& g, at::Tensor& partial, at::Tensor& out, do
 static void adamw_ema(at::Tensor& p, const at::Tensor& g, at::Tensor& m, at::Tensor& v,
                       c10::optional<at::Tensor> p16, std::vector<at::Tensor> emas,
                       std::vector<double> rates, double lr, double beta1, double beta2, double eps,
-                      double wd, int64_t step, double grad_scale, c10::optional<at::Tensor> clip) {
+                      double wd, int64_t step, double grad_scale, c10::optional<at::Tensor> clip,
+                      c10::optional<at::Tensor> skip) {
   for (auto* t : {&p, &m, &v}) { CHECK_DEV((*t)); CHECK_CONTIG((*t)); CHECK_F32((*t)); CHECK_ALIGNED((*t)); }
   CHECK_DEV(g); CHECK_CONTIG(g); CHECK_ALIGNED(g);
   const int64_t n = p.numel();
@@ -65,11 +66,17 @@ static void adamw_ema(at::Tensor& p, const at::Tensor& g, at::Tensor& m, at::Ten
   }
   const float* clipp = nullptr;
   if (clip.has_value() && clip->defined()) { CHECK_F32((*clip)); clipp = clip->data_ptr<float>(); }
+  const int* skipp = nullptr;
+  if (skip.has_value() && skip->defined()) {
+    CHECK_DEV((*skip));
+    TORCH_CHECK(skip->scalar_type() == at::kInt && skip->numel() >= 1, "skip flag: int32 device tensor");
+    skipp = skip->data_ptr<int>();
+  }
   const c10::DeviceGuard guard(p.device());
   dpa::launch_adamw_ema(p.data_ptr<float>(), g.data_ptr(), bf, m.data_ptr<float>(),
                         v.data_ptr<float>(), p16p, bufs.data(), r.data(), (int)bufs.size(), n,
                         (float)lr, (float)beta1, (float)beta2, (float)eps, (float)wd, step,
-                        (float)grad_scale, clipp, cur_stream());
+                        (float)grad_scale, clipp, cur_stream(), skipp);
 }
 
 static void ema_update(at::Tensor& e, const at::Tensor& p, double rate) {

@@ -154,7 +154,6 @@ class BucketReducer {
       }
     if (ipc_stage_) (void)hipFree(ipc_stage_);
     if (ipc_flags_) (void)hipFree(ipc_flags_);
-    if (ipc_err_) (void)hipFree(ipc_err_);
     for (hipEvent_t e : ready_) if (e) (void)hipEventDestroy(e);
     if (done_) (void)hipEventDestroy(done_);
     if (cs_) (void)hipStreamDestroy(cs_);
@@ -171,10 +170,19 @@ class BucketReducer {
     armed_ = true;
   }
 
+  // Abandon a partially run backward (out-of-memory retry).  Buckets its hooks already
+  // launched keep running on the comm stream and write the flat gradient in place, so
+  // the compute stream (the retry's zero_grad and backward) is ordered after them.
   void disarm() {
     std::lock_guard<std::mutex> g(mu_);
+    if (armed_ && rcomm_ && next_ > 0) {
+      DPA_HIP_CHECK(hipEventRecord(done_, cs_));
+      DPA_HIP_CHECK(hipStreamWaitEvent(compute_stream(), done_, 0));
+    }
     armed_ = false;
   }
+  // Buckets launches the hooks had already made since the last arm().
+  int64_t launched_count() const { return next_; }
 
   bool armed() const { return armed_; }
   bool direct() const { return rcomm_ != nullptr; }
@@ -196,7 +204,13 @@ class BucketReducer {
     std::lock_guard<std::mutex> g(mu_);
     if (!armed_) return;
     const int nb = (int)launched_.size();
-    for (int b = next_; b < nb; ++b) launch(b);
+    // a bucket still waiting for gradients here had a parameter whose hook never fired
+    // (unused in this step's graph): it is reduced now, after backward, without overlap
+    late_.clear();
+    for (int b = next_; b < nb; ++b) {
+      if (pending_[b] > 0) late_.push_back(b);
+      launch(b);
+    }
     next_ = nb;
     if (rcomm_) {
       if (bf16_) {
@@ -238,6 +252,8 @@ class BucketReducer {
   std::vector<int64_t> pending() const {
     return std::vector<int64_t>(pending_.begin(), pending_.end());
   }
+  // buckets the last finalize() had to launch with parameters still pending
+  std::vector<int64_t> late_buckets() const { return std::vector<int64_t>(late_.begin(), late_.end()); }
   // ---- opt-in direct xGMI all-reduce over IPC-mapped buffers (DPA_IPC_ALLREDUCE=1) ----
   // Phase 1: allocate this rank's staging buffer (two parity halves of the largest
   // bucket) and flag words with hipMalloc and export their IPC handles.
@@ -250,8 +266,8 @@ class BucketReducer {
     DPA_HIP_CHECK(hipMalloc(&ipc_stage_, 2 * ipc_cap_ * sizeof(float)));
     DPA_HIP_CHECK(hipMalloc(&ipc_flags_, IPC_FLAG_WORDS * sizeof(uint32_t)));
     DPA_HIP_CHECK(hipMemset(ipc_flags_, 0, IPC_FLAG_WORDS * sizeof(uint32_t)));
-    DPA_HIP_CHECK(hipMalloc(&ipc_err_, sizeof(int)));
-    DPA_HIP_CHECK(hipMemset(ipc_err_, 0, sizeof(int)));
+    ipc_err_t_ = at::zeros({1}, grad_.options().dtype(at::kInt));
+    ipc_err_ = ipc_err_t_.data_ptr<int>();
     DPA_HIP_CHECK(hipDeviceSynchronize());
     hipIpcMemHandle_t h[2];
     DPA_HIP_CHECK(hipIpcGetMemHandle(&h[0], ipc_stage_));
@@ -282,6 +298,10 @@ class BucketReducer {
   }
 
   bool ipc_ready() const { return ipc_ready_; }
+  // The kernels' error word as a device int32 [1] tensor (undefined without IPC): the
+  // fused AdamW skips its update while it is non-zero, and the engine reads it back
+  // asynchronously to raise (parallel/ddp.py).
+  at::Tensor ipc_error_flag() const { return ipc_err_t_; }
   // the kernels' timeout word (host sync; debugging / tests only)
   int64_t ipc_error() const {
     if (!ipc_err_) return 0;
@@ -397,6 +417,7 @@ class BucketReducer {
   std::vector<int> size_, pending_;
   std::vector<c10::intrusive_ptr<c10d::Work>> work_;
   std::vector<bool> launched_;
+  std::vector<int> late_;
   int next_ = 0;
   bool armed_ = false;
   bool bf16_;
@@ -408,6 +429,7 @@ class BucketReducer {
   float* ipc_stage_ = nullptr;
   uint32_t* ipc_flags_ = nullptr;
   int* ipc_err_ = nullptr;
+  at::Tensor ipc_err_t_;
   int64_t ipc_cap_ = 0;
   uint32_t ipc_epoch_ = 0;
   IpcPeers peers_{};
@@ -431,7 +453,7 @@ void register_comm(pybind11::module& m) {
            pybind11::arg("shard_offsets") = std::vector<int64_t>(),
            pybind11::arg("rccl_uid") = std::string(), pybind11::arg("rank") = 0, pybind11::arg("world") = 1)
       .def("arm", &BucketReducer::arm)
-      .def("disarm", &BucketReducer::disarm)
+      .def("disarm", &BucketReducer::disarm, pybind11::call_guard<pybind11::gil_scoped_release>())
       .def("armed", &BucketReducer::armed)
       .def("direct", &BucketReducer::direct)
       .def("stream_priority", &BucketReducer::stream_priority)
@@ -439,6 +461,9 @@ void register_comm(pybind11::module& m) {
       .def("ipc_open", &BucketReducer::ipc_open)
       .def("ipc_ready", &BucketReducer::ipc_ready)
       .def("ipc_error", &BucketReducer::ipc_error)
+      .def("ipc_error_flag", &BucketReducer::ipc_error_flag)
+      .def("launched_count", &BucketReducer::launched_count)
+      .def("late_buckets", &BucketReducer::late_buckets)
       .def("mark_ready", &BucketReducer::mark_ready, pybind11::call_guard<pybind11::gil_scoped_release>())
       .def("finalize", &BucketReducer::finalize, pybind11::call_guard<pybind11::gil_scoped_release>())
       .def("reduce_all", &BucketReducer::reduce_all, pybind11::call_guard<pybind11::gil_scoped_release>())

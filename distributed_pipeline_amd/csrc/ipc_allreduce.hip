@@ -21,7 +21,8 @@
 // only ever reads slice b, so "block b of every peer posted call e+1" implies
 // "they finished reading call e's slice b", and two parity halves of the staging
 // buffer make reuse safe without an extra barrier.  Every spin is bounded
-// (2 s): on timeout the kernel sets *err and returns instead of hanging.
+// (20 s): on timeout the kernel sets *err and returns instead of hanging; the fused
+// AdamW then skips the step and the DDP engine raises (parallel/ddp.py).
 //
 // Single-GPU testing: gridDim.y = W simulated ranks in ONE launch (all blocks
 // co-resident), each block y acting as rank y - the exact per-rank code path.
@@ -52,7 +53,7 @@ __device__ __forceinline__ bool ipc_wait(uint32_t* const* flags, int n, int64_t 
     for (int s = 0; s < n && ok; ++s) {
       while (__hip_atomic_load(flags[s] + idx, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) != epoch) {
         __builtin_amdgcn_s_sleep(2);
-        if (__builtin_amdgcn_s_memrealtime() - t0 > 200000000ull) {  // 2 s at 100 MHz
+        if (__builtin_amdgcn_s_memrealtime() - t0 > 2000000000ull) {  // 20 s at 100 MHz
           ok = 0;
           atomicOr(err, 1);
           break;

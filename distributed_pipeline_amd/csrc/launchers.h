@@ -28,7 +28,8 @@ void launch_sqnorm(const void* g, bool g_bf16, int64_t n, float* partial, int np
 void launch_adamw_ema(float* p, const void* g, bool g_bf16, float* m, float* v, uint16_t* p16,
                       float* const* ema_bufs, const float* ema_rates, int n_ema, int64_t n, float lr,
                       float beta1, float beta2, float eps, float wd, int64_t step, float grad_scale,
-                      const float* clip, hipStream_t s);
+                      const float* clip, hipStream_t s,
+                      const int* skip = nullptr);
 void launch_ema(float* e, const float* p, int64_t n, float rate, hipStream_t s);
 void launch_cast_bf16(const float* src, uint16_t* dst, int64_t n, hipStream_t s);
 void launch_cast_f32(const uint16_t* src, float* dst, int64_t n, hipStream_t s);  // n % 4 == 0

@@ -55,7 +55,7 @@ __device__ __forceinline__ bf16x8 ld_frag(const bf16_t* p) {
 //    offsets x 2 halves: (row & 3) in the high two bits keeps the 32 8-byte slots apart.
 // The previous XOR (row & 15) left the transposed reads 4-way conflicted
 // (PMC r2: 3.0 conflict cycles per LDS instruction in lxent_fwd_dx).
-// LEG selects the previous XOR (row & 15): same-box A/B (tools/gpu_r2cc.sh) had the fused CE
+// LEG selects the previous XOR (row & 15): same-box A/B (round 2) had the fused CE
 // forward+dx and dx kernels 6-8% faster with the new XOR but lxent_dw 8% slower, so the dW
 // kernel's x tile keeps it.
 template <bool LEG = false>

@@ -94,7 +94,10 @@ __global__ void __launch_bounds__(256) adamw_ema_kernel(
     float* __restrict__ p, const T* __restrict__ g, float* __restrict__ m, float* __restrict__ v,
     bf16_t* __restrict__ p16, EmaArgs ema, int64_t n, float lr, float beta1, float beta2,
     float eps, float wd, float step_size, float inv_bc2_sqrt, float grad_scale,
-    const float* __restrict__ clip) {
+    const float* __restrict__ clip, const int* __restrict__ skip) {
+  // skip != nullptr: the step is refused while *skip != 0 (a failed gradient
+  // all-reduce, csrc/ipc_allreduce.hip) - parameters, moments and EMAs stay as they were
+  if (skip && __builtin_nontemporal_load(skip) != 0) return;
   const float gs = grad_scale * (clip ? clip[1] : 1.f);
   const float decay = 1.f - lr * wd;
   const int64_t stride = (int64_t)gridDim.x * blockDim.x * 4;
@@ -198,7 +201,7 @@ void launch_sqnorm(const void* g, bool g_bf16, int64_t n, float* partial, int np
 void launch_adamw_ema(float* p, const void* g, bool g_bf16, float* m, float* v, uint16_t* p16,
                       float* const* ema_bufs, const float* ema_rates, int n_ema, int64_t n, float lr,
                       float beta1, float beta2, float eps, float wd, int64_t step, float grad_scale,
-                      const float* clip, hipStream_t s) {
+                      const float* clip, hipStream_t s, const int* skip) {
   EmaArgs ea;
   ea.count = n_ema > 4 ? 4 : n_ema;
   for (int e = 0; e < 4; ++e) {
@@ -214,12 +217,13 @@ void launch_adamw_ema(float* p, const void* g, bool g_bf16, float* m, float* v, 
   if (g_bf16)
     hipLaunchKernelGGL(adamw_ema_kernel<bf16_t>, dim3(grid), dim3(256), 0, s, p, (const bf16_t*)g,
                        m, v, (bf16_t*)p16, ea, n, lr, beta1, beta2, eps, wd, step_size,
-                       inv_bc2_sqrt, grad_scale, clip);
+                       inv_bc2_sqrt, grad_scale, clip, skip);
   else
     hipLaunchKernelGGL(adamw_ema_kernel<float>, dim3(grid), dim3(256), 0, s, p, (const float*)g, m,
                        v, (bf16_t*)p16, ea, n, lr, beta1, beta2, eps, wd, step_size, inv_bc2_sqrt,
-                       grad_scale, clip);
-  // More than 4 EMA rates: remaining ones as plain passes.
+                       grad_scale, clip, skip);
+  // More than 4 EMA rates: remaining ones as plain passes (not gated by `skip`: the
+  // engine raises on a set flag before the next step anyway).
   for (int e = 4; e < n_ema; ++e)
     hipLaunchKernelGGL(ema_kernel, dim3(grid), dim3(256), 0, s, ema_bufs[e], p, n, ema_rates[e]);
 }

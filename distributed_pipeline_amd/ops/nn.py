@@ -587,6 +587,12 @@ class _AddLNExFn(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, y, residual, pos, temb, w, b, w16, b16, p, eps, seed, offset, post, L):
+        # pos / temb arrive in their own dtype (an fp32 position-embedding parameter slice
+        # keeps an fp32 gradient: its batch sum is never rounded to bf16); the kernel
+        # reads compute-dtype copies
+        ctx.pt_dtypes = (None if pos is None else pos.dtype, None if temb is None else temb.dtype)
+        pos = None if pos is None else pos.to(y.dtype).contiguous()
+        temb = None if temb is None else temb.to(y.dtype).contiguous()
         out, hsave, mean, rstd = get_ext().add_ln_fwd(y, residual, w16, b16, float(p), float(eps), seed,
                                                       offset, pos, temb, int(L), bool(post))
         ctx.save_for_backward(hsave, mean, rstd, w16)
@@ -613,9 +619,9 @@ class _AddLNExFn(torch.autograd.Function):
             H = dy.shape[-1]
             d3 = dy.view(-1, L, H)
             if has_pos and ng[2]:
-                dpos = torch.sum(d3, 0, dtype=torch.float32).to(dy.dtype)
+                dpos = torch.sum(d3, 0, dtype=torch.float32).to(ctx.pt_dtypes[0])
             if has_temb and ng[3]:
-                dtemb = torch.sum(d3, 1, dtype=torch.float32).to(dy.dtype)
+                dtemb = torch.sum(d3, 1, dtype=torch.float32).to(ctx.pt_dtypes[1])
         return ((dy if ng[0] else None), (dres if has_res else None), dpos, dtemb, dw, db,
                 None, None, None, None, None, None, None, None)
 
@@ -629,8 +635,8 @@ def _add_ln_ex(y, residual, pos, temb, weight, bias, p, eps, training, post):
         out, h = _AddLNExFn.apply(
             y.reshape(-1, H).contiguous(),
             None if residual is None else residual.reshape(-1, H).contiguous(),
-            None if pos is None else pos.reshape(L, H).to(y.dtype).contiguous(),
-            None if temb is None else temb.reshape(B, H).to(y.dtype).contiguous(),
+            None if pos is None else pos.reshape(L, H),
+            None if temb is None else temb.reshape(B, H),
             weight, bias, shadow(weight, y.dtype), shadow(bias, y.dtype), p, eps, seed, off, post, L)
         return out.view(B, L, H), h.view(B, L, H)
     s_ = y

@@ -29,12 +29,16 @@ def grad_norm_(grad_flat, out, partial=None, scale=1.0, max_norm=0.0):
 
 
 def adamw_ema_(param, grad, exp_avg, exp_avg_sq, *, lr, beta1, beta2, eps, weight_decay, step,
-               grad_scale=1.0, clip=None, shadow_bf16=None, emas=(), ema_rates=()):
-    """One fused AdamW step (torch.optim.AdamW math) + EMA + bf16 shadow refresh, in place."""
+               grad_scale=1.0, clip=None, shadow_bf16=None, emas=(), ema_rates=(), skip=None):
+    """One fused AdamW step (torch.optim.AdamW math) + EMA + bf16 shadow refresh, in place.
+    ``skip``: optional int32 device flag; while it is non-zero the step changes nothing (the
+    kernel reads it, so a flag set by an earlier kernel on the stream needs no host sync)."""
     if use_native(param):
         get_ext().adamw_ema(param, grad, exp_avg, exp_avg_sq, shadow_bf16, list(emas),
                             [float(r) for r in ema_rates], float(lr), float(beta1), float(beta2),
-                            float(eps), float(weight_decay), int(step), float(grad_scale), clip)
+                            float(eps), float(weight_decay), int(step), float(grad_scale), clip, skip)
+        return
+    if skip is not None and int(skip.reshape(-1)[0]) != 0:
         return
     g = grad.float() * grad_scale
     if clip is not None:

@@ -34,6 +34,14 @@ implements the same protocol for the single-GPU multi-rank test transport.
   checksum all-reduce (replaces DDP's per-tensor broadcast, SURVEY X-4).
 * HIP-graph mode: when backward runs inside a captured graph no Python hook
   fires; :meth:`finalize` then launches every bucket after the replay.
+* Unused parameters: a bucket whose hooks have not all fired by ``finalize()`` is
+  launched there, after backward, without overlap (torch DDP raises instead).  The
+  first armed step records which hooks fired and warns once, naming the unused
+  parameters (``DPA_DDP_UNUSED=error`` raises instead).
+* IPC data plane (``DPA_IPC_ALLREDUCE=1``): the kernels' bounded spin sets an error
+  word on timeout instead of hanging; :meth:`step_skip_flag` hands it to the fused
+  AdamW (the step is refused on the device, no host sync) and the engine reads it
+  back asynchronously and raises at the next ``finalize()``.
 * ZeRO-1 (``shard_optimizer=True``, parallel/zero.py): buckets are padded to a
   multiple of world x 16 elements and REDUCE-SCATTERED instead of all-reduced;
   rank r receives the summed r-th chunk of every bucket in a compact
@@ -42,6 +50,7 @@ implements the same protocol for the single-GPU multi-rank test transport.
 """
 import contextlib
 import os
+import warnings
 
 import torch
 import torch.distributed as dist
@@ -127,6 +136,11 @@ class DDPEngine(nn.Module):
             for p in b.params:
                 self._bucket_of[id(p)] = b
         self._hooks = []
+        self._fired = set()          # layout indices whose hook fired (first armed step only)
+        self._track_unused = True
+        self._ipc_flag = None        # device int32 error word of the IPC all-reduce
+        self._ipc_host = None
+        self._ipc_event = None
         self._comm_buf = None
         self._comm_out = None
         self.grad_shard = None
@@ -180,6 +194,9 @@ class DDPEngine(nn.Module):
                     blobs = [None] * self.world_size
                     dist.all_gather_object(blobs, self._native.ipc_export(), group=self.pg)
                     self._native.ipc_open(blobs)
+                    self._ipc_flag = self._native.ipc_error_flag()
+                    self._ipc_host = torch.zeros(1, dtype=torch.int32, pin_memory=True)
+                    self._ipc_event = torch.cuda.Event()
         if self.distributed and self.world_size > 1 and self.space.device.type == "cuda":
             # collectives share the CUs with the persistent GEMMs: let late-starting GEMM
             # workgroups take fewer tiles instead of finishing last (csrc/gemm256.hip)
@@ -256,12 +273,16 @@ class DDPEngine(nn.Module):
             native = self._native
 
             def native_hook(_param):
+                if self._track_unused and self._armed:
+                    self._fired.add(index)
                 native.mark_ready(index)  # no-op unless armed
             return native_hook
 
         def hook(_param):
             if not self._armed:
                 return
+            if self._track_unused:
+                self._fired.add(index)
             b = self._bucket_of[id(p)]
             b.pending -= 1
             if b.pending == 0:
@@ -335,9 +356,15 @@ class DDPEngine(nn.Module):
         if not self.distributed or not self._armed:
             return
         if self._native is not None:
+            self._check_ipc_error()
             self._native.finalize()
             self._armed = False
+            self._check_unused(self._native.late_buckets())
+            if self._ipc_flag is not None:
+                self._ipc_host.copy_(self._ipc_flag, non_blocking=True)
+                self._ipc_event.record()
             return
+        late = [b.index for b in self.buckets[self._next_launch:] if b.pending > 0]
         for b in self.buckets[self._next_launch:]:
             self._launch(b)
         self._next_launch = len(self.buckets)
@@ -350,6 +377,45 @@ class DDPEngine(nn.Module):
                 w.wait()
             b.work = None
         self._armed = False
+        self._check_unused(late)
+
+    def _check_unused(self, late_buckets):
+        """First armed step: name the parameters whose grad-ready hook never fired (their
+        buckets were reduced late, after backward); later steps are not tracked."""
+        if not self._track_unused:
+            return
+        self._track_unused = False
+        if not late_buckets:
+            self._fired.clear()
+            return
+        idx = {id(p): i for i, p in enumerate(self.space.layout)}
+        names = {id(p): n for n, p in self.module.named_parameters()}
+        unused = [names.get(id(p), f"<param {idx[id(p)]}>") for b in late_buckets
+                  for p in self.buckets[b].params if idx[id(p)] not in self._fired]
+        self._fired.clear()
+        msg = (f"DDPEngine: {len(unused)} parameter(s) received no gradient in this step "
+               f"({', '.join(unused[:8])}{'...' if len(unused) > 8 else ''}); buckets {list(late_buckets)} "
+               "were all-reduced after backward, so their communication no longer overlaps it. "
+               "Remove the unused parameters from the model (DPA_DDP_UNUSED=error raises).")
+        if os.environ.get("DPA_DDP_UNUSED", "warn") == "error":
+            raise RuntimeError(msg)
+        warnings.warn(msg, RuntimeWarning, stacklevel=3)
+
+    def step_skip_flag(self):
+        """Device int32 word that is non-zero when this step's gradient reduction failed
+        (IPC all-reduce timeout); pass it to the fused optimizer's ``skip``.  None when no
+        such failure mode is active."""
+        return self._ipc_flag
+
+    def _check_ipc_error(self):
+        """Raise on a previous step's IPC all-reduce failure (read back asynchronously)."""
+        if self._ipc_flag is None or not self._ipc_event.query():
+            return
+        if int(self._ipc_host[0]) != 0:
+            raise RuntimeError("DDPEngine: the IPC all-reduce timed out waiting for a peer (its "
+                               "gradients were not reduced; the optimizer step was refused). "
+                               "Ranks drifted apart by more than the kernel's 20 s bound - "
+                               "unset DPA_IPC_ALLREDUCE to use RCCL, which blocks instead.")
 
     def reduce_all_now(self):
         """Graph mode: backward ran without hooks; reduce every bucket now."""

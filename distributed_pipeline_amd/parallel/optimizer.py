@@ -55,7 +55,7 @@ class FusedAdamW:
         fused.grad_norm_(self.space.grad_flat, self.norm_buf, self._partial, grad_scale, max_norm)
         return self.norm_buf
 
-    def step(self, grad_scale=1.0, clip=None, update_ema=True):
+    def step(self, grad_scale=1.0, clip=None, update_ema=True, skip=None):
         g = self.param_groups[0]
         self.step_count += 1
         b1, b2 = g["betas"]
@@ -64,7 +64,7 @@ class FusedAdamW:
                          step=self.step_count, grad_scale=grad_scale, clip=clip,
                          shadow_bf16=self.space.shadow_flat,
                          emas=self.ema_flats if update_ema else (),
-                         ema_rates=self.ema_rates if update_ema else ())
+                         ema_rates=self.ema_rates if update_ema else (), skip=skip)
 
     def zero_grad(self, set_to_none=False):  # noqa: ARG002
         self.space.zero_grad()

@@ -75,7 +75,7 @@ class ZeroFusedAdamW(FusedAdamW):
         self.norm_buf.copy_(torch.cat([norm, coef, norm * coef]))
         return self.norm_buf
 
-    def step(self, grad_scale=1.0, clip=None, update_ema=True):
+    def step(self, grad_scale=1.0, clip=None, update_ema=True, skip=None):
         g = self.param_groups[0]
         self.step_count += 1
         b1, b2 = g["betas"]
@@ -87,7 +87,7 @@ class ZeroFusedAdamW(FusedAdamW):
                              weight_decay=g["weight_decay"], step=self.step_count,
                              grad_scale=grad_scale, clip=clip, shadow_bf16=None,
                              emas=[e[sl] for e in self.ema_flats] if update_ema else (),
-                             ema_rates=self.ema_rates if update_ema else ())
+                             ema_rates=self.ema_rates if update_ema else (), skip=skip)
         self.engine.gather_params()
 
     def zero_grad(self, set_to_none=False):  # noqa: ARG002

@@ -174,6 +174,8 @@ class TrainLoop:
             self._exec_auto = False
         self.exec_microbatch = emb
         self.loss_scale = emb / self.microbatch
+        self._exec_settled = False
+        self._probing = False  # set while _settle_exec_microbatch runs its collective-free probe
 
         self.step = 0
         self.resume_step = 0
@@ -351,6 +353,9 @@ class TrainLoop:
                                 callback(self)
                         finally:
                             self._ema_snapshot = None
+                    # rank 0 may spend a long time in the callbacks (sampling): keep the
+                    # other ranks here instead of inside the next step's bucket collectives
+                    dist_util.barrier()
             if self.step > 0 and self.step % self.save_interval == 0:
                 self.save()
             self.step += 1
@@ -453,20 +458,92 @@ class TrainLoop:
     def forward_backward(self, batch):
         if not self._exec_auto or self.exec_microbatch <= self.microbatch:
             return self._forward_backward(batch)
+        if self.use_ddp and (dist_util.get_world_size() > 1 or self.engine_kind != "native"):
+            # A rank-local out-of-memory retry would desynchronise the collectives (buckets
+            # the failed backward launched, sampler all_gathers, torch DDP's pending
+            # reduction).  Instead the executed micro-batch is settled once, by a
+            # collective-free probe on every rank plus one MIN all-reduce; after that an
+            # out-of-memory error propagates.
+            if not self._exec_settled:
+                self._settle_exec_microbatch(batch)
+            return self._forward_backward(batch)
         while True:
+            snap = self._log_snapshot()
             try:
                 return self._forward_backward(batch)
             except torch.cuda.OutOfMemoryError:
-                # auto executed micro-batch: retry the whole step at half the size (the
-                # gradient buffer is zeroed again, so nothing of the failed try remains)
-                smaller = max(self.microbatch, (self.exec_microbatch // 2) // self.microbatch * self.microbatch)
-                if smaller == self.exec_microbatch:
+                # auto executed micro-batch (one rank): retry the whole step at half the
+                # size; the gradient buffer is zeroed again and the failed try's logged
+                # losses are dropped, so nothing of it remains
+                self._log_restore(snap)
+                if not self._shrink_exec_microbatch():
                     raise
-                logger.log(f"exec_microbatch {self.exec_microbatch} does not fit: retrying with {smaller}")
-                self.exec_microbatch = smaller
                 if self.use_ddp and hasattr(self.ddp_model, "disarm"):
                     self.ddp_model.disarm()
                 torch.cuda.empty_cache()
+
+    def _shrink_exec_microbatch(self):
+        smaller = max(self.microbatch, (self.exec_microbatch // 2) // self.microbatch * self.microbatch)
+        if smaller == self.exec_microbatch:
+            return False
+        logger.log(f"exec_microbatch {self.exec_microbatch} does not fit: retrying with {smaller}")
+        self.exec_microbatch = smaller
+        return True
+
+    def _settle_exec_microbatch(self, batch):
+        """Agree on the executed micro-batch across ranks before the first step: each
+        rank runs the step's forward/backward under ``no_sync`` (no bucket collective,
+        ``_probing`` turns off the hooks' own collectives), halving on out-of-memory,
+        then the ranks take the MIN.  A rank that cannot fit even ``microbatch`` reports
+        0, so every rank raises together instead of hanging in a collective."""
+        import torch.distributed as dist
+        snap = self._log_snapshot()
+        self._probing = True
+        ok = True
+        try:
+            with self.ddp_model.no_sync():
+                while True:
+                    try:
+                        self._forward_backward(batch)
+                        break
+                    except torch.cuda.OutOfMemoryError:
+                        torch.cuda.empty_cache()
+                        if not self._shrink_exec_microbatch():
+                            ok = False
+                            break
+        finally:
+            self._probing = False
+            self._log_restore(snap)
+        self._zero_grad()
+        if torch.cuda.is_available():
+            torch.cuda.empty_cache()
+        dev = dist_util.dev() if dist.get_backend() == "nccl" else torch.device("cpu")
+        t = torch.tensor([self.exec_microbatch if ok else 0], dtype=torch.int64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MIN)
+        agreed = int(t.item())
+        if agreed <= 0:
+            raise torch.cuda.OutOfMemoryError(
+                f"microbatch {self.microbatch} does not fit on some rank (exec_microbatch probe)")
+        if agreed != self.exec_microbatch:
+            logger.log(f"exec_microbatch: rank-agreed {agreed} (this rank fit {self.exec_microbatch})")
+        self.exec_microbatch = agreed
+        self._exec_settled = True
+
+    @staticmethod
+    def _log_snapshot():
+        cur = logger.get_current()
+        return (dict(cur.name2val), dict(cur.name2cnt),
+                {k: (a.clone(), b.clone()) for k, (a, b) in _QuartileAcc.store.items()})
+
+    @staticmethod
+    def _log_restore(snap):
+        cur = logger.get_current()
+        cur.name2val.clear()
+        cur.name2val.update(snap[0])
+        cur.name2cnt.clear()
+        cur.name2cnt.update(snap[1])
+        _QuartileAcc.store.clear()
+        _QuartileAcc.store.update(snap[2])
 
     def _forward_backward(self, batch):
         self._zero_grad()
@@ -522,7 +599,8 @@ class TrainLoop:
             return
         logger.logkv_mean("grad_norm", norm[2] if max_norm > 0 else norm[0])
         self._anneal_lr()
-        self.opt.step(grad_scale=scale, clip=norm if max_norm > 0 else None)
+        self.opt.step(grad_scale=scale, clip=norm if max_norm > 0 else None,
+                      skip=getattr(eng, "step_skip_flag", lambda: None)())
 
     def _grad_finite_or_skip(self, norm):
         """Non-finite gradient guard: ``nan_guard`` = off | skip | abort.
@@ -788,7 +866,8 @@ class DiffusionTrainLoop(TrainLoop):
         losses = self.diffusion.training_losses(
             self.ddp_model, None, t, model_kwargs=dict(input_ids=micro_batch["input_ids"],
                                                        input_mask=micro_batch["input_mask"]))
-        if hasattr(self.schedule_sampler, "update_with_local_losses") and torch.is_grad_enabled():
+        if (hasattr(self.schedule_sampler, "update_with_local_losses") and torch.is_grad_enabled()
+                and not self._probing):
             self.schedule_sampler.update_with_local_losses(t, losses["loss"].detach())
         return losses
 
