@@ -2,7 +2,7 @@
 // GEMMs on the DiffuSeq-base shapes, interleaved in one process (rounds x variants,
 // median reported), on uniform random [-1, 1) bf16 operands.
 //
-// build: hipcc -O3 --offload-arch=gfx950 -std=c++17 -I../../distributed_pipeline_amd/csrc \
+// build: hipcc -O3 --offload-arch=gfx950 -std=c++17 -I../../distributed_pipeline_amd/csrc -I. \
 //          gemm_lab.hip -o gemm_lab
 // run:   ./gemm_lab [rounds]
 #include <hip/hip_runtime.h>
@@ -16,6 +16,7 @@
 #include <vector>
 
 #include "gemm256.hip"
+#include "gemm_pp.hip"
 
 namespace dpa {
 int device_cu_count() {
@@ -256,6 +257,28 @@ int main(int argc, char** argv) {
                     }, fl, {}});
     }
   }
+  // ping-pong kernel (gemm_pp.hip): main loop alone, plain bias epilogue, GELU epilogue, dgrad
+  for (const Shape& sh : shapes) {
+    const int K = sh.K, N = sh.N;
+    const double fl = 2.0 * T * K * N;
+    const std::string nm = sh.name;
+    vs.push_back({nm + "/pp_fwd_nostore", [=](hipStream_t st) {
+                    dpa::launch_gemm_pp_nt(A, B, bias, C, nullptr, T, N, K, 0, ncu, st, -1);
+                  }, fl, {}});
+    vs.push_back({nm + "/pp_fwd", [=](hipStream_t st) {
+                    dpa::launch_gemm_pp_nt(A, B, bias, C, nullptr, T, N, K, 0, ncu, st, 0);
+                  }, fl, {}});
+    vs.push_back({nm + "/pp_dgrad_nostore", [=](hipStream_t st) {
+                    dpa::launch_gemm_pp_nn(A, B, C, T, N, K, ncu, st, -1);
+                  }, fl, {}});
+    vs.push_back({nm + "/pp_dgrad", [=](hipStream_t st) {
+                    dpa::launch_gemm_pp_nn(A, B, C, T, N, K, ncu, st, 0);
+                  }, fl, {}});
+    if (nm == "ffn_in")
+      vs.push_back({nm + "/pp_fwd_gelu", [=](hipStream_t st) {
+                      dpa::launch_gemm_pp_nt(A, B, bias, C, Z, T, N, K, 1, ncu, st, 0);
+                    }, fl, {}});
+  }
   // epilogue cost split: ldc = 0 makes every row of a column band hit the same L2 lines
   // (stores still issue, the HBM drain is ~gone) - issue/VALU cost vs drain cost
   {
@@ -356,6 +379,35 @@ int main(int argc, char** argv) {
     CK(hipStreamSynchronize(s));
     // dx[T][K] = dy[T][N] . W[N][K]: reference with reduction N, output width K, B = [N][K] as [k][n]
     printf("check %s gp_dgrad relerr %.3e\n", sh.name, check(A, B, true, C, T, K, N));
+    fflush(stdout);
+  }
+  for (const Shape& sh : shapes) {  // ping-pong kernel correctness
+    const int K = sh.K, N = sh.N;
+    CK(hipMemset(C, 0, (size_t)T * N * 2));
+    dpa::launch_gemm_pp_nt(A, B, nullptr, C, nullptr, T, N, K, 0, ncu, s, 0);
+    CK(hipStreamSynchronize(s));
+    printf("check %s pp_fwd relerr %.3e\n", sh.name, check(A, B, false, C, T, N, K));
+    CK(hipMemset(C, 0, (size_t)T * K * 2));
+    dpa::launch_gemm_pp_nn(A, B, C, T, N, K, ncu, s, 0);
+    CK(hipStreamSynchronize(s));
+    printf("check %s pp_dgrad relerr %.3e\n", sh.name, check(A, B, true, C, T, K, N));
+    fflush(stdout);
+  }
+  {  // ping-pong bias and GELU epilogues against the 256 x 256 persistent kernel
+    const int K = 768, N = 3072;
+    uint16_t *C2, *Z2;
+    CK(hipMalloc(&C2, (size_t)T * N * 2));
+    CK(hipMalloc(&Z2, (size_t)T * N * 2));
+    dpa::launch_gemmp_nt(A, B, bias, C, nullptr, T, N, K, 0, ncu, s);
+    dpa::launch_gemm_pp_nt(A, B, bias, C2, nullptr, T, N, K, 0, ncu, s, 0);
+    CK(hipStreamSynchronize(s));
+    printf("check pp bias y maxdiff %.3e\n", maxdiff(C, C2, (int64_t)T * N));
+    dpa::launch_gemmp_nt(A, B, bias, C, Z, T, N, K, 1, ncu, s, true);
+    dpa::launch_gemm_pp_nt(A, B, bias, C2, Z2, T, N, K, 1, ncu, s, 0);
+    CK(hipStreamSynchronize(s));
+    printf("check pp gelu y maxdiff %.3e d maxdiff %.3e\n", maxdiff(C, C2, (int64_t)T * N), maxdiff(Z, Z2, (int64_t)T * N));
+    CK(hipFree(C2));
+    CK(hipFree(Z2));
     fflush(stdout);
   }
   {  // fused epilogues against the unfused g256 kernels (bitwise-close: same bf16 rounding points)
