@@ -374,6 +374,52 @@ static std::tuple<at::Tensor, at::Tensor, bool> gemm_nt(const at::Tensor& x, con
   return {y, z, deriv};
 }
 
+// y = x . W^T (+ b) into a preallocated row-major [T, N] tensor (a row slice of a larger
+// buffer, e.g. the LM head's [tokens, padded vocab] logits).
+static void gemm_nt_into(const at::Tensor& x, const at::Tensor& W, c10::optional<at::Tensor> b,
+                         at::Tensor& out) {
+  CHECK_DEV(x); CHECK_BF16(x); CHECK_BF16(W); CHECK_BF16(out); CHECK_CONTIG(x); CHECK_CONTIG(W);
+  CHECK_CONTIG(out);
+  const int T = (int)x.size(0), K = (int)x.size(1), N = (int)W.size(0);
+  TORCH_CHECK(W.size(1) == K && out.dim() == 2 && out.size(0) == T && out.size(1) == N, "gemm_nt_into shapes");
+  const c10::DeviceGuard guard(x.device());
+  bool ok = dpa::launch_gemm_nt(bf_ptr(x), bf_ptr(W), opt_bf_ptr(b), reinterpret_cast<uint16_t*>(out.data_ptr()),
+                                nullptr, T, N, K, 0, cur_stream(), nullptr);
+  TORCH_CHECK(ok, "gemm_nt_into: unsupported shape T=", T, " N=", N, " K=", K);
+}
+
+// dx = dy . W into a preallocated [T, K] tensor.
+static void gemm_nn_into(const at::Tensor& dy, const at::Tensor& W, at::Tensor& dx) {
+  CHECK_DEV(dy); CHECK_BF16(dy); CHECK_BF16(W); CHECK_BF16(dx); CHECK_CONTIG(dy); CHECK_CONTIG(W);
+  CHECK_CONTIG(dx);
+  const int T = (int)dy.size(0), N = (int)dy.size(1), K = (int)W.size(1);
+  TORCH_CHECK(W.size(0) == N && dx.size(0) == T && dx.size(1) == K, "gemm_nn_into shapes");
+  const c10::DeviceGuard guard(dy.device());
+  bool ok = dpa::launch_gemm_nn(bf_ptr(dy), bf_ptr(W), reinterpret_cast<uint16_t*>(dx.data_ptr()), T, N, K,
+                                cur_stream());
+  TORCH_CHECK(ok, "gemm_nn_into: unsupported shape T=", T, " N=", N, " K=", K);
+}
+
+// dW[ids[i]] += dy[i] (fp32 accumulate): device sort of the ids, then one wave per run
+// of equal ids sums its rows in registers and adds once (csrc/diffusion.hip) - the
+// token-embedding backward without ATen's index_add.
+static void emb_grad(const at::Tensor& ids, const at::Tensor& dy, at::Tensor& dW) {
+  CHECK_DEV(ids); CHECK_DEV(dy); CHECK_DEV(dW); CHECK_CONTIG(dy); CHECK_CONTIG(dW); CHECK_F32(dW);
+  TORCH_CHECK(ids.scalar_type() == at::kLong, "emb_grad: int64 ids");
+  TORCH_CHECK(dy.scalar_type() == at::kBFloat16 || dy.scalar_type() == at::kFloat, "emb_grad: bf16/fp32 dy");
+  const int64_t NT = ids.numel(), E = dW.size(1);
+  TORCH_CHECK(dy.numel() == NT * E, "emb_grad: dy [ids..., E]");
+  if (NT == 0) return;
+  const c10::DeviceGuard guard(dW.device());
+  at::Tensor sorted, perm;
+  std::tie(sorted, perm) = at::sort(ids.reshape({-1}));
+  const bool b16 = dy.scalar_type() == at::kBFloat16;
+  TORCH_CHECK(dpa::launch_emb_grad(sorted.data_ptr<int64_t>(), perm.data_ptr<int64_t>(),
+                                   b16 ? nullptr : dy.data_ptr<float>(), b16 ? bf_ptr(dy) : nullptr, NT, (int)E,
+                                   (int)dW.size(0), dW.data_ptr<float>(), cur_stream()),
+              "emb_grad: unsupported embedding width ", E);
+}
+
 static at::Tensor gemm_nn(const at::Tensor& dy, const at::Tensor& W) {
   CHECK_DEV(dy); CHECK_BF16(dy); CHECK_BF16(W); CHECK_CONTIG(dy); CHECK_CONTIG(W);
   const int T = (int)dy.size(0), N = (int)dy.size(1), K = (int)W.size(1);
@@ -663,6 +709,9 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("dg_acc") = py::none(), py::arg("db_acc") = py::none(), py::arg("dyb_acc") = py::none());
   m.def("bias_act_fwd", &bias_act_fwd, "z += bias (in place); y = act(z) -> (z, y)");
   m.def("bias_act_bwd", &bias_act_bwd, "dz = dy*act'(zy); db = colsum(dz) -> (dz, db)");
+  m.def("gemm_nt_into", &gemm_nt_into, "y = x W^T (+b) into a preallocated [T, N] tensor");
+  m.def("gemm_nn_into", &gemm_nn_into, "dx = dy W into a preallocated [T, K] tensor");
+  m.def("emb_grad", &emb_grad, "dW[ids] += dy (sorted segment sum, fp32)");
   m.def("attn_fwd", &attn_fwd, "fused attention forward (head_dim 64/128) -> (out, lse)");
   m.def("attn_bwd", &attn_bwd, "fused attention backward -> (dqkv, colsum(dqkv) or None)",
         py::arg("dout"), py::arg("qkv"), py::arg("out"), py::arg("lse"), py::arg("heads"), py::arg("p"),

@@ -329,6 +329,27 @@ bool launch_emb_qsample_bwd(const int64_t* ids, const int64_t* mask, const int64
   return true;
 }
 
+// Plain token-embedding backward over sorted ids (GPT-2 wte / wpe): the same sorted
+// segment-sum kernel with only the upstream gradient as input.
+bool launch_emb_grad(const int64_t* sorted_ids, const int64_t* perm, const float* dy32, const uint16_t* dy16,
+                     int64_t NT, int E, int V, float* dW, hipStream_t s) {
+  constexpr int CHUNK = 16;
+  const unsigned grid = (unsigned)(((NT + CHUNK - 1) / CHUNK + 3) / 4);
+  auto go = [&](auto kern) {
+    hipLaunchKernelGGL(kern, dim3(grid), dim3(256), 0, s, sorted_ids, perm, (const int64_t*)nullptr,
+                       (const int64_t*)nullptr, (const float*)nullptr, dy32, (const bf16_t*)dy16,
+                       (const bf16_t*)nullptr, (const float*)nullptr, NT, 1, V, dW, CHUNK);
+  };
+  switch (E) {
+    case 128: go(emb_grad_sorted_kernel<2>); return true;
+    case 256: go(emb_grad_sorted_kernel<4>); return true;
+    case 768: go(emb_grad_sorted_kernel<12>); return true;
+    case 1024: go(emb_grad_sorted_kernel<16>); return true;
+    case 2048: go(emb_grad_sorted_kernel<32>); return true;
+    default: return false;
+  }
+}
+
 bool launch_diff_loss_fwd(const float* x_start, const void* out, bool out_bf16, const int64_t* ids,
                           const int64_t* t, const float* W, int B, int L, int E, int V, float sa_last,
                           float* mse, float* tT, hipStream_t s) {

@@ -105,6 +105,8 @@ bool launch_emb_qsample_fwd(const int64_t* ids, const int64_t* mask, const int64
                             const float* sa, const float* s1a, int64_t NT, int L, int E, int V,
                             float std0, uint32_t seed, uint32_t offset, float* x_start,
                             uint16_t* x_start16, uint16_t* x_t, hipStream_t s);
+bool launch_emb_grad(const int64_t* sorted_ids, const int64_t* perm, const float* dy32, const uint16_t* dy16,
+                     int64_t NT, int E, int V, float* dW, hipStream_t s);
 bool launch_emb_qsample_bwd(const int64_t* ids, const int64_t* mask, const int64_t* t, const float* sa,
                             const float* d_xs, const uint16_t* d_xs16, const uint16_t* d_xt16,
                             const float* d_xt32, int64_t NT, int L, int E, int V, float* dW,

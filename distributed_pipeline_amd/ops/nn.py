@@ -825,48 +825,53 @@ def _pad_vocab(w16, b16, mult=256):
     return wp, bp
 
 
-def _chunk_logits(xc, wp, bp):
-    """[chunk, Vp] logits of one token chunk.  hipBLASLt on purpose: a K = 768 GEMM
-    writing 0.5 GB of bf16 logits per chunk is store-bound, where the persistent
-    kernel's non-overlapped epilogue loses (measured r2: 21 vs 13 ms per GPT-2 step),
-    and the chunk's dx GEMM (output 768 wide, K = Vp) needs split-K."""
-    return torch.addmm(bp, xc, wp.t()) if bp is not None else xc @ wp.t()
+def _chunk_logits(xc, wp, bp, out=None):
+    """[chunk, Vp] logits of one token chunk on the persistent MFMA GEMM (bias fused,
+    written straight into ``out`` - a row slice of the [N, Vp] buffer - when given)."""
+    if out is None:
+        out = torch.empty(xc.shape[0], wp.shape[0], dtype=xc.dtype, device=xc.device)
+    get_ext().gemm_nt_into(xc, wp, bp, out)
+    return out
 
 
 class _ChunkedLinearXentFn(torch.autograd.Function):
-    """Per-token CE for WIDE inputs (E > 256, e.g. GPT-2's 768 x 50257 LM head): the
-    logits of one token chunk at a time come from hipBLASLt into a [chunk, Vp] bf16
-    buffer and the row kernels of ``csrc/xent_rows.hip`` turn them into (loss, lse) -
-    in backward into dlogits in place - so the [N, V] logits never exist whole.
-    Backward recomputes each chunk's logits (one GEMM) rather than storing them."""
+    """Per-token CE for WIDE inputs (E > 256, e.g. GPT-2's 768 x 50257 LM head).
+
+    All three GEMMs run on the hand-written gfx950 kernels (csrc/gemm256.hip): the logits
+    of one token chunk at a time (bias fused) into a [chunk, Vp] bf16 buffer, which the
+    row kernels of ``csrc/xent_rows.hip`` turn into (loss, lse) and - when the logits are
+    kept for the backward - into softmax - onehot in place; backward dx = dlogits W
+    (data-gradient GEMM, K = Vp) and dW = dlogits^T (g x) (split-K weight-gradient GEMM
+    over all tokens at once).  The vocabulary is padded to a multiple of 256 once per
+    forward (the padded weight is reused by the backward) and the token count to a
+    multiple of 256 (padded tokens have target -1: zero loss, zero gradient rows)."""
 
     @staticmethod
     def forward(ctx, x, w, b, w16, b16, target, chunk):
         ext = get_ext()
-        N, V = x.shape[0], w16.shape[0]
+        N0, V = x.shape[0], w16.shape[0]
+        N = (N0 + 255) // 256 * 256
+        if N != N0:  # token rows padded to the GEMM tile (zero rows, ignored targets)
+            xp = torch.zeros(N, x.shape[1], dtype=x.dtype, device=x.device)
+            xp[:N0].copy_(x)
+            tp = torch.full((N,), -1, dtype=target.dtype, device=target.device)
+            tp[:N0].copy_(target)
+            x, target = xp, tp
         wp, bp = _pad_vocab(w16, b16)
         loss = torch.empty(N, dtype=torch.float32, device=x.device)
         lse = torch.empty(N, dtype=torch.float32, device=x.device)
-        # 288 GB of HBM: keep the bf16 logit chunks for the backward (which turns them
-        # into dlogits in place) instead of recomputing them, when they fit the budget
+        # 288 GB of HBM: keep the bf16 logits for the backward (which then needs no logits
+        # GEMM of its own) when they fit the budget
         keep = any(ctx.needs_input_grad[:3]) and N * wp.shape[0] * 2 <= _XENT_KEEP_BYTES
-        kept = []
-        # kept chunks: one row pass leaves softmax - onehot (unscaled) in place of the
-        # logits (xent_rows_fwd_grad_), so the backward needs no row pass of its own;
-        # the chunks are row slices of ONE [N, Vp] buffer, so the backward's weight
-        # gradient is a single split-K GEMM over all N tokens
+        # kept logits: one row pass leaves softmax - onehot (unscaled) in place of the
+        # logits (xent_rows_fwd_grad_), so the backward needs no row pass of its own; all
+        # chunks are row slices of ONE [N, Vp] buffer, so the backward's weight gradient is
+        # a single split-K GEMM over all N tokens
         kept_is_grad = keep and _XENT_ROWS_FUSED
-        allg = torch.empty(N, wp.shape[0], dtype=x.dtype, device=x.device) if kept_is_grad else None
+        allg = torch.empty(N, wp.shape[0], dtype=x.dtype, device=x.device) if keep else None
         for s in range(0, N, chunk):
             e = min(N, s + chunk)
-            if allg is not None:
-                lg = allg[s:e]
-                if bp is not None:
-                    torch.addmm(bp, x[s:e], wp.t(), out=lg)
-                else:
-                    torch.mm(x[s:e], wp.t(), out=lg)
-            else:
-                lg = _chunk_logits(x[s:e], wp, bp)
+            lg = _chunk_logits(x[s:e], wp, bp, allg[s:e] if allg is not None else None)
             if kept_is_grad:
                 res = ext.xent_rows_fwd_grad_(lg, V, target[s:e])
                 assert res, "xent_rows_fwd_grad_ refused the row length"
@@ -875,67 +880,54 @@ class _ChunkedLinearXentFn(torch.autograd.Function):
                 l_c, lse_c = ext.xent_rows_fwd(lg, V, target[s:e])
             loss[s:e].copy_(l_c)
             lse[s:e].copy_(lse_c)
-            if keep:
-                kept.append(lg)
-        ctx.kept = kept if keep else None
-        ctx.kept_is_grad = kept_is_grad
         ctx.allg = allg
-        ctx.save_for_backward(x, w16, b16, target, lse)
+        ctx.kept_is_grad = kept_is_grad
+        ctx.save_for_backward(x, w16, b16, target, lse, wp, bp)
         ctx.params = (w, b)
         ctx.chunk = chunk
-        return loss
+        ctx.n0 = N0
+        return loss[:N0]
 
     @staticmethod
     def backward(ctx, dloss):
-        x, w16, b16, target, lse = ctx.saved_tensors
+        x, w16, b16, target, lse, wp, bp = ctx.saved_tensors
         w, b = ctx.params
         ext = get_ext()
         N, E, V = x.shape[0], x.shape[1], w16.shape[0]
-        wp, bp = _pad_vocab(w16, b16)
+        N0 = ctx.n0
         Vp = wp.shape[0]
-        dloss = dloss.contiguous().float()
+        g_all = torch.zeros(N, dtype=torch.float32, device=x.device)
+        g_all[:N0].copy_(dloss)
         need_dx, need_dw, need_db = ctx.needs_input_grad[0], ctx.needs_input_grad[1], (
             b is not None and ctx.needs_input_grad[2])
         dx = torch.empty_like(x) if need_dx else None
         dwp = torch.zeros(Vp, E, dtype=torch.float32, device=x.device) if need_dw else None
         db = torch.zeros(V, dtype=torch.float32, device=x.device) if need_db else None
-        native_wgrad = need_dw and Vp % 256 == 0 and E % 256 == 0 and hasattr(ext, "gemm_wgrad")
-        kept, ctx.kept = ctx.kept, None
         allg, ctx.allg = ctx.allg, None
-        unscaled = kept is not None and ctx.kept_is_grad
-        # all chunks in one buffer: dW = G^T (diag(g) x) as one GEMM after the chunk loop
-        whole_wgrad = (unscaled and allg is not None and need_dw and native_wgrad and N % 128 == 0)
-        for ci, s in enumerate(range(0, N, ctx.chunk)):
+        unscaled = allg is not None and ctx.kept_is_grad
+        for s in range(0, N, ctx.chunk):
             e = min(N, s + ctx.chunk)
-            dlg = kept[ci] if kept is not None else _chunk_logits(x[s:e], wp, bp)
-            if kept is not None:
-                kept[ci] = None  # freed as soon as its gradient GEMMs are queued
-            if unscaled:
-                # dlg = softmax - onehot; the per-token upstream gradient g scales rows:
-                # dx = diag(g) (G W), dW = G^T (diag(g) x), db = G^T g
-                g = dloss[s:e]
-                xg = (x[s:e] * g[:, None]).to(x.dtype) if need_dw and not whole_wgrad else None
-            else:
-                ext.xent_rows_bwd_(dlg, V, target[s:e], lse[s:e], dloss[s:e])
-                xg = x[s:e]
+            # a kept chunk is a row slice of allg: it is freed with the whole buffer at
+            # the end of the backward, not per chunk
+            dlg = allg[s:e] if allg is not None else _chunk_logits(x[s:e], wp, bp)
+            g = g_all[s:e]
+            if not unscaled:
+                ext.xent_rows_bwd_(dlg, V, target[s:e], lse[s:e], g)
             if need_dx:
-                torch.mm(dlg, wp, out=dx[s:e])
-                if unscaled:
+                ext.gemm_nn_into(dlg, wp, dx[s:e])
+                if unscaled:  # dlg = softmax - onehot: the upstream gradient scales rows
                     dx[s:e].mul_(g[:, None])
-            if need_dw and not whole_wgrad:
-                if native_wgrad and (e - s) % 128 == 0:
-                    ext.gemm_wgrad(dlg, xg, dwp, None)   # split-K MFMA, fp32 accumulate
-                else:
-                    dwp.add_(_mm_fp32(dlg.t(), xg))
+            if need_dw and allg is None:
+                ext.gemm_wgrad(dlg, x[s:e] if not unscaled else (x[s:e] * g[:, None]).to(x.dtype), dwp, None)
             if need_db:
-                if unscaled:
-                    db.add_(g @ dlg[:, :V].float())
-                else:
-                    db.add_(dlg[:, :V].float().sum(0))
-        if whole_wgrad:
-            ext.gemm_wgrad(allg, (x * dloss[:, None]).to(x.dtype), dwp, None)
+                db.add_((g @ dlg[:, :V].float()) if unscaled else dlg[:, :V].float().sum(0))
+        if need_dw and allg is not None:
+            # dW = G^T (diag(g) x) over all N tokens as one split-K GEMM
+            ext.gemm_wgrad(allg, (x * g_all[:, None]).to(x.dtype) if unscaled else x, dwp, None)
         del allg
         dw = dwp[:V] if need_dw else None
+        if dx is not None and N != N0:
+            dx = dx[:N0]
         return dx, dw, db, None, None, None, None
 
 
@@ -958,8 +950,8 @@ def linear_cross_entropy(x, weight, bias, target):
     """Per-token CE of logits = x @ W^T + b against ``target`` without materialising logits.
 
     x: [N, E]; weight: [V, E]; target: [N] int64 -> loss [N] fp32.  E in {128, 256}:
-    fully fused MFMA kernels (csrc/xent.hip); wider E: chunked hipBLASLt logits +
-    row kernels (csrc/xent_rows.hip).
+    fully fused MFMA kernels (csrc/xent.hip); wider E: chunked logits on the persistent
+    MFMA GEMM + row kernels (csrc/xent_rows.hip).
     """
     if x.dtype == torch.bfloat16 and native_ok(x, kernel="lxent_fwd") and x.shape[-1] in (128, 256):
         return _LinearXentFn.apply(x.contiguous(), weight, bias, shadow(weight, x.dtype),
@@ -988,7 +980,11 @@ class _EmbFn(torch.autograd.Function):
     def backward(ctx, dy):
         (ids,) = ctx.saved_tensors
         dw = torch.zeros(ctx.n, dy.shape[-1], dtype=torch.float32, device=dy.device)
-        dw.index_add_(0, ids.reshape(-1), dy.reshape(-1, dy.shape[-1]).float())
+        if native_ok(dy, kernel="emb_grad") and dy.shape[-1] in (128, 256, 768, 1024, 2048):
+            # sorted segment sum on the device (csrc/diffusion.hip), no ATen index_add
+            get_ext().emb_grad(ids.contiguous(), dy.contiguous(), dw)
+        else:
+            dw.index_add_(0, ids.reshape(-1), dy.reshape(-1, dy.shape[-1]).float())
         return None, dw, None
 
 

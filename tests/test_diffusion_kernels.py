@@ -175,3 +175,16 @@ def test_fused_training_losses_run_and_reach_embedding():
     for k in ("decoder_nll", "mse"):
         a, b = terms[k].mean().item(), ref[k].mean().item()
         assert abs(a - b) <= 0.05 * abs(b) + 1e-4, (k, a, b)
+
+
+@pytest.mark.parametrize("E,V,n", [(768, 50257, 32 * 1024), (128, 30522, 4096), (1024, 512, 2000)])
+def test_emb_grad_sorted_matches_index_add(E, V, n):
+    """Token-embedding backward (GPT-2 wte/wpe): sorted segment sum vs fp32 index_add."""
+    g = torch.Generator(device=DEV).manual_seed(3)
+    ids = torch.randint(0, V, (n,), device=DEV, generator=g)
+    ids[: n // 4] = 7  # one long run of a repeated id
+    dy = torch.randn(n, E, device=DEV, generator=g).to(torch.bfloat16)
+    dw = torch.zeros(V, E, device=DEV)
+    get_ext().emb_grad(ids, dy, dw)
+    ref = torch.zeros(V, E, device=DEV).index_add_(0, ids, dy.float())
+    torch.testing.assert_close(dw, ref, rtol=1e-4, atol=1e-3)
