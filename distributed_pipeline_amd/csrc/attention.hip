@@ -842,10 +842,16 @@ static void attn_fwd_general(const uint16_t* qkv, uint16_t* out, float* lse, int
                        (bf16_t*)out, lse, L, H, p, seed, offset);
 }
 
-void launch_attn_fwd(const uint16_t* qkv, uint16_t* out, float* lse, int B, int L, int H, int D,
-                     float p, bool causal, uint32_t seed, uint32_t offset, hipStream_t s) {
-  if (D == 128) return attn_fwd_general<128>(qkv, out, lse, B, L, H, p, causal, seed, offset, s);
-  if (launch_attn128_fwd(qkv, out, lse, B, L, H, p, causal, seed, offset, s)) return;
+bool launch_attn_fwd(const uint16_t* qkv, uint16_t* out, float* lse, int B, int L, int H, int D,
+                     float p, bool causal, uint32_t seed, uint32_t offset, hipStream_t s, bool head_major) {
+  if (head_major)  // only the persistent L = 128 kernels read the head-major layout
+    return attn128_supports(L, D, causal) &&
+           launch_attn128_fwd(qkv, out, lse, B, L, H, p, causal, seed, offset, s, true);
+  if (D == 128) {
+    attn_fwd_general<128>(qkv, out, lse, B, L, H, p, causal, seed, offset, s);
+    return true;
+  }
+  if (launch_attn128_fwd(qkv, out, lse, B, L, H, p, causal, seed, offset, s)) return true;
   if (L <= 128) {
     dim3 grid((L + 127) / 128, H, B);
     if (causal)
@@ -854,9 +860,10 @@ void launch_attn_fwd(const uint16_t* qkv, uint16_t* out, float* lse, int B, int 
     else
       hipLaunchKernelGGL(attn_fwd_small_kernel<false>, grid, dim3(256), 0, s, (const bf16_t*)qkv,
                          (bf16_t*)out, lse, L, H, p, seed, offset);
-    return;
+    return true;
   }
   attn_fwd_general<64>(qkv, out, lse, B, L, H, p, causal, seed, offset, s);
+  return true;
 }
 
 bool attn_bwd_needs_dq_acc(int L) { (void)L; return false; }
@@ -886,8 +893,11 @@ static void attn_bwd_general(const uint16_t* qkv, const uint16_t* out, const uin
 bool launch_attn_bwd(const uint16_t* qkv, const uint16_t* out, const uint16_t* dout, const float* lse,
                      float* delta, uint16_t* dqkv, float* dq_acc, float* colpart, float* dbias, int B,
                      int L, int H, int D, float p, bool causal, uint32_t seed, uint32_t offset,
-                     hipStream_t s) {
+                     hipStream_t s, bool head_major) {
   (void)dq_acc;
+  if (head_major)  // caller checked attn128_supports
+    return launch_attn128_bwd(qkv, out, dout, lse, dqkv, colpart, dbias, B, L, H, p, causal, seed, offset, s,
+                              true) && dbias != nullptr;
   if (D == 128) {
     attn_bwd_general<128>(qkv, out, dout, lse, delta, dqkv, B, L, H, p, causal, seed, offset, s);
     return false;

@@ -177,30 +177,56 @@ __device__ __forceinline__ void dma_img(char* img, const bf16_t* src, int64_t ld
 __device__ __forceinline__ float bflo(uint32_t w) { return __uint_as_float(w << 16); }
 __device__ __forceinline__ float bfhi(uint32_t w) { return __uint_as_float(w & 0xffff0000u); }
 
+// Where Q / K / V of (batch b, head h) live: element (l, d) of Q at
+// qkv + b sb + h sh + l ld + d, K and V at + sw and + 2 sw.
+//  token-major (the Linear output [B, L, 3, H, HD]): rows of 3 H HD elements, a head's
+//    128-byte row segments strided by the whole token row;
+//  head-major [B, 3 H, L, HD] (the QKV GEMM's head-major epilogue store): every [L][HD] head
+//    block is 16 KiB contiguous.
+struct QkvLayout {
+  int64_t sb, sh, sw, ld;
+};
+__device__ __forceinline__ QkvLayout qkv_layout(int H, int hmaj) {
+  QkvLayout q;
+  q.sb = 3LL * H * L * HD;
+  if (hmaj) {
+    q.sh = (int64_t)L * HD;
+    q.sw = (int64_t)H * L * HD;
+    q.ld = HD;
+  } else {
+    q.sh = HD;
+    q.sw = (int64_t)H * HD;
+    q.ld = 3LL * H * HD;
+  }
+  return q;
+}
+
 // ============================================================================
 // forward
 // ============================================================================
 __global__ void __launch_bounds__(256, 2) attn128_fwd_kernel(const bf16_t* __restrict__ qkv,
                                                             bf16_t* __restrict__ out,
                                                             float* __restrict__ lse, int B, int H,
-                                                            float p, uint32_t seed, uint32_t offset) {
+                                                            float p, uint32_t seed, uint32_t offset,
+                                                            int hmaj) {
   // two workgroups per CU (8 waves: one wave of each on every SIMD hides the
   // other's latencies); per workgroup 2 stages at s * 32K: K, V images.  Q goes
   // straight to fragment registers (each wave needs only its 32 queries).
   __shared__ __attribute__((aligned(1024))) char smem[2 * 2 * IMG];
   const int w = threadIdx.x >> 6;
   const int nitems = B * H;
-  const int64_t ld = 3LL * H * HD, ldo = (int64_t)H * HD;
+  const QkvLayout lay = qkv_layout(H, hmaj);
+  const int64_t ld = lay.ld, ldo = (int64_t)H * HD;
   const uint32_t sb = lds_u32(smem);
 
   bf16x8 qpf[4];
   const int tid = threadIdx.x, lane = tid & 63, hf = lane >> 5;
   auto issue = [&](int item, int stg) {
     const int b = item / H, hd = item - b * H;
-    const bf16_t* qb = qkv + (int64_t)b * L * ld + (int64_t)hd * HD;
+    const bf16_t* qb = qkv + (int64_t)b * lay.sb + (int64_t)hd * lay.sh;
     char* base = smem + stg * 2 * IMG;
-    dma_img(base, qb + (int64_t)H * HD, ld, w, lane);
-    dma_img(base + IMG, qb + 2LL * H * HD, ld, w, lane);
+    dma_img(base, qb + lay.sw, ld, w, lane);
+    dma_img(base + IMG, qb + 2 * lay.sw, ld, w, lane);
     const bf16_t* qrow = qb + (int64_t)(w * 32 + (lane & 31)) * ld;
 #pragma unroll
     for (int s = 0; s < 4; ++s) qpf[s] = ld_frag(qrow + 16 * s + 8 * hf);
@@ -494,9 +520,11 @@ __device__ __forceinline__ void bwd_stage_out(const f32x16& acc, float scale, ui
 __global__ void __launch_bounds__(256, 2) attn128_bwd_kernel(
     const bf16_t* __restrict__ qkv, const bf16_t* __restrict__ out, const bf16_t* __restrict__ dout,
     const float* __restrict__ lse, bf16_t* __restrict__ dqkv, float* __restrict__ colpart, int B,
-    int H, float p, uint32_t seed, uint32_t offset) {
+    int H, float p, uint32_t seed, uint32_t offset, int hmaj) {
   __shared__ __attribute__((aligned(1024))) char smem[BWD_STATS + 2 * L * 4];
   const int nitems = B * H;
+  const QkvLayout lay = qkv_layout(H, hmaj);
+  // qkv is read in its own layout; dqkv is always written token-major [B, L, 3 H HD]
   const int64_t ld = 3LL * H * HD, ldo = (int64_t)H * HD;
   const uint32_t sb = lds_u32(smem);
   const int w = threadIdx.x >> 6;
@@ -515,10 +543,10 @@ __global__ void __launch_bounds__(256, 2) attn128_bwd_kernel(
     const BwdBases BB = bwd_bases(lane, w, tid);
     const uint32_t base = sb;
     const int b = item / H, hd = item - b * H;
-    const bf16_t* qb = qkv + (int64_t)b * L * ld + (int64_t)hd * HD;
-    dma_img(smem + I_Q, qb, ld, w, lane);
+    const bf16_t* qb = qkv + (int64_t)b * lay.sb + (int64_t)hd * lay.sh;
+    dma_img(smem + I_Q, qb, lay.ld, w, lane);
     dma_img(smem + I_DO, dout + (int64_t)b * L * ldo + (int64_t)hd * HD, ldo, w, lane);
-    dma_img(smem + I_K, qb + (int64_t)H * HD, ld, w, lane);
+    dma_img(smem + I_K, qb + lay.sw, lay.ld, w, lane);
     uint4 opf[4];
     {
       const bf16_t* orow = out + ((int64_t)b * L + (tid >> 1)) * ldo + (int64_t)hd * HD + (tid & 1) * 32;
@@ -527,7 +555,7 @@ __global__ void __launch_bounds__(256, 2) attn128_bwd_kernel(
     }
     bf16x8 vf[4];
     {
-      const bf16_t* vrow = qb + (int64_t)key * ld + 2LL * H * HD;
+      const bf16_t* vrow = qb + (int64_t)key * lay.ld + 2 * lay.sw;
 #pragma unroll
       for (int s = 0; s < 4; ++s) vf[s] = ld_frag(vrow + 16 * s + 8 * hf);
     }
@@ -678,25 +706,27 @@ static int num_cus() {
 }  // namespace a128
 
 bool launch_attn128_fwd(const uint16_t* qkv, uint16_t* out, float* lse, int B, int Lq, int H,
-                        float p, bool causal, uint32_t seed, uint32_t offset, hipStream_t s) {
-  if (Lq != a128::L || causal || !a128::enabled()) return false;
+                        float p, bool causal, uint32_t seed, uint32_t offset, hipStream_t s, bool head_major) {
+  if (Lq != a128::L || causal || (!a128::enabled() && !head_major)) return false;
   const int items = B * H, slots = 2 * a128::num_cus();
   const int grid = items < slots ? items : slots;
   hipLaunchKernelGGL(a128::attn128_fwd_kernel, dim3(grid), dim3(256), 0, s, (const bf16_t*)qkv,
-                     (bf16_t*)out, lse, B, H, p, seed, offset);
+                     (bf16_t*)out, lse, B, H, p, seed, offset, head_major ? 1 : 0);
   return true;
 }
+
+bool attn128_supports(int L, int D, bool causal) { return L == a128::L && D == a128::HD && !causal; }
 
 bool launch_attn128_bwd(const uint16_t* qkv, const uint16_t* out, const uint16_t* dout,
                         const float* lse, uint16_t* dqkv, float* colpart, float* dbias, int B,
                         int Lq, int H, float p, bool causal, uint32_t seed, uint32_t offset,
-                        hipStream_t s) {
-  if (Lq != a128::L || causal || !a128::enabled()) return false;
+                        hipStream_t s, bool head_major) {
+  if (Lq != a128::L || causal || (!a128::enabled() && !head_major)) return false;
   const int items = B * H, slots = 2 * a128::num_cus();
   const int grid = items < slots ? items : slots;
   hipLaunchKernelGGL(a128::attn128_bwd_kernel, dim3(grid), dim3(256), 0, s, (const bf16_t*)qkv,
                      (const bf16_t*)out, (const bf16_t*)dout, lse, (bf16_t*)dqkv,
-                     dbias ? colpart : nullptr, B, H, p, seed, offset);
+                     dbias ? colpart : nullptr, B, H, p, seed, offset, head_major ? 1 : 0);
   if (dbias) {
     const int bchunk = 64, nch = (B + bchunk - 1) / bchunk;
     hipMemsetAsync(dbias, 0, sizeof(float) * 3 * H * a128::HD, s);

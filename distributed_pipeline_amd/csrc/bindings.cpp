@@ -307,7 +307,7 @@ static std::vector<at::Tensor> bias_act_bwd(const at::Tensor& dy, const at::Tens
 
 // ---- attention ---------------------------------------------------------------------
 static std::vector<at::Tensor> attn_fwd(const at::Tensor& qkv, int64_t heads, double p, bool causal,
-                                        int64_t seed, int64_t offset) {
+                                        int64_t seed, int64_t offset, bool head_major) {
   CHECK_DEV(qkv); CHECK_BF16(qkv); CHECK_CONTIG(qkv);
   TORCH_CHECK(qkv.dim() == 3, "qkv must be [B, L, 3*H*D]");
   const int B = (int)qkv.size(0), L = (int)qkv.size(1), H = (int)heads;
@@ -318,16 +318,19 @@ static std::vector<at::Tensor> attn_fwd(const at::Tensor& qkv, int64_t heads, do
   const c10::DeviceGuard guard(qkv.device());
   at::Tensor out = at::empty({B, L, (int64_t)H * D}, qkv.options());
   at::Tensor lse = at::empty({B, H, L}, qkv.options().dtype(at::kFloat));
-  dpa::launch_attn_fwd(bf_ptr(qkv), reinterpret_cast<uint16_t*>(out.data_ptr()),
-                       lse.data_ptr<float>(), B, L, H, D, (float)p, causal, (uint32_t)seed,
-                       (uint32_t)offset, cur_stream());
+  TORCH_CHECK(!head_major || dpa::attn128_supports(L, D, causal),
+              "attn_fwd: the head-major qkv layout needs L == 128, head_dim 64, bidirectional");
+  const bool ok = dpa::launch_attn_fwd(bf_ptr(qkv), reinterpret_cast<uint16_t*>(out.data_ptr()),
+                                       lse.data_ptr<float>(), B, L, H, D, (float)p, causal, (uint32_t)seed,
+                                       (uint32_t)offset, cur_stream(), head_major);
+  TORCH_CHECK(ok, "attn_fwd: no kernel for this shape");
   return {out, lse};
 }
 
 static std::vector<at::Tensor> attn_bwd(const at::Tensor& dout, const at::Tensor& qkv,
                                         const at::Tensor& out, const at::Tensor& lse, int64_t heads,
                                         double p, bool causal, int64_t seed, int64_t offset,
-                                        bool want_db) {
+                                        bool want_db, bool head_major) {
   CHECK_DEV(dout); CHECK_BF16(dout); CHECK_CONTIG(dout); CHECK_CONTIG(out); CHECK_CONTIG(qkv);
   const int B = (int)qkv.size(0), L = (int)qkv.size(1), H = (int)heads;
   TORCH_CHECK(dout.sizes() == out.sizes(), "dout shape");
@@ -336,6 +339,8 @@ static std::vector<at::Tensor> attn_bwd(const at::Tensor& dout, const at::Tensor
   TORCH_CHECK(D == 64 || D == 128, "attn: head_dim must be 64 or 128");
   TORCH_CHECK(L % 64 == 0 && out.size(2) == (int64_t)H * D, "attn_bwd: shapes");
   TORCH_CHECK(lse.numel() == (int64_t)B * H * L, "attn_bwd: lse shape");
+  TORCH_CHECK(!head_major || dpa::attn128_supports(L, D, causal),
+              "attn_bwd: the head-major qkv layout needs L == 128, head_dim 64, bidirectional");
   const c10::DeviceGuard guard(qkv.device());
   at::Tensor dqkv = at::empty_like(qkv);
   auto f32 = qkv.options().dtype(at::kFloat);
@@ -350,14 +355,14 @@ static std::vector<at::Tensor> attn_bwd(const at::Tensor& dout, const at::Tensor
       bf_ptr(qkv), bf_ptr(out), bf_ptr(dout), lse.data_ptr<float>(), delta.data_ptr<float>(),
       reinterpret_cast<uint16_t*>(dqkv.data_ptr()), dq.defined() ? dq.data_ptr<float>() : nullptr,
       want_db ? colpart.data_ptr<float>() : nullptr, want_db ? db.data_ptr<float>() : nullptr, B, L,
-      H, D, (float)p, causal, (uint32_t)seed, (uint32_t)offset, cur_stream());
+      H, D, (float)p, causal, (uint32_t)seed, (uint32_t)offset, cur_stream(), head_major);
   return {dqkv, got ? db : at::Tensor()};
 }
 
 // ---- GEMMs ---------------------------------------------------------------------------
 static std::tuple<at::Tensor, at::Tensor, bool> gemm_nt(const at::Tensor& x, const at::Tensor& W,
                                                         c10::optional<at::Tensor> b, int64_t act,
-                                                        bool want_deriv) {
+                                                        bool want_deriv, int64_t head_major_L) {
   CHECK_DEV(x); CHECK_BF16(x); CHECK_BF16(W); CHECK_CONTIG(x); CHECK_CONTIG(W);
   const int T = (int)x.size(0), K = (int)x.size(1), N = (int)W.size(0);
   TORCH_CHECK(W.size(1) == K, "gemm_nt: W [N, K]");
@@ -366,10 +371,17 @@ static std::tuple<at::Tensor, at::Tensor, bool> gemm_nt(const at::Tensor& x, con
   at::Tensor z;
   if (act == 1 || act == 3) z = at::empty({T, N}, x.options());
   bool deriv = want_deriv && z.defined();
+  // head_major_L > 0: y stored as [T / L, N / 64, L, 64] (heads of 64 columns; the L = 128
+  // attention reads each head contiguously)
+  int hm = 0;
+  if (head_major_L > 0) {
+    while ((1LL << hm) < head_major_L) ++hm;
+    TORCH_CHECK((1LL << hm) == head_major_L && act == 0, "gemm_nt: head-major store needs a power-of-2 L, no act");
+  }
   bool ok = dpa::launch_gemm_nt(bf_ptr(x), bf_ptr(W), opt_bf_ptr(b),
                                 reinterpret_cast<uint16_t*>(y.data_ptr()),
                                 z.defined() ? reinterpret_cast<uint16_t*>(z.data_ptr()) : nullptr, T, N,
-                                K, (int)act, cur_stream(), &deriv);
+                                K, (int)act, cur_stream(), &deriv, hm);
   TORCH_CHECK(ok, "gemm_nt: unsupported shape T=", T, " N=", N, " K=", K);
   return {y, z, deriv};
 }
@@ -712,14 +724,19 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("gemm_nt_into", &gemm_nt_into, "y = x W^T (+b) into a preallocated [T, N] tensor");
   m.def("gemm_nn_into", &gemm_nn_into, "dx = dy W into a preallocated [T, K] tensor");
   m.def("emb_grad", &emb_grad, "dW[ids] += dy (sorted segment sum, fp32)");
-  m.def("attn_fwd", &attn_fwd, "fused attention forward (head_dim 64/128) -> (out, lse)");
+  m.def("attn128_supports", &dpa::attn128_supports, "the persistent L = 128 attention covers (L, D, causal)");
+  m.def("attn_fwd", &attn_fwd, "fused attention forward (head_dim 64/128) -> (out, lse)", py::arg("qkv"),
+        py::arg("heads"), py::arg("p"), py::arg("causal"), py::arg("seed"), py::arg("offset"),
+        py::arg("head_major") = false);
   m.def("attn_bwd", &attn_bwd, "fused attention backward -> (dqkv, colsum(dqkv) or None)",
         py::arg("dout"), py::arg("qkv"), py::arg("out"), py::arg("lse"), py::arg("heads"), py::arg("p"),
-        py::arg("causal"), py::arg("seed"), py::arg("offset"), py::arg("want_db") = false);
+        py::arg("causal"), py::arg("seed"), py::arg("offset"), py::arg("want_db") = false,
+        py::arg("head_major") = false);
   m.def("gemm_nt", &gemm_nt,
         "y = act(x W^T + b) (bf16 MFMA) -> (y, z, z_is_derivative): z is the pre-activation, or "
         "act'(pre-activation) when want_deriv and the persistent kernel ran (backward act code 4)",
-        py::arg("x"), py::arg("W"), py::arg("b"), py::arg("act"), py::arg("want_deriv") = false);
+        py::arg("x"), py::arg("W"), py::arg("b"), py::arg("act"), py::arg("want_deriv") = false,
+        py::arg("head_major_L") = 0);
   m.def("gemm_nn", &gemm_nn, "dx = dy W (bf16 MFMA)");
   m.def("gemm_nn_dact", &gemm_nn_dact,
         "dz = (dy W) * act'(aux) (bf16 MFMA, fused act backward) -> (dz, colsum(dz) fp32 or None)",

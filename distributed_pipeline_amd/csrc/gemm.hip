@@ -282,9 +282,10 @@ int device_cu_count() {
 // zderiv (in/out, nullable): requests act'(pre-activation) in z instead of the
 // pre-activation; reset to false when the kernel that ran stored the pre-activation.
 bool launch_gemm_nt(const uint16_t* x, const uint16_t* W, const uint16_t* bias, uint16_t* y,
-                    uint16_t* z, int T, int N, int K, int act, hipStream_t s, bool* zderiv) {
+                    uint16_t* z, int T, int N, int K, int act, hipStream_t s, bool* zderiv, int hm) {
   const bool want_d = zderiv && *zderiv;
-  if (launch_gemmp_nt(x, W, bias, y, z, T, N, K, act, device_cu_count(), s, want_d)) return true;
+  if (launch_gemmp_nt(x, W, bias, y, z, T, N, K, act, device_cu_count(), s, want_d, hm)) return true;
+  if (hm) return false;  // the head-major store exists on the persistent kernel only
   if (zderiv) *zderiv = false;
   if (launch_gemm256_nt(x, W, bias, y, z, T, N, K, act, s)) return true;
   if (!gemm_shape_ok(T, N, K)) return false;

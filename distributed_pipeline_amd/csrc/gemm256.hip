@@ -609,7 +609,7 @@ __global__ void __launch_bounds__(512) gemmp_kernel(const bf16_t* __restrict__ A
                                                     int nk, bf16_t* __restrict__ C, int64_t ldc,
                                                     const bf16_t* __restrict__ bias,
                                                     bf16_t* __restrict__ Zout, float* __restrict__ colpart,
-                                                    int* __restrict__ tile_ctr) {
+                                                    int* __restrict__ tile_ctr, int hm) {
   __shared__ __attribute__((aligned(1024))) char smem[P_LDS];
   constexpr int XS = PEpi<EPI>::XS;
   constexpr bool DACT = EPI == 3 || EPI == 4 || EPI == 5;  // epilogues that read aux
@@ -658,8 +658,15 @@ __global__ void __launch_bounds__(512) gemmp_kernel(const bf16_t* __restrict__ A
   auto row_off = [&](int t, int ro, int k, int ln) -> int64_t {
     const int mt = t / NT, nt = t % NT;
     const int qa = ro >> 2, i = ro & 3;
-    return ((int64_t)mt * 256 + qa * 128 + wm * 64 + i * 16 + k * 8 + (ln >> 3)) * ldc + nt * 256 + wn * 64 +
-           (ln & 7) * 8;
+    const int64_t row = (int64_t)mt * 256 + qa * 128 + wm * 64 + i * 16 + k * 8 + (ln >> 3);
+    const int col = nt * 256 + wn * 64 + (ln & 7) * 8;
+    if (hm) {
+      // head-major store [R >> hm][ldc / 64][1 << hm][64]: row = (b, l), col = (head j, d); a
+      // wave's 64 columns are one head, so a store instruction's 8 rows are 1 KiB contiguous
+      const int64_t b = row >> hm, l = row & ((1 << hm) - 1);
+      return ((b * (ldc >> 6) + (col >> 6)) << hm) * 64 + l * 64 + (col & 63);
+    }
+    return row * ldc + col;
   };
 
   auto epilogue = [&](int t, int slot, uint4 (&aux)[2][2], bool has_next) {
@@ -961,21 +968,22 @@ static int* gemmp_queue(hipStream_t s) {
 template <bool B_TR, int EPI, int ACT>
 static void gemmp_go(const uint16_t* a, int64_t lda, const uint16_t* b, int64_t ldb, int M, int N, int K,
                      uint16_t* c, const uint16_t* bias, uint16_t* z, int ncu, hipStream_t s,
-                     float* colpart = nullptr) {
+                     float* colpart = nullptr, int hm = 0) {
   const int tiles = (M / 256) * (N / 256);
   const int grid = persistent_grid(tiles, ncu);
   int* q = (tiles > grid && grid >= 8) ? gemmp_queue(s) : nullptr;
   hipLaunchKernelGGL((g256::gemmp_kernel<B_TR, EPI, ACT>), dim3(grid), dim3(512), 0, s, (const bf16_t*)a,
                      lda, (const bf16_t*)b, ldb, M, N, K / 64, (bf16_t*)c, (int64_t)N, (const bf16_t*)bias,
-                     (bf16_t*)z, colpart, q);
+                     (bf16_t*)z, colpart, q, hm);
 }
 
 // y[T][N] = act(x[T][K] . W[N][K]^T + bias); z (nullable, act != 0) = the pre-activation,
 // or act'(pre-activation) when zderiv (the backward then multiplies: act code 4).
 bool launch_gemmp_nt(const uint16_t* x, const uint16_t* W, const uint16_t* bias, uint16_t* y,
-                     uint16_t* z, int T, int N, int K, int act, int ncu, hipStream_t s, bool zderiv) {
+                     uint16_t* z, int T, int N, int K, int act, int ncu, hipStream_t s, bool zderiv, int hm) {
   if (!g256_enabled() || T % 256 || N % 256 || K % 128 || K < 128 || act < 0 || act > 3) return false;
-  if (act == 0) gemmp_go<false, 0, 0>(x, K, W, K, T, N, K, y, bias, nullptr, ncu, s);
+  if (hm && (act != 0 || hm < 7 || hm > 30 || (T & ((1 << hm) - 1)) || N % 64)) return false;
+  if (act == 0) gemmp_go<false, 0, 0>(x, K, W, K, T, N, K, y, bias, nullptr, ncu, s, nullptr, hm);
   else if (z != nullptr && zderiv) {
     if (act == 1) gemmp_go<false, 6, 1>(x, K, W, K, T, N, K, y, bias, z, ncu, s);
     else if (act == 2) gemmp_go<false, 6, 2>(x, K, W, K, T, N, K, y, bias, z, ncu, s);

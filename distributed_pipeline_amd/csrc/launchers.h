@@ -73,23 +73,27 @@ void launch_bias_act_bwd(const uint16_t* dy, const uint16_t* zy, uint16_t* dz, f
                          int N, int act, hipStream_t s);
 
 // ---- attention.hip (head_dim 64 or 128, dropout, causal) ---------------------------------
-void launch_attn_fwd(const uint16_t* qkv, uint16_t* out, float* lse, int B, int L, int H, int D,
-                     float p, bool causal, uint32_t seed, uint32_t offset, hipStream_t s);
+// head_major: qkv is [B, 3H, L, D] (QKV GEMM head-major store; L == 128, D == 64, bidirectional only)
+bool launch_attn_fwd(const uint16_t* qkv, uint16_t* out, float* lse, int B, int L, int H, int D,
+                     float p, bool causal, uint32_t seed, uint32_t offset, hipStream_t s,
+                     bool head_major = false);
+bool attn128_supports(int L, int D, bool causal);
 bool attn_bwd_needs_dq_acc(int L);
 // attention128.hip: persistent L = 128 bidirectional kernels (false: not applicable)
 bool launch_attn128_fwd(const uint16_t* qkv, uint16_t* out, float* lse, int B, int L, int H,
-                        float p, bool causal, uint32_t seed, uint32_t offset, hipStream_t s);
+                        float p, bool causal, uint32_t seed, uint32_t offset, hipStream_t s,
+                        bool head_major = false);
 // colpart [B*H][192] fp32 scratch; when dbias != nullptr also writes the column sums of
 // dqkv (the qkv bias gradient) into dbias [3*H*64] (overwritten).
 bool launch_attn128_bwd(const uint16_t* qkv, const uint16_t* out, const uint16_t* dout,
                         const float* lse, uint16_t* dqkv, float* colpart, float* dbias, int B,
                         int L, int H, float p, bool causal, uint32_t seed, uint32_t offset,
-                        hipStream_t s);
+                        hipStream_t s, bool head_major = false);
 // Returns true when the column sums of dqkv were written to dbias (L == 128 path).
 bool launch_attn_bwd(const uint16_t* qkv, const uint16_t* out, const uint16_t* dout, const float* lse,
                      float* delta, uint16_t* dqkv, float* dq_acc, float* colpart, float* dbias, int B,
                      int L, int H, int D, float p, bool causal, uint32_t seed, uint32_t offset,
-                     hipStream_t s);
+                     hipStream_t s, bool head_major = false);
 
 // ---- xent_rows.hip: row softmax-CE over materialised logits (wide-E chunked path) ----
 // forward that leaves softmax - onehot (unscaled) in place of the logits (false: row too long)
@@ -125,7 +129,7 @@ void launch_timestep_emb(const float* ts, int B, int dim, float max_period, uint
 // ---- gemm.hip (bf16 MFMA GEMMs of Linear layers) ----------------------------------
 bool launch_gemm_nt(const uint16_t* x, const uint16_t* W, const uint16_t* bias, uint16_t* y,
                     uint16_t* z, int T, int N, int K, int act, hipStream_t s,
-                    bool* zderiv = nullptr);
+                    bool* zderiv = nullptr, int hm = 0);
 bool launch_gemm_nn(const uint16_t* dy, const uint16_t* W, uint16_t* dx, int T, int N, int K,
                     hipStream_t s);
 bool launch_gemm_wgrad(const uint16_t* dy, const uint16_t* x, float* dW, float* db, int T, int N,
@@ -152,7 +156,7 @@ int64_t gemm256_wgrad_workspace_floats(int T, int N, int K);
 //       aux): per-tile column-sum partials [(T/256)*2][K] of dx (the bias gradient)
 bool launch_gemmp_nt(const uint16_t* x, const uint16_t* W, const uint16_t* bias, uint16_t* y,
                      uint16_t* z, int T, int N, int K, int act, int ncu, hipStream_t s,
-                     bool zderiv = false);
+                     bool zderiv = false, int hm = 0);
 bool launch_gemmp_nn(const uint16_t* dy, const uint16_t* W, uint16_t* dx, const uint16_t* aux, int act,
                      int T, int N, int K, int ncu, hipStream_t s, float* colpart);
 bool launch_gemmp_nn_acc(const uint16_t* dy, const uint16_t* W, uint16_t* dx, int T, int N, int K, int ncu,

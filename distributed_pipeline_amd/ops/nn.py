@@ -128,6 +128,9 @@ def _bias_act_bwd(dy2d, z, y, act, want_db):
 #   "blas"   - every Linear GEMM on hipBLASLt (plus separate epilogue kernels), the
 #            A/B reference.
 GEMM_MODE = os.environ.get("DPA_GEMM", "auto")
+# post-LN attention sublayer at L = 128: QKV stored head-major for the attention kernels
+# (DPA_QKV_HEAD_MAJOR=0: token-major, the Linear layout)
+_QKV_HEAD_MAJOR = os.environ.get("DPA_QKV_HEAD_MAJOR", "1") != "0"
 # forward GEMM epilogues store act'(z) instead of z for the backward (DPA_SAVE_ACT_DERIV=0: z)
 _SAVE_ACT_DERIV = os.environ.get("DPA_SAVE_ACT_DERIV", "1") != "0"
 
@@ -451,9 +454,18 @@ class _AttnLNFn(torch.autograd.Function):
         B, L, D = shp
         x2 = x.reshape(-1, D)
         rq = _route(x2, wq16.shape[0], "none")
-        qkv, _, _ = _lin_fwd(x2, wq16, bq16, "none", rq)
+        ext = get_ext()
+        # head-major QKV (the L = 128 persistent attention): the GEMM epilogue stores
+        # [B, 3H, L, 64], so both attention kernels read each head's Q / K / V block as
+        # 16 KiB of contiguous memory instead of 128 rows strided by the token row
+        hm = (_QKV_HEAD_MAJOR and rq[0] and x2.shape[0] % 256 == 0 and wq16.shape[0] % 256 == 0
+              and ext.attn128_supports(L, D // heads, False))
+        if hm:
+            qkv, _, _ = ext.gemm_nt(x2, wq16, bq16, 0, False, L)
+        else:
+            qkv, _, _ = _lin_fwd(x2, wq16, bq16, "none", rq)
         qkv3 = qkv.view(B, L, wq16.shape[0])
-        o, lse = get_ext().attn_fwd(qkv3, heads, float(p_attn), False, seed_a, off_a)
+        o, lse = ext.attn_fwd(qkv3, heads, float(p_attn), False, seed_a, off_a, bool(hm))
         o2 = o.view(-1, o.shape[-1])
         ro = _route(o2, wo16.shape[0], "none")
         y, _, _ = _lin_fwd(o2, wo16, bo16, "none", ro)
@@ -462,7 +474,7 @@ class _AttnLNFn(torch.autograd.Function):
         ctx.save_for_backward(x2, qkv3, o, lse, wq16, wo16, hsave, mean, rstd, lw16)
         ctx.params = (wq, bq, wo, bo)
         ctx.ln_params = (lw, lb)
-        ctx.cfg = (heads, p_attn, seed_a, off_a, p, seed_l, off_l, rq, ro)
+        ctx.cfg = (heads, p_attn, seed_a, off_a, p, seed_l, off_l, rq, ro, bool(hm))
         ctx.shp = shp
         return out.reshape(shp)
 
@@ -470,7 +482,7 @@ class _AttnLNFn(torch.autograd.Function):
     def backward(ctx, dout):
         x2, qkv3, o, lse, wq16, wo16, hsave, mean, rstd, lw16 = ctx.saved_tensors
         wq, bq, wo, bo = ctx.params
-        heads, p_attn, seed_a, off_a, p, seed_l, off_l, rq, ro = ctx.cfg
+        heads, p_attn, seed_a, off_a, p, seed_l, off_l, rq, ro, hm = ctx.cfg
         need_dx = ctx.needs_input_grad[0]
         ext = get_ext()
         lw, lb = ctx.ln_params
@@ -485,7 +497,7 @@ class _AttnLNFn(torch.autograd.Function):
         dwo, dbo = _lin_param_grads(wo, bo, dy, o2, ro[2], dyb if bo is not None else None)
         # attention
         dqkv, dbq = ext.attn_bwd(do.view(o.shape), qkv3, o, lse, heads, float(p_attn), False, seed_a,
-                                 off_a, bq is not None)
+                                 off_a, bq is not None, hm)  # dqkv comes back token-major
         dz = dqkv.view(-1, dqkv.shape[-1])
         if bq is not None and dbq is None and not rq[2]:
             _, dbq = _bias_act_bwd(dz, None, None, "none", True)

@@ -135,3 +135,27 @@ def test_attention_head_dim_128_dropout_fwd_bwd_consistent():
         o, _ = _ext().attn_fwd(v_probe.view(B, L, -1), H, p, False, 7, 3)
         colsum[blk * D:(blk + 1) * D] = o.view(L, D).float().sum(0)
     torch.testing.assert_close(dv0, colsum, rtol=2e-2, atol=2e-2)
+
+
+def test_head_major_qkv_matches_token_major():
+    """QKV GEMM head-major store + L = 128 attention reading it: bit-identical to the
+    token-major path (same MFMA sums, only the memory layout differs); dqkv and the
+    qkv-bias column sums come back token-major in both cases."""
+    torch.manual_seed(5)
+    B, L, H, D, E = 4, 128, 12, 64, 768
+    x = (torch.randn(B * L, E, device="cuda") * 0.5).bfloat16()
+    W = (torch.randn(3 * H * D, E, device="cuda") * 0.03).bfloat16()
+    b = (torch.randn(3 * H * D, device="cuda") * 0.1).bfloat16()
+    ext = _ext()
+    tm, _, _ = ext.gemm_nt(x, W, b, 0, False)
+    hm, _, _ = ext.gemm_nt(x, W, b, 0, False, L)
+    ref_hm = tm.view(B, L, 3 * H, D).permute(0, 2, 1, 3).contiguous()
+    assert torch.equal(hm.view(B, 3 * H, L, D), ref_hm)
+    p = 0.1
+    o1, lse1 = ext.attn_fwd(tm.view(B, L, -1), H, p, False, 3, 9)
+    o2, lse2 = ext.attn_fwd(hm.view(B, L, -1), H, p, False, 3, 9, True)
+    assert torch.equal(o1, o2) and torch.equal(lse1, lse2)
+    dout = torch.randn_like(o1)
+    d1, db1 = ext.attn_bwd(dout, tm.view(B, L, -1), o1, lse1, H, p, False, 3, 9, True)
+    d2, db2 = ext.attn_bwd(dout, hm.view(B, L, -1), o2, lse2, H, p, False, 3, 9, True, True)
+    assert torch.equal(d1, d2) and torch.equal(db1, db2)
