@@ -123,6 +123,9 @@ class PerfSettings(S):
         = _(0, "Samples per executed forward/backward, a multiple of microbatch: 0 = auto (the whole "
                "per-rank batch, halved on out-of-memory), -1 = microbatch (the reference schedule). "
                "Gradients equal the reference's sum over micro-batches.")
+    overlap_microbatches: bool \
+        = _(True, "With several executed micro-batches per step (e.g. exec_microbatch=-1), run micro-batch "
+                  "k+1's forward on a second HIP stream while k's backward runs (bitwise-identical gradients).")
     shard_data: bool \
         = _(False, "Give each rank a disjoint shard of the data (DistributedSampler-style).")
     log_cross_rank_mean: bool \

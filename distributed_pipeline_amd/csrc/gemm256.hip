@@ -954,15 +954,22 @@ void set_gemmp_dynamic(bool on) {
 static int* gemmp_queue(hipStream_t s) {
   if (g_gemmp_dynamic < 0) set_gemmp_dynamic(false);
   if (!g_gemmp_dynamic) return nullptr;
-  static int* bufs[64] = {nullptr};
+  // one counter buffer per (device, stream): GEMMs on one stream never overlap, but the
+  // overlapped micro-batch schedule runs GEMMs on two streams at once
+  struct Q { int dev; hipStream_t s; int* buf; };
+  static Q qs[64];
+  static int nq = 0;
   int dev = 0;
-  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return nullptr;
-  if (!bufs[dev] && hipMalloc(&bufs[dev], 8 * 16 * sizeof(int)) != hipSuccess) {
-    bufs[dev] = nullptr;
-    return nullptr;
+  if (hipGetDevice(&dev) != hipSuccess) return nullptr;
+  int* buf = nullptr;
+  for (int i = 0; i < nq; ++i)
+    if (qs[i].dev == dev && qs[i].s == s) buf = qs[i].buf;
+  if (!buf) {
+    if (nq >= 64 || hipMalloc(&buf, 8 * 16 * sizeof(int)) != hipSuccess) return nullptr;
+    qs[nq++] = Q{dev, s, buf};
   }
-  if (hipMemsetAsync(bufs[dev], 0, 8 * 16 * sizeof(int), s) != hipSuccess) return nullptr;
-  return bufs[dev];
+  if (hipMemsetAsync(buf, 0, 8 * 16 * sizeof(int), s) != hipSuccess) return nullptr;
+  return buf;
 }
 
 template <bool B_TR, int EPI, int ACT>

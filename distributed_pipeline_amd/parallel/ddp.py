@@ -45,8 +45,14 @@ implements the same protocol for the single-GPU multi-rank test transport.
 * ZeRO-1 (``shard_optimizer=True``, parallel/zero.py): buckets are padded to a
   multiple of world x 16 elements and REDUCE-SCATTERED instead of all-reduced;
   rank r receives the summed r-th chunk of every bucket in a compact
-  ``grad_shard`` buffer, the sharded optimizer updates only those elements and
-  :meth:`gather_params` all-gathers the updated fp32 chunks back in place.
+  ``grad_shard`` buffer, the sharded optimizer updates only those elements (writing
+  their bf16 compute shadow in the same kernel) and :meth:`gather_params` all-gathers
+  the updated chunks of the bf16 SHADOW, half the bytes of the fp32 master, as async
+  per-bucket collectives issued in the order the next forward needs them (the first
+  layers' buckets first); the next forward waits for them.  The fp32 master is then
+  stale outside this rank's chunks until :meth:`materialize_master` (checkpoint saves,
+  replica checks) gathers it.  ``DPA_ZERO_GATHER=fp32`` gathers the fp32 master every
+  step instead (and refreshes the shadow from it), as before.
 """
 import contextlib
 import os
@@ -136,6 +142,8 @@ class DDPEngine(nn.Module):
             for p in b.params:
                 self._bucket_of[id(p)] = b
         self._hooks = []
+        self._shadow_works = []      # ZeRO-1: outstanding async shadow all-gathers
+        self._master_stale = False   # ZeRO-1: fp32 master valid only in this rank's chunks
         self._fired = set()          # layout indices whose hook fired (first armed step only)
         self._track_unused = True
         self._ipc_flag = None        # device int32 error word of the IPC all-reduce
@@ -239,6 +247,7 @@ class DDPEngine(nn.Module):
 
     # -- forward ---------------------------------------------------------------
     def forward(self, *args, **kwargs):
+        self.wait_shadow()
         if self.distributed and torch.is_grad_enabled() and self.training:
             self._armed = self._sync_enabled
             if self._native is not None:
@@ -250,6 +259,23 @@ class DDPEngine(nn.Module):
                     b.launched = False
                 self._next_launch = 0
         return self.module(*args, **kwargs)
+
+    def arm_for_backward(self):
+        """Arm the reducer for the next backward regardless of how the forward ran: the
+        overlapped micro-batch schedule (utils/trainer.py) runs every forward under
+        ``no_sync`` - the last micro-batch's forward is issued while an earlier backward
+        is still being issued - and arms right before the last backward."""
+        if not self.distributed:
+            return
+        self._armed = True
+        if self._native is not None:
+            self._native.arm()
+        else:
+            for b in self.buckets:
+                b.pending = len(b.params)
+                b.work = None
+                b.launched = False
+            self._next_launch = 0
 
     def disarm(self):
         """Abandon a partially run backward (e.g. an out-of-memory retry): no bucket of
@@ -452,12 +478,60 @@ class DDPEngine(nn.Module):
                 dist.all_gather_into_tensor(whole, mine.clone(), group=self.pg)
 
     def gather_params(self):
-        """After the sharded optimizer step: every rank's updated fp32 chunks to every
-        rank, then the bf16 compute shadow is refreshed from the full master buffer."""
+        """After the sharded optimizer step: every rank's updated chunks to every rank.
+        With a bf16 compute shadow (the optimizer wrote this rank's shadow chunks) only
+        the shadow is gathered - async, per bucket, first-needed first - and the fp32
+        master is marked stale; otherwise the fp32 chunks are gathered and the shadow
+        refreshed from them."""
         if not self.sharded:
             return
-        self.all_gather_chunks(self.space.param_flat)
-        self.space.refresh_shadow()
+        sh = self.space.shadow_flat
+        if sh is None or os.environ.get("DPA_ZERO_GATHER", "bf16") == "fp32":
+            self.all_gather_chunks(self.space.param_flat)
+            self.space.refresh_shadow()
+            self._master_stale = False
+            return
+        if os.environ.get("DPA_ZERO_POISON") == "1":
+            # test hook: NaN into the fp32 master outside this rank's chunks, so any read
+            # of a stale master element (instead of the gathered shadow) shows up
+            keep = torch.zeros(self.space.numel, dtype=torch.bool, device=self.space.param_flat.device)
+            for s_, c, _ in self.shard_chunks:
+                keep[s_:s_ + c] = True
+            self.space.param_flat.masked_fill_(~keep, float("nan"))
+        # bit copy as int32 pairs (gloo has no 16-bit all-gather; every bucket and chunk
+        # boundary is a multiple of 16 elements)
+        wire = sh.view(torch.int32)
+        # the layout runs from the last layers to the first: issue the buckets the next
+        # forward needs first (the highest) first
+        for b, (s_, c, _off) in reversed(list(zip(self.buckets, self.shard_chunks))):
+            whole = wire[b.start // 2:b.end // 2]
+            mine = wire[s_ // 2:(s_ + c) // 2]
+            if self._host_sync_before_comm:  # gloo on device tensors: host-staged, synchronous
+                host = whole.to("cpu")
+                lo = (s_ - b.start) // 2
+                dist.all_gather_into_tensor(host, host[lo:lo + c // 2].clone(), group=self.pg)
+                whole.copy_(host)
+            elif self._backend == "nccl":
+                self._shadow_works.append(dist.all_gather_into_tensor(whole, mine, group=self.pg,
+                                                                      async_op=True))
+            else:
+                dist.all_gather_into_tensor(whole, mine.clone(), group=self.pg)
+        self._master_stale = True
+
+    def wait_shadow(self):
+        """Order the outstanding shadow all-gathers before the current stream's next work
+        (a stream-side wait on RCCL, no host block)."""
+        works, self._shadow_works = self._shadow_works, []
+        for w in works:
+            w.wait()
+
+    def materialize_master(self):
+        """Collective (every rank): make the full fp32 master current after shadow-only
+        gathers (before checkpointing or reading parameters outside the forward)."""
+        if self.sharded and self._master_stale:
+            self.wait_shadow()
+            self.all_gather_chunks(self.space.param_flat)
+            self._master_stale = False
 
     def all_reduce_sum_(self, t):
         """Small control-plane sum (e.g. the squared grad norm) on this engine's transport."""

@@ -15,8 +15,10 @@ instead of 8 + 4 R (DiffuSeq-XL, 1.32 B parameters, R = 3 EMA rates, W = 8:
 * optimizer: the fused AdamW + EMA kernel (csrc/optim.hip) runs once per bucket
   chunk, on the rank's slice of the fp32 master buffer and its compact m / v /
   EMA shards;
-* all-gather: every bucket's updated fp32 chunk is gathered in place into the
-  flat master buffer and the bf16 compute shadow is refreshed.
+* all-gather: the kernel also writes the updated chunk's bf16 compute shadow, and every
+  bucket's shadow chunk is all-gathered (async, half the bytes of fp32); the fp32 master
+  outside this rank's chunks is gathered only when needed (``materialize_master``:
+  checkpoints, replica checks).
 
 Wire traffic equals DDP's (reduce-scatter + all-gather = all-reduce).  The
 checkpoint layout is unchanged: :meth:`state_dict` gathers the moments into
@@ -85,7 +87,8 @@ class ZeroFusedAdamW(FusedAdamW):
             fused.adamw_ema_(p[s:s + c], gs[sl], self.exp_avg[sl], self.exp_avg_sq[sl],
                              lr=g["lr"], beta1=b1, beta2=b2, eps=g["eps"],
                              weight_decay=g["weight_decay"], step=self.step_count,
-                             grad_scale=grad_scale, clip=clip, shadow_bf16=None,
+                             grad_scale=grad_scale, clip=clip,
+                             shadow_bf16=None if self.space.shadow_flat is None else self.space.shadow_flat[s:s + c],
                              emas=[e[sl] for e in self.ema_flats] if update_ema else (),
                              ema_rates=self.ema_rates if update_ema else (), skip=skip)
         self.engine.gather_params()

@@ -90,3 +90,69 @@ def test_zero1_matches_unsharded_engine(world):
         if ref0 is None:
             ref0 = ref[0]
         torch.testing.assert_close(torch.from_numpy(ref[0]), torch.from_numpy(ref0))  # replicas agree
+
+
+def _bf16_model(seed):
+    from distributed_pipeline_amd.models.layers import Linear
+    torch.manual_seed(seed)
+    return torch.nn.Sequential(Linear(16, 64, act="tanh"), Linear(64, 64, act="tanh"), Linear(64, 4))
+
+
+def _run_bf16(rank, world, sharded):
+    """bf16 compute through the shadow: the sharded engine gathers only the bf16 shadow
+    (the fp32 master outside this rank's chunks is poisoned with NaN and must never be
+    read by the forward) and materialises the master on demand."""
+    from distributed_pipeline_amd.parallel.ddp import DDPEngine
+    from distributed_pipeline_amd.parallel.optimizer import FusedAdamW
+    from distributed_pipeline_amd.parallel.zero import ZeroFusedAdamW
+    os.environ["DPA_ZERO_POISON"] = "1" if sharded else "0"
+    model = _bf16_model(100 + rank)
+    eng = DDPEngine(model, bucket_cap_mb=0.004, first_bucket_mb=0.001, shard_optimizer=sharded,
+                    shadow_dtype=torch.bfloat16)
+    kw = dict(lr=1e-2, weight_decay=0.01, ema_rates=(0.9,))
+    opt = ZeroFusedAdamW(eng, **kw) if sharded else FusedAdamW(eng.space, **kw)
+    g = torch.Generator().manual_seed(0)
+    losses = []
+    for _ in range(3):
+        x = torch.randn(world * 8, 16, generator=g).bfloat16()
+        y = torch.randn(world * 8, 4, generator=g)
+        eng.zero_grad()
+        out = eng(x[rank * 8:(rank + 1) * 8]).float()
+        loss = torch.nn.functional.mse_loss(out, y[rank * 8:(rank + 1) * 8])
+        loss.backward()
+        eng.finalize()
+        norm = opt.compute_grad_norm(grad_scale=1.0 / world)
+        opt.step(grad_scale=1.0 / world)  # the sharded optimizer ends with gather_params()
+        losses.append(float(loss.detach()))
+    stale = bool(torch.isnan(eng.space.param_flat).any()) if sharded else False
+    eng.materialize_master()
+    flat = lambda f: torch.cat([v.reshape(-1) for v in eng.space.views(f)]).float().numpy().copy()  # noqa: E731
+    return flat(eng.space.param_flat), flat(eng.space.shadow_flat), losses, stale, float(norm[0])
+
+
+def _worker_bf16(rank, world, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        q.put((rank, _run_bf16(rank, world, False), _run_bf16(rank, world, True)))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_zero1_bf16_shadow_gather_matches_unsharded():
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = find_free_port()
+    procs = [ctx.Process(target=_worker_bf16, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=240) for _ in range(world)]
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    for _rank, ref, shd in res:
+        assert shd[3], "the poisoned stale master should still hold NaN before materialize"
+        assert ref[2] == shd[2]                                # identical losses: forward read shadows only
+        assert (ref[0] == shd[0]).all()                        # master after materialize_master
+        assert (ref[1] == shd[1]).all()                        # gathered bf16 shadow

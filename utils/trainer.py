@@ -127,6 +127,7 @@ class TrainLoop:
             grad_reduce_dtype="fp32",
             shard_optimizer=False,
             exec_microbatch=0,
+            overlap_microbatches=True,
             log_cross_rank_mean=False,
             # ---- observability / robustness (all optional) ----
             nan_guard="off",
@@ -176,6 +177,10 @@ class TrainLoop:
         self.loss_scale = emb / self.microbatch
         self._exec_settled = False
         self._probing = False  # set while _settle_exec_microbatch runs its collective-free probe
+        # several executed chunks per step: overlap chunk k + 1's forward with k's backward
+        # on a second stream (DPA_OVERLAP_MB=0 disables)
+        self.overlap_microbatches = (bool(overlap_microbatches)
+                                     and os.environ.get("DPA_OVERLAP_MB", "1") != "0")
 
         self.step = 0
         self.resume_step = 0
@@ -407,6 +412,8 @@ class TrainLoop:
         if not dist_util.is_initialized():
             return
         import torch.distributed as dist
+        if hasattr(self.ddp_model, "materialize_master"):
+            self.ddp_model.materialize_master()
         params = [p.detach().reshape(-1) for p in self.model.parameters()]
         flat = torch.cat(params).double()
         sig = torch.stack([flat.sum(), (flat * flat).sum(),
@@ -551,13 +558,79 @@ class TrainLoop:
             v = next(iter(batch.values()))
             self._tokens_per_sample = int(v.shape[1]) if torch.is_tensor(v) and v.dim() > 1 else 1
         n = self.get_batch_length(batch)
-        for i in range(0, n, self.exec_microbatch):
+        starts = list(range(0, n, self.exec_microbatch))
+        if self._overlap_ok(len(starts)):
+            return self._forward_backward_overlapped(batch, starts, n)
+        for i in starts:
             with self._range("forward"):
                 losses = self._common_forward(batch, i, self.exec_microbatch)
             self.log_loss_dict(mode="train", losses=losses)
             self.loss_scale = self._chunk_loss_scale(i, min(n, i + self.exec_microbatch), n)
             with self._range("backward"):
                 self.backward_from_losses(losses)
+
+    # ---- overlapped micro-batch schedule (several executed chunks per step) ----------
+    def _overlap_ok(self, nchunks):
+        return (nchunks > 1 and self.overlap_microbatches and not self._probing
+                and self.engine_kind == "native" and self.device.type == "cuda")
+
+    def _chunk_state(self):
+        """Per-chunk hook state (``_last_*`` attributes set by compute_losses and read by
+        backward_from_losses / log_loss_dict), saved while the next chunk's forward runs."""
+        return {k: v for k, v in vars(self).items() if k.startswith("_last_")}
+
+    def _forward_backward_overlapped(self, batch, starts, n):
+        """Executed micro-batch k + 1's forward runs on a second HIP stream while k's
+        backward runs: the persistent GEMMs of a small micro-batch (an 8192-token chunk
+        has 96 output tiles for 256 CUs at N = 768) leave most CUs idle, and the other
+        stream's kernels take them.  Backwards stay serialised (they accumulate into the
+        same flat gradient buffer) and every forward runs in the same order as before
+        (same dropout / noise offsets, same timesteps), so the gradients are bitwise
+        those of the sequential loop.  All forwards run under ``no_sync``; the reducer is
+        armed right before the last backward, which runs on the current stream so its
+        grad-ready events are recorded where the gradients are produced."""
+        cur = torch.cuda.current_stream()
+        if getattr(self, "_side_stream", None) is None:
+            self._side_stream = torch.cuda.Stream(device=self.device)
+        side = self._side_stream
+        side.wait_stream(cur)  # batch copies / last step's optimizer update
+        nch = len(starts)
+        streams = [cur, side]
+
+        def stream_of(k):  # the last chunk on the current stream
+            return streams[(nch - 1 - k) % 2]
+
+        def fwd(k):
+            with torch.cuda.stream(stream_of(k)):
+                with self._range("forward"):
+                    if self.use_ddp:
+                        with self.ddp_model.no_sync():
+                            losses = self.compute_losses(
+                                self._slice_to_device(batch, starts[k], self.exec_microbatch))
+                    else:
+                        losses = self.compute_losses(self._slice_to_device(batch, starts[k], self.exec_microbatch))
+                self.log_loss_dict(mode="train", losses=losses)
+            return losses, self._chunk_state()
+
+        done = None
+        nxt = fwd(0)
+        for k in range(nch):
+            losses, state = nxt
+            nxt = fwd(k + 1) if k + 1 < nch else None
+            st = stream_of(k)
+            with torch.cuda.stream(st):
+                if done is not None:
+                    st.wait_event(done)
+                for key, v in state.items():
+                    setattr(self, key, v)
+                if k == nch - 1 and self.use_ddp:
+                    self.ddp_model.arm_for_backward()
+                self.loss_scale = self._chunk_loss_scale(starts[k], min(n, starts[k] + self.exec_microbatch), n)
+                with self._range("backward"):
+                    self.backward_from_losses(losses)
+                done = torch.cuda.Event()
+                done.record(st)
+        cur.wait_stream(side)
 
     def _chunk_loss_scale(self, start, end, n):
         """Factor that turns the MEAN loss of executed chunk [start, end) into the sum of
@@ -665,6 +738,8 @@ class TrainLoop:
 
     # -------------------------------------------------------------- checkpoints
     def save(self):
+        if hasattr(self.ddp_model, "materialize_master"):
+            self.ddp_model.materialize_master()  # ZeRO-1: fp32 master gathered on demand
         self._save_checkpoint(0, self.master_params)
         for r, p in zip(self.ema_rate, self.ema_params):
             self._save_checkpoint(r, p)
