@@ -893,17 +893,17 @@ static void attn_bwd_general(const uint16_t* qkv, const uint16_t* out, const uin
 bool launch_attn_bwd(const uint16_t* qkv, const uint16_t* out, const uint16_t* dout, const float* lse,
                      float* delta, uint16_t* dqkv, float* dq_acc, float* colpart, float* dbias, int B,
                      int L, int H, int D, float p, bool causal, uint32_t seed, uint32_t offset,
-                     hipStream_t s, bool head_major) {
+                     hipStream_t s, bool head_major, bool db_accumulate) {
   (void)dq_acc;
   if (head_major)  // caller checked attn128_supports
     return launch_attn128_bwd(qkv, out, dout, lse, dqkv, colpart, dbias, B, L, H, p, causal, seed, offset, s,
-                              true) && dbias != nullptr;
+                              true, db_accumulate) && dbias != nullptr;
   if (D == 128) {
     attn_bwd_general<128>(qkv, out, dout, lse, delta, dqkv, B, L, H, p, causal, seed, offset, s);
     return false;
   }
   if (launch_attn128_bwd(qkv, out, dout, lse, dqkv, colpart, dbias, B, L, H, p, causal, seed, offset,
-                         s))
+                         s, false, db_accumulate))
     return dbias != nullptr;
   attn_bwd_general<64>(qkv, out, dout, lse, delta, dqkv, B, L, H, p, causal, seed, offset, s);
   return false;

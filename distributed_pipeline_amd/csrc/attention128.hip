@@ -720,7 +720,7 @@ bool attn128_supports(int L, int D, bool causal) { return L == a128::L && D == a
 bool launch_attn128_bwd(const uint16_t* qkv, const uint16_t* out, const uint16_t* dout,
                         const float* lse, uint16_t* dqkv, float* colpart, float* dbias, int B,
                         int Lq, int H, float p, bool causal, uint32_t seed, uint32_t offset,
-                        hipStream_t s, bool head_major) {
+                        hipStream_t s, bool head_major, bool db_accumulate) {
   if (Lq != a128::L || causal || (!a128::enabled() && !head_major)) return false;
   const int items = B * H, slots = 2 * a128::num_cus();
   const int grid = items < slots ? items : slots;
@@ -729,7 +729,7 @@ bool launch_attn128_bwd(const uint16_t* qkv, const uint16_t* out, const uint16_t
                      dbias ? colpart : nullptr, B, H, p, seed, offset, head_major ? 1 : 0);
   if (dbias) {
     const int bchunk = 64, nch = (B + bchunk - 1) / bchunk;
-    hipMemsetAsync(dbias, 0, sizeof(float) * 3 * H * a128::HD, s);
+    if (!db_accumulate) hipMemsetAsync(dbias, 0, sizeof(float) * 3 * H * a128::HD, s);
     hipLaunchKernelGGL(a128::colpart_reduce_kernel, dim3(3 * H, nch), dim3(256), 0, s, colpart,
                        dbias, B, H, bchunk);
   }

@@ -258,13 +258,16 @@ static std::vector<at::Tensor> add_ln_bwd(const at::Tensor& dout, const at::Tens
   if (ext_g) { dg = *dg_acc; zero_mask &= ~1; }
   if (ext_b) { db = *db_acc; zero_mask &= ~2; }
   if (ext_y) { dyb = *dyb_acc; zero_mask &= ~4; }
+  const int64_t wsn = dpa::ln_bwd_ws_floats(R, D);
+  at::Tensor ws;
+  if (wsn > 0) ws = at::empty({wsn}, f32);
   bool ok = dpa::launch_add_ln_bwd(
       bf_ptr(dout), bf_ptr(hs), mean.data_ptr<float>(), rstd.data_ptr<float>(), bf_ptr(g),
       need_dres ? reinterpret_cast<uint16_t*>(dres.data_ptr()) : nullptr,
       need_dy ? reinterpret_cast<uint16_t*>(dy.data_ptr()) : nullptr,
       dyb.defined() ? dyb.data_ptr<float>() : nullptr,
       dg.data_ptr<float>(), db.data_ptr<float>(), R, D, (float)p, (uint32_t)seed, (uint32_t)offset,
-      cur_stream(), dhp, post, zero_mask);
+      cur_stream(), dhp, post, zero_mask, wsn > 0 ? ws.data_ptr<float>() : nullptr);
   TORCH_CHECK(ok, "add_ln_bwd: unsupported hidden size ", D);
   return {dres, dy, ext_g ? at::Tensor() : dg, ext_b ? at::Tensor() : db, ext_y ? at::Tensor() : dyb};
 }
@@ -330,7 +333,7 @@ static std::vector<at::Tensor> attn_fwd(const at::Tensor& qkv, int64_t heads, do
 static std::vector<at::Tensor> attn_bwd(const at::Tensor& dout, const at::Tensor& qkv,
                                         const at::Tensor& out, const at::Tensor& lse, int64_t heads,
                                         double p, bool causal, int64_t seed, int64_t offset,
-                                        bool want_db, bool head_major) {
+                                        bool want_db, bool head_major, c10::optional<at::Tensor> db_acc) {
   CHECK_DEV(dout); CHECK_BF16(dout); CHECK_CONTIG(dout); CHECK_CONTIG(out); CHECK_CONTIG(qkv);
   const int B = (int)qkv.size(0), L = (int)qkv.size(1), H = (int)heads;
   TORCH_CHECK(dout.sizes() == out.sizes(), "dout shape");
@@ -347,16 +350,24 @@ static std::vector<at::Tensor> attn_bwd(const at::Tensor& dout, const at::Tensor
   at::Tensor delta = at::empty({B, H, L}, f32);
   at::Tensor dq, colpart, db;
   if (dpa::attn_bwd_needs_dq_acc(L)) dq = at::zeros({B, L, H, D}, f32);
+  // db_acc: the qkv bias gradient accumulated straight onto this fp32 .grad (returned undefined)
+  const bool acc = want_db && db_acc.has_value() && db_acc->defined() && db_acc->scalar_type() == at::kFloat &&
+                   db_acc->is_contiguous() && db_acc->numel() == 3LL * H * D && db_acc->device() == qkv.device();
   if (want_db) {
     colpart = at::empty({(int64_t)B * H * 192}, f32);
-    db = at::empty({3 * H * D}, f32);
+    db = acc ? *db_acc : at::empty({3 * H * D}, f32);
   }
-  const bool got = dpa::launch_attn_bwd(
+  bool got = dpa::launch_attn_bwd(
       bf_ptr(qkv), bf_ptr(out), bf_ptr(dout), lse.data_ptr<float>(), delta.data_ptr<float>(),
       reinterpret_cast<uint16_t*>(dqkv.data_ptr()), dq.defined() ? dq.data_ptr<float>() : nullptr,
       want_db ? colpart.data_ptr<float>() : nullptr, want_db ? db.data_ptr<float>() : nullptr, B, L,
-      H, D, (float)p, causal, (uint32_t)seed, (uint32_t)offset, cur_stream(), head_major);
-  return {dqkv, got ? db : at::Tensor()};
+      H, D, (float)p, causal, (uint32_t)seed, (uint32_t)offset, cur_stream(), head_major, acc);
+  if (acc && !got) {  // no fused column sums on this path: add them here
+    db_acc->add_(dqkv.view({-1, 3LL * H * D}).sum(0, false, at::kFloat));
+    got = true;
+  }
+  // contract: with a usable db_acc the bias gradient is always accumulated (result undefined)
+  return {dqkv, got && !acc ? db : at::Tensor()};
 }
 
 // ---- GEMMs ---------------------------------------------------------------------------
@@ -461,7 +472,8 @@ static bool gemm_nn_acc_(const at::Tensor& dy, const at::Tensor& W, at::Tensor& 
 // separate act backward).  The persistent kernel writes per-tile column partials that
 // one reduction turns into db (no second pass over dz).
 static std::vector<at::Tensor> gemm_nn_dact(const at::Tensor& dy, const at::Tensor& W,
-                                            const at::Tensor& aux, int64_t act, bool want_db) {
+                                            const at::Tensor& aux, int64_t act, bool want_db,
+                                            c10::optional<at::Tensor> db_acc) {
   CHECK_DEV(dy); CHECK_BF16(dy); CHECK_BF16(W); CHECK_BF16(aux);
   CHECK_CONTIG(dy); CHECK_CONTIG(W); CHECK_CONTIG(aux);
   const int T = (int)dy.size(0), N = (int)dy.size(1), K = (int)W.size(1);
@@ -472,8 +484,19 @@ static std::vector<at::Tensor> gemm_nn_dact(const at::Tensor& dy, const at::Tens
   at::Tensor part;
   if (want_db && T % 256 == 0) part = at::empty({(int64_t)(T / 256) * 2, K}, dy.options().dtype(at::kFloat));
   if (dpa::launch_gemmp_nn(bf_ptr(dy), bf_ptr(W), dzp, bf_ptr(aux), (int)act, T, N, K, dpa::device_cu_count(),
-                           cur_stream(), part.defined() ? part.data_ptr<float>() : nullptr))
+                           cur_stream(), part.defined() ? part.data_ptr<float>() : nullptr)) {
+    // db_acc: the column sums accumulated straight onto this fp32 .grad (contract: always
+    // accumulated when db_acc is usable; the result is then undefined)
+    const bool acc = want_db && db_acc.has_value() && db_acc->defined() && db_acc->scalar_type() == at::kFloat &&
+                     db_acc->is_contiguous() && db_acc->numel() == K && db_acc->device() == dy.device();
+    if (acc) {
+      if (!part.defined() || !dpa::launch_colsum_acc(part.data_ptr<float>(), (int)part.size(0), K,
+                                                     db_acc->data_ptr<float>(), cur_stream()))
+        db_acc->add_(dz.sum(0, false, at::kFloat));
+      return {dz, at::Tensor()};
+    }
     return {dz, part.defined() ? part.sum(0) : at::Tensor()};
+  }
   if (dpa::launch_gemm256_nn_dact(bf_ptr(dy), bf_ptr(W), bf_ptr(aux), dzp, T, N, K, (int)act, cur_stream()))
     return {dz, at::Tensor()};
   return {at::Tensor(), at::Tensor()};
@@ -731,7 +754,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("attn_bwd", &attn_bwd, "fused attention backward -> (dqkv, colsum(dqkv) or None)",
         py::arg("dout"), py::arg("qkv"), py::arg("out"), py::arg("lse"), py::arg("heads"), py::arg("p"),
         py::arg("causal"), py::arg("seed"), py::arg("offset"), py::arg("want_db") = false,
-        py::arg("head_major") = false);
+        py::arg("head_major") = false, py::arg("db_acc") = py::none());
   m.def("gemm_nt", &gemm_nt,
         "y = act(x W^T + b) (bf16 MFMA) -> (y, z, z_is_derivative): z is the pre-activation, or "
         "act'(pre-activation) when want_deriv and the persistent kernel ran (backward act code 4)",
@@ -740,7 +763,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("gemm_nn", &gemm_nn, "dx = dy W (bf16 MFMA)");
   m.def("gemm_nn_dact", &gemm_nn_dact,
         "dz = (dy W) * act'(aux) (bf16 MFMA, fused act backward) -> (dz, colsum(dz) fp32 or None)",
-        py::arg("dy"), py::arg("W"), py::arg("aux"), py::arg("act"), py::arg("want_db") = false);
+        py::arg("dy"), py::arg("W"), py::arg("aux"), py::arg("act"), py::arg("want_db") = false,
+        py::arg("db_acc") = py::none());
   m.def("gemm_nn_acc_", &gemm_nn_acc_, "dx += dy W in place (bf16 MFMA); False if the shape does not tile");
   m.def("gemm_wgrad", &gemm_wgrad, "dW += dy^T x, db += colsum(dy) (fp32 atomics, split-K)");
   m.def("gemm_supported", &gemm_supported, "shape check for the native GEMMs");

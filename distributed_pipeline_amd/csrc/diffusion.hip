@@ -333,7 +333,11 @@ bool launch_emb_qsample_bwd(const int64_t* ids, const int64_t* mask, const int64
 // segment-sum kernel with only the upstream gradient as input.
 bool launch_emb_grad(const int64_t* sorted_ids, const int64_t* perm, const float* dy32, const uint16_t* dy16,
                      int64_t NT, int E, int V, float* dW, hipStream_t s) {
-  constexpr int CHUNK = 16;
+  // tokens per wave: 16 for large NT (runs of equal ids summed in registers), down to 1 for
+  // a few hundred rows (e.g. a position-embedding gradient of 128 distinct ids), so the
+  // launch still spans the chip instead of a handful of latency-bound waves
+  int64_t chunk = NT / 8192;
+  const int CHUNK = (int)(chunk < 1 ? 1 : chunk > 16 ? 16 : chunk);
   const unsigned grid = (unsigned)(((NT + CHUNK - 1) / CHUNK + 3) / 4);
   auto go = [&](auto kern) {
     hipLaunchKernelGGL(kern, dim3(grid), dim3(256), 0, s, sorted_ids, perm, (const int64_t*)nullptr,

@@ -64,7 +64,10 @@ bool launch_add_ln_bwd(const uint16_t* dout, const uint16_t* hsave, const float*
                        const float* rstd, const uint16_t* g, uint16_t* dres, uint16_t* dy, float* dyb,
                        float* dg, float* db, int64_t R, int D, float p, uint32_t seed, uint32_t off,
                        hipStream_t s, const uint16_t* dh_in = nullptr, bool post = false,
-                       int zero_mask = 7);
+                       int zero_mask = 7, float* ws = nullptr);
+bool launch_colsum_acc(const float* part, int rows, int cols, float* dst, hipStream_t s);
+// fp32 workspace (floats) the small-R two-stage column sums of launch_add_ln_bwd use (0: none)
+int64_t ln_bwd_ws_floats(int64_t R, int D);
 
 // ---- elementwise.hip (bias + activation epilogues) -------------------------------
 void launch_bias_act_fwd(uint16_t* z, const uint16_t* bias, uint16_t* y, int64_t R, int N, int act,
@@ -88,12 +91,12 @@ bool launch_attn128_fwd(const uint16_t* qkv, uint16_t* out, float* lse, int B, i
 bool launch_attn128_bwd(const uint16_t* qkv, const uint16_t* out, const uint16_t* dout,
                         const float* lse, uint16_t* dqkv, float* colpart, float* dbias, int B,
                         int L, int H, float p, bool causal, uint32_t seed, uint32_t offset,
-                        hipStream_t s, bool head_major = false);
+                        hipStream_t s, bool head_major = false, bool db_accumulate = false);
 // Returns true when the column sums of dqkv were written to dbias (L == 128 path).
 bool launch_attn_bwd(const uint16_t* qkv, const uint16_t* out, const uint16_t* dout, const float* lse,
                      float* delta, uint16_t* dqkv, float* dq_acc, float* colpart, float* dbias, int B,
                      int L, int H, int D, float p, bool causal, uint32_t seed, uint32_t offset,
-                     hipStream_t s, bool head_major = false);
+                     hipStream_t s, bool head_major = false, bool db_accumulate = false);
 
 // ---- xent_rows.hip: row softmax-CE over materialised logits (wide-E chunked path) ----
 // forward that leaves softmax - onehot (unscaled) in place of the logits (false: row too long)

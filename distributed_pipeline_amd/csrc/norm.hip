@@ -154,7 +154,7 @@ __global__ void __launch_bounds__(256, VEC <= 12 ? 4 : VEC <= 24 ? 2 : 1) add_ln
     const float* __restrict__ mean_in, const float* __restrict__ rstd_in,
     const bf16_t* __restrict__ gamma, bf16_t* __restrict__ dres, bf16_t* __restrict__ dy,
     float* __restrict__ dyb, float* __restrict__ part_dg, float* __restrict__ part_db, int64_t R,
-    float p, uint32_t seed, uint32_t offset, const bf16_t* __restrict__ dh_in) {
+    float p, uint32_t seed, uint32_t offset, const bf16_t* __restrict__ dh_in, float* __restrict__ part) {
   constexpr int D = VEC * 64;
   __shared__ float red[4][D];  // reused for dgamma, dbeta, dyb in turn (D = 2048: 32 KiB)
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
@@ -213,8 +213,9 @@ __global__ void __launch_bounds__(256, VEC <= 12 ? 4 : VEC <= 24 ? 2 : 1) add_ln
       }
     }
   }
-  // one fp32 atomic per column per block and accumulator (dg/db/dyb zeroed by the
-  // launcher or accumulated onto the parameter grads)
+  // per block and accumulator: one fp32 atomic per column (dg/db/dyb zeroed by the
+  // launcher or accumulated onto the parameter grads), or - part != nullptr - a plain
+  // store of the block's column sums into part[block][3][D] (ln_colreduce_kernel adds them)
   float* const dst[3] = {part_dg, part_db, dyb};
 #pragma unroll
   for (int a = 0; a < 3; ++a) {
@@ -223,8 +224,33 @@ __global__ void __launch_bounds__(256, VEC <= 12 ? 4 : VEC <= 24 ? 2 : 1) add_ln
 #pragma unroll
     for (int i = 0; i < VEC; ++i) red[w][col0 + i] = a == 0 ? adg[i] : a == 1 ? adb[i] : ady[i];
     __syncthreads();
-    for (int c = threadIdx.x; c < D; c += blockDim.x)
-      atomicAdd(dst[a] + c, red[0][c] + red[1][c] + red[2][c] + red[3][c]);
+    if (part) {
+      float* pr = part + ((int64_t)blockIdx.x * 3 + a) * D;
+      for (int c = threadIdx.x; c < D; c += blockDim.x) pr[c] = red[0][c] + red[1][c] + red[2][c] + red[3][c];
+    } else {
+      for (int c = threadIdx.x; c < D; c += blockDim.x)
+        atomicAdd(dst[a] + c, red[0][c] + red[1][c] + red[2][c] + red[3][c]);
+    }
+  }
+}
+
+// Second stage of the small-R column sums: grid (D / 64, #accumulators, NSEG); a block sums
+// column chunk x of accumulator y over its segment of the nb block partials (64 columns x 4
+// row lanes, 16-byte-free coalesced 256-B rows) and adds one atomic per column.
+__global__ void __launch_bounds__(256) ln_colreduce_kernel(const float* __restrict__ part, int nb, int D,
+                                                          float* __restrict__ d0, float* __restrict__ d1,
+                                                          float* __restrict__ d2, int astride) {
+  __shared__ float red[4][64];
+  const int c = blockIdx.x * 64 + (threadIdx.x & 63), rl = threadIdx.x >> 6, a = blockIdx.y;
+  const int per = (nb + gridDim.z - 1) / gridDim.z;
+  const int r0 = blockIdx.z * per, r1 = min(nb, r0 + per);
+  float t = 0.f;
+  for (int r = r0 + rl; r < r1; r += 4) t += part[((int64_t)r * astride + a) * D + c];
+  red[rl][threadIdx.x & 63] = t;
+  __syncthreads();
+  if (rl == 0) {
+    float* dst = a == 0 ? d0 : a == 1 ? d1 : d2;
+    atomicAdd(dst + c, red[0][threadIdx.x] + red[1][threadIdx.x] + red[2][threadIdx.x] + red[3][threadIdx.x]);
   }
 }
 
@@ -271,13 +297,27 @@ int ln_bwd_blocks(int64_t R) {
   return (int)(nb < 512 ? nb : 512);
 }
 
+// Small R (a 64-sample micro-batch of the reference schedule is 8192 rows): 32 rows per
+// block left 4 waves per CU, each walking 8 rows back to back - latency-bound at ~1.7 TB/s
+// (29 us per call).  Two rows per wave instead (8 per block), with the block column sums
+// stored as partials (9.4 MB at 8192 x 768, plain 16-byte stores) and reduced by a second
+// kernel - more blocks would otherwise cost one fp32 atomic per column per block.
+constexpr int64_t LN_SMALL_R = 65536;
+int64_t ln_bwd_ws_floats(int64_t R, int D) {
+  if (R > LN_SMALL_R) return 0;
+  const int64_t nb = (R + 7) / 8;
+  return nb * 3 * D;
+}
+
 template <int VEC>
 static void ln_bwd_impl(const uint16_t* dout, const uint16_t* hsave, const float* mean,
                         const float* rstd, const uint16_t* g, uint16_t* dres, uint16_t* dy,
                         float* dyb, float* dg, float* db, int64_t R, float p, uint32_t seed,
-                        uint32_t off, const uint16_t* dh_in, bool post, int zero_mask, hipStream_t s) {
+                        uint32_t off, const uint16_t* dh_in, bool post, int zero_mask, hipStream_t s,
+                        float* ws) {
   constexpr int D = VEC * 64;
-  const int nb = ln_bwd_blocks(R);
+  const bool two_stage = ws != nullptr && R <= LN_SMALL_R;
+  const int nb = two_stage ? (int)((R + 7) / 8) : ln_bwd_blocks(R);
   // zero the accumulators that are scratch (zero_mask bits: 1 dg, 2 db, 4 dyb); the others
   // are parameter .grad buffers the kernel accumulates onto.  One memset when the scratch
   // ones are consecutive rows of one buffer (the binding allocates them so).
@@ -289,22 +329,40 @@ static void ln_bwd_impl(const uint16_t* dout, const uint16_t* hsave, const float
     if (zb) (void)hipMemsetAsync(db, 0, sizeof(float) * D, s);
     if (zy) (void)hipMemsetAsync(dyb, 0, sizeof(float) * D, s);
   }
+  float* part = two_stage ? ws : nullptr;
   if (post)
     hipLaunchKernelGGL((add_ln_bwd_kernel<VEC, true>), dim3(nb), dim3(256), 0, s, (const bf16_t*)dout,
                        (const bf16_t*)hsave, mean, rstd, (const bf16_t*)g, (bf16_t*)dres, (bf16_t*)dy,
-                       dy ? dyb : nullptr, dg, db, R, p, seed, off, (const bf16_t*)dh_in);
+                       dy ? dyb : nullptr, dg, db, R, p, seed, off, (const bf16_t*)dh_in, part);
   else
     hipLaunchKernelGGL((add_ln_bwd_kernel<VEC, false>), dim3(nb), dim3(256), 0, s, (const bf16_t*)dout,
                        (const bf16_t*)hsave, mean, rstd, (const bf16_t*)g, (bf16_t*)dres, (bf16_t*)dy,
-                       dy ? dyb : nullptr, dg, db, R, p, seed, off, (const bf16_t*)dh_in);
+                       dy ? dyb : nullptr, dg, db, R, p, seed, off, (const bf16_t*)dh_in, part);
+  if (two_stage) {
+    const int nacc = (dy && dyb) ? 3 : 2;
+    const int nseg = nb >= 256 ? 16 : nb >= 32 ? 4 : 1;
+    hipLaunchKernelGGL(ln_colreduce_kernel, dim3(D / 64, nacc, nseg), dim3(256), 0, s, part, nb, D, dg, db,
+                       dy ? dyb : nullptr, 3);
+  }
+}
+
+// dst[c] += sum_r part[r][c] (fp32 [rows][cols] partials, cols % 64 == 0): the bias
+// gradient of a fused epilogue's per-tile column sums, accumulated straight onto the
+// parameter's fp32 .grad (no ATen reduce + autograd add per micro-batch)
+bool launch_colsum_acc(const float* part, int rows, int cols, float* dst, hipStream_t s) {
+  if (cols % 64 || rows <= 0) return false;
+  const int nseg = rows >= 256 ? 16 : rows >= 32 ? 4 : 1;
+  hipLaunchKernelGGL(ln_colreduce_kernel, dim3(cols / 64, 1, nseg), dim3(256), 0, s, part, rows, cols, dst,
+                     (float*)nullptr, (float*)nullptr, 1);
+  return true;
 }
 
 bool launch_add_ln_bwd(const uint16_t* dout, const uint16_t* hsave, const float* mean,
                        const float* rstd, const uint16_t* g, uint16_t* dres, uint16_t* dy, float* dyb,
                        float* dg, float* db, int64_t R, int D, float p, uint32_t seed, uint32_t off,
-                       hipStream_t s, const uint16_t* dh_in, bool post, int zero_mask) {
+                       hipStream_t s, const uint16_t* dh_in, bool post, int zero_mask, float* ws) {
   DPA_LN_DISPATCH(D, ln_bwd_impl, dout, hsave, mean, rstd, g, dres, dy, dyb, dg, db, R, p, seed,
-                  off, dh_in, post, zero_mask, s)
+                  off, dh_in, post, zero_mask, s, ws)
   return true;
 }
 

@@ -350,9 +350,12 @@ def _mlp_bwd(dy2, x2, w1_16, w2_16, h, z1, params, cfg, need_dx, db2=None, dx_ac
     aux = h if act == "tanh" else z1
     dz1 = db1 = None
     if act != "none" and r2[1] and _gemm_shape_ok(dy2, w2_16.shape[1]):
-        dz1, db1 = get_ext().gemm_nn_dact(dy2, w2_16, aux, _ACTS.index(act), b1 is not None)
+        gb1 = _grad_acc(b1)
+        dz1, db1 = get_ext().gemm_nn_dact(dy2, w2_16, aux, _ACTS.index(act), b1 is not None, db_acc=gb1)
         if dz1 is None:
             db1 = None
+        elif gb1 is not None:
+            db1 = _ACCUMULATED  # fc1's bias gradient went straight onto b1.grad
     if dz1 is None:
         db1 = None
         dh = _dgrad(dy2, w2_16, r2[1])
@@ -496,8 +499,11 @@ class _AttnLNFn(torch.autograd.Function):
         do = _dgrad(dy, wo16, ro[1])
         dwo, dbo = _lin_param_grads(wo, bo, dy, o2, ro[2], dyb if bo is not None else None)
         # attention
+        gbq = _grad_acc(bq)
         dqkv, dbq = ext.attn_bwd(do.view(o.shape), qkv3, o, lse, heads, float(p_attn), False, seed_a,
-                                 off_a, bq is not None, hm)  # dqkv comes back token-major
+                                 off_a, bq is not None, hm, db_acc=gbq)  # dqkv comes back token-major
+        if gbq is not None:
+            dbq = _ACCUMULATED  # the column sums went straight onto bq.grad
         dz = dqkv.view(-1, dqkv.shape[-1])
         if bq is not None and dbq is None and not rq[2]:
             _, dbq = _bias_act_bwd(dz, None, None, "none", True)
