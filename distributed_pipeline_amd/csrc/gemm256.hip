@@ -603,7 +603,40 @@ __device__ __forceinline__ int lds_read_b32_sync(uint32_t addr) {
 __device__ __forceinline__ float bf_lo(uint32_t w) { return __uint_as_float(w << 16); }
 __device__ __forceinline__ float bf_hi(uint32_t w) { return __uint_as_float(w & 0xffff0000u); }
 
-template <bool B_TR, int EPI, int ACT>
+// Lab knobs (tools/gemm_lab; the library uses the defaults): POL bit 0 = non-temporal
+// epilogue stores, bit 1 = non-temporal aux loads; GM > 1 walks tiles in groups of GM tile
+// rows, column-major inside a group (GM x NT tiles share GM A panels and NT B panels).
+template <int POL>
+__device__ __forceinline__ void st_out(bf16_t* p, const uint4& v) {
+  if constexpr (POL & 1) {
+    const u32x4_v x = {v.x, v.y, v.z, v.w};
+    __builtin_nontemporal_store(x, reinterpret_cast<u32x4_v*>(p));
+  } else {
+    *reinterpret_cast<uint4*>(p) = v;
+  }
+}
+template <int POL>
+__device__ __forceinline__ uint4 ld_aux(const bf16_t* p) {
+  if constexpr (POL & 2) {
+    const u32x4_v x = __builtin_nontemporal_load(reinterpret_cast<const u32x4_v*>(p));
+    return make_uint4(x[0], x[1], x[2], x[3]);
+  } else {
+    return *reinterpret_cast<const uint4*>(p);
+  }
+}
+template <int GM>
+__device__ __forceinline__ void tile_mn(int t, int NT, int& mt, int& nt) {
+  if constexpr (GM <= 1) {
+    mt = t / NT;
+    nt = t - mt * NT;
+  } else {
+    const int gs = GM * NT, g = t / gs, r = t - g * gs;
+    mt = g * GM + r % GM;
+    nt = r / GM;
+  }
+}
+
+template <bool B_TR, int EPI, int ACT, int POL = 0, int GM = 1>
 __global__ void __launch_bounds__(512) gemmp_kernel(const bf16_t* __restrict__ A, int64_t lda,
                                                     const bf16_t* __restrict__ B, int64_t ldb, int M, int N,
                                                     int nk, bf16_t* __restrict__ C, int64_t ldc,
@@ -633,7 +666,8 @@ __global__ void __launch_bounds__(512) gemmp_kernel(const bf16_t* __restrict__ A
   const uint32_t csa[2] = {0u, 0u};
 
   auto prologue = [&](int t, int slot) {
-    const int mt = t / NT, nt = t % NT;
+    int mt, nt;
+    tile_mn<GM>(t, NT, mt, nt);
     const int lane = lane_id();
     opA.init(A, lda, mt * 256, w, lane, wm, 64, sbase);
     opB.init(B, ldb, nt * 256, w, lane, wn, 32, sbase + B_REGION, /*remap=*/true);
@@ -656,7 +690,8 @@ __global__ void __launch_bounds__(512) gemmp_kernel(const bf16_t* __restrict__ A
   // the tile, its 64 columns wn*64 + (0..63).  In the row-major domain (after the LDS
   // transpose) lane l handles rows 8k + (l >> 3) (k = 0, 1) of the round, columns 8 (l & 7) .. +7.
   auto row_off = [&](int t, int ro, int k, int ln) -> int64_t {
-    const int mt = t / NT, nt = t % NT;
+    int mt, nt;
+    tile_mn<GM>(t, NT, mt, nt);
     const int qa = ro >> 2, i = ro & 3;
     const int64_t row = (int64_t)mt * 256 + qa * 128 + wm * 64 + i * 16 + k * 8 + (ln >> 3);
     const int col = nt * 256 + wn * 64 + (ln & 7) * 8;
@@ -758,20 +793,20 @@ __global__ void __launch_bounds__(512) gemmp_kernel(const bf16_t* __restrict__ A
         if (ro + 2 < 8) {
 #pragma unroll
           for (int k = 0; k < 2; ++k)
-            aux[ro & 1][k] = *reinterpret_cast<const uint4*>(Zout + row_off(t, ro + 2, k, ln));
+            aux[ro & 1][k] = ld_aux<POL>(Zout + row_off(t, ro + 2, k, ln));
         }
       }
 #pragma unroll
       for (int k = 0; k < 2; ++k) {
         const int64_t o = row_off(t, ro, k, ln);
-        if constexpr (EPI == 2) *reinterpret_cast<uint4*>(Zout + o) = val[k];
+        if constexpr (EPI == 2) st_out<POL>(Zout + o, val[k]);
         if constexpr (EPI == 1 || EPI == 2) val[k] = act8<ACT>(val[k]);
         if constexpr (EPI == 6) {
           uint4 dv;
           val[k] = act_dact8<ACT>(val[k], dv);
-          *reinterpret_cast<uint4*>(Zout + o) = dv;
+          st_out<POL>(Zout + o, dv);
         }
-        *reinterpret_cast<uint4*>(C + o) = val[k];
+        st_out<POL>(C + o, val[k]);
       }
     }
     if constexpr (EPI == 4) {
@@ -787,7 +822,8 @@ __global__ void __launch_bounds__(512) gemmp_kernel(const bf16_t* __restrict__ A
         x += __shfl_xor(x, 32, 64);
         csum[e] = x;
       }
-      const int mt = t / NT, nt = t % NT;
+      int mt, nt;
+    tile_mn<GM>(t, NT, mt, nt);
       float* dst = colpart + ((int64_t)mt * 2 + wm) * (int64_t)(NT * 256) + nt * 256 + wn * 64 + ch * 8;
       if (ln < 8) {
         *reinterpret_cast<float4*>(dst) = make_float4(csum[0], csum[1], csum[2], csum[3]);
@@ -878,7 +914,7 @@ __global__ void __launch_bounds__(512) gemmp_kernel(const bf16_t* __restrict__ A
 #pragma unroll
       for (int ro = 0; ro < 2; ++ro)
 #pragma unroll
-        for (int k = 0; k < 2; ++k) aux[ro][k] = *reinterpret_cast<const uint4*>(Zout + row_off(tile, ro, k, ln));
+        for (int k = 0; k < 2; ++k) aux[ro][k] = ld_aux<POL>(Zout + row_off(tile, ro, k, ln));
     }
     if (has_next) prologue(next, slot ^ 1);
     epilogue(tile, slot, aux, has_next);
@@ -972,16 +1008,37 @@ static int* gemmp_queue(hipStream_t s) {
   return buf;
 }
 
+template <bool B_TR, int EPI, int ACT, int POL = 0, int GM = 1>
+static void gemmp_launch(const uint16_t* a, int64_t lda, const uint16_t* b, int64_t ldb, int M, int N, int K,
+                         uint16_t* c, const uint16_t* bias, uint16_t* z, int ncu, hipStream_t s,
+                         float* colpart, int hm) {
+  const int tiles = (M / 256) * (N / 256);
+  const int grid = persistent_grid(tiles, ncu);
+  int* q = (tiles > grid && grid >= 8) ? gemmp_queue(s) : nullptr;
+  hipLaunchKernelGGL((g256::gemmp_kernel<B_TR, EPI, ACT, POL, GM>), dim3(grid), dim3(512), 0, s,
+                     (const bf16_t*)a, lda, (const bf16_t*)b, ldb, M, N, K / 64, (bf16_t*)c, (int64_t)N,
+                     (const bf16_t*)bias, (bf16_t*)z, colpart, q, hm);
+}
+
+// The two GELU-side GEMMs (EPI 6: y and act' stored; EPI 4: times act' plus column sums) of
+// wide layers (>= 8 column tiles) walk tiles in groups of 8 tile rows with non-temporal
+// epilogue stores: 2.1% / 2.6% faster on the 3072-wide MLP GEMMs at T = 262144 (gemm_lab
+// "policy" study, profiles/gemm_lab_r3_policy.txt); neither helps the narrow GEMMs.
 template <bool B_TR, int EPI, int ACT>
 static void gemmp_go(const uint16_t* a, int64_t lda, const uint16_t* b, int64_t ldb, int M, int N, int K,
                      uint16_t* c, const uint16_t* bias, uint16_t* z, int ncu, hipStream_t s,
                      float* colpart = nullptr, int hm = 0) {
-  const int tiles = (M / 256) * (N / 256);
-  const int grid = persistent_grid(tiles, ncu);
-  int* q = (tiles > grid && grid >= 8) ? gemmp_queue(s) : nullptr;
-  hipLaunchKernelGGL((g256::gemmp_kernel<B_TR, EPI, ACT>), dim3(grid), dim3(512), 0, s, (const bf16_t*)a,
-                     lda, (const bf16_t*)b, ldb, M, N, K / 64, (bf16_t*)c, (int64_t)N, (const bf16_t*)bias,
-                     (bf16_t*)z, colpart, q, hm);
+  static const bool grouped = [] {
+    const char* e = std::getenv("DPA_GEMMP_GROUPED");  // "0": default policy (A/B runs)
+    return !(e && e[0] == '0');
+  }();
+  if constexpr (EPI == 4 || EPI == 6) {
+    if (grouped && (M / 256) % 8 == 0 && N / 256 >= 8) {
+      gemmp_launch<B_TR, EPI, ACT, 1, 8>(a, lda, b, ldb, M, N, K, c, bias, z, ncu, s, colpart, hm);
+      return;
+    }
+  }
+  gemmp_launch<B_TR, EPI, ACT>(a, lda, b, ldb, M, N, K, c, bias, z, ncu, s, colpart, hm);
 }
 
 // y[T][N] = act(x[T][K] . W[N][K]^T + bias); z (nullable, act != 0) = the pre-activation,

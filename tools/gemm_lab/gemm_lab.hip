@@ -183,6 +183,45 @@ static double check(const uint16_t* A, const uint16_t* B, bool btr, const uint16
   return me / (mx + 1e-30);
 }
 
+// persistent kernel with the lab knobs (store policy POL, tile grouping GM)
+template <bool BTR, int EPI, int ACT, int POL, int GM>
+static void gp(const uint16_t* a, int64_t lda, const uint16_t* b, int64_t ldb, int M, int N, int K, uint16_t* c,
+               const uint16_t* bias, uint16_t* z, float* colpart, int ncu, hipStream_t st) {
+  const int tiles = (M / 256) * (N / 256);
+  const int grid = std::min(tiles, ncu);
+  hipLaunchKernelGGL((dpa::g256::gemmp_kernel<BTR, EPI, ACT, POL, GM>), dim3(grid), dim3(512), 0, st,
+                     (const dpa::bf16_t*)a, lda, (const dpa::bf16_t*)b, ldb, M, N, K / 64, (dpa::bf16_t*)c,
+                     (int64_t)N, (const dpa::bf16_t*)bias, (dpa::bf16_t*)z, colpart, (int*)nullptr, 0);
+}
+
+// Study "policy": non-temporal epilogue stores / aux loads and grouped tile order on the
+// model's persistent GEMMs (fwd: y[T][N] = x[T][K] W[N][K]^T; dgrad: dx[T][K] = dy[T][N] W[N][K])
+template <int POL, int GM>
+static void add_policy(std::vector<Variant>& vs, const std::string& tag, uint16_t* A, uint16_t* B, uint16_t* C,
+                       uint16_t* Z, uint16_t* bias, float* CP, int T, int ncu) {
+  auto fl = [&](int K, int N) { return 2.0 * T * K * N; };
+  vs.push_back({"qkv/fwd_bias" + tag, [=](hipStream_t st) {
+                  gp<false, 0, 0, POL, 1>(A, 768, B, 768, T, 2304, 768, C, bias, nullptr, nullptr, ncu, st);
+                }, fl(768, 2304), {}});
+  vs.push_back({"attn_out/fwd_bias" + tag, [=](hipStream_t st) {
+                  gp<false, 0, 0, POL, 1>(A, 768, B, 768, T, 768, 768, C, bias, nullptr, nullptr, ncu, st);
+                }, fl(768, 768), {}});
+  vs.push_back({"ffn_in/fwd_gelu_d" + tag, [=](hipStream_t st) {
+                  gp<false, 6, 1, POL, GM>(A, 768, B, 768, T, 3072, 768, C, bias, Z, nullptr, ncu, st);
+                }, fl(768, 3072), {}});
+  vs.push_back({"ffn_out/fwd_bias" + tag, [=](hipStream_t st) {
+                  gp<false, 0, 0, POL, 1>(A, 3072, B, 3072, T, 768, 3072, C, bias, nullptr, nullptr, ncu, st);
+                }, fl(3072, 768), {}});
+  // dh[T][3072] = dy[T][768] W2[768][3072] * d, plus column-sum partials (EPI 4, act code 4)
+  vs.push_back({"ffn_out/dgrad_dact_db" + tag, [=](hipStream_t st) {
+                  gp<true, 4, 4, POL, GM>(A, 768, B, 3072, T, 3072, 768, C, nullptr, Z, CP, ncu, st);
+                }, fl(768, 3072), {}});
+  // dx[T][768] = dh[T][3072] W1[3072][768] + dx (EPI 5, in place)
+  vs.push_back({"ffn_in/dgrad_res" + tag, [=](hipStream_t st) {
+                  gp<true, 5, 0, POL, 1>(A, 3072, B, 768, T, 768, 3072, C, nullptr, C, nullptr, ncu, st);
+                }, fl(3072, 768), {}});
+}
+
 int main(int argc, char** argv) {
   const int rounds = argc > 1 ? atoi(argv[1]) : 5;
   const int iters = 10;
@@ -211,6 +250,44 @@ int main(int argc, char** argv) {
   hipLaunchKernelGGL(fill_rand, dim3(16), dim3(256), 0, 0, bias, (int64_t)4096, 3u, 0.1f);
   hipLaunchKernelGGL(fill_rand, dim3(4096), dim3(256), 0, 0, Z, maxC, 4u, 1.f);
   CK(hipDeviceSynchronize());
+
+  if (argc > 2 && std::string(argv[2]) == "policy") {
+    std::vector<Variant> pv;
+    add_policy<0, 1>(pv, "", A, B, C, Z, bias, CP, T, ncu);
+    add_policy<1, 1>(pv, "_nt", A, B, C, Z, bias, CP, T, ncu);
+    add_policy<3, 1>(pv, "_nt_ntaux", A, B, C, Z, bias, CP, T, ncu);
+    add_policy<0, 8>(pv, "_gm8", A, B, C, Z, bias, CP, T, ncu);
+    add_policy<0, 4>(pv, "_gm4", A, B, C, Z, bias, CP, T, ncu);
+    add_policy<1, 8>(pv, "_nt_gm8", A, B, C, Z, bias, CP, T, ncu);
+    {  // bitwise: every policy / grouping writes the same y and d as the default
+      const int K = 768, N = 3072;
+      uint16_t *C2, *Z2;
+      CK(hipMalloc(&C2, (size_t)T * N * 2));
+      CK(hipMalloc(&Z2, (size_t)T * N * 2));
+      gp<false, 6, 1, 0, 1>(A, K, B, K, T, N, K, C, bias, Z, nullptr, ncu, s);
+      gp<false, 6, 1, 1, 8>(A, K, B, K, T, N, K, C2, bias, Z2, nullptr, ncu, s);
+      CK(hipStreamSynchronize(s));
+      printf("check nt_gm8 gelu y maxdiff %.3e d maxdiff %.3e\n", maxdiff(C, C2, (int64_t)T * N),
+             maxdiff(Z, Z2, (int64_t)T * N));
+      gp<true, 4, 4, 0, 1>(A, 768, B, 3072, T, 3072, 768, C, nullptr, Z, CP, ncu, s);
+      gp<true, 4, 4, 3, 8>(A, 768, B, 3072, T, 3072, 768, C2, nullptr, Z, CP, ncu, s);
+      CK(hipStreamSynchronize(s));
+      printf("check nt_gm8 dact maxdiff %.3e\n", maxdiff(C, C2, (int64_t)T * N));
+      CK(hipFree(C2));
+      CK(hipFree(Z2));
+      hipLaunchKernelGGL(fill_rand, dim3(4096), dim3(256), 0, 0, Z, maxC, 4u, 1.f);
+      CK(hipDeviceSynchronize());
+    }
+    for (auto& v : pv) time_it(v, s, 2);
+    for (int r = 0; r < rounds; ++r)
+      for (auto& v : pv) v.ms.push_back(time_it(v, s, iters));
+    for (auto& v : pv) {
+      std::sort(v.ms.begin(), v.ms.end());
+      const float med = v.ms[v.ms.size() / 2];
+      printf("%-32s median %.4f ms  min %.4f ms  %.1f TF/s\n", v.name.c_str(), med, v.ms[0], v.flop / med / 1e9);
+    }
+    return 0;
+  }
 
   std::vector<Variant> vs;
   // shape (K = layer input width, N = layer output width)
@@ -289,38 +366,38 @@ int main(int argc, char** argv) {
                     hipLaunchKernelGGL((dpa::g256::gemmp_kernel<false, 0, 0>), dim3(grid), dim3(512), 0, st,
                                        (const dpa::bf16_t*)A, (int64_t)K, (const dpa::bf16_t*)B, (int64_t)K, T, N,
                                        K / 64, (dpa::bf16_t*)C, (int64_t)0, (const dpa::bf16_t*)bias,
-                                       (dpa::bf16_t*)nullptr, (float*)nullptr, (int*)nullptr);
+                                       (dpa::bf16_t*)nullptr, (float*)nullptr, (int*)nullptr, 0);
                   }, fl, {}});
     vs.push_back({"ffn_in/fwd_gelu_z_gp_ldc0", [=](hipStream_t st) {
                     hipLaunchKernelGGL((dpa::g256::gemmp_kernel<false, 2, 1>), dim3(grid), dim3(512), 0, st,
                                        (const dpa::bf16_t*)A, (int64_t)K, (const dpa::bf16_t*)B, (int64_t)K, T, N,
                                        K / 64, (dpa::bf16_t*)C, (int64_t)0, (const dpa::bf16_t*)bias,
-                                       (dpa::bf16_t*)Z, (float*)nullptr, (int*)nullptr);
+                                       (dpa::bf16_t*)Z, (float*)nullptr, (int*)nullptr, 0);
                   }, fl, {}});
     vs.push_back({"ffn_in/fwd_z_noact_gp_ldc0", [=](hipStream_t st) {
                     hipLaunchKernelGGL((dpa::g256::gemmp_kernel<false, 2, 0>), dim3(grid), dim3(512), 0, st,
                                        (const dpa::bf16_t*)A, (int64_t)K, (const dpa::bf16_t*)B, (int64_t)K, T, N,
                                        K / 64, (dpa::bf16_t*)C, (int64_t)0, (const dpa::bf16_t*)bias,
-                                       (dpa::bf16_t*)Z, (float*)nullptr, (int*)nullptr);
+                                       (dpa::bf16_t*)Z, (float*)nullptr, (int*)nullptr, 0);
                   }, fl, {}});
     vs.push_back({"ffn_in/fwd_z_noact_gp", [=](hipStream_t st) {
                     hipLaunchKernelGGL((dpa::g256::gemmp_kernel<false, 2, 0>), dim3(grid), dim3(512), 0, st,
                                        (const dpa::bf16_t*)A, (int64_t)K, (const dpa::bf16_t*)B, (int64_t)K, T, N,
                                        K / 64, (dpa::bf16_t*)C, (int64_t)N, (const dpa::bf16_t*)bias,
-                                       (dpa::bf16_t*)Z, (float*)nullptr, (int*)nullptr);
+                                       (dpa::bf16_t*)Z, (float*)nullptr, (int*)nullptr, 0);
                   }, fl, {}});
     vs.push_back({"ffn_out/dgrad_dact_noact_gp_ldc0", [=](hipStream_t st) {
                     hipLaunchKernelGGL((dpa::g256::gemmp_kernel<true, 3, 0>), dim3(grid), dim3(512), 0, st,
                                        (const dpa::bf16_t*)A, (int64_t)768, (const dpa::bf16_t*)B, (int64_t)3072, T,
                                        3072, 768 / 64, (dpa::bf16_t*)C, (int64_t)0, (const dpa::bf16_t*)nullptr,
-                                       (dpa::bf16_t*)Z, (float*)nullptr, (int*)nullptr);
+                                       (dpa::bf16_t*)Z, (float*)nullptr, (int*)nullptr, 0);
                   }, fl, {}});
     // dgrad of ffn_out with dgelu: dh[T][3072] = dy[T][768] . W2[768][3072] * gelu'(z)
     vs.push_back({"ffn_out/dgrad_dgelu_gp_ldc0", [=](hipStream_t st) {
                     hipLaunchKernelGGL((dpa::g256::gemmp_kernel<true, 3, 1>), dim3(grid), dim3(512), 0, st,
                                        (const dpa::bf16_t*)A, (int64_t)768, (const dpa::bf16_t*)B, (int64_t)3072, T,
                                        3072, 768 / 64, (dpa::bf16_t*)C, (int64_t)0, (const dpa::bf16_t*)nullptr,
-                                       (dpa::bf16_t*)Z, (float*)nullptr, (int*)nullptr);
+                                       (dpa::bf16_t*)Z, (float*)nullptr, (int*)nullptr, 0);
                   }, fl, {}});
     vs.push_back({"ffn_out/dgrad_nostore_g256", [=](hipStream_t st) {
                     hipLaunchKernelGGL((dpa::g256::gemm256_kernel<false, true, dpa::g256::EPI_NONE>),
