@@ -636,7 +636,7 @@ __device__ __forceinline__ void tile_mn(int t, int NT, int& mt, int& nt) {
   }
 }
 
-template <bool B_TR, int EPI, int ACT, int POL = 0, int GM = 1>
+template <bool B_TR, int EPI, int ACT, int POL = 0, int GM = 1, int STG = 0, int DU = 0>
 __global__ void __launch_bounds__(512) gemmp_kernel(const bf16_t* __restrict__ A, int64_t lda,
                                                     const bf16_t* __restrict__ B, int64_t ldb, int M, int N,
                                                     int nk, bf16_t* __restrict__ C, int64_t ldc,
@@ -864,6 +864,12 @@ __global__ void __launch_bounds__(512) gemmp_kernel(const bf16_t* __restrict__ A
   int slot = 0;
   bool extra = false;
   zero_acc();
+  if constexpr (STG > 1) {
+    // start-phase stagger: workgroup j of an XCD starts (j % STG) * DU x ~1 us late, so the
+    // epilogue store bursts of the workgroups no longer coincide
+    const int ph = (blockIdx.x >> 3) % STG;
+    for (int i = 0; i < ph * DU; ++i) __builtin_amdgcn_s_sleep(32);
+  }
   prologue(tile, slot);
   wait_vm<8>();  // K-tile 0 halves A0, B0 (and the bias slot) landed
   barrier();

@@ -222,6 +222,46 @@ static void add_policy(std::vector<Variant>& vs, const std::string& tag, uint16_
                 }, fl(3072, 768), {}});
 }
 
+// Study "stagger": start-phase offsets between workgroups (STG phases of DU x ~1 us) so the
+// epilogue store bursts of the 256 persistent workgroups stop coinciding; q != nullptr runs
+// the dynamic tile queue (a late workgroup takes fewer tiles).  Library store policy.
+template <bool BTR, int EPI, int ACT, int POL, int GM, int STG, int DU>
+static void gps(const uint16_t* a, int64_t lda, const uint16_t* b, int64_t ldb, int M, int N, int K, uint16_t* c,
+                const uint16_t* bias, uint16_t* z, float* colpart, int ncu, int* q, hipStream_t st) {
+  const int tiles = (M / 256) * (N / 256);
+  const int grid = std::min(tiles, ncu);
+  if (q) CK(hipMemsetAsync(q, 0, 8 * 16 * sizeof(int), st));
+  hipLaunchKernelGGL((dpa::g256::gemmp_kernel<BTR, EPI, ACT, POL, GM, STG, DU>), dim3(grid), dim3(512), 0, st,
+                     (const dpa::bf16_t*)a, lda, (const dpa::bf16_t*)b, ldb, M, N, K / 64, (dpa::bf16_t*)c,
+                     (int64_t)N, (const dpa::bf16_t*)bias, (dpa::bf16_t*)z, colpart, q, 0);
+}
+template <int STG, int DU>
+static void add_stag(std::vector<Variant>& vs, const std::string& tag, uint16_t* A, uint16_t* B, uint16_t* C,
+                     uint16_t* Z, uint16_t* bias, float* CP, int T, int ncu, int* q) {
+  auto fl = [&](int K, int N) { return 2.0 * T * K * N; };
+  vs.push_back({"qkv/fwd_bias" + tag, [=](hipStream_t st) {
+                  gps<false, 0, 0, 0, 1, STG, DU>(A, 768, B, 768, T, 2304, 768, C, bias, nullptr, nullptr, ncu, q, st);
+                }, fl(768, 2304), {}});
+  vs.push_back({"attn_out/fwd_bias" + tag, [=](hipStream_t st) {
+                  gps<false, 0, 0, 0, 1, STG, DU>(A, 768, B, 768, T, 768, 768, C, bias, nullptr, nullptr, ncu, q, st);
+                }, fl(768, 768), {}});
+  vs.push_back({"ffn_in/fwd_gelu_d" + tag, [=](hipStream_t st) {
+                  gps<false, 6, 1, 1, 8, STG, DU>(A, 768, B, 768, T, 3072, 768, C, bias, Z, nullptr, ncu, q, st);
+                }, fl(768, 3072), {}});
+  vs.push_back({"ffn_out/fwd_bias" + tag, [=](hipStream_t st) {
+                  gps<false, 0, 0, 0, 1, STG, DU>(A, 3072, B, 3072, T, 768, 3072, C, bias, nullptr, nullptr, ncu, q, st);
+                }, fl(3072, 768), {}});
+  vs.push_back({"ffn_out/dgrad_dact_db" + tag, [=](hipStream_t st) {
+                  gps<true, 4, 4, 1, 8, STG, DU>(A, 768, B, 3072, T, 3072, 768, C, nullptr, Z, CP, ncu, q, st);
+                }, fl(768, 3072), {}});
+  vs.push_back({"ffn_in/dgrad_res" + tag, [=](hipStream_t st) {
+                  gps<true, 5, 0, 0, 1, STG, DU>(A, 3072, B, 768, T, 768, 3072, C, nullptr, C, nullptr, ncu, q, st);
+                }, fl(3072, 768), {}});
+  vs.push_back({"qkv/dgrad" + tag, [=](hipStream_t st) {
+                  gps<true, 0, 0, 0, 1, STG, DU>(A, 2304, B, 768, T, 768, 2304, C, nullptr, nullptr, nullptr, ncu, q, st);
+                }, fl(2304, 768), {}});
+}
+
 int main(int argc, char** argv) {
   const int rounds = argc > 1 ? atoi(argv[1]) : 5;
   const int iters = 10;
@@ -250,6 +290,43 @@ int main(int argc, char** argv) {
   hipLaunchKernelGGL(fill_rand, dim3(16), dim3(256), 0, 0, bias, (int64_t)4096, 3u, 0.1f);
   hipLaunchKernelGGL(fill_rand, dim3(4096), dim3(256), 0, 0, Z, maxC, 4u, 1.f);
   CK(hipDeviceSynchronize());
+
+  if (argc > 2 && std::string(argv[2]) == "stagger") {
+    int* q;
+    CK(hipMalloc(&q, 8 * 16 * sizeof(int)));
+    std::vector<Variant> pv;
+    add_stag<0, 0>(pv, "", A, B, C, Z, bias, CP, T, ncu, nullptr);
+    add_stag<4, 5>(pv, "_s4x5", A, B, C, Z, bias, CP, T, ncu, nullptr);
+    add_stag<4, 10>(pv, "_s4x10", A, B, C, Z, bias, CP, T, ncu, nullptr);
+    add_stag<8, 3>(pv, "_s8x3", A, B, C, Z, bias, CP, T, ncu, nullptr);
+    add_stag<0, 0>(pv, "_dyn", A, B, C, Z, bias, CP, T, ncu, q);
+    add_stag<4, 10>(pv, "_dyn_s4x10", A, B, C, Z, bias, CP, T, ncu, q);
+    add_stag<8, 3>(pv, "_dyn_s8x3", A, B, C, Z, bias, CP, T, ncu, q);
+    {  // bitwise: the stagger only moves start times
+      const int K = 768, N = 3072;
+      uint16_t *C2, *Z2;
+      CK(hipMalloc(&C2, (size_t)T * N * 2));
+      CK(hipMalloc(&Z2, (size_t)T * N * 2));
+      gps<false, 6, 1, 1, 8, 0, 0>(A, K, B, K, T, N, K, C, bias, Z, nullptr, ncu, nullptr, s);
+      gps<false, 6, 1, 1, 8, 8, 3>(A, K, B, K, T, N, K, C2, bias, Z2, nullptr, ncu, q, s);
+      CK(hipStreamSynchronize(s));
+      printf("check stagger gelu y maxdiff %.3e d maxdiff %.3e\n", maxdiff(C, C2, (int64_t)T * N),
+             maxdiff(Z, Z2, (int64_t)T * N));
+      CK(hipFree(C2));
+      CK(hipFree(Z2));
+      hipLaunchKernelGGL(fill_rand, dim3(4096), dim3(256), 0, 0, Z, maxC, 4u, 1.f);
+      CK(hipDeviceSynchronize());
+    }
+    for (auto& v : pv) time_it(v, s, 2);
+    for (int r = 0; r < rounds; ++r)
+      for (auto& v : pv) v.ms.push_back(time_it(v, s, iters));
+    for (auto& v : pv) {
+      std::sort(v.ms.begin(), v.ms.end());
+      const float med = v.ms[v.ms.size() / 2];
+      printf("%-32s median %.4f ms  min %.4f ms  %.1f TF/s\n", v.name.c_str(), med, v.ms[0], v.flop / med / 1e9);
+    }
+    return 0;
+  }
 
   if (argc > 2 && std::string(argv[2]) == "policy") {
     std::vector<Variant> pv;

@@ -10,3 +10,6 @@ timeout -k 10 300 python bench.py --steps 10 --warmup 3 --json-out gpurun_out/ch
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT" &&
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/chk/prof -o run --output-format csv -- python3 bench.py --steps 3 --warmup 1 --ref-steps 0 > gpurun_out/chk/prof.log 2>&1
 echo "exit=$?"
+[ "$DPA_CHK_REFPROF" = 1 ] && cd "$GRAFT_REPO_ROOT" &&
+timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/chk/rprof -o run --output-format csv -- python3 bench.py --steps 3 --warmup 1 --ref-steps 0 --exec-microbatch 64 > gpurun_out/chk/rprof.log 2>&1
+echo "exit=$?"
