@@ -522,6 +522,38 @@ static void gemm_wgrad(const at::Tensor& dy, const at::Tensor& x, at::Tensor& dW
   TORCH_CHECK(ok, "gemm_wgrad: unsupported shape");
 }
 
+// dW += sum_s dy_s^T x_s (+ db += colsum) over equal-length token segments in one launch
+// (the reference schedule's deferred micro-batch weight gradients); false if the shape is not
+// supported by the multi-segment kernel (the caller then runs the segments one by one)
+static bool gemm_wgrad_multi(const std::vector<at::Tensor>& dys, const std::vector<at::Tensor>& xs, at::Tensor& dW,
+                             c10::optional<at::Tensor> db) {
+  TORCH_CHECK(!dys.empty() && dys.size() == xs.size(), "gemm_wgrad_multi: segment lists");
+  const int nseg = (int)dys.size();
+  if (nseg > 4) return false;
+  CHECK_F32(dW); CHECK_CONTIG(dW);
+  const int T = (int)dys[0].size(0), N = (int)dys[0].size(1), K = (int)xs[0].size(1);
+  std::vector<const uint16_t*> dp(nseg), xp(nseg);
+  for (int i = 0; i < nseg; ++i) {
+    CHECK_DEV(dys[i]); CHECK_BF16(dys[i]); CHECK_BF16(xs[i]); CHECK_CONTIG(dys[i]); CHECK_CONTIG(xs[i]);
+    TORCH_CHECK(dys[i].dim() == 2 && xs[i].dim() == 2 && dys[i].size(0) == T && dys[i].size(1) == N &&
+                xs[i].size(0) == T && xs[i].size(1) == K, "gemm_wgrad_multi: segment shapes");
+    TORCH_CHECK(dys[i].device() == dW.device() && xs[i].device() == dW.device(), "gemm_wgrad_multi: devices");
+    dp[i] = bf_ptr(dys[i]);
+    xp[i] = bf_ptr(xs[i]);
+  }
+  TORCH_CHECK(dW.size(0) == N && dW.size(1) == K, "gemm_wgrad_multi: dW shape");
+  float* dbp = nullptr;
+  if (db.has_value() && db->defined()) {
+    CHECK_F32((*db)); TORCH_CHECK(db->numel() == N, "db size");
+    dbp = db->data_ptr<float>();
+  }
+  const c10::DeviceGuard guard(dW.device());
+  const int64_t wsn = dpa::gemm256_wgrad_workspace_floats(T, N, K, nseg);
+  at::Tensor ws = at::empty({wsn}, dW.options());
+  return dpa::launch_gemm256_wgrad_multi(dp.data(), xp.data(), nseg, dW.data_ptr<float>(), dbp, T, N, K,
+                                         cur_stream(), wsn ? ws.data_ptr<float>() : nullptr);
+}
+
 // ---- row softmax cross-entropy (chunked wide-E linear-CE) ------------------------------
 static void check_i64(const at::Tensor& t, const char* name) {
   TORCH_CHECK(t.is_cuda() && t.scalar_type() == at::kLong && t.is_contiguous(), name,
@@ -767,6 +799,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("db_acc") = py::none());
   m.def("gemm_nn_acc_", &gemm_nn_acc_, "dx += dy W in place (bf16 MFMA); False if the shape does not tile");
   m.def("gemm_wgrad", &gemm_wgrad, "dW += dy^T x, db += colsum(dy) (fp32 atomics, split-K)");
+  m.def("gemm_wgrad_multi", &gemm_wgrad_multi, "dW += sum_s dy_s^T x_s over equal token segments, one launch",
+        py::arg("dys"), py::arg("xs"), py::arg("dW"), py::arg("db") = py::none());
   m.def("gemm_supported", &gemm_supported, "shape check for the native GEMMs");
   m.def("set_gemm256", &dpa::set_gemm256, "enable/disable the 256x256 8-phase GEMM path");
   m.def("set_gemmp_dynamic", &dpa::set_gemmp_dynamic,

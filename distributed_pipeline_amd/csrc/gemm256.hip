@@ -294,21 +294,41 @@ __device__ __forceinline__ void phase(f32x4 (&acc)[2][2][4][2], bf16x8 (&fa)[4][
   barrier();
 }
 
+// Token segments of a multi-segment weight gradient: dW += sum_s dy_s^T x_s, every segment
+// ktiles_total K-tiles long (the reference schedule's deferred micro-batch pairs).
+constexpr int WG_MAXSEG = 4;
+struct WgSegs {
+  const bf16_t* a[WG_MAXSEG];
+  const bf16_t* b[WG_MAXSEG];
+  int n;  // 0: the kernel's A / B are the only segment
+};
+
 template <bool A_TR, bool B_TR, int EPI>
 __global__ void __launch_bounds__(512) gemm256_kernel(
     const bf16_t* __restrict__ A, int64_t lda, const bf16_t* __restrict__ B, int64_t ldb, int M,
     int N, int ktiles_total, int ktiles_per_split, int splits, bf16_t* __restrict__ C, int64_t ldc,
     float* __restrict__ Cf, const bf16_t* __restrict__ bias, int act, bf16_t* __restrict__ Zout,
-    float* __restrict__ colsum, float* __restrict__ wsp = nullptr) {
+    float* __restrict__ colsum, float* __restrict__ wsp = nullptr, WgSegs segs = WgSegs{}) {
   __shared__ __attribute__((aligned(1024))) char smem[2 * B_REGION];
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int wm = (w >> 2) & 1, wn = w & 3;  // 2 x 4 waves over a 128 x 128 quadrant
   const int grp = __builtin_amdgcn_readfirstlane(w >> 2);
   const int MT = M / 256, NT = N / 256;
-  const int tile = xcd_remap(blockIdx.x, MT * NT * splits);
-  const int nt = tile % NT, mt = (tile / NT) % MT, z = tile / (NT * MT);
+  const int nseg = segs.n > 0 ? segs.n : 1;
+  const int tile = xcd_remap(blockIdx.x, MT * NT * splits * nseg);
+  const int nt = tile % NT, mt = (tile / NT) % MT, z = tile / (NT * MT);  // z: workspace slab
   const int m0 = mt * 256, n0 = nt * 256;
-  const int t0 = z * ktiles_per_split;
+  const int zs = z % splits;  // split within the segment
+  if (segs.n > 0) {
+    const int sg = z / splits;
+#pragma unroll
+    for (int i = 0; i < WG_MAXSEG; ++i)  // uniform selects: no dynamic index into the kernarg struct
+      if (sg == i) {
+        A = segs.a[i];
+        B = segs.b[i];
+      }
+  }
+  const int t0 = zs * ktiles_per_split;
   const int nk = min(ktiles_total - t0, ktiles_per_split);  // even, >= 2 (host guarantees)
 
   Operand<A_TR> opA;
@@ -1108,9 +1128,10 @@ bool launch_gemmp_nn(const uint16_t* dy, const uint16_t* W, uint16_t* dx, const 
 // workspace plus one reduce pass over it ((2 s + 2) x the gradient bytes at HBM rate).
 // The old rule (fill two rounds regardless of T) split an 8192-token micro-batch 32
 // ways: 54x atomic amplification, 107 us per call.
+// nseg > 1: that many equal token segments (multi-segment launch, one slab per (segment, split)).
 struct WgradPlan { int splits, kps; bool ws; };
-static WgradPlan wgrad_plan(int T, int N, int K) {
-  const int tiles = (N / 256) * (K / 256);
+static WgradPlan wgrad_plan(int T, int N, int K, int nseg = 1) {
+  const int tiles = (N / 256) * (K / 256) * nseg;
   const int ktot = T / 64;
   const int ncu = device_cu_count();
   const double mb = (double)N * K * 4.0 / 1e6;  // gradient bytes, MB
@@ -1134,10 +1155,11 @@ static WgradPlan wgrad_plan(int T, int N, int K) {
     const int wgs = tiles * s_eff;
     const int rounds = (wgs + ncu - 1) / ncu;
     const double main = rounds * (kps * 1.5 + 4.0);
+    const int slabs = s_eff * nseg;  // partials merged per gradient element
     for (int w = 0; w < 2; ++w) {
-      if (w == 1 && s_eff < 2) continue;
-      if (force_ws >= 0 && w != force_ws && !(w == 0 && s_eff < 2)) continue;
-      const double t = w ? main + (2.0 * s_eff + 2.0) * mb / 4.0 : fmax(main, wgs * 0.35);
+      if (w == 1 && slabs < 2) continue;
+      if (force_ws >= 0 && w != force_ws && !(w == 0 && slabs < 2)) continue;
+      const double t = w ? main + (2.0 * slabs + 2.0) * mb / 4.0 : fmax(main, wgs * 0.35);
       if (t < best * 0.98) {
         best = t;
         best_p = WgradPlan{s_eff, kps, w == 1};
@@ -1148,10 +1170,11 @@ static WgradPlan wgrad_plan(int T, int N, int K) {
   return best_p;
 }
 
-int64_t gemm256_wgrad_workspace_floats(int T, int N, int K) {
-  if (!g256_enabled() || N % 256 || K % 256 || T % 128 || T < 128) return 0;
-  const WgradPlan p = wgrad_plan(T, N, K);
-  return p.ws ? (int64_t)p.splits * N * K : 0;
+int64_t gemm256_wgrad_workspace_floats(int T, int N, int K, int nseg) {
+  if (!g256_enabled() || N % 256 || K % 256 || T % 128 || T < 128 || nseg < 1 || nseg > g256::WG_MAXSEG)
+    return 0;
+  const WgradPlan p = wgrad_plan(T, N, K, nseg);
+  return p.ws ? (int64_t)p.splits * nseg * N * K : 0;
 }
 
 __global__ void __launch_bounds__(256) wgrad_reduce_kernel(const float* __restrict__ ws, float* __restrict__ dW,
@@ -1179,6 +1202,35 @@ bool launch_gemm256_wgrad(const uint16_t* dy, const uint16_t* x, float* dW, floa
     const int64_t n4 = (int64_t)N * K / 4;
     hipLaunchKernelGGL(wgrad_reduce_kernel, dim3((unsigned)((n4 + 255) / 256)), dim3(256), 0, s, wsp, dW, n4,
                        p.splits);
+  }
+  return true;
+}
+
+// dW[N][K] += sum_s dy_s[T][N]^T . x_s[T][K] over nseg equal token segments in ONE launch: the
+// split-K plan sees nseg x the tiles, so each segment is split fewer ways (fewer fp32 partial
+// slabs per token than nseg separate launches) and one reduce pass merges everything.
+bool launch_gemm256_wgrad_multi(const uint16_t* const* dys, const uint16_t* const* xs, int nseg, float* dW,
+                                float* db, int T, int N, int K, hipStream_t s, float* ws) {
+  if (!g256_enabled() || N % 256 || K % 256 || T % 128 || T < 128 || nseg < 1 || nseg > g256::WG_MAXSEG)
+    return false;
+  if (nseg == 1) return launch_gemm256_wgrad(dys[0], xs[0], dW, db, T, N, K, s, ws);
+  g256::WgSegs sg{};
+  for (int i = 0; i < nseg; ++i) {
+    sg.a[i] = (const bf16_t*)dys[i];
+    sg.b[i] = (const bf16_t*)xs[i];
+  }
+  sg.n = nseg;
+  const int tiles = (N / 256) * (K / 256);
+  const int ktot = T / 64;
+  const WgradPlan p = wgrad_plan(T, N, K, nseg);
+  float* wsp = (p.ws && ws != nullptr) ? ws : nullptr;
+  hipLaunchKernelGGL((g256::gemm256_kernel<true, true, g256::EPI_ATOMIC_F32>),
+                     dim3(tiles * p.splits * nseg), dim3(512), 0, s, sg.a[0], (int64_t)N, sg.b[0], (int64_t)K,
+                     N, K, ktot, p.kps, p.splits, nullptr, (int64_t)K, dW, nullptr, 0, nullptr, db, wsp, sg);
+  if (wsp) {
+    const int64_t n4 = (int64_t)N * K / 4;
+    hipLaunchKernelGGL(wgrad_reduce_kernel, dim3((unsigned)((n4 + 255) / 256)), dim3(256), 0, s, wsp, dW, n4,
+                       p.splits * nseg);
   }
   return true;
 }

@@ -150,7 +150,10 @@ bool launch_gemm256_nn_dact(const uint16_t* dy, const uint16_t* W, const uint16_
 bool launch_gemm256_wgrad(const uint16_t* dy, const uint16_t* x, float* dW, float* db, int T,
                           int N, int K, hipStream_t s, float* ws = nullptr);
 // fp32 workspace the split-K weight gradient merges through (0: atomics / no split)
-int64_t gemm256_wgrad_workspace_floats(int T, int N, int K);
+int64_t gemm256_wgrad_workspace_floats(int T, int N, int K, int nseg = 1);
+// dW += sum_s dy_s^T x_s over nseg (<= 4) equal token segments in one split-K launch
+bool launch_gemm256_wgrad_multi(const uint16_t* const* dys, const uint16_t* const* xs, int nseg, float* dW,
+                                float* db, int T, int N, int K, hipStream_t s, float* ws);
 // gemm256.hip persistent forward / data-gradient kernels with fused epilogues (false when
 // the shape does not tile).  ncu: compute units (grid = min(tiles, ncu)).
 //   nt: y[T][N] = act(x[T][K] W[N][K]^T + bias); z (nullable) = pre-activation, or act'(it)

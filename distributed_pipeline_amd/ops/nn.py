@@ -147,6 +147,76 @@ def _route(x2, n_out, act):
     return True, True, True
 
 
+class _WgradDeferral:
+    """Weight-gradient deferral for the reference (micro-batch) schedule.
+
+    Under ``no_sync`` the weight gradient of micro-batch k is only needed once the whole
+    step's micro-batches have been accumulated (reference: ``loss.backward()`` per micro-batch
+    inside ``no_sync``, /root/reference/utils/trainer.py:209-235).  An 8192-token micro-batch
+    gives a 768 x 768 weight 9 output tiles, so the split-K GEMM splits the tokens ~14 ways and
+    merges 14 fp32 partial slabs per call - more HBM traffic than the GEMM's own operands.
+    With ``depth`` = d the (dy, x) operands of a Linear are held for d - 1 micro-batches and
+    the d segments run as ONE multi-segment split-K launch (each segment split fewer ways, one
+    reduce pass): the same sum into the same fp32 gradient, at most d - 1 micro-batches of
+    extra operand memory.  ``active`` is set by the trainer around every backward except the
+    last (DDP-armed) one, before which ``flush()`` runs whatever is still held."""
+
+    def __init__(self):
+        self.depth = 0
+        self.active = False
+        self.pending = {}  # id(weight) -> (weight, bias, [(dz, x2), ...])
+        self.stats = {"deferred": 0, "multi_launches": 0, "segments": 0}
+
+    def _run(self, p, bias, segs):
+        ext = get_ext()
+        gw = p.grad
+        gb = bias.grad if (bias is not None and bias.requires_grad) else None
+        cur = torch.cuda.current_stream(segs[0][0].device) if segs[0][0].is_cuda else None
+        if cur is not None:
+            for dz, x2 in segs:  # produced on another micro-batch's stream: keep them alive
+                dz.record_stream(cur)
+                x2.record_stream(cur)
+        if len(segs) > 1 and ext.gemm_wgrad_multi([s[0] for s in segs], [s[1] for s in segs], gw, gb):
+            self.stats["multi_launches"] += 1
+            self.stats["segments"] += len(segs)
+            return
+        for dz, x2 in segs:
+            ext.gemm_wgrad(dz, x2, gw, gb)
+
+    def offer(self, p, dz, x2, bias, gw, gb):
+        """True when the weight gradient was deferred or run here (grads preallocated)."""
+        if self.depth < 2 or gw is not p.grad or (gb is not None and gb is not bias.grad):
+            return False
+        key = id(p)
+        ent = self.pending.pop(key, None)
+        segs = ent[2] if ent is not None else []
+        if segs and (segs[0][0].shape != dz.shape or segs[0][1].shape != x2.shape
+                     or (ent[1] is not None) != (bias is not None)):
+            self._run(ent[0], ent[1], segs)
+            segs = []
+        segs.append((dz, x2))
+        if self.active and len(segs) < self.depth:
+            self.pending[key] = (p, bias, segs)
+            self.stats["deferred"] += 1
+            return True
+        self._run(p, bias, segs)
+        return True
+
+    def flush(self):
+        """Run every held weight gradient (on the current stream)."""
+        pend, self.pending = self.pending, {}
+        for p, bias, segs in pend.values():
+            self._run(p, bias, segs)
+
+    def drop(self):
+        """Forget held operands (an abandoned backward whose gradients are discarded)."""
+        self.pending = {}
+        self.active = False
+
+
+WGRAD_DEFER = _WgradDeferral()
+
+
 def _accumulate_wgrad(p, dz, x2, bias):
     """dW (+db) straight into the parameters' fp32 .grad buffers via the split-K GEMM.
 
@@ -162,6 +232,8 @@ def _accumulate_wgrad(p, dz, x2, bias):
         gb = bias.grad
         if gb is None or gb.dtype != torch.float32:
             gb = db_out = torch.zeros(bias.shape, dtype=torch.float32, device=dz.device)
+    if WGRAD_DEFER.offer(p, dz, x2, bias, gw, gb):
+        return None, None
     ext.gemm_wgrad(dz, x2, gw, gb)
     # Readiness needs no explicit signal: autograd still runs the parameter's
     # AccumulateGrad node (with an undefined grad) after this backward, and its

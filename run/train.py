@@ -119,7 +119,7 @@ def main(namespace):
         first_bucket_mb=args.ddp_first_bucket_mb, grad_reduce_dtype=args.grad_reduce_dtype,
         shard_optimizer=args.shard_optimizer,
         exec_microbatch=args.exec_microbatch,
-        overlap_microbatches=args.overlap_microbatches,
+        overlap_microbatches=args.overlap_microbatches, defer_wgrad=args.defer_wgrad,
         log_cross_rank_mean=args.log_cross_rank_mean, nan_guard=args.nan_guard,
         debug_anomaly=args.debug_anomaly, consistency_check_interval=args.consistency_check_interval,
         profile_steps=args.profile_steps, roctx=args.roctx, save_rng_state=args.save_rng_state)

@@ -64,6 +64,25 @@ def test_gemm_wgrad_accumulates(T, N, K, tile):
     _close(db, refb, 1e-3)
 
 
+@pytest.mark.parametrize("nseg", [2, 3, 4])
+@pytest.mark.parametrize("T,N,K", [(8192, 768, 768), (8192, 2304, 768), (2048, 768, 3072), (256, 256, 512)])
+def test_gemm_wgrad_multi_segment(T, N, K, nseg):
+    """One multi-segment split-K launch == the sum of per-segment weight gradients."""
+    torch.manual_seed(0)
+    dys = [torch.randn(T, N, device="cuda").bfloat16() for _ in range(nseg)]
+    xs = [torch.randn(T, K, device="cuda").bfloat16() for _ in range(nseg)]
+    dW = torch.randn(N, K, device="cuda")
+    db = torch.randn(N, device="cuda")
+    ref = dW.clone()
+    refb = db.clone()
+    for dy, x in zip(dys, xs):
+        ref += dy.float().t() @ x.float()
+        refb += dy.float().sum(0)
+    assert _ext().gemm_wgrad_multi(dys, xs, dW, db)
+    _close(dW, ref, 1e-3)
+    _close(db, refb, 1e-3)
+
+
 @pytest.mark.parametrize("T,N,K,act", [(512, 768, 3072, 1), (256, 768, 768, 2), (512, 512, 256, 3)])
 def test_gemm_nn_dact(T, N, K, act):
     """dz = (dy W) * act'(aux) with the activation backward fused into the epilogue."""

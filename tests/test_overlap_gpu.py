@@ -10,7 +10,7 @@ import torch
 pytestmark = pytest.mark.gpu
 
 
-def _loop(overlap):
+def _loop(overlap, defer=0):
     from basic_utils import logger
     from distributed_pipeline_amd.ops.nn import RNG
     from utils.initialization import create_diffusion_from_config, create_model_from_config, seed_all
@@ -34,7 +34,7 @@ def _loop(overlap):
                               ema_rate="0.9999", log_interval=1, save_interval=10 ** 9, resume_checkpoint="",
                               learning_steps=2, checkpoint_path="/tmp/dpa_overlap_test", ddp_engine="native",
                               precision="bf16", exec_microbatch=-1, overlap_microbatches=overlap,
-                              device_prefetch=False)
+                              device_prefetch=False, defer_wgrad=defer)
     torch.manual_seed(7)
     losses = []
     for _ in range(2):
@@ -53,5 +53,27 @@ def test_overlapped_schedule_matches_sequential():
     err = (g0 - g1).abs().max().item()
     assert err <= max(4 * noise, 1e-6 * scale), (err, noise, scale)
     assert (p0 - p1).abs().max().item() <= max(4 * (p0 - pa).abs().max().item(), 1e-6)
+    for a, b in zip(l0, l1):
+        assert abs(a - b) <= 1e-4 * abs(a)
+
+
+@pytest.mark.parametrize("depth", [2, 4])
+def test_deferred_wgrad_matches_sequential(depth):
+    """Weight-gradient deferral (ops/nn.py _WgradDeferral): the held (dy, x) operands of
+    ``depth`` micro-batches run as one multi-segment split-K GEMM.  Same fp32 sum in another
+    order: gradients within fp32 rounding of the sequential loop's, and the multi-segment
+    launch must actually have run."""
+    from distributed_pipeline_amd.ops.nn import WGRAD_DEFER
+    g0, p0, l0 = _loop(False)
+    before = dict(WGRAD_DEFER.stats)
+    g1, p1, l1 = _loop(True, defer=depth)
+    assert WGRAD_DEFER.stats["multi_launches"] > before["multi_launches"]
+    assert not WGRAD_DEFER.pending
+    scale = g0.abs().max().item()
+    err = (g0 - g1).abs().max().item()
+    assert err <= 2e-5 * scale, (err, scale)
+    # Adam turns rounding-level gradient differences of near-zero elements into at most
+    # ~lr-sized parameter differences (lr = 1e-4, two steps)
+    assert (p0 - p1).abs().max().item() <= 2.5e-4
     for a, b in zip(l0, l1):
         assert abs(a - b) <= 1e-4 * abs(a)

@@ -128,6 +128,7 @@ class TrainLoop:
             shard_optimizer=False,
             exec_microbatch=0,
             overlap_microbatches=True,
+            defer_wgrad=4,
             log_cross_rank_mean=False,
             # ---- observability / robustness (all optional) ----
             nan_guard="off",
@@ -181,6 +182,9 @@ class TrainLoop:
         # on a second stream (DPA_OVERLAP_MB=0 disables)
         self.overlap_microbatches = (bool(overlap_microbatches)
                                      and os.environ.get("DPA_OVERLAP_MB", "1") != "0")
+        # ...and hold each Linear's weight-gradient operands for defer_wgrad micro-batches, run as
+        # one multi-segment split-K GEMM (ops/nn.py _WgradDeferral; DPA_DEFER_WGRAD overrides)
+        self.defer_wgrad = max(0, min(4, int(os.environ.get("DPA_DEFER_WGRAD", defer_wgrad))))
 
         self.step = 0
         self.resume_step = 0
@@ -612,24 +616,42 @@ class TrainLoop:
                 self.log_loss_dict(mode="train", losses=losses)
             return losses, self._chunk_state()
 
+        # weight-gradient deferral (ops/nn.py _WgradDeferral): every backward but the last
+        # holds its Linear (dy, x) operands; the held ones run before the last backward, so
+        # the armed backward's grad-ready events follow every contribution to the buffer
+        from distributed_pipeline_amd.ops import nn as nn_ops
+        defer = nn_ops.WGRAD_DEFER
+        defer.depth = self.defer_wgrad
         done = None
-        nxt = fwd(0)
-        for k in range(nch):
-            losses, state = nxt
-            nxt = fwd(k + 1) if k + 1 < nch else None
-            st = stream_of(k)
-            with torch.cuda.stream(st):
-                if done is not None:
-                    st.wait_event(done)
-                for key, v in state.items():
-                    setattr(self, key, v)
-                if k == nch - 1 and self.use_ddp:
-                    self.ddp_model.arm_for_backward()
-                self.loss_scale = self._chunk_loss_scale(starts[k], min(n, starts[k] + self.exec_microbatch), n)
-                with self._range("backward"):
-                    self.backward_from_losses(losses)
-                done = torch.cuda.Event()
-                done.record(st)
+        try:
+            nxt = fwd(0)
+            for k in range(nch):
+                losses, state = nxt
+                nxt = fwd(k + 1) if k + 1 < nch else None
+                st = stream_of(k)
+                with torch.cuda.stream(st):
+                    if done is not None:
+                        st.wait_event(done)
+                    for key, v in state.items():
+                        setattr(self, key, v)
+                    last = k == nch - 1
+                    if last:
+                        defer.active = False
+                        defer.flush()
+                    else:
+                        defer.active = defer.depth > 1
+                    if last and self.use_ddp:
+                        self.ddp_model.arm_for_backward()
+                    self.loss_scale = self._chunk_loss_scale(starts[k], min(n, starts[k] + self.exec_microbatch), n)
+                    with self._range("backward"):
+                        self.backward_from_losses(losses)
+                    done = torch.cuda.Event()
+                    done.record(st)
+        except BaseException:
+            defer.drop()  # the abandoned backward's gradients are discarded by the caller
+            raise
+        finally:
+            defer.active = False
         cur.wait_stream(side)
 
     def _chunk_loss_scale(self, start, end, n):
