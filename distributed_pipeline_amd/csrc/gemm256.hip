@@ -1001,7 +1001,14 @@ bool launch_gemm256_nn_dact(const uint16_t* dy, const uint16_t* W, const uint16_
 }
 
 // ---- persistent forward / data-gradient launchers ---------------------------
-static int persistent_grid(int tiles, int ncu) { return tiles < ncu ? tiles : ncu; }
+// Grid cap of the persistent kernels (0 = none): the overlapped micro-batch schedule caps the
+// forward stream's GEMMs so the concurrent backward's kernels find free CUs.
+static int g_gemmp_grid_cap = 0;
+void set_gemmp_grid_cap(int cap) { g_gemmp_grid_cap = cap > 0 ? cap : 0; }
+static int persistent_grid(int tiles, int ncu) {
+  if (g_gemmp_grid_cap > 0 && g_gemmp_grid_cap < ncu) ncu = g_gemmp_grid_cap;
+  return tiles < ncu ? tiles : ncu;
+}
 
 // Dynamic tile schedule of the persistent kernels (see gemmp_kernel): on when the
 // compute stream shares the chip with collectives (the DDP engine turns it on for

@@ -147,6 +147,14 @@ def _route(x2, n_out, act):
     return True, True, True
 
 
+class _nullctx:
+    def __enter__(self):
+        return None
+
+    def __exit__(self, *a):
+        return False
+
+
 class _WgradDeferral:
     """Weight-gradient deferral for the reference (micro-batch) schedule.
 
@@ -165,23 +173,42 @@ class _WgradDeferral:
         self.depth = 0
         self.active = False
         self.pending = {}  # id(weight) -> (weight, bias, [(dz, x2), ...])
+        self.held_bytes = 0
+        # operands are only held while their total stays under this budget (a large executed
+        # micro-batch - DiffuSeq-XL's 1024-sample chunks hold ~100 GB of Linear operands -
+        # gains nothing from deferral and must not double its memory)
+        self.budget_bytes = int(float(os.environ.get("DPA_DEFER_WGRAD_GB", "32")) * (1 << 30))
         self.stats = {"deferred": 0, "multi_launches": 0, "segments": 0}
+        self.stream = None  # side stream for the un-armed micro-batches' launches (trainer-set)
 
-    def _run(self, p, bias, segs):
+    @staticmethod
+    def _nbytes(segs):
+        return sum(dz.numel() * dz.element_size() + x2.numel() * x2.element_size() for dz, x2 in segs)
+
+    def _run(self, p, bias, segs, side=False):
+        """Launch the held segments.  ``side``: on ``self.stream`` (ordered after the current
+        stream's work so far) instead of the current stream - the weight gradients of the
+        un-armed micro-batches are off the backward chain's critical path; nothing reads
+        them before the trainer joins that stream ahead of the last backward."""
         ext = get_ext()
         gw = p.grad
         gb = bias.grad if (bias is not None and bias.requires_grad) else None
         cur = torch.cuda.current_stream(segs[0][0].device) if segs[0][0].is_cuda else None
-        if cur is not None:
-            for dz, x2 in segs:  # produced on another micro-batch's stream: keep them alive
-                dz.record_stream(cur)
-                x2.record_stream(cur)
-        if len(segs) > 1 and ext.gemm_wgrad_multi([s[0] for s in segs], [s[1] for s in segs], gw, gb):
-            self.stats["multi_launches"] += 1
-            self.stats["segments"] += len(segs)
-            return
-        for dz, x2 in segs:
-            ext.gemm_wgrad(dz, x2, gw, gb)
+        run_on = cur
+        if cur is not None and side and self.stream is not None:
+            run_on = self.stream
+            run_on.wait_stream(cur)
+        if run_on is not None:
+            for dz, x2 in segs:  # produced on other streams: keep them alive for run_on
+                dz.record_stream(run_on)
+                x2.record_stream(run_on)
+        with torch.cuda.stream(run_on) if run_on is not None and run_on is not cur else _nullctx():
+            if len(segs) > 1 and ext.gemm_wgrad_multi([s[0] for s in segs], [s[1] for s in segs], gw, gb):
+                self.stats["multi_launches"] += 1
+                self.stats["segments"] += len(segs)
+                return
+            for dz, x2 in segs:
+                ext.gemm_wgrad(dz, x2, gw, gb)
 
     def offer(self, p, dz, x2, bias, gw, gb):
         """True when the weight gradient was deferred or run here (grads preallocated)."""
@@ -190,27 +217,32 @@ class _WgradDeferral:
         key = id(p)
         ent = self.pending.pop(key, None)
         segs = ent[2] if ent is not None else []
+        self.held_bytes -= self._nbytes(segs)
         if segs and (segs[0][0].shape != dz.shape or segs[0][1].shape != x2.shape
                      or (ent[1] is not None) != (bias is not None)):
             self._run(ent[0], ent[1], segs)
             segs = []
         segs.append((dz, x2))
-        if self.active and len(segs) < self.depth:
+        nb = self._nbytes(segs)
+        if self.active and len(segs) < self.depth and self.held_bytes + nb <= self.budget_bytes:
             self.pending[key] = (p, bias, segs)
+            self.held_bytes += nb
             self.stats["deferred"] += 1
             return True
-        self._run(p, bias, segs)
+        self._run(p, bias, segs, side=self.active)
         return True
 
     def flush(self):
         """Run every held weight gradient (on the current stream)."""
         pend, self.pending = self.pending, {}
+        self.held_bytes = 0
         for p, bias, segs in pend.values():
-            self._run(p, bias, segs)
+            self._run(p, bias, segs, side=True)
 
     def drop(self):
         """Forget held operands (an abandoned backward whose gradients are discarded)."""
         self.pending = {}
+        self.held_bytes = 0
         self.active = False
 
 

@@ -88,3 +88,21 @@ def test_deferral_off_or_unowned_grads_are_not_taken(monkeypatch):
     other = torch.zeros(8, 4)  # not p.grad: the caller needs the gradient returned
     assert not d.offer(w, torch.ones(16, 8).bfloat16(), torch.ones(16, 4).bfloat16(), None, other, None)
     assert fake.calls == [] and not d.pending
+
+
+def test_deferral_respects_the_memory_budget(monkeypatch):
+    fake = _FakeExt()
+    monkeypatch.setattr(nn_ops, "get_ext", lambda *a, **k: fake)
+    d = nn_ops._WgradDeferral()
+    d.depth = 4
+    d.budget_bytes = 16 * 8 * 2 + 16 * 4 * 2  # room for exactly one held (dz, x2) pair
+    w1, w2 = _param((8, 4)), _param((8, 4))
+    d.active = True
+    assert d.offer(w1, torch.ones(16, 8).bfloat16(), torch.ones(16, 4).bfloat16(), None, w1.grad, None)
+    assert d.held_bytes == d.budget_bytes and fake.calls == []
+    # over budget: w2's gradient runs immediately instead of being held
+    assert d.offer(w2, torch.ones(16, 8).bfloat16(), torch.ones(16, 4).bfloat16(), None, w2.grad, None)
+    assert fake.calls == [1] and id(w2) not in d.pending
+    # w1's second segment would need twice the budget: both run now as one launch
+    assert d.offer(w1, torch.ones(16, 8).bfloat16(), torch.ones(16, 4).bfloat16(), None, w1.grad, None)
+    assert fake.calls == [1, 2] and d.held_bytes == 0 and not d.pending

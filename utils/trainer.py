@@ -604,7 +604,24 @@ class TrainLoop:
         def stream_of(k):  # the last chunk on the current stream
             return streams[(nch - 1 - k) % 2]
 
+        # grid cap of the forward stream's persistent GEMMs (DPA_OVERLAP_FWD_CAP, 0 = none):
+        # the concurrent backward's kernels then find free CUs
+        fwd_cap = int(os.environ.get("DPA_OVERLAP_FWD_CAP", "0"))
+        ext = None
+        if fwd_cap > 0:
+            from distributed_pipeline_amd.ops._ext import get_ext
+            ext = get_ext()
+
         def fwd(k):
+            if ext is not None:
+                ext.set_gemmp_grid_cap(fwd_cap)
+            try:
+                return fwd_(k)
+            finally:
+                if ext is not None:
+                    ext.set_gemmp_grid_cap(0)
+
+        def fwd_(k):
             with torch.cuda.stream(stream_of(k)):
                 with self._range("forward"):
                     if self.use_ddp:
@@ -622,6 +639,14 @@ class TrainLoop:
         from distributed_pipeline_amd.ops import nn as nn_ops
         defer = nn_ops.WGRAD_DEFER
         defer.depth = self.defer_wgrad
+        # the un-armed micro-batches' weight-gradient launches run on a third stream, off the
+        # backward chain (DPA_WGRAD_SIDE_STREAM=0: on the backward's own stream)
+        if os.environ.get("DPA_WGRAD_SIDE_STREAM", "1") != "0":
+            if getattr(self, "_wgrad_stream", None) is None:
+                self._wgrad_stream = torch.cuda.Stream(device=self.device)
+            defer.stream = self._wgrad_stream
+        else:
+            defer.stream = None
         done = None
         try:
             nxt = fwd(0)
@@ -638,6 +663,8 @@ class TrainLoop:
                     if last:
                         defer.active = False
                         defer.flush()
+                        if defer.stream is not None:
+                            st.wait_stream(defer.stream)  # every earlier weight gradient is in
                     else:
                         defer.active = defer.depth > 1
                     if last and self.use_ddp:
@@ -652,6 +679,9 @@ class TrainLoop:
             raise
         finally:
             defer.active = False
+            if defer.stream is not None:
+                cur.wait_stream(defer.stream)
+            defer.stream = None
         cur.wait_stream(side)
 
     def _chunk_loss_scale(self, start, end, n):
