@@ -406,16 +406,18 @@ __global__ void __launch_bounds__(256, D == 64 ? 2 : 1) attn_fwd_online_kernel(c
           if (t >= nsub) continue;
           // key pair of register i: (kv0 + 32 t + 4 hf + acc_off(i)) / 2, all terms even
           const uint32_t kt0 = (uint32_t)((kv0 + t * 32 + 4 * hf) >> 1) * DROP_CK;
-          uint32_t hsh = 0;
 #pragma unroll
           for (int i = 0; i < 16; ++i) {
-            float pr = fexp2(fmaf(acc[t][i], att_c<D>(), -m));
+            const float pr = fexp2(fmaf(acc[t][i], att_c<D>(), -m));
             add += pr;
-            if (dc.on) {
-              if ((i & 1) == 0) hsh = drop_hash_t(dc, qterm, kt0 + (uint32_t)(acc_off(i) >> 1) * DROP_CK);
-              pr = keep_from(dc, hsh, i & 1) ? pr * dc.scale : 0.f;
-            }
             acc[t][i] = pr;
+          }
+          if (dc.on) {  // hashes as an independent batch after the exps (ILP), then the keep selects
+            uint32_t hh[8];
+#pragma unroll
+            for (int j = 0; j < 8; ++j) hh[j] = drop_hash_t(dc, qterm, kt0 + (uint32_t)(acc_off(2 * j) >> 1) * DROP_CK);
+#pragma unroll
+            for (int i = 0; i < 16; ++i) acc[t][i] = keep_from(dc, hh[i >> 1], i & 1) ? acc[t][i] * dc.scale : 0.f;
           }
         }
         l += add;
@@ -644,11 +646,20 @@ __global__ void __launch_bounds__(256, D == 64 ? 2 : 1) attn_bwd_kv_kernel(
           }
         }
 #pragma unroll
+        for (int i = 0; i < 16; ++i) sacc[i] = fexp2(fmaf(sacc[i], att_c<D>(), -s_lse[qt * 32 + acc_row(i, hf)]));
+        // the causal instance serves every subtile: its element mask runs behind a wave-uniform
+        // branch, only on subtiles that cross the diagonal or L (not a per-element select on all)
+        if (MASKED && (!CAUSAL || sub_masked)) {
+#pragma unroll
+          for (int i = 0; i < 16; ++i) {
+            const int qq = q0 + qt * 32 + acc_row(i, hf);
+            if ((CAUSAL && key > qq) || !k_ok || qq >= L) sacc[i] = 0.f;
+          }
+        }
+#pragma unroll
         for (int i = 0; i < 16; ++i) {
           const int r = qt * 32 + acc_row(i, hf);
-          const int qq = q0 + r;
-          float pr = fexp2(fmaf(sacc[i], att_c<D>(), -s_lse[r]));
-          if (MASKED && ((CAUSAL && key > qq) || !k_ok || qq >= L)) pr = 0.f;
+          const float pr = sacc[i];
           float pd = pr, dpd = dpacc[i];
           if (dc.on) {
             const bool kp = keep_from(dc, hh[i], key);
@@ -778,17 +789,27 @@ __global__ void __launch_bounds__(256, D == 64 ? 2 : 1) attn_bwd_q_kernel(
           dpacc = mfma32(lds_frag<2 * D>(vt_lds, t * 32 + (lane & 31), 2 * s + hf), df[s], dpacc);
         }
         const uint32_t kt0 = (uint32_t)((kv0 + t * 32 + 4 * hf) >> 1) * DROP_CK;
-        uint32_t hsh = 0;
+        // dropout hashes first, one per key pair, as an independent batch (ILP)
+        uint32_t hh[8];
+        if (dc.on) {
+#pragma unroll
+          for (int j = 0; j < 8; ++j) hh[j] = drop_hash_t(dc, qterm, kt0 + (uint32_t)(acc_off(2 * j) >> 1) * DROP_CK);
+        }
+#pragma unroll
+        for (int i = 0; i < 16; ++i) sacc[i] = fexp2(fmaf(sacc[i], att_c<D>(), -lse2));
+        // element mask behind a wave-uniform branch (see the dK/dV kernel)
+        if (MASKED && (!CAUSAL || sub_masked)) {
+#pragma unroll
+          for (int i = 0; i < 16; ++i) {
+            const int kk = kv0 + t * 32 + acc_row(i, hf);
+            if ((CAUSAL && kk > q) || !q_ok || kk >= L) sacc[i] = 0.f;
+          }
+        }
 #pragma unroll
         for (int i = 0; i < 16; ++i) {
-          const int kk = kv0 + t * 32 + acc_row(i, hf);
-          float pr = fexp2(fmaf(sacc[i], att_c<D>(), -lse2));
-          if (MASKED && ((CAUSAL && kk > q) || !q_ok || kk >= L)) pr = 0.f;
+          const float pr = sacc[i];
           float dpd = dpacc[i];
-          if (dc.on) {
-            if ((i & 1) == 0) hsh = drop_hash_t(dc, qterm, kt0 + (uint32_t)(acc_off(i) >> 1) * DROP_CK);
-            dpd = keep_from(dc, hsh, i & 1) ? dpd * dc.scale : 0.f;
-          }
+          if (dc.on) dpd = keep_from(dc, hh[i >> 1], i & 1) ? dpd * dc.scale : 0.f;
           sacc[i] = pr * (dpd - dlt);
         }
 #pragma unroll

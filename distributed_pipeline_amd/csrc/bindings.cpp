@@ -362,8 +362,12 @@ static std::vector<at::Tensor> attn_bwd(const at::Tensor& dout, const at::Tensor
       reinterpret_cast<uint16_t*>(dqkv.data_ptr()), dq.defined() ? dq.data_ptr<float>() : nullptr,
       want_db ? colpart.data_ptr<float>() : nullptr, want_db ? db.data_ptr<float>() : nullptr, B, L,
       H, D, (float)p, causal, (uint32_t)seed, (uint32_t)offset, cur_stream(), head_major, acc);
-  if (acc && !got) {  // no fused column sums on this path: add them here
-    db_acc->add_(dqkv.view({-1, 3LL * H * D}).sum(0, false, at::kFloat));
+  if (want_db && !got) {
+    // no fused column sums on this path (L != 128): one column-sum pass over the bf16 dqkv,
+    // accumulated onto db (zeroed unless it is the parameter's .grad)
+    if (!acc) db.zero_();
+    dpa::launch_bias_act_bwd(bf_ptr(dqkv), nullptr, nullptr, db.data_ptr<float>(), (int64_t)B * L,
+                             (int)(3LL * H * D), 0, cur_stream());
     got = true;
   }
   // contract: with a usable db_acc the bias gradient is always accumulated (result undefined)

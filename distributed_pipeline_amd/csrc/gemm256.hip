@@ -1025,20 +1025,29 @@ static int* gemmp_queue(hipStream_t s) {
   if (!g_gemmp_dynamic) return nullptr;
   // one counter buffer per (device, stream): GEMMs on one stream never overlap, but the
   // overlapped micro-batch schedule runs GEMMs on two streams at once
-  struct Q { int dev; hipStream_t s; int* buf; };
+  // A ring of NSLOT counter sets per (device, stream), zeroed by ONE memset each time the ring
+  // wraps (every earlier launch on the stream has finished by then: stream order) instead of a
+  // memset per launch - the reference schedule issues ~3000 GEMMs per step.
+  constexpr int NSLOT = 256, SLOT_INTS = 8 * 16;
+  struct Q { int dev; hipStream_t s; int* buf; int cursor; };
   static Q qs[64];
   static int nq = 0;
   int dev = 0;
   if (hipGetDevice(&dev) != hipSuccess) return nullptr;
-  int* buf = nullptr;
+  Q* q = nullptr;
   for (int i = 0; i < nq; ++i)
-    if (qs[i].dev == dev && qs[i].s == s) buf = qs[i].buf;
-  if (!buf) {
-    if (nq >= 64 || hipMalloc(&buf, 8 * 16 * sizeof(int)) != hipSuccess) return nullptr;
-    qs[nq++] = Q{dev, s, buf};
+    if (qs[i].dev == dev && qs[i].s == s) q = &qs[i];
+  if (!q) {
+    int* buf = nullptr;
+    if (nq >= 64 || hipMalloc(&buf, (size_t)NSLOT * SLOT_INTS * sizeof(int)) != hipSuccess) return nullptr;
+    qs[nq] = Q{dev, s, buf, 0};
+    q = &qs[nq++];
   }
-  if (hipMemsetAsync(buf, 0, 8 * 16 * sizeof(int), s) != hipSuccess) return nullptr;
-  return buf;
+  if (q->cursor == 0 && hipMemsetAsync(q->buf, 0, (size_t)NSLOT * SLOT_INTS * sizeof(int), s) != hipSuccess)
+    return nullptr;
+  int* slot = q->buf + (size_t)q->cursor * SLOT_INTS;
+  q->cursor = (q->cursor + 1) % NSLOT;
+  return slot;
 }
 
 template <bool B_TR, int EPI, int ACT, int POL = 0, int GM = 1>

@@ -10,9 +10,10 @@
 // Dropout(LayerNorm(...))); GPT-2 pre-LN residual streams (h is the new residual
 // stream, out the next sublayer's LN input; the backward adds h's own incoming
 // gradient dh_in).  Backward (dy, dresidual, dgamma, dbeta) in one pass per row.  One
-// wave64 owns a row: D/64 contiguous elements per lane (D = 768 -> 12), loaded
-// as 8-byte vectors, so a row is one fully coalesced 1.5 KiB transaction and
-// both reductions are a single wave-wide shuffle tree (no LDS, no barriers).
+// wave64 owns a row: D/64 elements per lane (D = 768 -> 12) in groups of 8 (16-byte
+// vectors) or 4 (8-byte) interleaved over the lanes (RowMap), so every load/store
+// instruction covers 512 B - 1 KiB of the row contiguously, and both reductions
+// are a single wave-wide shuffle tree (no LDS, no barriers).
 // The dropout mask is never stored: it is regenerated from the counter-based
 // Philox stream (seed, offset, row, column) in the backward.
 //
@@ -23,53 +24,90 @@
 
 namespace dpa {
 
+// Element -> lane map of a D = 64 * VEC row: lane `ln` holds VEC / CH groups of CH consecutive
+// elements, group g at column g * 64 * CH + ln * CH, so one load instruction of a wave covers
+// 64 * CH contiguous elements (1 KiB for CH = 8) instead of 64 strided VEC-element runs.
+template <int VEC>
+struct RowMap {
+  static constexpr int CH = VEC % 8 == 0 ? 8 : VEC % 4 == 0 ? 4 : VEC;
+  static constexpr int NG = VEC / CH;
+  __device__ __forceinline__ static int col(int ln, int i) { return (i / CH) * 64 * CH + ln * CH + i % CH; }
+};
+
 template <int VEC>
 struct RowIO {
-  // load VEC bf16 (VEC % 4 == 0 uses 8-byte vectors)
-  __device__ __forceinline__ static void load(const bf16_t* p, float* v) {
-    if constexpr (VEC % 4 == 0) {
+  using M = RowMap<VEC>;
+  // load this lane's VEC elements of a row (16-B vectors for CH = 8, 8-B for CH = 4)
+  __device__ __forceinline__ static void load(const bf16_t* row, int ln, float* v) {
 #pragma unroll
-      for (int c = 0; c < VEC / 4; ++c) {
-        uint2 raw = *reinterpret_cast<const uint2*>(p + 4 * c);
-        v[4 * c + 0] = __uint_as_float(raw.x << 16);
-        v[4 * c + 1] = __uint_as_float(raw.x & 0xffff0000u);
-        v[4 * c + 2] = __uint_as_float(raw.y << 16);
-        v[4 * c + 3] = __uint_as_float(raw.y & 0xffff0000u);
+    for (int g = 0; g < M::NG; ++g) {
+      const bf16_t* p = row + g * 64 * M::CH + ln * M::CH;
+      float* o = v + g * M::CH;
+      if constexpr (M::CH == 8) {
+        const uint4 raw = *reinterpret_cast<const uint4*>(p);
+        const uint32_t w[4] = {raw.x, raw.y, raw.z, raw.w};
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          o[2 * k] = __uint_as_float(w[k] << 16);
+          o[2 * k + 1] = __uint_as_float(w[k] & 0xffff0000u);
+        }
+      } else if constexpr (M::CH == 4) {
+        const uint2 raw = *reinterpret_cast<const uint2*>(p);
+        o[0] = __uint_as_float(raw.x << 16);
+        o[1] = __uint_as_float(raw.x & 0xffff0000u);
+        o[2] = __uint_as_float(raw.y << 16);
+        o[3] = __uint_as_float(raw.y & 0xffff0000u);
+      } else {
+#pragma unroll
+        for (int c = 0; c < M::CH; ++c) o[c] = bf2f(p[c]);
       }
-    } else {
-#pragma unroll
-      for (int c = 0; c < VEC; ++c) v[c] = bf2f(p[c]);
     }
   }
-  __device__ __forceinline__ static void store(bf16_t* p, const float* v) {
-    if constexpr (VEC % 4 == 0) {
+  __device__ __forceinline__ static void store(bf16_t* row, int ln, const float* v) {
 #pragma unroll
-      for (int c = 0; c < VEC / 4; ++c) {
-        uint2 raw;
-        raw.x = pack_bf2(v[4 * c + 0], v[4 * c + 1]);
-        raw.y = pack_bf2(v[4 * c + 2], v[4 * c + 3]);
-        *reinterpret_cast<uint2*>(p + 4 * c) = raw;
+    for (int g = 0; g < M::NG; ++g) {
+      bf16_t* p = row + g * 64 * M::CH + ln * M::CH;
+      const float* o = v + g * M::CH;
+      if constexpr (M::CH == 8) {
+        *reinterpret_cast<uint4*>(p) = make_uint4(pack_bf2(o[0], o[1]), pack_bf2(o[2], o[3]),
+                                                  pack_bf2(o[4], o[5]), pack_bf2(o[6], o[7]));
+      } else if constexpr (M::CH == 4) {
+        *reinterpret_cast<uint2*>(p) = make_uint2(pack_bf2(o[0], o[1]), pack_bf2(o[2], o[3]));
+      } else {
+#pragma unroll
+        for (int c = 0; c < M::CH; ++c) p[c] = f2bf(o[c]);
       }
-    } else {
-#pragma unroll
-      for (int c = 0; c < VEC; ++c) p[c] = f2bf(v[c]);
     }
   }
 };
 
-// keep-mask bits for this lane's VEC elements of `row`, from one Philox call per 4.
+// keep-mask bits for this lane's VEC elements of `row`: element (row, col) keeps iff word
+// col & 3 of the Philox block (row, col >> 2) is >= p * 2^32 - one call per 4 aligned columns
+// (a function of (row, col) only, whatever the element -> lane map).
 template <int VEC>
-__device__ __forceinline__ void dropout_keep(uint32_t seed, uint32_t offset, int64_t row, int col0,
+__device__ __forceinline__ void dropout_keep(uint32_t seed, uint32_t offset, int64_t row, int ln,
                                              float p, bool* keep) {
+  using M = RowMap<VEC>;
   const uint32_t thr = (uint32_t)(p * 4294967296.0);
+  if constexpr (M::CH % 4 == 0) {
 #pragma unroll
-  for (int c = 0; c < (VEC + 3) / 4; ++c) {
-    uint32_t r[4];
-    philox4(seed, 0x5bd1e995u, (uint32_t)row, (uint32_t)(row >> 32) ^ (uint32_t)((col0 >> 2) + c),
-            offset, 0xdeadbeefu, r);
+    for (int c = 0; c < VEC / 4; ++c) {
+      const int col = M::col(ln, 4 * c);
+      uint32_t r[4];
+      philox4(seed, 0x5bd1e995u, (uint32_t)row, (uint32_t)(row >> 32) ^ (uint32_t)(col >> 2), offset,
+              0xdeadbeefu, r);
 #pragma unroll
-    for (int k = 0; k < 4; ++k)
-      if (4 * c + k < VEC) keep[4 * c + k] = r[k] >= thr;
+      for (int k = 0; k < 4; ++k) keep[4 * c + k] = r[k] >= thr;
+    }
+  } else {
+#pragma unroll
+    for (int i = 0; i < VEC; ++i) {
+      const int col = M::col(ln, i);
+      uint32_t r[4];
+      philox4(seed, 0x5bd1e995u, (uint32_t)row, (uint32_t)(row >> 32) ^ (uint32_t)(col >> 2), offset,
+              0xdeadbeefu, r);
+      keep[i] = r[col & 3] >= thr;
+    }
   }
 }
 
@@ -84,38 +122,37 @@ __global__ void __launch_bounds__(256) add_ln_fwd_kernel(
   const int lane = threadIdx.x & 63;
   const int64_t row = (int64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
   if (row >= R) return;
-  const int col0 = lane * VEC;
   float h[VEC];
-  RowIO<VEC>::load(y + row * D + col0, h);
+  RowIO<VEC>::load(y + row * D, lane, h);
   if (pos) {
     float t[VEC];
-    RowIO<VEC>::load(pos + (row % L) * D + col0, t);
+    RowIO<VEC>::load(pos + (row % L) * D, lane, t);
 #pragma unroll
     for (int i = 0; i < VEC; ++i) h[i] += t[i];
   }
   if (temb) {
     float t[VEC];
-    RowIO<VEC>::load(temb + (row / L) * D + col0, t);
+    RowIO<VEC>::load(temb + (row / L) * D, lane, t);
 #pragma unroll
     for (int i = 0; i < VEC; ++i) h[i] += t[i];
   }
   if (p > 0.f && !post) {
     bool keep[VEC];
-    dropout_keep<VEC>(seed, offset, row, col0, p, keep);
+    dropout_keep<VEC>(seed, offset, row, lane, p, keep);
     const float sc = 1.f / (1.f - p);
 #pragma unroll
     for (int i = 0; i < VEC; ++i) h[i] = keep[i] ? h[i] * sc : 0.f;
   }
   if (res) {
     float r[VEC];
-    RowIO<VEC>::load(res + row * D + col0, r);
+    RowIO<VEC>::load(res + row * D, lane, r);
 #pragma unroll
     for (int i = 0; i < VEC; ++i) h[i] += r[i];
   }
   // round h to bf16 first so the backward (which reloads the bf16 copy) is consistent
 #pragma unroll
   for (int i = 0; i < VEC; ++i) h[i] = bf2f(f2bf(h[i]));
-  if (hsave) RowIO<VEC>::store(hsave + row * D + col0, h);
+  if (hsave) RowIO<VEC>::store(hsave + row * D, lane, h);
   float s = 0.f;
 #pragma unroll
   for (int i = 0; i < VEC; ++i) s += h[i];
@@ -125,18 +162,18 @@ __global__ void __launch_bounds__(256) add_ln_fwd_kernel(
   for (int i = 0; i < VEC; ++i) { const float d = h[i] - mean; v += d * d; }
   const float rstd = rsqrtf(wave_sum(v) * (1.f / D) + eps);
   float g[VEC], b[VEC], o[VEC];
-  RowIO<VEC>::load(gamma + col0, g);
-  RowIO<VEC>::load(beta + col0, b);
+  RowIO<VEC>::load(gamma, lane, g);
+  RowIO<VEC>::load(beta, lane, b);
 #pragma unroll
   for (int i = 0; i < VEC; ++i) o[i] = (h[i] - mean) * rstd * g[i] + b[i];
   if (p > 0.f && post) {
     bool keep[VEC];
-    dropout_keep<VEC>(seed, offset, row, col0, p, keep);
+    dropout_keep<VEC>(seed, offset, row, lane, p, keep);
     const float sc = 1.f / (1.f - p);
 #pragma unroll
     for (int i = 0; i < VEC; ++i) o[i] = keep[i] ? o[i] * sc : 0.f;
   }
-  RowIO<VEC>::store(out + row * D + col0, o);
+  RowIO<VEC>::store(out + row * D, lane, o);
   if (lane == 0) {
     mean_out[row] = mean;
     rstd_out[row] = rstd;
@@ -146,31 +183,30 @@ __global__ void __launch_bounds__(256) add_ln_fwd_kernel(
 // grid-stride over rows; block = 4 waves; partial dgamma/dbeta per block.
 // POST at compile time (the two dropout placements share no loop body) and <= 128 VGPRs
 // (4 waves per SIMD: the LDS reduction buffer allows 4 blocks per CU); D > 768 keeps
-// 6 x VEC live accumulator/row floats: 2 waves per SIMD up to D = 1536, 1 for D = 2048
-// (512 VGPRs) - no scratch spills at any width
+// 6 x VEC live accumulator/row floats: 4 waves per SIMD up to D = 768, 2-3 up to D = 1024.
+// D >= 1536 takes add_ln_bwd_rowblk_kernel (one row per block) instead.
 template <int VEC, bool POST>
-__global__ void __launch_bounds__(256, VEC <= 12 ? 4 : VEC <= 24 ? 2 : 1) add_ln_bwd_kernel(
+__global__ void __launch_bounds__(256, VEC <= 12 ? 4 : VEC <= 16 ? 2 : 1) add_ln_bwd_kernel(
     const bf16_t* __restrict__ dout, const bf16_t* __restrict__ hsave,
     const float* __restrict__ mean_in, const float* __restrict__ rstd_in,
     const bf16_t* __restrict__ gamma, bf16_t* __restrict__ dres, bf16_t* __restrict__ dy,
     float* __restrict__ dyb, float* __restrict__ part_dg, float* __restrict__ part_db, int64_t R,
     float p, uint32_t seed, uint32_t offset, const bf16_t* __restrict__ dh_in, float* __restrict__ part) {
   constexpr int D = VEC * 64;
-  __shared__ float red[4][D];  // reused for dgamma, dbeta, dyb in turn (D = 2048: 32 KiB)
+  __shared__ float red[4][D];  // reused for dgamma, dbeta, dyb in turn
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  const int col0 = lane * VEC;
   float g[VEC], adg[VEC], adb[VEC], ady[VEC];
-  RowIO<VEC>::load(gamma + col0, g);
+  RowIO<VEC>::load(gamma, lane, g);
 #pragma unroll
   for (int i = 0; i < VEC; ++i) { adg[i] = 0.f; adb[i] = 0.f; ady[i] = 0.f; }
   const float sc = p > 0.f ? 1.f / (1.f - p) : 1.f;
   for (int64_t row = (int64_t)blockIdx.x * 4 + w; row < R; row += (int64_t)gridDim.x * 4) {
     float h[VEC], d[VEC];
-    RowIO<VEC>::load(hsave + row * D + col0, h);
-    RowIO<VEC>::load(dout + row * D + col0, d);
+    RowIO<VEC>::load(hsave + row * D, lane, h);
+    RowIO<VEC>::load(dout + row * D, lane, d);
     if (POST && p > 0.f) {
       bool keep[VEC];
-      dropout_keep<VEC>(seed, offset, row, col0, p, keep);
+      dropout_keep<VEC>(seed, offset, row, lane, p, keep);
 #pragma unroll
       for (int i = 0; i < VEC; ++i) d[i] = keep[i] ? d[i] * sc : 0.f;
     }
@@ -193,19 +229,19 @@ __global__ void __launch_bounds__(256, VEC <= 12 ? 4 : VEC <= 24 ? 2 : 1) add_ln
     for (int i = 0; i < VEC; ++i) d[i] = rstd * (d[i] - s1 - h[i] * s2);
     if (dh_in) {
       float e[VEC];
-      RowIO<VEC>::load(dh_in + row * D + col0, e);
+      RowIO<VEC>::load(dh_in + row * D, lane, e);
 #pragma unroll
       for (int i = 0; i < VEC; ++i) d[i] += e[i];
     }
-    if (dres) RowIO<VEC>::store(dres + row * D + col0, d);
+    if (dres) RowIO<VEC>::store(dres + row * D, lane, d);
     if (dy) {
       if (!POST && p > 0.f) {
         bool keep[VEC];
-        dropout_keep<VEC>(seed, offset, row, col0, p, keep);
+        dropout_keep<VEC>(seed, offset, row, lane, p, keep);
 #pragma unroll
         for (int i = 0; i < VEC; ++i) d[i] = keep[i] ? d[i] * sc : 0.f;
       }
-      RowIO<VEC>::store(dy + row * D + col0, d);
+      RowIO<VEC>::store(dy + row * D, lane, d);
       if (dyb) {
         // bias gradient of the layer that produced y: column sums of the bf16 dy
 #pragma unroll
@@ -222,7 +258,7 @@ __global__ void __launch_bounds__(256, VEC <= 12 ? 4 : VEC <= 24 ? 2 : 1) add_ln
     if (a == 2 && !dyb) break;
     if (a) __syncthreads();  // previous accumulator's columns have been read
 #pragma unroll
-    for (int i = 0; i < VEC; ++i) red[w][col0 + i] = a == 0 ? adg[i] : a == 1 ? adb[i] : ady[i];
+    for (int i = 0; i < VEC; ++i) red[w][RowMap<VEC>::col(lane, i)] = a == 0 ? adg[i] : a == 1 ? adb[i] : ady[i];
     __syncthreads();
     if (part) {
       float* pr = part + ((int64_t)blockIdx.x * 3 + a) * D;
@@ -231,6 +267,152 @@ __global__ void __launch_bounds__(256, VEC <= 12 ? 4 : VEC <= 24 ? 2 : 1) add_ln
       for (int c = threadIdx.x; c < D; c += blockDim.x)
         atomicAdd(dst[a] + c, red[0][c] + red[1][c] + red[2][c] + red[3][c]);
     }
+  }
+}
+
+// Wide rows (D = 1536, 2048): one row per 256-thread block, VT = D / 256 elements per thread in
+// groups of CH interleaved over the threads (a load instruction covers 256 CH contiguous
+// elements).  A thread owns the same VT columns for every row, so its column accumulators are
+// 3 VT registers (24 at D = 2048, vs 96 for the wave-per-row kernel, which held D = 2048 at 256
+// VGPRs - one wave per SIMD), and the block's column sums need no cross-wave reduction.  The two
+// row sums cross the 4 waves through LDS (double-buffered by row parity: one barrier per row).
+// Column sums always two-stage: part[block][3][D].
+template <int D, bool POST>
+__global__ void __launch_bounds__(256) add_ln_bwd_rowblk_kernel(
+    const bf16_t* __restrict__ dout, const bf16_t* __restrict__ hsave,
+    const float* __restrict__ mean_in, const float* __restrict__ rstd_in,
+    const bf16_t* __restrict__ gamma, bf16_t* __restrict__ dres, bf16_t* __restrict__ dy,
+    bool want_dyb, int64_t R, float p, uint32_t seed, uint32_t offset, const bf16_t* __restrict__ dh_in,
+    float* __restrict__ part) {
+  constexpr int VT = D / 256;
+  constexpr int CH = VT % 8 == 0 ? 8 : VT % 4 == 0 ? 4 : VT % 2 == 0 ? 2 : 1;
+  constexpr int NG = VT / CH;
+  static_assert(VT * 256 == D && CH % 2 == 0, "rowblk: D = 256 * even");
+  __shared__ float rsum[2][4][2];
+  const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+  auto col = [&](int i) { return (i / CH) * 256 * CH + t * CH + i % CH; };
+  auto ld = [&](const bf16_t* row, float* v) {
+#pragma unroll
+    for (int gi = 0; gi < NG; ++gi) {
+      const bf16_t* q = row + gi * 256 * CH + t * CH;
+      uint32_t wv[CH / 2];
+      if constexpr (CH == 8) {
+        const uint4 r = *reinterpret_cast<const uint4*>(q);
+        wv[0] = r.x; wv[1] = r.y; wv[2] = r.z; wv[3] = r.w;
+      } else if constexpr (CH == 4) {
+        const uint2 r = *reinterpret_cast<const uint2*>(q);
+        wv[0] = r.x; wv[1] = r.y;
+      } else {
+        wv[0] = *reinterpret_cast<const uint32_t*>(q);
+      }
+#pragma unroll
+      for (int k = 0; k < CH / 2; ++k) {
+        v[gi * CH + 2 * k] = __uint_as_float(wv[k] << 16);
+        v[gi * CH + 2 * k + 1] = __uint_as_float(wv[k] & 0xffff0000u);
+      }
+    }
+  };
+  auto st = [&](bf16_t* row, const float* v) {
+#pragma unroll
+    for (int gi = 0; gi < NG; ++gi) {
+      bf16_t* q = row + gi * 256 * CH + t * CH;
+      const float* o = v + gi * CH;
+      if constexpr (CH == 8) {
+        *reinterpret_cast<uint4*>(q) = make_uint4(pack_bf2(o[0], o[1]), pack_bf2(o[2], o[3]),
+                                                  pack_bf2(o[4], o[5]), pack_bf2(o[6], o[7]));
+      } else if constexpr (CH == 4) {
+        *reinterpret_cast<uint2*>(q) = make_uint2(pack_bf2(o[0], o[1]), pack_bf2(o[2], o[3]));
+      } else {
+        *reinterpret_cast<uint32_t*>(q) = pack_bf2(o[0], o[1]);
+      }
+    }
+  };
+  // same (row, col) -> Philox word map as dropout_keep
+  auto keep_mask = [&](int64_t row, bool* keep) {
+    const uint32_t thr = (uint32_t)(p * 4294967296.0);
+#pragma unroll
+    for (int i = 0; i < VT; i += 2) {
+      const int c = col(i);  // pairs never straddle a 4-column Philox block (c even)
+      uint32_t r[4];
+      if (CH >= 4 && (i % 4) != 0) continue;
+      philox4(seed, 0x5bd1e995u, (uint32_t)row, (uint32_t)(row >> 32) ^ (uint32_t)(c >> 2), offset,
+              0xdeadbeefu, r);
+      if constexpr (CH >= 4) {
+#pragma unroll
+        for (int k = 0; k < 4; ++k) keep[i + k] = r[k] >= thr;
+      } else {
+        keep[i] = r[c & 3] >= thr;
+        keep[i + 1] = r[(c & 3) + 1] >= thr;
+      }
+    }
+  };
+  float g[VT], adg[VT], adb[VT], ady[VT];
+  ld(gamma, g);
+#pragma unroll
+  for (int i = 0; i < VT; ++i) { adg[i] = 0.f; adb[i] = 0.f; ady[i] = 0.f; }
+  const float sc = p > 0.f ? 1.f / (1.f - p) : 1.f;
+  int par = 0;
+  for (int64_t row = blockIdx.x; row < R; row += gridDim.x, par ^= 1) {
+    float h[VT], d[VT];
+    ld(hsave + row * D, h);
+    ld(dout + row * D, d);
+    if (POST && p > 0.f) {
+      bool keep[VT];
+      keep_mask(row, keep);
+#pragma unroll
+      for (int i = 0; i < VT; ++i) d[i] = keep[i] ? d[i] * sc : 0.f;
+    }
+    const float mean = mean_in[row], rstd = rstd_in[row];
+    float s1 = 0.f, s2 = 0.f;
+#pragma unroll
+    for (int i = 0; i < VT; ++i) {
+      const float xh = (h[i] - mean) * rstd;
+      adg[i] += d[i] * xh;
+      adb[i] += d[i];
+      const float gx = d[i] * g[i];
+      h[i] = xh;
+      d[i] = gx;
+      s1 += gx;
+      s2 += gx * xh;
+    }
+    s1 = wave_sum(s1);
+    s2 = wave_sum(s2);
+    if (lane == 0) {
+      rsum[par][w][0] = s1;
+      rsum[par][w][1] = s2;
+    }
+    __syncthreads();  // the other parity's slots were read before this barrier (previous row)
+    s1 = (rsum[par][0][0] + rsum[par][1][0] + rsum[par][2][0] + rsum[par][3][0]) * (1.f / D);
+    s2 = (rsum[par][0][1] + rsum[par][1][1] + rsum[par][2][1] + rsum[par][3][1]) * (1.f / D);
+#pragma unroll
+    for (int i = 0; i < VT; ++i) d[i] = rstd * (d[i] - s1 - h[i] * s2);
+    if (dh_in) {
+      float e[VT];
+      ld(dh_in + row * D, e);
+#pragma unroll
+      for (int i = 0; i < VT; ++i) d[i] += e[i];
+    }
+    if (dres) st(dres + row * D, d);
+    if (dy) {
+      if (!POST && p > 0.f) {
+        bool keep[VT];
+        keep_mask(row, keep);
+#pragma unroll
+        for (int i = 0; i < VT; ++i) d[i] = keep[i] ? d[i] * sc : 0.f;
+      }
+      st(dy + row * D, d);
+      if (want_dyb) {
+#pragma unroll
+        for (int i = 0; i < VT; ++i) ady[i] += bf2f(f2bf(d[i]));
+      }
+    }
+  }
+  float* pr = part + (int64_t)blockIdx.x * 3 * D;
+#pragma unroll
+  for (int i = 0; i < VT; ++i) {
+    pr[col(i)] = adg[i];
+    pr[D + col(i)] = adb[i];
+    if (want_dyb) pr[2 * D + col(i)] = ady[i];
   }
 }
 
@@ -303,11 +485,15 @@ int ln_bwd_blocks(int64_t R) {
 // stored as partials (9.4 MB at 8192 x 768, plain 16-byte stores) and reduced by a second
 // kernel - more blocks would otherwise cost one fp32 atomic per column per block.
 constexpr int64_t LN_SMALL_R = 65536;
-int64_t ln_bwd_ws_floats(int64_t R, int D) {
-  if (R > LN_SMALL_R) return 0;
-  const int64_t nb = (R + 7) / 8;
-  return nb * 3 * D;
+// wide rows (D >= 1536, add_ln_bwd_rowblk_kernel): always two-stage, up to 1024 blocks (the
+// partials are 3 x D floats per block; the second stage reads them once)
+constexpr int LN_WIDE_D = 1536;
+static int64_t ln_bwd_two_stage_blocks(int64_t R, int D) {
+  if (D >= LN_WIDE_D) return R < 1024 ? R : 1024;  // add_ln_bwd_rowblk_kernel: one row per block at a time
+  if (R <= LN_SMALL_R) return (R + 7) / 8;
+  return 0;
 }
+int64_t ln_bwd_ws_floats(int64_t R, int D) { return ln_bwd_two_stage_blocks(R, D) * 3 * D; }
 
 template <int VEC>
 static void ln_bwd_impl(const uint16_t* dout, const uint16_t* hsave, const float* mean,
@@ -316,8 +502,9 @@ static void ln_bwd_impl(const uint16_t* dout, const uint16_t* hsave, const float
                         uint32_t off, const uint16_t* dh_in, bool post, int zero_mask, hipStream_t s,
                         float* ws) {
   constexpr int D = VEC * 64;
-  const bool two_stage = ws != nullptr && R <= LN_SMALL_R;
-  const int nb = two_stage ? (int)((R + 7) / 8) : ln_bwd_blocks(R);
+  const int64_t nb2 = ln_bwd_two_stage_blocks(R, D);
+  const bool two_stage = ws != nullptr && nb2 > 0;
+  const int nb = two_stage ? (int)nb2 : ln_bwd_blocks(R);
   // zero the accumulators that are scratch (zero_mask bits: 1 dg, 2 db, 4 dyb); the others
   // are parameter .grad buffers the kernel accumulates onto.  One memset when the scratch
   // ones are consecutive rows of one buffer (the binding allocates them so).
@@ -330,6 +517,23 @@ static void ln_bwd_impl(const uint16_t* dout, const uint16_t* hsave, const float
     if (zy) (void)hipMemsetAsync(dyb, 0, sizeof(float) * D, s);
   }
   float* part = two_stage ? ws : nullptr;
+  if constexpr (D >= LN_WIDE_D) {
+    if (two_stage) {
+      const bool wy = dy != nullptr && dyb != nullptr;
+      if (post)
+        hipLaunchKernelGGL((add_ln_bwd_rowblk_kernel<D, true>), dim3(nb), dim3(256), 0, s, (const bf16_t*)dout,
+                           (const bf16_t*)hsave, mean, rstd, (const bf16_t*)g, (bf16_t*)dres, (bf16_t*)dy, wy, R,
+                           p, seed, off, (const bf16_t*)dh_in, part);
+      else
+        hipLaunchKernelGGL((add_ln_bwd_rowblk_kernel<D, false>), dim3(nb), dim3(256), 0, s, (const bf16_t*)dout,
+                           (const bf16_t*)hsave, mean, rstd, (const bf16_t*)g, (bf16_t*)dres, (bf16_t*)dy, wy, R,
+                           p, seed, off, (const bf16_t*)dh_in, part);
+      const int nseg = nb >= 256 ? 16 : nb >= 32 ? 4 : 1;
+      hipLaunchKernelGGL(ln_colreduce_kernel, dim3(D / 64, wy ? 3 : 2, nseg), dim3(256), 0, s, part, nb, D, dg,
+                         db, wy ? dyb : nullptr, 3);
+      return;
+    }
+  }
   if (post)
     hipLaunchKernelGGL((add_ln_bwd_kernel<VEC, true>), dim3(nb), dim3(256), 0, s, (const bf16_t*)dout,
                        (const bf16_t*)hsave, mean, rstd, (const bf16_t*)g, (bf16_t*)dres, (bf16_t*)dy,

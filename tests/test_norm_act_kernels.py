@@ -12,7 +12,8 @@ def _ext():
     return get_ext(required=True)
 
 
-@pytest.mark.parametrize("R,D,res", [(1000, 768, True), (37, 128, False), (4096, 2048, True), (64, 64, True)])
+@pytest.mark.parametrize("R,D,res", [(1000, 768, True), (37, 128, False), (4096, 2048, True), (64, 64, True),
+                                     (70000, 2048, True), (3000, 1536, False), (70000, 768, True)])
 def test_add_ln_no_dropout(R, D, res):
     torch.manual_seed(0)
     y = torch.randn(R, D, device="cuda").bfloat16()
@@ -38,9 +39,10 @@ def test_add_ln_no_dropout(R, D, res):
     torch.testing.assert_close(db, bf.grad, rtol=1e-2, atol=1e-2 * bf.grad.abs().max().item())
 
 
-def test_add_ln_dropout_statistics_and_consistency():
+@pytest.mark.parametrize("R,D", [(2048, 768), (2048, 2048), (70000, 2048), (512, 128)])
+def test_add_ln_dropout_statistics_and_consistency(R, D):
     torch.manual_seed(0)
-    R, D, p = 2048, 768, 0.1
+    p = 0.1
     y = torch.ones(R, D, device="cuda").bfloat16()
     g = torch.ones(D, device="cuda").bfloat16()
     b = torch.zeros(D, device="cuda").bfloat16()

@@ -575,8 +575,14 @@ class TrainLoop:
 
     # ---- overlapped micro-batch schedule (several executed chunks per step) ----------
     def _overlap_ok(self, nchunks):
+        # only tile-starved chunks gain from a second stream: at <= 64K tokens a 768-wide GEMM
+        # has <= 768 output tiles (3 rounds of 256 CUs); larger chunks (DiffuSeq-XL's 1024-sample
+        # chunks) fill the chip alone, and overlapping two of them doubles the live activations
+        # (DPA_OVERLAP_MAX_TOKENS overrides)
+        toks = self.exec_microbatch * (self._tokens_per_sample or 1)
+        max_toks = int(os.environ.get("DPA_OVERLAP_MAX_TOKENS", "65536"))
         return (nchunks > 1 and self.overlap_microbatches and not self._probing
-                and self.engine_kind == "native" and self.device.type == "cuda")
+                and self.engine_kind == "native" and self.device.type == "cuda" and toks <= max_toks)
 
     def _chunk_state(self):
         """Per-chunk hook state (``_last_*`` attributes set by compute_losses and read by
