@@ -869,6 +869,7 @@ bool launch_attn_fwd(const uint16_t* qkv, uint16_t* out, float* lse, int B, int 
     return attn128_supports(L, D, causal) &&
            launch_attn128_fwd(qkv, out, lse, B, L, H, p, causal, seed, offset, s, true);
   if (D == 128) {
+    if (launch_attn128_fwd_d128(qkv, out, lse, B, L, H, p, causal, seed, offset, s)) return true;
     attn_fwd_general<128>(qkv, out, lse, B, L, H, p, causal, seed, offset, s);
     return true;
   }

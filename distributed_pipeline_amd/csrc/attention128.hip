@@ -287,13 +287,19 @@ __global__ void __launch_bounds__(256, 2) attn128_fwd_kernel(const bf16_t* __res
     f32x16 o[2];
     o[0] = zero16();
     o[1] = zero16();
+    const float fk = dc.on ? inv_l * dc.scale : inv_l;
 #pragma unroll
     for (int t = 0; t < 4; ++t) {
+      if (dc.on) {
+        // one hash per key pair (registers 2j, 2j + 1 are keys 2m, 2m + 1), as one batch
+        uint32_t hh[8];
 #pragma unroll
-      for (int i = 0; i < 16; ++i) {
-        float pr = acc[t][i] * inv_l;
-        if (dc.on) pr = keep_bit(dc, q, t * 32 + acc_row(i, hf)) ? pr * dc.scale : 0.f;
-        acc[t][i] = pr;
+        for (int j = 0; j < 8; ++j) hh[j] = drop_hash(dc, q, t * 32 + acc_row(2 * j, hf));
+#pragma unroll
+        for (int i = 0; i < 16; ++i) acc[t][i] = keep_from(dc, hh[i >> 1], i & 1) ? acc[t][i] * fk : 0.f;
+      } else {
+#pragma unroll
+        for (int i = 0; i < 16; ++i) acc[t][i] *= fk;
       }
 #pragma unroll
       for (int s = 0; s < 2; ++s) {
@@ -668,6 +674,172 @@ __global__ void __launch_bounds__(256, 2) attn128_bwd_kernel(
   }
 }
 
+// ============================================================================
+// forward, head_dim 128 (DiffuSeq-XL: 2048 / 16 heads), token-major qkv
+// ============================================================================
+// Same item stream as attn128_fwd_kernel, with [128][128] K / V images (256-B rows, the
+// swz_x256 chunk XOR: conflict-free for both the row-form ds_read_b128 S^T operand and the
+// transposed V reads).  Two stages of 64 KiB fill the LDS, so ONE workgroup per CU (4 waves,
+// up to 512 registers each): the next item's K / V DMA and Q loads are always in flight
+// while this item computes; at ~8.4 MFLOP per 128 KiB of traffic the kernel is HBM-bound.
+// Dropout / LSE / output conventions are those of the general kernels in attention.hip,
+// whose backward it pairs with.
+constexpr int HD2 = 128;
+constexpr int IMG2 = L * HD2 * 2;  // 32 KiB
+constexpr float ATT_C2 = 1.4426950408889634f * 0.08838834764831845f;  // log2(e) / sqrt(128)
+
+__device__ __forceinline__ uint32_t off2(int row, int ch) {
+  return (uint32_t)(row * 256 + ((ch ^ (((row & 3) << 2) | ((row >> 2) & 3))) << 4));
+}
+// Row-form fragment of a [128][128] image: rows r0 + (lane & 31), k = 16s + 8h + j (s < 8)
+__device__ __forceinline__ bf16x8 frag_r2(uint32_t img, int r0, int s, int lane) {
+  return rd128(img + off2(r0 + (lane & 31), 2 * s + (lane >> 5)));
+}
+// Transposed read, permuted k order (accumulator operand): rows r0 + 4h + q and r0 + 8 + 4h + q
+__device__ __forceinline__ bf16x8 frag_tp2(uint32_t img, int r0, int col0, int lane) {
+  const int g = lane >> 4, li = lane & 15, q = li >> 2, p = li & 3, h = lane >> 5;
+  const int col = col0 + 16 * (g & 1) + 4 * p;
+  const int ra = r0 + 4 * h + q;
+  return cat44(rdtr(img + off2(ra, col >> 3) + (col & 7) * 2),
+               rdtr(img + off2(ra + 8, col >> 3) + (col & 7) * 2));
+}
+// DMA a [128 rows][128] bf16 tile (row stride ld elements): 32 pieces of 4 rows, wave w issues 8w..8w+7
+__device__ __forceinline__ void dma_img2(char* img, const bf16_t* src, int64_t ld, int w, int lane) {
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    const int pc = w * 8 + i;
+    const int row = pc * 4 + (lane >> 4), phys = lane & 15;
+    const bf16_t* g = src + (int64_t)row * ld + ((phys ^ (((row & 3) << 2) | ((row >> 2) & 3))) << 3);
+    __builtin_amdgcn_global_load_lds((glob_void*)g, (lds_void*)(img + pc * 1024), 16, 0, 0);
+  }
+}
+
+__global__ void __launch_bounds__(256, 1) attn128_fwd_d128_kernel(const bf16_t* __restrict__ qkv,
+                                                                 bf16_t* __restrict__ out,
+                                                                 float* __restrict__ lse, int B, int H,
+                                                                 float p, uint32_t seed, uint32_t offset) {
+  __shared__ __attribute__((aligned(1024))) char smem[2 * 2 * IMG2];
+  const int w = threadIdx.x >> 6;
+  const int nitems = B * H;
+  const int64_t ld = 3LL * H * HD2, ldo = (int64_t)H * HD2, sb = 3LL * H * L * HD2;
+  const uint32_t sbase = lds_u32(smem);
+  const int tid = threadIdx.x, lane = tid & 63, hf = lane >> 5;
+
+  bf16x8 qpf[8];
+  auto issue = [&](int item, int stg) {
+    const int b = item / H, hd = item - b * H;
+    const bf16_t* qb = qkv + (int64_t)b * sb + (int64_t)hd * HD2;
+    char* base = smem + stg * 2 * IMG2;
+    dma_img2(base, qb + (int64_t)H * HD2, ld, w, lane);
+    dma_img2(base + IMG2, qb + 2LL * H * HD2, ld, w, lane);
+    const bf16_t* qrow = qb + (int64_t)(w * 32 + (lane & 31)) * ld;
+#pragma unroll
+    for (int s = 0; s < 8; ++s) qpf[s] = ld_frag(qrow + 16 * s + 8 * hf);
+  };
+
+  const int G = gridDim.x;
+  int item = blockIdx.x;
+  if (item < nitems) issue(item, 0);
+  for (int k = 0; item < nitems; ++k, item += G) {
+    const int cur = k & 1;
+    // this item's K/V DMA and Q loads landed; only the previous item's 9 stores (lse + 8 O
+    // chunks) were issued after them (in-order retire)
+    if (k == 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    else asm volatile("s_waitcnt vmcnt(9)" ::: "memory");
+    barrier();
+    bf16x8 qf[8];
+#pragma unroll
+    for (int s = 0; s < 8; ++s) qf[s] = qpf[s];
+    if (item + G < nitems) issue(item + G, cur ^ 1);
+    const uint32_t ki = sbase + cur * 2 * IMG2, vi = ki + IMG2;
+    const int b = item / H, hd = item - b * H;
+    const DropCfg dc = make_drop(p, seed, offset, (uint32_t)item);
+    const int q = w * 32 + (lane & 31);
+
+    // S^T (keys in registers, query on the lane)
+    f32x16 acc[4];
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+      acc[t] = zero16();
+#pragma unroll
+      for (int hs = 0; hs < 2; ++hs) {
+        bf16x8 kf[4];
+#pragma unroll
+        for (int s = 0; s < 4; ++s) kf[s] = frag_r2(ki, t * 32, 4 * hs + s, lane);
+        lgkm0();
+#pragma unroll
+        for (int s = 0; s < 4; ++s) acc[t] = mfma32(kf[s], qf[4 * hs + s], acc[t]);
+      }
+    }
+    float m = -INFINITY;
+#pragma unroll
+    for (int t = 0; t < 4; ++t)
+#pragma unroll
+      for (int i = 0; i < 16; ++i) {
+        acc[t][i] *= ATT_C2;
+        m = fmaxf(m, acc[t][i]);
+      }
+    m = fmaxf(m, __shfl_xor(m, 32, 64));
+    float l = 0.f;
+#pragma unroll
+    for (int t = 0; t < 4; ++t)
+#pragma unroll
+      for (int i = 0; i < 16; ++i) {
+        const float e = fexp2(acc[t][i] - m);
+        acc[t][i] = e;
+        l += e;
+      }
+    l += __shfl_xor(l, 32, 64);
+    const float inv_l = 1.f / l;
+    const float fk = dc.on ? inv_l * dc.scale : inv_l;
+    f32x16 o[4];
+#pragma unroll
+    for (int dt = 0; dt < 4; ++dt) o[dt] = zero16();
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+      if (dc.on) {
+        uint32_t hh[8];  // one hash per key pair, as a batch
+#pragma unroll
+        for (int j = 0; j < 8; ++j) hh[j] = drop_hash(dc, q, t * 32 + acc_row(2 * j, hf));
+#pragma unroll
+        for (int i = 0; i < 16; ++i) acc[t][i] = keep_from(dc, hh[i >> 1], i & 1) ? acc[t][i] * fk : 0.f;
+      } else {
+#pragma unroll
+        for (int i = 0; i < 16; ++i) acc[t][i] *= fk;
+      }
+#pragma unroll
+      for (int s = 0; s < 2; ++s) {
+        const bf16x8 af = acc_to_frag(acc[t], s);
+        bf16x8 vf[4];
+#pragma unroll
+        for (int dt = 0; dt < 4; ++dt) vf[dt] = frag_tp2(vi, t * 32 + 16 * s, dt * 32, lane);
+        lgkm0();
+#pragma unroll
+        for (int dt = 0; dt < 4; ++dt) o[dt] = mfma32(af, vf[dt], o[dt]);
+      }
+    }
+    if (hf == 0) lse[(int64_t)item * L + q] = (m + log2f(l)) * LN2f;
+    // stage O (rows = queries) in the K image (dead: every wave passed its S^T)
+    barrier();
+#pragma unroll
+    for (int dt = 0; dt < 4; ++dt)
+#pragma unroll
+      for (int i = 0; i < 16; ++i) {
+        const int row = w * 32 + acc_row(i, hf), col = dt * 32 + (lane & 31);
+        wr_b16(ki + off2(row, col >> 3) + (col & 7) * 2, f2bf(o[dt][i]));
+      }
+    barrier();
+    bf16_t* ob = out + (int64_t)b * L * ldo + (int64_t)hd * HD2;
+#pragma unroll
+    for (int c = 0; c < 8; ++c) {
+      const int idx = tid + c * 256, row = idx >> 4, ch = idx & 15;
+      const bf16x8 v = rd128(ki + off2(row, ch));
+      lgkm0();
+      *reinterpret_cast<bf16x8*>(ob + (int64_t)row * ldo + ch * 8) = v;
+    }
+  }
+}
+
 // db[q*H*64 + h*64 + d] += sum_b colpart[(b*H + h)*192 + q*64 + d]: grid (H*3, chunks of B)
 __global__ void __launch_bounds__(256) colpart_reduce_kernel(const float* __restrict__ colpart,
                                                              float* __restrict__ db, int B, int H,
@@ -716,6 +888,18 @@ bool launch_attn128_fwd(const uint16_t* qkv, uint16_t* out, float* lse, int B, i
 }
 
 bool attn128_supports(int L, int D, bool causal) { return L == a128::L && D == a128::HD && !causal; }
+
+// L = 128, head_dim 128, bidirectional, token-major (DiffuSeq-XL): persistent forward, one
+// workgroup per CU; paired with the general backward kernels (same dropout / LSE conventions)
+bool launch_attn128_fwd_d128(const uint16_t* qkv, uint16_t* out, float* lse, int B, int Lq, int H,
+                             float p, bool causal, uint32_t seed, uint32_t offset, hipStream_t s) {
+  if (Lq != a128::L || causal || !a128::enabled()) return false;
+  const int items = B * H, slots = a128::num_cus();
+  const int grid = items < slots ? items : slots;
+  hipLaunchKernelGGL(a128::attn128_fwd_d128_kernel, dim3(grid), dim3(256), 0, s, (const bf16_t*)qkv,
+                     (bf16_t*)out, lse, B, H, p, seed, offset);
+  return true;
+}
 
 bool launch_attn128_bwd(const uint16_t* qkv, const uint16_t* out, const uint16_t* dout,
                         const float* lse, uint16_t* dqkv, float* colpart, float* dbias, int B,

@@ -54,11 +54,13 @@ def test_attention_no_dropout(B, L, H, causal):
         torch.testing.assert_close(a, r, rtol=3e-2, atol=3e-2 * r.abs().max().item(), msg=name)
 
 
-def test_attention_dropout_consistent_with_mask():
-    """Dropout: recover the mask from a V = one-hot probe and check fwd/bwd against it."""
+@pytest.mark.parametrize("D", [64, 128])
+def test_attention_dropout_consistent_with_mask(D):
+    """Dropout: recover the mask from a V = one-hot probe and check fwd/bwd against it.  D = 128
+    pairs the persistent L = 128 forward (attention128.hip) with the general backward kernels."""
     torch.manual_seed(0)
     B, L, H, p = 2, 128, 2, 0.1
-    qkv = (torch.randn(B, L, 3 * H * 64, device="cuda") * 0.5).bfloat16()
+    qkv = (torch.randn(B, L, 3 * H * D, device="cuda") * 0.5).bfloat16()
     out, lse = _ext().attn_fwd(qkv, H, p, False, 11, 5)
     # Deterministic for equal (seed, offset); differs for another offset
     out2, _ = _ext().attn_fwd(qkv, H, p, False, 11, 5)
@@ -66,17 +68,18 @@ def test_attention_dropout_consistent_with_mask():
     assert torch.equal(out, out2) and not torch.equal(out, out3)
     # probe keep mask: set V rows to identity blocks so O reveals P_drop columns
     keep = torch.zeros(B, H, L, L, device="cuda")
-    for blk in range(L // 64):
-        probe = qkv.clone().view(B, L, 3, H, 64)
+    for blk in range(L // D):
+        probe = qkv.clone().view(B, L, 3, H, D)
         probe[:, :, 2] = 0
-        idx = torch.arange(64, device="cuda")
-        probe[:, blk * 64 + idx, 2, :, idx] = 1.0
+        idx = torch.arange(D, device="cuda")
+        probe[:, blk * D + idx, 2, :, idx] = 1.0
         o, _ = _ext().attn_fwd(probe.view(B, L, -1).contiguous(), H, p, False, 11, 5)
-        keep[..., blk * 64:(blk + 1) * 64] = (o.view(B, L, H, 64).permute(0, 2, 1, 3).float() != 0).float()
+        keep[..., blk * D:(blk + 1) * D] = (o.view(B, L, H, D).permute(0, 2, 1, 3).float() != 0).float()
     frac = keep.mean().item()
     assert abs(frac - (1 - p)) < 0.02
     x = qkv.float().requires_grad_(True)
-    ref_o, _ = _ref(x, H, False, keep, p)
+    ref_o, ref_lse = _ref(x, H, False, keep, p)
+    torch.testing.assert_close(lse, ref_lse, rtol=1e-3, atol=1e-2)
     torch.testing.assert_close(out.float(), ref_o, rtol=3e-2, atol=3e-2)
     dout = torch.randn_like(ref_o)
     ref_o.backward(dout)
@@ -86,7 +89,8 @@ def test_attention_dropout_consistent_with_mask():
 
 @pytest.mark.parametrize("B,L,H,causal", [(2, 128, 4, False), (2, 256, 2, False), (2, 192, 2, True),
                                             (4, 256, 2, True),
-                                            (1, 512, 2, True)])
+                                            (1, 512, 2, True),
+                                            (160, 128, 2, False)])  # > #CUs items: persistent L=128 loop
 def test_attention_head_dim_128(B, L, H, causal):
     """DiffuSeq-XL heads (2048 / 16 = 128): the general two-pass kernels templated on D."""
     torch.manual_seed(1)
