@@ -921,7 +921,8 @@ bool launch_attn_bwd(const uint16_t* qkv, const uint16_t* out, const uint16_t* d
     return launch_attn128_bwd(qkv, out, dout, lse, dqkv, colpart, dbias, B, L, H, p, causal, seed, offset, s,
                               true, db_accumulate) && dbias != nullptr;
   if (D == 128) {
-    attn_bwd_general<128>(qkv, out, dout, lse, delta, dqkv, B, L, H, p, causal, seed, offset, s);
+    if (!launch_attn128_bwd_d128(qkv, out, dout, lse, delta, dqkv, B, L, H, p, causal, seed, offset, s))
+      attn_bwd_general<128>(qkv, out, dout, lse, delta, dqkv, B, L, H, p, causal, seed, offset, s);
     return false;
   }
   if (launch_attn128_bwd(qkv, out, dout, lse, dqkv, colpart, dbias, B, L, H, p, causal, seed, offset,

@@ -704,12 +704,14 @@ __device__ __forceinline__ bf16x8 frag_tp2(uint32_t img, int r0, int col0, int l
                rdtr(img + off2(ra + 8, col >> 3) + (col & 7) * 2));
 }
 // DMA a [128 rows][128] bf16 tile (row stride ld elements): 32 pieces of 4 rows, wave w issues 8w..8w+7
-__device__ __forceinline__ void dma_img2(char* img, const bf16_t* src, int64_t ld, int w, int lane) {
+// (32-bit row offsets: 128 rows x ld < 2^31 elements; 64-bit products were hoisted out of the
+// item loop and spilled)
+__device__ __forceinline__ void dma_img2(char* img, const bf16_t* src, int ld, int w, int lane) {
 #pragma unroll
   for (int i = 0; i < 8; ++i) {
     const int pc = w * 8 + i;
     const int row = pc * 4 + (lane >> 4), phys = lane & 15;
-    const bf16_t* g = src + (int64_t)row * ld + ((phys ^ (((row & 3) << 2) | ((row >> 2) & 3))) << 3);
+    const bf16_t* g = src + (row * ld + ((phys ^ (((row & 3) << 2) | ((row >> 2) & 3))) << 3));
     __builtin_amdgcn_global_load_lds((glob_void*)g, (lds_void*)(img + pc * 1024), 16, 0, 0);
   }
 }
@@ -730,8 +732,8 @@ __global__ void __launch_bounds__(256, 1) attn128_fwd_d128_kernel(const bf16_t* 
     const int b = item / H, hd = item - b * H;
     const bf16_t* qb = qkv + (int64_t)b * sb + (int64_t)hd * HD2;
     char* base = smem + stg * 2 * IMG2;
-    dma_img2(base, qb + (int64_t)H * HD2, ld, w, lane);
-    dma_img2(base + IMG2, qb + 2LL * H * HD2, ld, w, lane);
+    dma_img2(base, qb + (int64_t)H * HD2, (int)ld, w, lane);
+    dma_img2(base + IMG2, qb + 2LL * H * HD2, (int)ld, w, lane);
     const bf16_t* qrow = qb + (int64_t)(w * 32 + (lane & 31)) * ld;
 #pragma unroll
     for (int s = 0; s < 8; ++s) qpf[s] = ld_frag(qrow + 16 * s + 8 * hf);
@@ -840,6 +842,307 @@ __global__ void __launch_bounds__(256, 1) attn128_fwd_d128_kernel(const bf16_t* 
   }
 }
 
+// ============================================================================
+// backward, head_dim 128 (DiffuSeq-XL), token-major qkv / dqkv: two persistent kernels
+// ============================================================================
+// The computation of the general kernels (attention.hip attn_bwd_q_kernel, then
+// attn_bwd_kv_kernel; same dropout hashes, same delta hand-off), restructured for L = 128:
+// one workgroup per CU walks (b, h) items; the item's operand images for all 128 rows come
+// into one of two 64 KiB LDS stages by DMA while the previous item computes, and the next
+// item's register operands are loaded one item ahead.  Outputs are staged through the dead
+// stage image and written as 16-B row chunks (the general kernels store 2 B per lane).
+// wave-uniform vmcnt(N) for the counts used below
+__device__ __forceinline__ void wait_vm2(int n) {
+  switch (n) {
+    case 8: asm volatile("s_waitcnt vmcnt(8)" ::: "memory"); break;
+    case 16: asm volatile("s_waitcnt vmcnt(16)" ::: "memory"); break;
+    default: asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); break;
+  }
+}
+
+// dQ (and delta = rowsum(dO * O), published for the dK/dV kernel).  Wave w owns queries
+// 32w .. 32w + 31 (Q, dO fragments in registers); K, V images [128][128] per stage.
+__global__ void __launch_bounds__(256, 1) attn128_bwd_q_d128_kernel(
+    const bf16_t* __restrict__ qkv, const bf16_t* __restrict__ out, const bf16_t* __restrict__ dout,
+    const float* __restrict__ lse, float* __restrict__ delta, bf16_t* __restrict__ dqkv, int B, int H, float p,
+    uint32_t seed, uint32_t offset) {
+  __shared__ __attribute__((aligned(1024))) char smem[2 * 2 * IMG2];
+  const int w = threadIdx.x >> 6;
+  const int nitems = B * H;
+  const int64_t ld = 3LL * H * HD2, ldo = (int64_t)H * HD2, sb = 3LL * H * L * HD2;
+  const uint32_t sbase = lds_u32(smem);
+  const int tid = threadIdx.x, lane = tid & 63, hf = lane >> 5;
+  const int q = w * 32 + (lane & 31);
+
+  bf16x8 qn[8], dn[8], on[8];
+  auto issue = [&](int item, int stg) {
+    const int b = item / H, hd = item - b * H;
+    const bf16_t* qb = qkv + (int64_t)b * sb + (int64_t)hd * HD2;
+    char* base = smem + stg * 2 * IMG2;
+    dma_img2(base, qb + (int64_t)H * HD2, (int)ld, w, lane);
+    dma_img2(base + IMG2, qb + 2LL * H * HD2, (int)ld, w, lane);
+    const bf16_t* qrow = qb + (int64_t)q * ld;
+    const bf16_t* drow = dout + ((int64_t)b * L + q) * ldo + (int64_t)hd * HD2;
+    const bf16_t* orow = out + ((int64_t)b * L + q) * ldo + (int64_t)hd * HD2;
+#pragma unroll
+    for (int s = 0; s < 8; ++s) {
+      qn[s] = ld_frag(qrow + 16 * s + 8 * hf);
+      dn[s] = ld_frag(drow + 16 * s + 8 * hf);
+      on[s] = ld_frag(orow + 16 * s + 8 * hf);
+    }
+  };
+
+  const int G = gridDim.x;
+  int item = blockIdx.x;
+  if (item < nitems) issue(item, 0);
+  for (int k = 0; item < nitems; ++k, item += G) {
+    const int cur = k & 1;
+    // this item's DMA and register loads landed; only the previous item's 8 dq stores are younger
+    wait_vm2(k == 0 ? 0 : 8);
+    barrier();
+    bf16x8 qf[8], df[8];
+    float dlt = 0.f;
+#pragma unroll
+    for (int s = 0; s < 8; ++s) {
+      qf[s] = qn[s];
+      df[s] = dn[s];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) dlt += bf2f(df[s][j]) * bf2f(on[s][j]);
+    }
+    dlt += __shfl_xor(dlt, 32, 64);
+    if (item + G < nitems) issue(item + G, cur ^ 1);
+    const int b = item / H, hd = item - b * H;
+    const int64_t lrow = (int64_t)item * L;
+    if (hf == 0) delta[lrow + q] = dlt;
+    const float lse2 = lse[lrow + q] * 1.4426950408889634f;
+    const uint32_t ki = sbase + cur * 2 * IMG2, vi = ki + IMG2;
+    const DropCfg dc = make_drop(p, seed, offset, (uint32_t)item);
+    const uint32_t qterm = (uint32_t)q * 0x9E3779B1u;
+    f32x16 dq[4];
+#pragma unroll
+    for (int dt = 0; dt < 4; ++dt) dq[dt] = zero16();
+#pragma unroll 1
+    for (int t = 0; t < 4; ++t) {
+      f32x16 sacc = zero16(), dpacc = zero16();
+#pragma unroll
+      for (int hs = 0; hs < 2; ++hs) {
+        bf16x8 kf[4], vf[4];
+#pragma unroll
+        for (int s = 0; s < 4; ++s) {
+          kf[s] = frag_r2(ki, t * 32, 4 * hs + s, lane);
+          vf[s] = frag_r2(vi, t * 32, 4 * hs + s, lane);
+        }
+        lgkm0();
+#pragma unroll
+        for (int s = 0; s < 4; ++s) {
+          sacc = mfma32(kf[s], qf[4 * hs + s], sacc);
+          dpacc = mfma32(vf[s], df[4 * hs + s], dpacc);
+        }
+      }
+      uint32_t hh[8];
+      if (dc.on) {
+        const uint32_t kt0 = (uint32_t)((t * 32 + 4 * hf) >> 1) * 0x85EBCA77u;
+#pragma unroll
+        for (int j = 0; j < 8; ++j)
+          hh[j] = mix32(dc.seedmix ^ qterm ^ (kt0 + (uint32_t)(((2 * j & 3) + 8 * (j >> 1)) >> 1) * 0x85EBCA77u));
+      }
+#pragma unroll
+      for (int i = 0; i < 16; ++i) sacc[i] = fexp2(fmaf(sacc[i], ATT_C2, -lse2));
+#pragma unroll
+      for (int i = 0; i < 16; ++i) {
+        float dpd = dpacc[i];
+        if (dc.on) dpd = keep_from(dc, hh[i >> 1], i & 1) ? dpd * dc.scale : 0.f;
+        sacc[i] = sacc[i] * (dpd - dlt);
+      }
+#pragma unroll
+      for (int s = 0; s < 2; ++s) {
+        const bf16x8 sf = acc_to_frag(sacc, s);
+        bf16x8 kt[4];
+#pragma unroll
+        for (int dt = 0; dt < 4; ++dt) kt[dt] = frag_tp2(ki, t * 32 + 16 * s, dt * 32, lane);
+        lgkm0();
+#pragma unroll
+        for (int dt = 0; dt < 4; ++dt) dq[dt] = mfma32(sf, kt[dt], dq[dt]);
+      }
+    }
+    // stage dq (rows = queries, scaled by 1/sqrt(D)) in the K image, then 16-B row stores
+    barrier();
+#pragma unroll
+    for (int dt = 0; dt < 4; ++dt)
+#pragma unroll
+      for (int i = 0; i < 16; ++i) {
+        const int row = w * 32 + acc_row(i, hf), col = dt * 32 + (lane & 31);
+        wr_b16(ki + off2(row, col >> 3) + (col & 7) * 2, f2bf(dq[dt][i] * 0.08838834764831845f));
+      }
+    barrier();
+    bf16_t* db = dqkv + (int64_t)b * L * ld + (int64_t)hd * HD2;
+#pragma unroll
+    for (int c = 0; c < 8; ++c) {
+      const int idx = tid + c * 256, row = idx >> 4, ch = idx & 15;
+      const bf16x8 v = rd128(ki + off2(row, ch));
+      lgkm0();
+      *reinterpret_cast<bf16x8*>(db + (int64_t)row * ld + ch * 8) = v;
+    }
+  }
+}
+
+// dK, dV.  Wave w owns keys 32w .. 32w + 31 (K, V fragments in registers); Q, dO images
+// [128][128] plus the item's scaled LSE and delta per stage.
+__global__ void __launch_bounds__(256, 1) attn128_bwd_kv_d128_kernel(
+    const bf16_t* __restrict__ qkv, const bf16_t* __restrict__ dout, const float* __restrict__ lse,
+    const float* __restrict__ delta, bf16_t* __restrict__ dqkv, int B, int H, float p, uint32_t seed,
+    uint32_t offset) {
+  constexpr int STG = 2 * IMG2 + 1024;  // Q, dO images + lse[128] + delta[128]
+  __shared__ __attribute__((aligned(1024))) char smem[2 * STG];
+  const int w = threadIdx.x >> 6;
+  const int nitems = B * H;
+  const int64_t ld = 3LL * H * HD2, ldo = (int64_t)H * HD2, sb = 3LL * H * L * HD2;
+  const uint32_t sbase = lds_u32(smem);
+  const int tid = threadIdx.x, lane = tid & 63, hf = lane >> 5;
+  const int key = w * 32 + (lane & 31);
+
+  bf16x8 kf[8], vf[8];
+  // this wave's K / V rows of `item` into kf / vf (issued for the next item once the current
+  // item's last S / dP products have consumed them: no second register set)
+  auto load_kv = [&](int item) {
+    const int b = item / H, hd = item - b * H;
+    const bf16_t* krow = qkv + (int64_t)b * sb + (int64_t)hd * HD2 + (int64_t)key * ld + (int64_t)H * HD2;
+#pragma unroll
+    for (int s = 0; s < 8; ++s) {
+      kf[s] = ld_frag(krow + 16 * s + 8 * hf);
+      vf[s] = ld_frag(krow + (int64_t)H * HD2 + 16 * s + 8 * hf);
+    }
+  };
+  auto issue = [&](int item, int stg) {
+    const int b = item / H, hd = item - b * H;
+    const bf16_t* qb = qkv + (int64_t)b * sb + (int64_t)hd * HD2;
+    char* base = smem + stg * STG;
+    dma_img2(base, qb, (int)ld, w, lane);
+    dma_img2(base + IMG2, dout + (int64_t)b * L * ldo + (int64_t)hd * HD2, (int)ldo, w, lane);
+    // stats: wave 0/1 the LSE halves, wave 2/3 the delta halves (4 B per lane, one DMA each)
+    const float* st = (w < 2 ? lse : delta) + (int64_t)item * L + (w & 1) * 64 + lane;
+    __builtin_amdgcn_global_load_lds((glob_void*)st, (lds_void*)(base + 2 * IMG2 + w * 256), 4, 0, 0);
+  };
+
+  const int G = gridDim.x;
+  int item = blockIdx.x;
+  if (item < nitems) {
+    issue(item, 0);
+    load_kv(item);
+  }
+  for (int k = 0; item < nitems; ++k, item += G) {
+    const int cur = k & 1;
+    // this item's DMA (issued first) and K/V loads (issued after it) landed; only the previous
+    // item's 16 dk/dv stores are younger
+    wait_vm2(k == 0 ? 0 : 16);
+    barrier();
+    const bool has_next = item + G < nitems;
+    if (has_next) issue(item + G, cur ^ 1);
+    const int b = item / H, hd = item - b * H;
+    const uint32_t qi = sbase + cur * STG, doi = qi + IMG2, sti = qi + 2 * IMG2;
+    const DropCfg dc = make_drop(p, seed, offset, (uint32_t)item);
+    f32x16 dk[4], dv[4];
+#pragma unroll
+    for (int dt = 0; dt < 4; ++dt) { dk[dt] = zero16(); dv[dt] = zero16(); }
+    const int par = lane & 1;
+    const uint32_t kt = (uint32_t)(key >> 1) * 0x85EBCA77u;
+#pragma unroll 1
+    for (int qt = 0; qt < 4; ++qt) {
+      f32x16 sacc = zero16(), dpacc = zero16();
+#pragma unroll
+      for (int hs = 0; hs < 4; ++hs) {
+        bf16x8 qa[2], da[2];
+#pragma unroll
+        for (int s = 0; s < 2; ++s) {
+          qa[s] = frag_r2(qi, qt * 32, 2 * hs + s, lane);
+          da[s] = frag_r2(doi, qt * 32, 2 * hs + s, lane);
+        }
+        lgkm0();
+#pragma unroll
+        for (int s = 0; s < 2; ++s) {
+          sacc = mfma32(qa[s], kf[2 * hs + s], sacc);
+          dpacc = mfma32(da[s], vf[2 * hs + s], dpacc);
+        }
+      }
+      if (qt == 3 && has_next) load_kv(item + G);  // kf / vf are dead for this item now
+      // this lane's key, register i's query qt*32 + acc_row(i, hf) = rows 8G + 4hf + (0..3) of
+      // group G: its LSE and delta as one 16-B LDS read each; dropout hashes per key pair
+      // (lanes key, key^1 share them: each computes two of four and swaps the rest by DPP)
+#pragma unroll
+      for (int G = 0; G < 4; ++G) {
+        const f32x4 lv = rd_f4(sti + (uint32_t)(qt * 32 + 8 * G + 4 * hf) * 4);
+        const f32x4 dl = rd_f4(sti + 512 + (uint32_t)(qt * 32 + 8 * G + 4 * hf) * 4);
+        uint32_t hh[4];
+        if (dc.on) {
+#pragma unroll
+          for (int j = 0; j < 2; ++j) {
+            const uint32_t qq = (uint32_t)(qt * 32 + 8 * G + 4 * hf + 2 * j + par);
+            const uint32_t mine = mix32(dc.seedmix ^ (qq * 0x9E3779B1u) ^ kt);
+            const uint32_t other = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)mine, 0xB1, 0xF, 0xF, true);
+            hh[2 * j] = par ? other : mine;
+            hh[2 * j + 1] = par ? mine : other;
+          }
+        }
+        lgkm0();
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int i = 4 * G + r;
+          const float pr = fexp2(fmaf(sacc[i], ATT_C2, -lv[r] * 1.4426950408889634f));
+          float pd = pr, dpd = dpacc[i];
+          if (dc.on) {
+            const bool kp = keep_from(dc, hh[r], key);
+            pd = kp ? pr * dc.scale : 0.f;
+            dpd = kp ? dpd * dc.scale : 0.f;
+          }
+          sacc[i] = pd;
+          dpacc[i] = pr * (dpd - dl[r]);
+        }
+      }
+#pragma unroll
+      for (int s = 0; s < 2; ++s) {
+        const bf16x8 pf = acc_to_frag(sacc, s);
+        const bf16x8 sf = acc_to_frag(dpacc, s);
+#pragma unroll
+        for (int dh = 0; dh < 2; ++dh) {
+          bf16x8 tdo[2], tq[2];
+#pragma unroll
+          for (int e = 0; e < 2; ++e) {
+            tdo[e] = frag_tp2(doi, qt * 32 + 16 * s, (2 * dh + e) * 32, lane);
+            tq[e] = frag_tp2(qi, qt * 32 + 16 * s, (2 * dh + e) * 32, lane);
+          }
+          lgkm0();
+#pragma unroll
+          for (int e = 0; e < 2; ++e) {
+            dv[2 * dh + e] = mfma32(pf, tdo[e], dv[2 * dh + e]);
+            dk[2 * dh + e] = mfma32(sf, tq[e], dk[2 * dh + e]);
+          }
+        }
+      }
+    }
+    // stage dK (scaled by 1/sqrt(D)) in the Q image and dV in the dO image, 16-B row stores
+    barrier();
+#pragma unroll
+    for (int dt = 0; dt < 4; ++dt)
+#pragma unroll
+      for (int i = 0; i < 16; ++i) {
+        const int row = w * 32 + acc_row(i, hf), col = dt * 32 + (lane & 31);
+        wr_b16(qi + off2(row, col >> 3) + (col & 7) * 2, f2bf(dk[dt][i] * 0.08838834764831845f));
+        wr_b16(doi + off2(row, col >> 3) + (col & 7) * 2, f2bf(dv[dt][i]));
+      }
+    barrier();
+    bf16_t* kb = dqkv + (int64_t)b * L * ld + (int64_t)H * HD2 + (int64_t)hd * HD2;
+#pragma unroll
+    for (int c = 0; c < 8; ++c) {
+      const int idx = tid + c * 256, row = idx >> 4, ch = idx & 15;
+      const bf16x8 vk = rd128(qi + off2(row, ch));
+      const bf16x8 vv = rd128(doi + off2(row, ch));
+      lgkm0();
+      *reinterpret_cast<bf16x8*>(kb + (int64_t)row * ld + ch * 8) = vk;
+      *reinterpret_cast<bf16x8*>(kb + (int64_t)H * HD2 + (int64_t)row * ld + ch * 8) = vv;
+    }
+  }
+}
+
 // db[q*H*64 + h*64 + d] += sum_b colpart[(b*H + h)*192 + q*64 + d]: grid (H*3, chunks of B)
 __global__ void __launch_bounds__(256) colpart_reduce_kernel(const float* __restrict__ colpart,
                                                              float* __restrict__ db, int B, int H,
@@ -888,6 +1191,21 @@ bool launch_attn128_fwd(const uint16_t* qkv, uint16_t* out, float* lse, int B, i
 }
 
 bool attn128_supports(int L, int D, bool causal) { return L == a128::L && D == a128::HD && !causal; }
+
+// L = 128, head_dim 128, bidirectional, token-major (DiffuSeq-XL): the persistent backward
+// (dQ + delta, then dK / dV), one workgroup per CU each
+bool launch_attn128_bwd_d128(const uint16_t* qkv, const uint16_t* out, const uint16_t* dout, const float* lse,
+                             float* delta, uint16_t* dqkv, int B, int Lq, int H, float p, bool causal,
+                             uint32_t seed, uint32_t offset, hipStream_t s) {
+  if (Lq != a128::L || causal || !a128::enabled()) return false;
+  const int items = B * H, slots = a128::num_cus();
+  const int grid = items < slots ? items : slots;
+  hipLaunchKernelGGL(a128::attn128_bwd_q_d128_kernel, dim3(grid), dim3(256), 0, s, (const bf16_t*)qkv,
+                     (const bf16_t*)out, (const bf16_t*)dout, lse, delta, (bf16_t*)dqkv, B, H, p, seed, offset);
+  hipLaunchKernelGGL(a128::attn128_bwd_kv_d128_kernel, dim3(grid), dim3(256), 0, s, (const bf16_t*)qkv,
+                     (const bf16_t*)dout, lse, (const float*)delta, (bf16_t*)dqkv, B, H, p, seed, offset);
+  return true;
+}
 
 // L = 128, head_dim 128, bidirectional, token-major (DiffuSeq-XL): persistent forward, one
 // workgroup per CU; paired with the general backward kernels (same dropout / LSE conventions)

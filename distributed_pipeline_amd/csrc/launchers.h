@@ -83,6 +83,9 @@ bool launch_attn_fwd(const uint16_t* qkv, uint16_t* out, float* lse, int B, int 
 bool attn128_supports(int L, int D, bool causal);
 bool attn_bwd_needs_dq_acc(int L);
 // attention128.hip: persistent L = 128 bidirectional kernels (false: not applicable)
+bool launch_attn128_bwd_d128(const uint16_t* qkv, const uint16_t* out, const uint16_t* dout, const float* lse,
+                             float* delta, uint16_t* dqkv, int B, int L, int H, float p, bool causal,
+                             uint32_t seed, uint32_t offset, hipStream_t s);
 bool launch_attn128_fwd_d128(const uint16_t* qkv, uint16_t* out, float* lse, int B, int L, int H,
                              float p, bool causal, uint32_t seed, uint32_t offset, hipStream_t s);
 bool launch_attn128_fwd(const uint16_t* qkv, uint16_t* out, float* lse, int B, int L, int H,
