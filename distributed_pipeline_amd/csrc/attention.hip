@@ -558,12 +558,44 @@ __global__ void __launch_bounds__(256) attn_fwd_small_kernel(const bf16_t* __res
 //   dV += dropout(P)^T dO,  dK += dS^T Q   with dS = P (dropout'(dP) - delta),
 // both straight from the accumulators (dO / Q read transposed from LDS).
 // ---------------------------------------------------------------------------
+// Column-sum partials of one 128-row block of a backward output (the qkv bias gradient):
+// lane-local sums of the bf16-rounded values over the wave's 16 rows per register column,
+// the two lane halves, then the 4 waves through LDS -> dst[D] (= on pass 0, += after).
+// rows_ok(i) tells whether register i's row exists (the tail past L).
+template <int D, class RowOk>
+__device__ __forceinline__ void block_colsum(const f32x16 (&v)[D / 32], float scale, RowOk rows_ok, float* red,
+                                             float* dst, bool accumulate, int w, int lane, int tid) {
+  const int hf = lane >> 5;
+#pragma unroll
+  for (int dt = 0; dt < D / 32; ++dt) {
+    float cs = 0.f;
+#pragma unroll
+    for (int i = 0; i < 16; ++i)
+      if (rows_ok(i)) cs += bf2f(f2bf(v[dt][i] * scale));
+    cs += __shfl_xor(cs, 32, 64);
+    if (hf == 0) red[w * D + dt * 32 + (lane & 31)] = cs;
+  }
+  __syncthreads();
+  if (tid < D) {
+    const float t = red[tid] + red[D + tid] + red[2 * D + tid] + red[3 * D + tid];
+    dst[tid] = accumulate ? dst[tid] + t : t;
+  }
+  __syncthreads();
+}
+
+// colpart slot of the block: [(b * NI + r) * H + h][3 * D] with r the block's (first) row tile
+__device__ __forceinline__ int64_t colpart_slot(const AttnItem& it0, int L, int H, bool causal) {
+  const int NT = (L + 127) / 128, NI = causal ? (NT + 1) / 2 : NT;
+  return ((int64_t)it0.b * NI + it0.t) * H + it0.hd;
+}
+
 template <int D, bool CAUSAL>
 __global__ void __launch_bounds__(256, D == 64 ? 2 : 1) attn_bwd_kv_kernel(
     const bf16_t* __restrict__ qkv, const bf16_t* __restrict__ dout, const float* __restrict__ lse,
     const float* __restrict__ delta, bf16_t* __restrict__ dqkv, int L, int H, float p,
-    uint32_t seed, uint32_t offset) {
+    uint32_t seed, uint32_t offset, float* __restrict__ colpart) {
   __shared__ __attribute__((aligned(16))) char smem[2 * 64 * 2 * D + 2 * 64 * 4];
+  __shared__ float cred[4 * D];
   char* qt_lds = smem;
   char* dot_lds = smem + 64 * 2 * D;
   float* s_lse = reinterpret_cast<float*>(smem + 2 * 64 * 2 * D);
@@ -698,6 +730,12 @@ __global__ void __launch_bounds__(256, D == 64 ? 2 : 1) attn_bwd_kv_kernel(
         base[2LL * H * D] = f2bf(dv[dt][i]);
       }
     }
+  if (colpart) {  // k and v bias-gradient partials of this block's keys
+    float* cp = colpart + colpart_slot(it0, L, H, CAUSAL) * (3 * D);
+    auto ok = [&](int i) { return kbase + acc_row(i, hf) < L; };
+    block_colsum<D>(dk, rsqrt_d<D>(), ok, cred, cp + D, pass > 0, w, lane, tid);
+    block_colsum<D>(dv, 1.f, ok, cred, cp + 2 * D, pass > 0, w, lane, tid);
+  }
   __syncthreads();  // LDS reuse by the next pass
   }
 }
@@ -713,8 +751,9 @@ template <int D, bool CAUSAL>
 __global__ void __launch_bounds__(256, D == 64 ? 2 : 1) attn_bwd_q_kernel(
     const bf16_t* __restrict__ qkv, const bf16_t* __restrict__ dout, const float* __restrict__ lse,
     float* __restrict__ delta, bf16_t* __restrict__ dqkv, int L, int H, float p,
-    uint32_t seed, uint32_t offset, const bf16_t* __restrict__ out) {
+    uint32_t seed, uint32_t offset, const bf16_t* __restrict__ out, float* __restrict__ colpart) {
   __shared__ __attribute__((aligned(16))) char smem[2 * 64 * 2 * D];
+  __shared__ float cred[4 * D];
   char* kt_lds = smem;
   char* vt_lds = smem + 64 * 2 * D;
   const AttnItem it0 = attn_item(L, H, CAUSAL);
@@ -834,6 +873,11 @@ __global__ void __launch_bounds__(256, D == 64 ? 2 : 1) attn_bwd_q_kernel(
       const int qq = qbase + acc_row(i, hf);
       if (qq < L) dqkv[((int64_t)b * L + qq) * ld + (int64_t)hd * D + dt * 32 + (lane & 31)] = f2bf(dq[dt][i] * rsqrt_d<D>());
     }
+  if (colpart) {  // q bias-gradient partials of this block's queries
+    float* cp = colpart + colpart_slot(it0, L, H, CAUSAL) * (3 * D);
+    block_colsum<D>(dq, rsqrt_d<D>(), [&](int i) { return qbase + acc_row(i, hf) < L; }, cred, cp, pass > 0, w,
+                    lane, tid);
+  }
   __syncthreads();  // LDS reuse by the next pass
   }
 }
@@ -893,22 +937,23 @@ bool attn_bwd_needs_dq_acc(int L) { (void)L; return false; }
 template <int D>
 static void attn_bwd_general(const uint16_t* qkv, const uint16_t* out, const uint16_t* dout,
                              const float* lse, float* delta, uint16_t* dqkv, int B, int L, int H,
-                             float p, bool causal, uint32_t seed, uint32_t offset, hipStream_t s) {
+                             float p, bool causal, uint32_t seed, uint32_t offset, hipStream_t s,
+                             float* colpart = nullptr) {
   // dQ kernel first: it forms delta = rowsum(dO * O) in-kernel and publishes it for the
   // dK/dV kernel (no separate delta pass over O and dO)
   dim3 grid(attn_grid(B, L, H, causal));  // attn_item() layout
   if (causal) {
     hipLaunchKernelGGL((attn_bwd_q_kernel<D, true>), grid, dim3(256), 0, s, (const bf16_t*)qkv,
                        (const bf16_t*)dout, lse, delta, (bf16_t*)dqkv, L, H, p, seed, offset,
-                       (const bf16_t*)out);
+                       (const bf16_t*)out, colpart);
     hipLaunchKernelGGL((attn_bwd_kv_kernel<D, true>), grid, dim3(256), 0, s, (const bf16_t*)qkv,
-                       (const bf16_t*)dout, lse, delta, (bf16_t*)dqkv, L, H, p, seed, offset);
+                       (const bf16_t*)dout, lse, delta, (bf16_t*)dqkv, L, H, p, seed, offset, colpart);
   } else {
     hipLaunchKernelGGL((attn_bwd_q_kernel<D, false>), grid, dim3(256), 0, s, (const bf16_t*)qkv,
                        (const bf16_t*)dout, lse, delta, (bf16_t*)dqkv, L, H, p, seed, offset,
-                       (const bf16_t*)out);
+                       (const bf16_t*)out, colpart);
     hipLaunchKernelGGL((attn_bwd_kv_kernel<D, false>), grid, dim3(256), 0, s, (const bf16_t*)qkv,
-                       (const bf16_t*)dout, lse, delta, (bf16_t*)dqkv, L, H, p, seed, offset);
+                       (const bf16_t*)dout, lse, delta, (bf16_t*)dqkv, L, H, p, seed, offset, colpart);
   }
 }
 
@@ -920,16 +965,58 @@ bool launch_attn_bwd(const uint16_t* qkv, const uint16_t* out, const uint16_t* d
   if (head_major)  // caller checked attn128_supports
     return launch_attn128_bwd(qkv, out, dout, lse, dqkv, colpart, dbias, B, L, H, p, causal, seed, offset, s,
                               true, db_accumulate) && dbias != nullptr;
+  // dbias != nullptr: the kernels also write per-block column-sum partials of dq / dk / dv
+  // into colpart ([attn_colpart_rows][3 D], attn_colpart_floats) and one reduce pass adds
+  // them into dbias (zeroed first unless db_accumulate)
+  float* cp = dbias ? colpart : nullptr;
   if (D == 128) {
-    if (!launch_attn128_bwd_d128(qkv, out, dout, lse, delta, dqkv, B, L, H, p, causal, seed, offset, s))
-      attn_bwd_general<128>(qkv, out, dout, lse, delta, dqkv, B, L, H, p, causal, seed, offset, s);
-    return false;
+    if (!launch_attn128_bwd_d128(qkv, out, dout, lse, delta, dqkv, B, L, H, p, causal, seed, offset, s, cp))
+      attn_bwd_general<128>(qkv, out, dout, lse, delta, dqkv, B, L, H, p, causal, seed, offset, s, cp);
+  } else {
+    if (launch_attn128_bwd(qkv, out, dout, lse, dqkv, colpart, dbias, B, L, H, p, causal, seed, offset,
+                           s, false, db_accumulate))
+      return dbias != nullptr;
+    attn_bwd_general<64>(qkv, out, dout, lse, delta, dqkv, B, L, H, p, causal, seed, offset, s, cp);
   }
-  if (launch_attn128_bwd(qkv, out, dout, lse, dqkv, colpart, dbias, B, L, H, p, causal, seed, offset,
-                         s, false, db_accumulate))
-    return dbias != nullptr;
-  attn_bwd_general<64>(qkv, out, dout, lse, delta, dqkv, B, L, H, p, causal, seed, offset, s);
-  return false;
+  if (!dbias) return false;
+  if (!db_accumulate) (void)hipMemsetAsync(dbias, 0, sizeof(float) * 3 * H * D, s);
+  launch_colpart_reduce(colpart, dbias, (int)(attn_colpart_rows(B, L, H, D, causal) / H), H, D, s);
+  return true;
+}
+
+// rows of the colpart scratch: one per (b, row-tile block, h) of the general kernels (the
+// persistent L = 128 kernels: NI = 1, one per (b, h) item)
+int64_t attn_colpart_rows(int B, int L, int H, int D, bool causal) {
+  (void)D;
+  const int NT = (L + 127) / 128, NI = causal ? (NT + 1) / 2 : NT;
+  return (int64_t)B * NI * H;
+}
+
+// db[part * H * D + h * D + d] += sum_r colpart[(r * H + h) * 3 D + part * D + d] over the R row
+// groups: grid (3 * H * D / 64, chunks of R), 4 row lanes x 64 columns per block, one atomic
+// per column and chunk
+__global__ void __launch_bounds__(256) colpart_reduce_d_kernel(const float* __restrict__ colpart,
+                                                               float* __restrict__ db, int R, int H, int D,
+                                                               int rchunk) {
+  __shared__ float red[4][64];
+  const int c64 = D / 64, x = blockIdx.x;
+  const int part = x / (H * c64), h = (x / c64) % H, cc = x % c64;
+  const int d = cc * 64 + (threadIdx.x & 63), rl = threadIdx.x >> 6;
+  const int r0 = blockIdx.y * rchunk, r1 = min(R, r0 + rchunk);
+  float t = 0.f;
+  for (int r = r0 + rl; r < r1; r += 4) t += colpart[((int64_t)r * H + h) * 3 * D + part * D + d];
+  red[rl][threadIdx.x & 63] = t;
+  __syncthreads();
+  if (rl == 0) {
+    const int i = threadIdx.x;
+    atomicAdd(db + part * H * D + h * D + d, red[0][i] + red[1][i] + red[2][i] + red[3][i]);
+  }
+}
+
+void launch_colpart_reduce(const float* colpart, float* db, int R, int H, int D, hipStream_t s) {
+  const int rchunk = 64, nch = (R + rchunk - 1) / rchunk;
+  hipLaunchKernelGGL(colpart_reduce_d_kernel, dim3(3 * H * (D / 64), nch), dim3(256), 0, s, colpart, db, R, H,
+                     D, rchunk);
 }
 
 }  // namespace dpa

@@ -860,13 +860,32 @@ __device__ __forceinline__ void wait_vm2(int n) {
   }
 }
 
+// column sums of one item's 128 x 128 output block (bf16-rounded, scaled) -> dst[128]: lane sums
+// over the wave's 16 rows per register column, the two lane halves, then the 4 waves via LDS
+__device__ __forceinline__ void item_colsum128(const f32x16 (&v)[4], float scale, float* red, float* dst, int w,
+                                               int lane, int tid) {
+  const int hf = lane >> 5;
+#pragma unroll
+  for (int dt = 0; dt < 4; ++dt) {
+    float cs = 0.f;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) cs += bf2f(f2bf(v[dt][i] * scale));
+    cs += __shfl_xor(cs, 32, 64);
+    if (hf == 0) red[w * HD2 + dt * 32 + (lane & 31)] = cs;
+  }
+  __syncthreads();
+  if (tid < HD2) dst[tid] = red[tid] + red[HD2 + tid] + red[2 * HD2 + tid] + red[3 * HD2 + tid];
+  __syncthreads();
+}
+
 // dQ (and delta = rowsum(dO * O), published for the dK/dV kernel).  Wave w owns queries
 // 32w .. 32w + 31 (Q, dO fragments in registers); K, V images [128][128] per stage.
 __global__ void __launch_bounds__(256, 1) attn128_bwd_q_d128_kernel(
     const bf16_t* __restrict__ qkv, const bf16_t* __restrict__ out, const bf16_t* __restrict__ dout,
     const float* __restrict__ lse, float* __restrict__ delta, bf16_t* __restrict__ dqkv, int B, int H, float p,
-    uint32_t seed, uint32_t offset) {
+    uint32_t seed, uint32_t offset, float* __restrict__ colpart) {
   __shared__ __attribute__((aligned(1024))) char smem[2 * 2 * IMG2];
+  __shared__ float cred[4 * HD2];
   const int w = threadIdx.x >> 6;
   const int nitems = B * H;
   const int64_t ld = 3LL * H * HD2, ldo = (int64_t)H * HD2, sb = 3LL * H * L * HD2;
@@ -983,6 +1002,7 @@ __global__ void __launch_bounds__(256, 1) attn128_bwd_q_d128_kernel(
       lgkm0();
       *reinterpret_cast<bf16x8*>(db + (int64_t)row * ld + ch * 8) = v;
     }
+    if (colpart) item_colsum128(dq, 0.08838834764831845f, cred, colpart + (int64_t)item * 3 * HD2, w, lane, tid);
   }
 }
 
@@ -991,9 +1011,10 @@ __global__ void __launch_bounds__(256, 1) attn128_bwd_q_d128_kernel(
 __global__ void __launch_bounds__(256, 1) attn128_bwd_kv_d128_kernel(
     const bf16_t* __restrict__ qkv, const bf16_t* __restrict__ dout, const float* __restrict__ lse,
     const float* __restrict__ delta, bf16_t* __restrict__ dqkv, int B, int H, float p, uint32_t seed,
-    uint32_t offset) {
+    uint32_t offset, float* __restrict__ colpart) {
   constexpr int STG = 2 * IMG2 + 1024;  // Q, dO images + lse[128] + delta[128]
   __shared__ __attribute__((aligned(1024))) char smem[2 * STG];
+  __shared__ float cred[4 * HD2];
   const int w = threadIdx.x >> 6;
   const int nitems = B * H;
   const int64_t ld = 3LL * H * HD2, ldo = (int64_t)H * HD2, sb = 3LL * H * L * HD2;
@@ -1140,6 +1161,11 @@ __global__ void __launch_bounds__(256, 1) attn128_bwd_kv_d128_kernel(
       *reinterpret_cast<bf16x8*>(kb + (int64_t)row * ld + ch * 8) = vk;
       *reinterpret_cast<bf16x8*>(kb + (int64_t)H * HD2 + (int64_t)row * ld + ch * 8) = vv;
     }
+    if (colpart) {
+      float* cp = colpart + (int64_t)item * 3 * HD2;
+      item_colsum128(dk, 0.08838834764831845f, cred, cp + HD2, w, lane, tid);
+      item_colsum128(dv, 1.f, cred, cp + 2 * HD2, w, lane, tid);
+    }
   }
 }
 
@@ -1196,14 +1222,16 @@ bool attn128_supports(int L, int D, bool causal) { return L == a128::L && D == a
 // (dQ + delta, then dK / dV), one workgroup per CU each
 bool launch_attn128_bwd_d128(const uint16_t* qkv, const uint16_t* out, const uint16_t* dout, const float* lse,
                              float* delta, uint16_t* dqkv, int B, int Lq, int H, float p, bool causal,
-                             uint32_t seed, uint32_t offset, hipStream_t s) {
+                             uint32_t seed, uint32_t offset, hipStream_t s, float* colpart) {
   if (Lq != a128::L || causal || !a128::enabled()) return false;
   const int items = B * H, slots = a128::num_cus();
   const int grid = items < slots ? items : slots;
   hipLaunchKernelGGL(a128::attn128_bwd_q_d128_kernel, dim3(grid), dim3(256), 0, s, (const bf16_t*)qkv,
-                     (const bf16_t*)out, (const bf16_t*)dout, lse, delta, (bf16_t*)dqkv, B, H, p, seed, offset);
+                     (const bf16_t*)out, (const bf16_t*)dout, lse, delta, (bf16_t*)dqkv, B, H, p, seed, offset,
+                     colpart);
   hipLaunchKernelGGL(a128::attn128_bwd_kv_d128_kernel, dim3(grid), dim3(256), 0, s, (const bf16_t*)qkv,
-                     (const bf16_t*)dout, lse, (const float*)delta, (bf16_t*)dqkv, B, H, p, seed, offset);
+                     (const bf16_t*)dout, lse, (const float*)delta, (bf16_t*)dqkv, B, H, p, seed, offset,
+                     colpart);
   return true;
 }
 

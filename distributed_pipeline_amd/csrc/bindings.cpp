@@ -354,7 +354,7 @@ static std::vector<at::Tensor> attn_bwd(const at::Tensor& dout, const at::Tensor
   const bool acc = want_db && db_acc.has_value() && db_acc->defined() && db_acc->scalar_type() == at::kFloat &&
                    db_acc->is_contiguous() && db_acc->numel() == 3LL * H * D && db_acc->device() == qkv.device();
   if (want_db) {
-    colpart = at::empty({(int64_t)B * H * 192}, f32);
+    colpart = at::empty({dpa::attn_colpart_rows(B, L, H, D, causal) * 3 * D}, f32);
     db = acc ? *db_acc : at::empty({3 * H * D}, f32);
   }
   bool got = dpa::launch_attn_bwd(

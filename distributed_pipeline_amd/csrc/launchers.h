@@ -85,7 +85,11 @@ bool attn_bwd_needs_dq_acc(int L);
 // attention128.hip: persistent L = 128 bidirectional kernels (false: not applicable)
 bool launch_attn128_bwd_d128(const uint16_t* qkv, const uint16_t* out, const uint16_t* dout, const float* lse,
                              float* delta, uint16_t* dqkv, int B, int L, int H, float p, bool causal,
-                             uint32_t seed, uint32_t offset, hipStream_t s);
+                             uint32_t seed, uint32_t offset, hipStream_t s, float* colpart = nullptr);
+// attention backward bias-gradient partials: rows of the colpart scratch ([rows][3 D] fp32) and
+// the reduce pass db[3 H D] += column sums
+int64_t attn_colpart_rows(int B, int L, int H, int D, bool causal);
+void launch_colpart_reduce(const float* colpart, float* db, int R, int H, int D, hipStream_t s);
 bool launch_attn128_fwd_d128(const uint16_t* qkv, uint16_t* out, float* lse, int B, int L, int H,
                              float p, bool causal, uint32_t seed, uint32_t offset, hipStream_t s);
 bool launch_attn128_fwd(const uint16_t* qkv, uint16_t* out, float* lse, int B, int L, int H,
