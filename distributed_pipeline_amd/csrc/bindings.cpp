@@ -228,7 +228,8 @@ static std::vector<at::Tensor> add_ln_bwd(const at::Tensor& dout, const at::Tens
                                           int64_t offset, bool need_dres, bool need_dy,
                                           bool want_dyb, c10::optional<at::Tensor> dh_in, bool post,
                                           c10::optional<at::Tensor> dg_acc, c10::optional<at::Tensor> db_acc,
-                                          c10::optional<at::Tensor> dyb_acc) {
+                                          c10::optional<at::Tensor> dyb_acc, c10::optional<at::Tensor> part_buf,
+                                          bool part_acc) {
   CHECK_DEV(dout); CHECK_BF16(dout); CHECK_CONTIG(dout); CHECK_BF16(hs); CHECK_CONTIG(hs);
   const uint16_t* dhp = nullptr;
   if (dh_in.has_value() && dh_in->defined()) {
@@ -260,16 +261,60 @@ static std::vector<at::Tensor> add_ln_bwd(const at::Tensor& dout, const at::Tens
   if (ext_y) { dyb = *dyb_acc; zero_mask &= ~4; }
   const int64_t wsn = dpa::ln_bwd_ws_floats(R, D);
   at::Tensor ws;
-  if (wsn > 0) ws = at::empty({wsn}, f32);
+  int part_mode = 0;
+  if (part_buf.has_value() && part_buf->defined()) {
+    // deferred column sums (caller-owned partials, reduced later by ln_colreduce): only
+    // when every accumulator is a caller buffer - nothing is returned for them
+    TORCH_CHECK(wsn > 0 && part_buf->numel() == wsn && part_buf->scalar_type() == at::kFloat &&
+                    part_buf->is_contiguous() && part_buf->device() == dout.device(),
+                "add_ln_bwd: part_buf must be fp32 [ln_bwd_partials(R, D)] on the device");
+    TORCH_CHECK(ext_g && ext_b && (!dyb.defined() || ext_y), "add_ln_bwd: part_buf needs dg/db/dyb_acc");
+    ws = *part_buf;
+    part_mode = part_acc ? 2 : 1;
+  } else if (wsn > 0) {
+    ws = at::empty({wsn}, f32);
+  }
   bool ok = dpa::launch_add_ln_bwd(
       bf_ptr(dout), bf_ptr(hs), mean.data_ptr<float>(), rstd.data_ptr<float>(), bf_ptr(g),
       need_dres ? reinterpret_cast<uint16_t*>(dres.data_ptr()) : nullptr,
       need_dy ? reinterpret_cast<uint16_t*>(dy.data_ptr()) : nullptr,
       dyb.defined() ? dyb.data_ptr<float>() : nullptr,
       dg.data_ptr<float>(), db.data_ptr<float>(), R, D, (float)p, (uint32_t)seed, (uint32_t)offset,
-      cur_stream(), dhp, post, zero_mask, wsn > 0 ? ws.data_ptr<float>() : nullptr);
+      cur_stream(), dhp, post, zero_mask, wsn > 0 ? ws.data_ptr<float>() : nullptr, part_mode);
   TORCH_CHECK(ok, "add_ln_bwd: unsupported hidden size ", D);
   return {dres, dy, ext_g ? at::Tensor() : dg, ext_b ? at::Tensor() : db, ext_y ? at::Tensor() : dyb};
+}
+
+// floats of the caller-owned partial buffer add_ln_bwd(part_buf=...) takes for R x D (0: the
+// shape has no two-stage column sums, no deferral)
+static int64_t ln_bwd_partials(int64_t R, int64_t D) { return dpa::ln_bwd_ws_floats(R, (int)D); }
+
+// dg += colsum, db += colsum (, dyb += colsum) of partials accumulated by add_ln_bwd(part_buf=...)
+static void ln_colreduce(const at::Tensor& part, int64_t R, int64_t D, at::Tensor& dg, at::Tensor& db,
+                         c10::optional<at::Tensor> dyb) {
+  CHECK_DEV(part); CHECK_F32(part); CHECK_CONTIG(part); CHECK_F32(dg); CHECK_F32(db);
+  TORCH_CHECK(part.numel() == dpa::ln_bwd_ws_floats(R, (int)D) && dg.numel() == D && db.numel() == D,
+              "ln_colreduce shapes");
+  float* yp = nullptr;
+  if (dyb.has_value() && dyb->defined()) {
+    CHECK_F32((*dyb));
+    TORCH_CHECK(dyb->numel() == D, "ln_colreduce dyb");
+    yp = dyb->data_ptr<float>();
+  }
+  const c10::DeviceGuard guard(part.device());
+  TORCH_CHECK(dpa::launch_ln_colreduce(part.data_ptr<float>(), R, (int)D, dg.data_ptr<float>(),
+                                       db.data_ptr<float>(), yp, cur_stream()),
+              "ln_colreduce: no two-stage shape");
+}
+
+// dst += column sums of fp32 partials [rows, cols] (the kept gemm_nn_dact partials)
+static void colsum_acc(const at::Tensor& part, at::Tensor& dst) {
+  CHECK_DEV(part); CHECK_F32(part); CHECK_CONTIG(part); CHECK_F32(dst); CHECK_CONTIG(dst);
+  TORCH_CHECK(part.dim() == 2 && dst.numel() == part.size(1), "colsum_acc shapes");
+  const c10::DeviceGuard guard(part.device());
+  if (!dpa::launch_colsum_acc(part.data_ptr<float>(), (int)part.size(0), (int)part.size(1), dst.data_ptr<float>(),
+                              cur_stream()))
+    dst.add_(part.sum(0));
 }
 
 // ---- bias + activation epilogues ------------------------------------------------------
@@ -477,7 +522,8 @@ static bool gemm_nn_acc_(const at::Tensor& dy, const at::Tensor& W, at::Tensor& 
 // one reduction turns into db (no second pass over dz).
 static std::vector<at::Tensor> gemm_nn_dact(const at::Tensor& dy, const at::Tensor& W,
                                             const at::Tensor& aux, int64_t act, bool want_db,
-                                            c10::optional<at::Tensor> db_acc) {
+                                            c10::optional<at::Tensor> db_acc,
+                                            c10::optional<at::Tensor> part_out) {
   CHECK_DEV(dy); CHECK_BF16(dy); CHECK_BF16(W); CHECK_BF16(aux);
   CHECK_CONTIG(dy); CHECK_CONTIG(W); CHECK_CONTIG(aux);
   const int T = (int)dy.size(0), N = (int)dy.size(1), K = (int)W.size(1);
@@ -485,14 +531,26 @@ static std::vector<at::Tensor> gemm_nn_dact(const at::Tensor& dy, const at::Tens
   const c10::DeviceGuard guard(dy.device());
   at::Tensor dz = at::empty({T, K}, dy.options());
   uint16_t* dzp = reinterpret_cast<uint16_t*>(dz.data_ptr());
+  // part_out: the caller keeps the column-sum partials [(T/256)*2, K] and reduces them later
+  // (several micro-batches' partials in one colsum_acc launch); nothing is returned for db
+  const bool keep = want_db && part_out.has_value() && part_out->defined();
+  // db_acc: the column sums accumulated straight onto this fp32 .grad (contract: always
+  // accumulated when db_acc is usable; the result is then undefined)
+  const bool acc = !keep && want_db && db_acc.has_value() && db_acc->defined() &&
+                   db_acc->scalar_type() == at::kFloat && db_acc->is_contiguous() && db_acc->numel() == K &&
+                   db_acc->device() == dy.device();
   at::Tensor part;
-  if (want_db && T % 256 == 0) part = at::empty({(int64_t)(T / 256) * 2, K}, dy.options().dtype(at::kFloat));
+  if (keep) {
+    TORCH_CHECK(T % 256 == 0 && part_out->scalar_type() == at::kFloat && part_out->is_contiguous() &&
+                    part_out->numel() == (int64_t)(T / 256) * 2 * K && part_out->device() == dy.device(),
+                "gemm_nn_dact: part_out must be fp32 [(T/256)*2, K]");
+    part = *part_out;
+  } else if (want_db && T % 256 == 0) {
+    part = at::empty({(int64_t)(T / 256) * 2, K}, dy.options().dtype(at::kFloat));
+  }
   if (dpa::launch_gemmp_nn(bf_ptr(dy), bf_ptr(W), dzp, bf_ptr(aux), (int)act, T, N, K, dpa::device_cu_count(),
                            cur_stream(), part.defined() ? part.data_ptr<float>() : nullptr)) {
-    // db_acc: the column sums accumulated straight onto this fp32 .grad (contract: always
-    // accumulated when db_acc is usable; the result is then undefined)
-    const bool acc = want_db && db_acc.has_value() && db_acc->defined() && db_acc->scalar_type() == at::kFloat &&
-                     db_acc->is_contiguous() && db_acc->numel() == K && db_acc->device() == dy.device();
+    if (keep) return {dz, at::Tensor()};
     if (acc) {
       if (!part.defined() || !dpa::launch_colsum_acc(part.data_ptr<float>(), (int)part.size(0), K,
                                                      db_acc->data_ptr<float>(), cur_stream()))
@@ -501,8 +559,20 @@ static std::vector<at::Tensor> gemm_nn_dact(const at::Tensor& dy, const at::Tens
     }
     return {dz, part.defined() ? part.sum(0) : at::Tensor()};
   }
-  if (dpa::launch_gemm256_nn_dact(bf_ptr(dy), bf_ptr(W), bf_ptr(aux), dzp, T, N, K, (int)act, cur_stream()))
-    return {dz, at::Tensor()};
+  // no persistent kernel for this shape: the column sums from dz itself (a kept partial slot
+  // gets them in row 0, zeros elsewhere; all zeros when no fused kernel ran either - the
+  // caller then computes db itself)
+  if (keep) part_out->zero_();
+  if (dpa::launch_gemm256_nn_dact(bf_ptr(dy), bf_ptr(W), bf_ptr(aux), dzp, T, N, K, (int)act, cur_stream())) {
+    if (!want_db) return {dz, at::Tensor()};
+    at::Tensor cs = dz.sum(0, false, at::kFloat);
+    if (keep) (*part_out)[0].copy_(cs);
+    if (keep || acc) {
+      if (acc) db_acc->add_(cs);
+      return {dz, at::Tensor()};
+    }
+    return {dz, cs};
+  }
   return {at::Tensor(), at::Tensor()};
 }
 
@@ -777,7 +847,12 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("dout"), py::arg("hsave"), py::arg("mean"), py::arg("rstd"), py::arg("gamma"),
         py::arg("p"), py::arg("seed"), py::arg("offset"), py::arg("need_dres"), py::arg("need_dy"),
         py::arg("want_dy_colsum") = false, py::arg("dh_in") = py::none(), py::arg("post") = false,
-        py::arg("dg_acc") = py::none(), py::arg("db_acc") = py::none(), py::arg("dyb_acc") = py::none());
+        py::arg("dg_acc") = py::none(), py::arg("db_acc") = py::none(), py::arg("dyb_acc") = py::none(),
+        py::arg("part_buf") = py::none(), py::arg("part_acc") = false);
+  m.def("colsum_acc", &colsum_acc, "dst += colsum(part) (fp32 partials [rows, cols])");
+  m.def("ln_bwd_partials", &ln_bwd_partials, "floats of add_ln_bwd's deferred partial buffer (0: none)");
+  m.def("ln_colreduce", &ln_colreduce, "dg/db(/dyb) += column sums of add_ln_bwd partials",
+        py::arg("part"), py::arg("R"), py::arg("D"), py::arg("dg"), py::arg("db"), py::arg("dyb") = py::none());
   m.def("bias_act_fwd", &bias_act_fwd, "z += bias (in place); y = act(z) -> (z, y)");
   m.def("bias_act_bwd", &bias_act_bwd, "dz = dy*act'(zy); db = colsum(dz) -> (dz, db)");
   m.def("gemm_nt_into", &gemm_nt_into, "y = x W^T (+b) into a preallocated [T, N] tensor");
@@ -800,7 +875,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("gemm_nn_dact", &gemm_nn_dact,
         "dz = (dy W) * act'(aux) (bf16 MFMA, fused act backward) -> (dz, colsum(dz) fp32 or None)",
         py::arg("dy"), py::arg("W"), py::arg("aux"), py::arg("act"), py::arg("want_db") = false,
-        py::arg("db_acc") = py::none());
+        py::arg("db_acc") = py::none(), py::arg("part_out") = py::none());
   m.def("gemm_nn_acc_", &gemm_nn_acc_, "dx += dy W in place (bf16 MFMA); False if the shape does not tile");
   m.def("gemm_wgrad", &gemm_wgrad, "dW += dy^T x, db += colsum(dy) (fp32 atomics, split-K)");
   m.def("gemm_wgrad_multi", &gemm_wgrad_multi, "dW += sum_s dy_s^T x_s over equal token segments, one launch",

@@ -191,7 +191,8 @@ __global__ void __launch_bounds__(256, VEC <= 12 ? 4 : VEC <= 16 ? 2 : 1) add_ln
     const float* __restrict__ mean_in, const float* __restrict__ rstd_in,
     const bf16_t* __restrict__ gamma, bf16_t* __restrict__ dres, bf16_t* __restrict__ dy,
     float* __restrict__ dyb, float* __restrict__ part_dg, float* __restrict__ part_db, int64_t R,
-    float p, uint32_t seed, uint32_t offset, const bf16_t* __restrict__ dh_in, float* __restrict__ part) {
+    float p, uint32_t seed, uint32_t offset, const bf16_t* __restrict__ dh_in, float* __restrict__ part,
+    bool part_acc) {
   constexpr int D = VEC * 64;
   __shared__ float red[4][D];  // reused for dgamma, dbeta, dyb in turn
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
@@ -262,7 +263,10 @@ __global__ void __launch_bounds__(256, VEC <= 12 ? 4 : VEC <= 16 ? 2 : 1) add_ln
     __syncthreads();
     if (part) {
       float* pr = part + ((int64_t)blockIdx.x * 3 + a) * D;
-      for (int c = threadIdx.x; c < D; c += blockDim.x) pr[c] = red[0][c] + red[1][c] + red[2][c] + red[3][c];
+      for (int c = threadIdx.x; c < D; c += blockDim.x) {
+        const float v = red[0][c] + red[1][c] + red[2][c] + red[3][c];
+        pr[c] = part_acc ? pr[c] + v : v;  // part_acc: partials summed over micro-batches
+      }
     } else {
       for (int c = threadIdx.x; c < D; c += blockDim.x)
         atomicAdd(dst[a] + c, red[0][c] + red[1][c] + red[2][c] + red[3][c]);
@@ -283,7 +287,7 @@ __global__ void __launch_bounds__(256) add_ln_bwd_rowblk_kernel(
     const float* __restrict__ mean_in, const float* __restrict__ rstd_in,
     const bf16_t* __restrict__ gamma, bf16_t* __restrict__ dres, bf16_t* __restrict__ dy,
     bool want_dyb, int64_t R, float p, uint32_t seed, uint32_t offset, const bf16_t* __restrict__ dh_in,
-    float* __restrict__ part) {
+    float* __restrict__ part, bool part_acc) {
   constexpr int VT = D / 256;
   constexpr int CH = VT % 8 == 0 ? 8 : VT % 4 == 0 ? 4 : VT % 2 == 0 ? 2 : 1;
   constexpr int NG = VT / CH;
@@ -410,6 +414,11 @@ __global__ void __launch_bounds__(256) add_ln_bwd_rowblk_kernel(
   float* pr = part + (int64_t)blockIdx.x * 3 * D;
 #pragma unroll
   for (int i = 0; i < VT; ++i) {
+    if (part_acc) {
+      adg[i] += pr[col(i)];
+      adb[i] += pr[D + col(i)];
+      if (want_dyb) ady[i] += pr[2 * D + col(i)];
+    }
     pr[col(i)] = adg[i];
     pr[D + col(i)] = adb[i];
     if (want_dyb) pr[2 * D + col(i)] = ady[i];
@@ -495,16 +504,29 @@ static int64_t ln_bwd_two_stage_blocks(int64_t R, int D) {
 }
 int64_t ln_bwd_ws_floats(int64_t R, int D) { return ln_bwd_two_stage_blocks(R, D) * 3 * D; }
 
+// Second stage of the two-stage column sums: part[nb][3][D] -> dg, db (, dyb) (+=)
+static void ln_colreduce_launch(const float* part, int nb, int D, float* dg, float* db, float* dyb,
+                                hipStream_t s) {
+  const int nseg = nb >= 256 ? 16 : nb >= 32 ? 4 : 1;
+  hipLaunchKernelGGL(ln_colreduce_kernel, dim3(D / 64, dyb ? 3 : 2, nseg), dim3(256), 0, s, part, nb, D, dg, db,
+                     dyb, 3);
+}
+
+// part_mode (two-stage shapes only, ws = a caller-owned partial buffer of ln_bwd_ws_floats):
+// 0 the partials are reduced onto dg / db / dyb right away; 1 they are stored and 2 added
+// onto the buffer's previous contents, with no reduction - the caller runs
+// launch_ln_colreduce once over the sum of several micro-batches' partials.
 template <int VEC>
 static void ln_bwd_impl(const uint16_t* dout, const uint16_t* hsave, const float* mean,
                         const float* rstd, const uint16_t* g, uint16_t* dres, uint16_t* dy,
                         float* dyb, float* dg, float* db, int64_t R, float p, uint32_t seed,
                         uint32_t off, const uint16_t* dh_in, bool post, int zero_mask, hipStream_t s,
-                        float* ws) {
+                        float* ws, int part_mode) {
   constexpr int D = VEC * 64;
   const int64_t nb2 = ln_bwd_two_stage_blocks(R, D);
   const bool two_stage = ws != nullptr && nb2 > 0;
   const int nb = two_stage ? (int)nb2 : ln_bwd_blocks(R);
+  const bool pacc = two_stage && part_mode == 2, reduce = !two_stage || part_mode == 0;
   // zero the accumulators that are scratch (zero_mask bits: 1 dg, 2 db, 4 dyb); the others
   // are parameter .grad buffers the kernel accumulates onto.  One memset when the scratch
   // ones are consecutive rows of one buffer (the binding allocates them so).
@@ -517,37 +539,37 @@ static void ln_bwd_impl(const uint16_t* dout, const uint16_t* hsave, const float
     if (zy) (void)hipMemsetAsync(dyb, 0, sizeof(float) * D, s);
   }
   float* part = two_stage ? ws : nullptr;
+  float* const dyb_k = dy ? dyb : nullptr;
   if constexpr (D >= LN_WIDE_D) {
     if (two_stage) {
-      const bool wy = dy != nullptr && dyb != nullptr;
       if (post)
         hipLaunchKernelGGL((add_ln_bwd_rowblk_kernel<D, true>), dim3(nb), dim3(256), 0, s, (const bf16_t*)dout,
-                           (const bf16_t*)hsave, mean, rstd, (const bf16_t*)g, (bf16_t*)dres, (bf16_t*)dy, wy, R,
-                           p, seed, off, (const bf16_t*)dh_in, part);
+                           (const bf16_t*)hsave, mean, rstd, (const bf16_t*)g, (bf16_t*)dres, (bf16_t*)dy,
+                           dyb_k != nullptr, R, p, seed, off, (const bf16_t*)dh_in, part, pacc);
       else
         hipLaunchKernelGGL((add_ln_bwd_rowblk_kernel<D, false>), dim3(nb), dim3(256), 0, s, (const bf16_t*)dout,
-                           (const bf16_t*)hsave, mean, rstd, (const bf16_t*)g, (bf16_t*)dres, (bf16_t*)dy, wy, R,
-                           p, seed, off, (const bf16_t*)dh_in, part);
-      const int nseg = nb >= 256 ? 16 : nb >= 32 ? 4 : 1;
-      hipLaunchKernelGGL(ln_colreduce_kernel, dim3(D / 64, wy ? 3 : 2, nseg), dim3(256), 0, s, part, nb, D, dg,
-                         db, wy ? dyb : nullptr, 3);
+                           (const bf16_t*)hsave, mean, rstd, (const bf16_t*)g, (bf16_t*)dres, (bf16_t*)dy,
+                           dyb_k != nullptr, R, p, seed, off, (const bf16_t*)dh_in, part, pacc);
+      if (reduce) ln_colreduce_launch(part, nb, D, dg, db, dyb_k, s);
       return;
     }
   }
   if (post)
     hipLaunchKernelGGL((add_ln_bwd_kernel<VEC, true>), dim3(nb), dim3(256), 0, s, (const bf16_t*)dout,
-                       (const bf16_t*)hsave, mean, rstd, (const bf16_t*)g, (bf16_t*)dres, (bf16_t*)dy,
-                       dy ? dyb : nullptr, dg, db, R, p, seed, off, (const bf16_t*)dh_in, part);
+                       (const bf16_t*)hsave, mean, rstd, (const bf16_t*)g, (bf16_t*)dres, (bf16_t*)dy, dyb_k, dg,
+                       db, R, p, seed, off, (const bf16_t*)dh_in, part, pacc);
   else
     hipLaunchKernelGGL((add_ln_bwd_kernel<VEC, false>), dim3(nb), dim3(256), 0, s, (const bf16_t*)dout,
-                       (const bf16_t*)hsave, mean, rstd, (const bf16_t*)g, (bf16_t*)dres, (bf16_t*)dy,
-                       dy ? dyb : nullptr, dg, db, R, p, seed, off, (const bf16_t*)dh_in, part);
-  if (two_stage) {
-    const int nacc = (dy && dyb) ? 3 : 2;
-    const int nseg = nb >= 256 ? 16 : nb >= 32 ? 4 : 1;
-    hipLaunchKernelGGL(ln_colreduce_kernel, dim3(D / 64, nacc, nseg), dim3(256), 0, s, part, nb, D, dg, db,
-                       dy ? dyb : nullptr, 3);
-  }
+                       (const bf16_t*)hsave, mean, rstd, (const bf16_t*)g, (bf16_t*)dres, (bf16_t*)dy, dyb_k, dg,
+                       db, R, p, seed, off, (const bf16_t*)dh_in, part, pacc);
+  if (two_stage && reduce) ln_colreduce_launch(part, nb, D, dg, db, dyb_k, s);
+}
+
+bool launch_ln_colreduce(const float* part, int64_t R, int D, float* dg, float* db, float* dyb, hipStream_t s) {
+  const int64_t nb = ln_bwd_two_stage_blocks(R, D);
+  if (nb <= 0 || D % 64) return false;
+  ln_colreduce_launch(part, (int)nb, D, dg, db, dyb, s);
+  return true;
 }
 
 // dst[c] += sum_r part[r][c] (fp32 [rows][cols] partials, cols % 64 == 0): the bias
@@ -564,9 +586,10 @@ bool launch_colsum_acc(const float* part, int rows, int cols, float* dst, hipStr
 bool launch_add_ln_bwd(const uint16_t* dout, const uint16_t* hsave, const float* mean,
                        const float* rstd, const uint16_t* g, uint16_t* dres, uint16_t* dy, float* dyb,
                        float* dg, float* db, int64_t R, int D, float p, uint32_t seed, uint32_t off,
-                       hipStream_t s, const uint16_t* dh_in, bool post, int zero_mask, float* ws) {
+                       hipStream_t s, const uint16_t* dh_in, bool post, int zero_mask, float* ws,
+                       int part_mode) {
   DPA_LN_DISPATCH(D, ln_bwd_impl, dout, hsave, mean, rstd, g, dres, dy, dyb, dg, db, R, p, seed,
-                  off, dh_in, post, zero_mask, s, ws)
+                  off, dh_in, post, zero_mask, s, ws, part_mode)
   return true;
 }
 

@@ -178,8 +178,18 @@ class _WgradDeferral:
         # micro-batch - DiffuSeq-XL's 1024-sample chunks hold ~100 GB of Linear operands -
         # gains nothing from deferral and must not double its memory)
         self.budget_bytes = int(float(os.environ.get("DPA_DEFER_WGRAD_GB", "32")) * (1 << 30))
-        self.stats = {"deferred": 0, "multi_launches": 0, "segments": 0}
+        self.stats = {"deferred": 0, "multi_launches": 0, "segments": 0, "ln_deferred": 0, "ln_reduces": 0,
+                      "bias_deferred": 0, "bias_reduces": 0}
         self.stream = None  # side stream for the un-armed micro-batches' launches (trainer-set)
+        # Column-sum deferral (same window): a LayerNorm backward at 8192 rows writes 1024
+        # block partials of its dgamma / dbeta / dy column sums and a second kernel reduces
+        # them (~7 us, on the backward chain, 26 per micro-batch); a fused dact GEMM's bias
+        # partials likewise.  While deferring, the LN kernel ADDS its partials onto a per-site
+        # buffer and the dact GEMM writes into consecutive slots of a per-bias buffer; one
+        # reduction per site runs at flush().
+        self.ln_sites = {}    # id(gamma) -> [buf, R, D, dg, db, dyb, filled]
+        self.bias_sites = {}  # id(bias) -> [buf, rows, K, gb, used]
+        self.colsum = os.environ.get("DPA_DEFER_COLSUM", "1") != "0"
 
     @staticmethod
     def _nbytes(segs):
@@ -233,17 +243,98 @@ class _WgradDeferral:
         return True
 
     def flush(self):
-        """Run every held weight gradient (on the current stream)."""
+        """Run every held weight gradient (on the side stream when set) and every deferred
+        column-sum reduction (on the current stream)."""
         pend, self.pending = self.pending, {}
         self.held_bytes = 0
         for p, bias, segs in pend.values():
             self._run(p, bias, segs, side=True)
+        for e in self.ln_sites.values():
+            self._ln_reduce(e)
+        for e in self.bias_sites.values():
+            self._bias_reduce(e)
 
     def drop(self):
         """Forget held operands (an abandoned backward whose gradients are discarded)."""
         self.pending = {}
         self.held_bytes = 0
         self.active = False
+        for e in self.ln_sites.values():
+            e[6] = False
+        for e in self.bias_sites.values():
+            e[4] = 0
+
+    # ---- column sums -----------------------------------------------------------------
+    def _colsum_on(self):
+        return self.colsum and self.active and self.depth >= 2
+
+    @staticmethod
+    def _same(a, b):
+        return (a is None) == (b is None) and (a is None or a.data_ptr() == b.data_ptr())
+
+    def _ln_reduce(self, e):
+        if e[6]:
+            e[0].record_stream(torch.cuda.current_stream(e[0].device))
+            get_ext().ln_colreduce(e[0], e[1], e[2], e[3], e[4], e[5])
+            e[6] = False
+            self.stats["ln_reduces"] += 1
+
+    def ln_part(self, gamma, R, D, dg, db, dyb):
+        """(partial buffer, accumulate) for a deferred LayerNorm backward of gamma's site, or
+        (None, False).  dg / db (/ dyb) must be the .grad buffers the reduction adds onto."""
+        if not self._colsum_on() or dg is None or db is None:
+            return None, False
+        n = get_ext().ln_bwd_partials(R, D)
+        if n <= 0:
+            return None, False
+        e = self.ln_sites.get(id(gamma))
+        if e is not None and (e[1] != R or e[2] != D or not self._same(e[3], dg) or not self._same(e[4], db)
+                              or not self._same(e[5], dyb)):
+            self._ln_reduce(e)
+            buf = e[0] if e[0].numel() == n else None
+            e = None
+        else:
+            buf = None if e is None else e[0]
+        if e is None:
+            if buf is None:
+                buf = torch.empty(n, dtype=torch.float32, device=dg.device)
+            e = [buf, R, D, dg, db, dyb, False]
+            self.ln_sites[id(gamma)] = e
+        buf.record_stream(torch.cuda.current_stream(buf.device))
+        acc = e[6]
+        e[6] = True
+        self.stats["ln_deferred"] += 1
+        return buf, acc
+
+    BIAS_SLOTS = 8
+
+    def _bias_reduce(self, e):
+        if e[4]:
+            e[0].record_stream(torch.cuda.current_stream(e[0].device))
+            get_ext().colsum_acc(e[0][: e[4] * e[1]], e[3])
+            e[4] = 0
+            self.stats["bias_reduces"] += 1
+
+    def bias_part(self, bias, gb, T, K):
+        """A [(T/256)*2, K] fp32 slot for a fused dact GEMM's bias partials (reduced onto gb
+        at flush or when the site's slots are full), or None."""
+        if not self._colsum_on() or gb is None or T % 256:
+            return None
+        rows = (T // 256) * 2
+        e = self.bias_sites.get(id(bias))
+        if e is not None and (e[1] != rows or e[2] != K or not self._same(e[3], gb)):
+            self._bias_reduce(e)
+            e = None
+        if e is None:
+            e = [torch.empty(self.BIAS_SLOTS * rows, K, dtype=torch.float32, device=gb.device), rows, K, gb, 0]
+            self.bias_sites[id(bias)] = e
+        if e[4] == self.BIAS_SLOTS:
+            self._bias_reduce(e)
+        e[0].record_stream(torch.cuda.current_stream(e[0].device))
+        slot = e[0][e[4] * rows:(e[4] + 1) * rows]
+        e[4] += 1
+        self.stats["bias_deferred"] += 1
+        return slot
 
 
 WGRAD_DEFER = _WgradDeferral()
@@ -455,11 +546,13 @@ def _mlp_bwd(dy2, x2, w1_16, w2_16, h, z1, params, cfg, need_dx, db2=None, dx_ac
     dz1 = db1 = None
     if act != "none" and r2[1] and _gemm_shape_ok(dy2, w2_16.shape[1]):
         gb1 = _grad_acc(b1)
-        dz1, db1 = get_ext().gemm_nn_dact(dy2, w2_16, aux, _ACTS.index(act), b1 is not None, db_acc=gb1)
+        slot = WGRAD_DEFER.bias_part(b1, gb1, dy2.shape[0], w2_16.shape[1]) if b1 is not None else None
+        dz1, db1 = get_ext().gemm_nn_dact(dy2, w2_16, aux, _ACTS.index(act), b1 is not None, db_acc=gb1,
+                                          part_out=slot)
         if dz1 is None:
             db1 = None
         elif gb1 is not None:
-            db1 = _ACCUMULATED  # fc1's bias gradient went straight onto b1.grad
+            db1 = _ACCUMULATED  # fc1's bias gradient went onto b1.grad (or its deferred slot)
     if dz1 is None:
         db1 = None
         dh = _dgrad(dy2, w2_16, r2[1])
@@ -533,9 +626,13 @@ class _MLPLNFn(torch.autograd.Function):
         lw, lb = ctx.ln_params
         b2 = ctx.params[3]
         gb2 = _grad_acc(b2)
+        dg, dbl = _grad_acc(lw), _grad_acc(lb)
+        d2 = dout.reshape(-1, dout.shape[-1]).contiguous()
+        part, pacc = (WGRAD_DEFER.ln_part(lw, d2.shape[0], d2.shape[1], dg, dbl, gb2)
+                      if gb2 is not None else (None, False))
         dres, dy, dlw, dlb, dyb = get_ext().add_ln_bwd(
-            dout.reshape(-1, dout.shape[-1]).contiguous(), hsave, mean, rstd, lw16, float(p), seed,
-            off, need_dx, True, True, dg_acc=_grad_acc(lw), db_acc=_grad_acc(lb), dyb_acc=gb2)
+            d2, hsave, mean, rstd, lw16, float(p), seed, off, need_dx, True, True, dg_acc=dg, db_acc=dbl,
+            dyb_acc=gb2, part_buf=part, part_acc=pacc)
         if b2 is not None and dyb is None:
             dyb = _ACCUMULATED  # fc2's bias gradient went onto b2.grad in the LN kernel
         dx, dw1, db1, dw2, db2 = _mlp_bwd(dy, x2, w1_16, w2_16, h, z1, ctx.params, ctx.cfg, need_dx,
@@ -593,9 +690,13 @@ class _AttnLNFn(torch.autograd.Function):
         need_dx = ctx.needs_input_grad[0]
         ext = get_ext()
         lw, lb = ctx.ln_params
+        dg, dbl, gbo = _grad_acc(lw), _grad_acc(lb), _grad_acc(bo)
+        d2 = dout.reshape(-1, dout.shape[-1]).contiguous()
+        part, pacc = (WGRAD_DEFER.ln_part(lw, d2.shape[0], d2.shape[1], dg, dbl, gbo)
+                      if gbo is not None else (None, False))
         dres, dy, dlw, dlb, dyb = ext.add_ln_bwd(
-            dout.reshape(-1, dout.shape[-1]).contiguous(), hsave, mean, rstd, lw16, float(p), seed_l,
-            off_l, need_dx, True, True, dg_acc=_grad_acc(lw), db_acc=_grad_acc(lb), dyb_acc=_grad_acc(bo))
+            d2, hsave, mean, rstd, lw16, float(p), seed_l, off_l, need_dx, True, True, dg_acc=dg, db_acc=dbl,
+            dyb_acc=gbo, part_buf=part, part_acc=pacc)
         if bo is not None and dyb is None:
             dyb = _ACCUMULATED  # the out projection's bias gradient went onto bo.grad
         # out projection
@@ -732,10 +833,13 @@ class _AddLNExFn(torch.autograd.Function):
         if dout is None:
             dout = torch.zeros_like(hsave)
         w, b = ctx.wb
+        dg, dbl = _grad_acc(w), _grad_acc(b)
+        dout = dout.contiguous()
+        part, pacc = WGRAD_DEFER.ln_part(w, dout.shape[0], dout.shape[1], dg, dbl, None)
         dres, dy, dw, db, _ = get_ext().add_ln_bwd(
-            dout.contiguous(), hsave, mean, rstd, w16, float(p), seed, offset, has_res and ng[1], need_dy,
+            dout, hsave, mean, rstd, w16, float(p), seed, offset, has_res and ng[1], need_dy,
             False, dh_in=None if dh is None else dh.contiguous(), post=bool(post),
-            dg_acc=_grad_acc(w), db_acc=_grad_acc(b))
+            dg_acc=dg, db_acc=dbl, part_buf=part, part_acc=pacc)
         dpos = dtemb = None
         if need_dy:
             H = dy.shape[-1]

@@ -60,6 +60,57 @@ def test_add_ln_dropout_statistics_and_consistency(R, D):
     torch.testing.assert_close(dyb, dy.float().sum(0), rtol=1e-3, atol=1e-2)
 
 
+@pytest.mark.parametrize("R,D", [(2048, 768), (8192, 768), (1024, 2048)])
+def test_add_ln_bwd_deferred_partials(R, D):
+    """add_ln_bwd(part_buf=...) over three micro-batches (store, add, add) and one
+    ln_colreduce give the dgamma / dbeta / colsum(dy) that three immediate calls accumulate."""
+    ext = _ext()
+    n = ext.ln_bwd_partials(R, D)
+    assert n > 0
+    torch.manual_seed(0)
+    g = (1 + 0.1 * torch.randn(D, device="cuda")).bfloat16()
+    b = (0.1 * torch.randn(D, device="cuda")).bfloat16()
+    acc_ref = [torch.zeros(D, device="cuda") for _ in range(3)]
+    acc_def = [torch.zeros(D, device="cuda") for _ in range(3)]
+    part = torch.full((n,), float("nan"), device="cuda")  # stale contents must be overwritten
+    for k in range(3):
+        y = torch.randn(R, D, device="cuda").bfloat16()
+        r = torch.randn(R, D, device="cuda").bfloat16()
+        _, hs, mean, rstd = ext.add_ln_fwd(y, r, g, b, 0.1, 1e-12, 5, k)
+        dout = torch.randn(R, D, device="cuda").bfloat16()
+        d0 = ext.add_ln_bwd(dout, hs, mean, rstd, g, 0.1, 5, k, True, True, True, dg_acc=acc_ref[0],
+                            db_acc=acc_ref[1], dyb_acc=acc_ref[2])
+        d1 = ext.add_ln_bwd(dout, hs, mean, rstd, g, 0.1, 5, k, True, True, True, dg_acc=acc_def[0],
+                            db_acc=acc_def[1], dyb_acc=acc_def[2], part_buf=part, part_acc=k > 0)
+        assert torch.equal(d0[0], d1[0]) and torch.equal(d0[1], d1[1])
+    assert all(torch.count_nonzero(a).item() == 0 for a in acc_def)  # nothing reduced yet
+    ext.ln_colreduce(part, R, D, acc_def[0], acc_def[1], acc_def[2])
+    for a, e in zip(acc_def, acc_ref):
+        torch.testing.assert_close(a, e, rtol=1e-4, atol=1e-4 * e.abs().max().item())
+
+
+def test_gemm_nn_dact_kept_bias_partials():
+    """gemm_nn_dact(part_out=slot) for two micro-batches, one colsum_acc over both slots ==
+    the bias gradient accumulated immediately."""
+    ext = _ext()
+    torch.manual_seed(0)
+    T, N, K = 1024, 256, 1024
+    W = (0.05 * torch.randn(N, K, device="cuda")).bfloat16()
+    ref = torch.zeros(K, device="cuda")
+    got = torch.zeros(K, device="cuda")
+    rows = (T // 256) * 2
+    buf = torch.empty(2 * rows, K, device="cuda")
+    for k in range(2):
+        dy = torch.randn(T, N, device="cuda").bfloat16()
+        aux = torch.randn(T, K, device="cuda").bfloat16()
+        dz0, _ = ext.gemm_nn_dact(dy, W, aux, 1, True, db_acc=ref)
+        dz1, db1 = ext.gemm_nn_dact(dy, W, aux, 1, True, db_acc=got, part_out=buf[k * rows:(k + 1) * rows])
+        assert db1 is None and torch.equal(dz0, dz1)
+    assert torch.count_nonzero(got).item() == 0
+    ext.colsum_acc(buf, got)
+    torch.testing.assert_close(got, ref, rtol=1e-4, atol=1e-4 * ref.abs().max().item())
+
+
 @pytest.mark.parametrize("act", ["none", "gelu", "tanh", "silu"])
 def test_linear_bias_act_autograd(act):
     torch.manual_seed(0)
