@@ -56,6 +56,9 @@ def parse():
                          "allocator pools in the first steps)")
     ap.add_argument("--ref-steps", type=int, default=3,
                     help="also time this many steps of the reference 32 x 64 schedule (0 = skip)")
+    ap.add_argument("--ref-windows", type=int, default=1,
+                    help="time the reference schedule in this many back-to-back windows of --ref-steps "
+                         "(the mean over all is reported, each window under windows_ms)")
     ap.add_argument("--seq-len", type=int, default=128)
     ap.add_argument("--config-name", default="bert-base-uncased")
     ap.add_argument("--model", default="diffuseq")
@@ -200,10 +203,39 @@ def main():
         loop.exec_microbatch = a.microbatch
         for _ in range(max(1, a.ref_warmup)):  # warm the small-shape kernels and stream pools
             one_step()
-        e = timed(a.ref_steps)
-        ref_sched = {"exec_microbatch": a.microbatch, "steps": a.ref_steps,
-                     "ms_per_step": round(e / a.ref_steps * 1e3, 3),
-                     "value": round(a.ref_steps / e * world, 4)}
+        diag = []
+        if a.ref_windows > 1:  # per-window diagnostics: allocator growth and Python GC time
+            import gc
+            gc_t = [0.0, 0.0]
+
+            def _gc_cb(phase, info):
+                if phase == "start":
+                    gc_t[1] = time.perf_counter()
+                else:
+                    gc_t[0] += time.perf_counter() - gc_t[1]
+            gc.callbacks.append(_gc_cb)
+
+        def win():
+            if a.ref_windows <= 1 or dev.type != "cuda":
+                return timed(a.ref_steps)
+            m0 = torch.cuda.memory_stats(dev)
+            g0 = gc_t[0]
+            e = timed(a.ref_steps)
+            m1 = torch.cuda.memory_stats(dev)
+            diag.append({k: m1.get(k, 0) - m0.get(k, 0) for k in ("num_device_alloc", "num_device_free",
+                                                                  "num_alloc_retries")})
+            diag[-1]["gc_ms"] = round((gc_t[0] - g0) * 1e3, 1)
+            diag[-1]["alloc_gb"] = round(torch.cuda.memory_allocated(dev) / 2 ** 30, 2)
+            diag[-1]["reserved_gb"] = round(torch.cuda.memory_reserved(dev) / 2 ** 30, 2)
+            return e
+        wins = [win() for _ in range(max(1, a.ref_windows))]
+        e, n_ref = sum(wins), a.ref_steps * len(wins)
+        ref_sched = {"exec_microbatch": a.microbatch, "steps": n_ref,
+                     "ms_per_step": round(e / n_ref * 1e3, 3),
+                     "value": round(n_ref / e * world, 4)}
+        if len(wins) > 1:
+            ref_sched["windows_ms"] = [round(w / a.ref_steps * 1e3, 2) for w in wins]
+            ref_sched["windows_diag"] = diag
 
     ms = elapsed / a.steps * 1e3
     steps_per_s = a.steps / elapsed

@@ -610,9 +610,14 @@ class TrainLoop:
         def stream_of(k):  # the last chunk on the current stream
             return streams[(nch - 1 - k) % 2]
 
-        # grid cap of the forward stream's persistent GEMMs (DPA_OVERLAP_FWD_CAP, 0 = none):
-        # the concurrent backward's kernels then find free CUs
-        fwd_cap = int(os.environ.get("DPA_OVERLAP_FWD_CAP", "0"))
+        # grid cap of the forward stream's persistent GEMMs (DPA_OVERLAP_FWD_CAP, 0 = none;
+        # default half the CUs): the concurrent backward's kernels - the critical chain - then
+        # always find free CUs.  Uncapped, a forward GEMM of 1.5 waves of workgroups can hold
+        # every CU while the backward waits; same-box runs of the 32 x 64 schedule spread
+        # 227-306 ms/step uncapped vs 223.4-226.3 capped at 128 (profiles/ref_schedule_fwd_cap_r3.txt)
+        cap_env = os.environ.get("DPA_OVERLAP_FWD_CAP", "")
+        fwd_cap = (int(cap_env) if cap_env.strip() else
+                   torch.cuda.get_device_properties(self.device).multi_processor_count // 2)
         ext = None
         if fwd_cap > 0:
             from distributed_pipeline_amd.ops._ext import get_ext
