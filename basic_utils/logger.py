@@ -233,6 +233,11 @@ def logkv_mean(key, val):
     get_current().logkv_mean(key, val)
 
 
+def logkv_mean_sum(key, total, count):
+    """Record ``count`` values summing to ``total`` for ``key`` (as that many logkv_mean calls)."""
+    get_current().logkv_mean_sum(key, total, count)
+
+
 def logkvs(d):
     for k, v in d.items():
         logkv(k, v)
@@ -350,6 +355,16 @@ class _MeanAcc:
             self.total = self.total + val
         self.count += 1
 
+    def add_sum(self, total, count):
+        """``count`` recorded values at once, given their sum (a device scalar or float)."""
+        if _is_tensor(total):
+            total = total.detach().float()
+            self.total = total.clone() if not _is_tensor(self.total) and self.total == 0.0 \
+                else self.total + total
+        else:
+            self.total = self.total + total
+        self.count += count
+
     def value(self):
         return self.total / max(self.count, 1)
 
@@ -389,6 +404,19 @@ class Logger(object):
     def logkv(self, key, val):
         self._means.pop(key, None)
         self.name2val[key] = val
+
+    def logkv_mean_sum(self, key, total, count):
+        """As ``count`` logkv_mean calls whose values sum to ``total``."""
+        acc = self._means.get(key)
+        if acc is None:
+            acc = self._means[key] = _MeanAcc()
+            if key in self.name2val and self.name2cnt.get(key, 0):
+                acc.total = self.name2val[key] * self.name2cnt[key]
+                acc.count = self.name2cnt[key]
+        acc.add_sum(total, count)
+        self.name2cnt[key] = acc.count
+        if not _is_tensor(acc.total):
+            self.name2val[key] = acc.value()
 
     def logkv_mean(self, key, val):
         acc = self._means.get(key)

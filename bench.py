@@ -182,11 +182,14 @@ def main():
 
     exec_used = loop.exec_microbatch
 
+    host = [0.0]  # host time to enqueue the last timed window (before its closing sync)
+
     def timed(n):
         sync()
         t = time.perf_counter()
         for _ in range(n):
             one_step()
+        host[0] = time.perf_counter() - t
         sync()
         e = time.perf_counter() - t
         if world > 1:
@@ -220,11 +223,15 @@ def main():
                 return timed(a.ref_steps)
             m0 = torch.cuda.memory_stats(dev)
             g0 = gc_t[0]
+            h0 = dict(getattr(loop, "host_time", {}))
             e = timed(a.ref_steps)
             m1 = torch.cuda.memory_stats(dev)
             diag.append({k: m1.get(k, 0) - m0.get(k, 0) for k in ("num_device_alloc", "num_device_free",
                                                                   "num_alloc_retries")})
             diag[-1]["gc_ms"] = round((gc_t[0] - g0) * 1e3, 1)
+            diag[-1]["host_ms_per_step"] = round(host[0] / a.ref_steps * 1e3, 1)
+            for k, v in getattr(loop, "host_time", {}).items():
+                diag[-1][f"host_{k}_ms_per_step"] = round((v - h0.get(k, 0.0)) / a.ref_steps * 1e3, 1)
             diag[-1]["alloc_gb"] = round(torch.cuda.memory_allocated(dev) / 2 ** 30, 2)
             diag[-1]["reserved_gb"] = round(torch.cuda.memory_reserved(dev) / 2 ** 30, 2)
             return e

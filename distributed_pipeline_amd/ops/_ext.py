@@ -71,9 +71,17 @@ def gpu_present():
     return torch.cuda.is_available()
 
 
+_REQUIRED = None  # default of get_ext(required=None), evaluated once per process
+
+
 def get_ext(required=None):
-    """Return the ``_C`` module.  ``required`` defaults to "a GPU is present"."""
-    global _EXT, _ERR
+    """Return the ``_C`` module.  ``required`` defaults to "a GPU is present".
+
+    Called once or more per op on the hot path (a reference-schedule micro-batch makes ~200
+    calls): once loaded, the common case returns before any device query or env read."""
+    global _EXT, _ERR, _REQUIRED
+    if required is None and _EXT is not None:
+        return _EXT if _NATIVE_ENABLED else None
     if not _NATIVE_ENABLED and not required:
         return None
     if _EXT is None and _ERR is None:
@@ -86,7 +94,9 @@ def get_ext(required=None):
         except Exception as exc:  # noqa: BLE001
             _ERR = exc
     if required is None:
-        required = gpu_present() and os.environ.get("DPA_ALLOW_NO_EXT", "0") != "1"
+        if _REQUIRED is None:
+            _REQUIRED = gpu_present() and os.environ.get("DPA_ALLOW_NO_EXT", "0") != "1"
+        required = _REQUIRED
     if _EXT is None and required:
         raise RuntimeError(
             "distributed_pipeline_amd native extension is not built/loadable "

@@ -181,6 +181,8 @@ class _WgradDeferral:
         self.stats = {"deferred": 0, "multi_launches": 0, "segments": 0, "ln_deferred": 0, "ln_reduces": 0,
                       "bias_deferred": 0, "bias_reduces": 0}
         self.stream = None  # side stream for the un-armed micro-batches' launches (trainer-set)
+        self.cur = None     # the stream the current backward runs on (trainer-set, optional)
+        self._retired = []  # replaced column-sum buffers (other streams may still use them)
         # Column-sum deferral (same window): a LayerNorm backward at 8192 rows writes 1024
         # block partials of its dgamma / dbeta / dy column sums and a second kernel reduces
         # them (~7 us, on the backward chain, 26 per micro-batch); a fused dact GEMM's bias
@@ -191,9 +193,12 @@ class _WgradDeferral:
         self.bias_sites = {}  # id(bias) -> [buf, rows, K, gb, used]
         self.colsum = os.environ.get("DPA_DEFER_COLSUM", "1") != "0"
 
-    @staticmethod
-    def _nbytes(segs):
-        return sum(dz.numel() * dz.element_size() + x2.numel() * x2.element_size() for dz, x2 in segs)
+    def _cur(self, t):
+        """The current stream (``cur``: set by the trainer per micro-batch, saving the
+        device-index lookup of ``torch.cuda.current_stream`` on every offer)."""
+        if self.cur is not None:
+            return self.cur
+        return torch.cuda.current_stream(t.device) if t.is_cuda else None
 
     def _run(self, p, bias, segs, side=False):
         """Launch the held segments.  ``side``: on ``self.stream`` (ordered after the current
@@ -203,7 +208,7 @@ class _WgradDeferral:
         ext = get_ext()
         gw = p.grad
         gb = bias.grad if (bias is not None and bias.requires_grad) else None
-        cur = torch.cuda.current_stream(segs[0][0].device) if segs[0][0].is_cuda else None
+        cur = self._cur(segs[0][0])
         run_on = cur
         if cur is not None and side and self.stream is not None:
             run_on = self.stream
@@ -226,16 +231,19 @@ class _WgradDeferral:
             return False
         key = id(p)
         ent = self.pending.pop(key, None)
-        segs = ent[2] if ent is not None else []
-        self.held_bytes -= self._nbytes(segs)
-        if segs and (segs[0][0].shape != dz.shape or segs[0][1].shape != x2.shape
-                     or (ent[1] is not None) != (bias is not None)):
-            self._run(ent[0], ent[1], segs)
-            segs = []
+        if ent is not None:
+            segs, nb = ent[2], ent[3]
+            self.held_bytes -= nb
+            if (segs[0][0].shape != dz.shape or segs[0][1].shape != x2.shape
+                    or (ent[1] is not None) != (bias is not None)):
+                self._run(ent[0], ent[1], segs)
+                segs, nb = [], 0
+        else:
+            segs, nb = [], 0
         segs.append((dz, x2))
-        nb = self._nbytes(segs)
+        nb += dz.numel() * dz.element_size() + x2.numel() * x2.element_size()
         if self.active and len(segs) < self.depth and self.held_bytes + nb <= self.budget_bytes:
-            self.pending[key] = (p, bias, segs)
+            self.pending[key] = (p, bias, segs, nb)
             self.held_bytes += nb
             self.stats["deferred"] += 1
             return True
@@ -247,7 +255,7 @@ class _WgradDeferral:
         column-sum reduction (on the current stream)."""
         pend, self.pending = self.pending, {}
         self.held_bytes = 0
-        for p, bias, segs in pend.values():
+        for p, bias, segs, _ in pend.values():
             self._run(p, bias, segs, side=True)
         for e in self.ln_sites.values():
             self._ln_reduce(e)
@@ -274,7 +282,6 @@ class _WgradDeferral:
 
     def _ln_reduce(self, e):
         if e[6]:
-            e[0].record_stream(torch.cuda.current_stream(e[0].device))
             get_ext().ln_colreduce(e[0], e[1], e[2], e[3], e[4], e[5])
             e[6] = False
             self.stats["ln_reduces"] += 1
@@ -292,6 +299,8 @@ class _WgradDeferral:
                               or not self._same(e[5], dyb)):
             self._ln_reduce(e)
             buf = e[0] if e[0].numel() == n else None
+            if buf is None:
+                self._retired.append(e[0])
             e = None
         else:
             buf = None if e is None else e[0]
@@ -300,7 +309,8 @@ class _WgradDeferral:
                 buf = torch.empty(n, dtype=torch.float32, device=dg.device)
             e = [buf, R, D, dg, db, dyb, False]
             self.ln_sites[id(gamma)] = e
-        buf.record_stream(torch.cuda.current_stream(buf.device))
+        # the site buffers live as long as this object (replaced ones in _retired): no
+        # record_stream needed when the backward alternates streams
         acc = e[6]
         e[6] = True
         self.stats["ln_deferred"] += 1
@@ -310,7 +320,6 @@ class _WgradDeferral:
 
     def _bias_reduce(self, e):
         if e[4]:
-            e[0].record_stream(torch.cuda.current_stream(e[0].device))
             get_ext().colsum_acc(e[0][: e[4] * e[1]], e[3])
             e[4] = 0
             self.stats["bias_reduces"] += 1
@@ -324,13 +333,13 @@ class _WgradDeferral:
         e = self.bias_sites.get(id(bias))
         if e is not None and (e[1] != rows or e[2] != K or not self._same(e[3], gb)):
             self._bias_reduce(e)
+            self._retired.append(e[0])
             e = None
         if e is None:
             e = [torch.empty(self.BIAS_SLOTS * rows, K, dtype=torch.float32, device=gb.device), rows, K, gb, 0]
             self.bias_sites[id(bias)] = e
         if e[4] == self.BIAS_SLOTS:
             self._bias_reduce(e)
-        e[0].record_stream(torch.cuda.current_stream(e[0].device))
         slot = e[0][e[4] * rows:(e[4] + 1) * rows]
         e[4] += 1
         self.stats["bias_deferred"] += 1

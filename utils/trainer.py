@@ -72,6 +72,11 @@ def _atomic_torch_save(obj, path):
 class TrainLoop:
 
     # ------------------------------------------------------------------ hooks
+    _loss_log_buf = None  # a list while a workload batches its loss logging (see _flush_loss_log)
+
+    def _flush_loss_log(self):
+        self._loss_log_buf = None
+
     def log_loss_dict(self, mode, losses, *args, **kwargs):  # mode: train or eval
         """Log a dict of per-sample loss tensors (override for custom keys)."""
         prefix = "eval_" if mode == "eval" else ""
@@ -185,6 +190,9 @@ class TrainLoop:
         # ...and hold each Linear's weight-gradient operands for defer_wgrad micro-batches, run as
         # one multi-segment split-K GEMM (ops/nn.py _WgradDeferral; DPA_DEFER_WGRAD overrides)
         self.defer_wgrad = max(0, min(4, int(os.environ.get("DPA_DEFER_WGRAD", defer_wgrad))))
+        # host seconds spent enqueueing the overlapped schedule's forwards / backwards (the
+        # reference schedule's 32 micro-batches per step can be host-bound)
+        self.host_time = {"fwd": 0.0, "bwd": 0.0}
 
         self.step = 0
         self.resume_step = 0
@@ -633,6 +641,13 @@ class TrainLoop:
                     ext.set_gemmp_grid_cap(0)
 
         def fwd_(k):
+            t0 = time.perf_counter()
+            try:
+                return fwd_s(k)
+            finally:
+                self.host_time["fwd"] += time.perf_counter() - t0
+
+        def fwd_s(k):
             with torch.cuda.stream(stream_of(k)):
                 with self._range("forward"):
                     if self.use_ddp:
@@ -659,6 +674,7 @@ class TrainLoop:
         else:
             defer.stream = None
         done = None
+        self._loss_log_buf = []
         try:
             nxt = fwd(0)
             for k in range(nch):
@@ -668,6 +684,7 @@ class TrainLoop:
                 with torch.cuda.stream(st):
                     if done is not None:
                         st.wait_event(done)
+                    defer.cur = st
                     for key, v in state.items():
                         setattr(self, key, v)
                     last = k == nch - 1
@@ -681,19 +698,28 @@ class TrainLoop:
                     if last and self.use_ddp:
                         self.ddp_model.arm_for_backward()
                     self.loss_scale = self._chunk_loss_scale(starts[k], min(n, starts[k] + self.exec_microbatch), n)
+                    t0 = time.perf_counter()
                     with self._range("backward"):
                         self.backward_from_losses(losses)
+                    self.host_time["bwd"] += time.perf_counter() - t0
                     done = torch.cuda.Event()
                     done.record(st)
         except BaseException:
             defer.drop()  # the abandoned backward's gradients are discarded by the caller
+            self._loss_log_buf = None  # ... and its logged losses (as the sequential retry)
             raise
         finally:
             defer.active = False
+            defer.cur = None
             if defer.stream is not None:
                 cur.wait_stream(defer.stream)
             defer.stream = None
         cur.wait_stream(side)
+        # the buffered loss terms of the side stream's chunks are read on this stream now
+        for _, t, w, vals in self._loss_log_buf or ():
+            for x in (t, w, *vals):
+                x.record_stream(cur)
+        self._flush_loss_log()
 
     def _chunk_loss_scale(self, start, end, n):
         """Factor that turns the MEAN loss of executed chunk [start, end) into the sum of
@@ -1022,19 +1048,44 @@ class DiffusionTrainLoop(TrainLoop):
 
     def log_loss_dict(self, mode, losses, *args, **kwargs):
         t = self._last_t
-        prefix = "eval_" if mode == "eval" else ""
         w = self._last_weights
-        T = self.diffusion.num_timesteps
-        q = (4 * t // T).clamp_(0, 3)
         keys = [k for k in ("loss", "mse", "nll", "decoder_nll") if k in losses]
-        vals = torch.stack([losses[k].detach().float() * (w if k == "loss" else 1.0) for k in keys])
-        onehot = torch.nn.functional.one_hot(q, 4).float()                    # [B, 4]
+        if mode == "train" and self._loss_log_buf is not None:
+            # the overlapped schedule logs its chunks in one batched pass at the end of the
+            # step (a 32-chunk reference step otherwise spends ~1 ms of host time per chunk here)
+            self._loss_log_buf.append((tuple(keys), t, w, [losses[k].detach() for k in keys]))
+            return
+        self._log_losses(mode, keys, [(t, w, [losses[k].detach() for k in keys])])
+
+    def _log_losses(self, mode, keys, entries):
+        """DiffuSeq's per-term means and ``{term}_q{i}`` quartile means of ``entries`` =
+        [(t, weights, [per-sample term tensors])] (each entry one logged chunk: the term
+        means are averaged over chunks, the quartile means over samples)."""
+        prefix = "eval_" if mode == "eval" else ""
+        T = self.diffusion.num_timesteps
+        t = entries[0][0] if len(entries) == 1 else torch.cat([e[0] for e in entries])
+        w = entries[0][1] if len(entries) == 1 else torch.cat([e[1] for e in entries])
+        vals = torch.stack([(entries[0][2][i] if len(entries) == 1 else torch.cat([e[2][i] for e in entries]))
+                            .float() * (w if k == "loss" else 1.0) for i, k in enumerate(keys)])
+        q = (4 * t // T).clamp_(0, 3)
+        onehot = torch.nn.functional.one_hot(q, 4).float()                    # [N, 4]
         qsum = vals @ onehot                                                    # [K, 4]
         qcnt = onehot.sum(0)                                                    # [4]
-        means = vals.mean(1)
+        n = len(entries)
+        means = vals.view(len(keys), n, -1).mean(2).sum(1)                     # sum of chunk means
         for i, k in enumerate(keys):
-            logger.logkv_mean(prefix + k, means[i])
+            logger.logkv_mean_sum(prefix + k, means[i], n)
         _QuartileAcc.add(prefix, keys, qsum, qcnt)
+
+    def _flush_loss_log(self):
+        buf, self._loss_log_buf = self._loss_log_buf, None
+        if not buf:
+            return
+        groups = {}
+        for keys, t, w, vals in buf:  # equal chunk sizes batch together (the usual case)
+            groups.setdefault((keys, t.shape[0]), []).append((t, w, vals))
+        for (keys, _), entries in groups.items():
+            self._log_losses("train", list(keys), entries)
 
 
 class _QuartileAcc:
