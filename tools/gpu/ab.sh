@@ -1,6 +1,6 @@
 #!/bin/bash
 # A/B of an environment switch on the headline bench, interleaved on one box:
-#   bash tools/gpu_ab.sh VAR VALUE_A VALUE_B [tests...]
+#   bash tools/gpu/ab.sh VAR VALUE_A VALUE_B [tests...]
 set -o pipefail
 cd "$GRAFT_REPO_ROOT"
 mkdir -p gpurun_out
