@@ -184,7 +184,7 @@ static std::vector<at::Tensor> add_ln_fwd(const at::Tensor& y, c10::optional<at:
                                           const at::Tensor& g, const at::Tensor& b, double p,
                                           double eps, int64_t seed, int64_t offset,
                                           c10::optional<at::Tensor> pos, c10::optional<at::Tensor> temb,
-                                          int64_t L, bool post) {
+                                          int64_t L, bool post, bool save_h) {
   CHECK_DEV(y); CHECK_BF16(y); CHECK_CONTIG(y); CHECK_BF16(g); CHECK_BF16(b);
   TORCH_CHECK(y.dim() == 2, "y must be [R, D]");
   const int64_t R = y.size(0);
@@ -210,12 +210,14 @@ static std::vector<at::Tensor> add_ln_fwd(const at::Tensor& y, c10::optional<at:
     tp = bf_ptr(*temb);
   }
   const c10::DeviceGuard guard(y.device());
-  at::Tensor out = at::empty_like(y), hs = at::empty_like(y);
+  // save_h = false: no bf16 copy of h (the backward reconstructs xhat from the output)
+  at::Tensor out = at::empty_like(y), hs = save_h ? at::empty_like(y) : at::Tensor();
   auto f32 = y.options().dtype(at::kFloat);
   at::Tensor mean = at::empty({R}, f32), rstd = at::empty({R}, f32);
   bool ok = dpa::launch_add_ln_fwd(bf_ptr(y), rp, bf_ptr(g), bf_ptr(b),
                                    reinterpret_cast<uint16_t*>(out.data_ptr()),
-                                   reinterpret_cast<uint16_t*>(hs.data_ptr()), mean.data_ptr<float>(),
+                                   save_h ? reinterpret_cast<uint16_t*>(hs.data_ptr()) : nullptr,
+                                   mean.data_ptr<float>(),
                                    rstd.data_ptr<float>(), R, D, (float)p, (float)eps,
                                    (uint32_t)seed, (uint32_t)offset, cur_stream(), pp, tp, (int)L, post);
   TORCH_CHECK(ok, "add_ln_fwd: unsupported hidden size ", D);
@@ -229,8 +231,16 @@ static std::vector<at::Tensor> add_ln_bwd(const at::Tensor& dout, const at::Tens
                                           bool want_dyb, c10::optional<at::Tensor> dh_in, bool post,
                                           c10::optional<at::Tensor> dg_acc, c10::optional<at::Tensor> db_acc,
                                           c10::optional<at::Tensor> dyb_acc, c10::optional<at::Tensor> part_buf,
-                                          bool part_acc) {
+                                          bool part_acc, c10::optional<at::Tensor> beta) {
   CHECK_DEV(dout); CHECK_BF16(dout); CHECK_CONTIG(dout); CHECK_BF16(hs); CHECK_CONTIG(hs);
+  TORCH_CHECK(hs.sizes() == dout.sizes(), "add_ln_bwd: hsave/out shape");
+  // beta given: `hs` is the LN output (forward with save_h=false), xhat = (out - beta) / gamma
+  const uint16_t* btp = nullptr;
+  if (beta.has_value() && beta->defined()) {
+    CHECK_BF16((*beta)); CHECK_CONTIG((*beta));
+    TORCH_CHECK(beta->numel() == dout.size(1) && !post, "add_ln_bwd: beta [D], pre-dropout placement only");
+    btp = bf_ptr(*beta);
+  }
   const uint16_t* dhp = nullptr;
   if (dh_in.has_value() && dh_in->defined()) {
     CHECK_BF16((*dh_in)); CHECK_CONTIG((*dh_in));
@@ -280,7 +290,7 @@ static std::vector<at::Tensor> add_ln_bwd(const at::Tensor& dout, const at::Tens
       need_dy ? reinterpret_cast<uint16_t*>(dy.data_ptr()) : nullptr,
       dyb.defined() ? dyb.data_ptr<float>() : nullptr,
       dg.data_ptr<float>(), db.data_ptr<float>(), R, D, (float)p, (uint32_t)seed, (uint32_t)offset,
-      cur_stream(), dhp, post, zero_mask, wsn > 0 ? ws.data_ptr<float>() : nullptr, part_mode);
+      cur_stream(), dhp, post, zero_mask, wsn > 0 ? ws.data_ptr<float>() : nullptr, part_mode, btp);
   TORCH_CHECK(ok, "add_ln_bwd: unsupported hidden size ", D);
   return {dres, dy, ext_g ? at::Tensor() : dg, ext_b ? at::Tensor() : db, ext_y ? at::Tensor() : dyb};
 }
@@ -842,13 +852,13 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         "LN(dropout(y [+pos] [+temb]) + res) (post: dropout(LN(...))) -> (out, hsave, mean, rstd)",
         py::arg("y"), py::arg("res"), py::arg("gamma"), py::arg("beta"), py::arg("p"), py::arg("eps"),
         py::arg("seed"), py::arg("offset"), py::arg("pos") = py::none(), py::arg("temb") = py::none(),
-        py::arg("L") = 1, py::arg("post") = false);
+        py::arg("L") = 1, py::arg("post") = false, py::arg("save_h") = true);
   m.def("add_ln_bwd", &add_ln_bwd, "backward of add_ln_fwd -> (dres, dy, dgamma, dbeta, colsum(dy))",
         py::arg("dout"), py::arg("hsave"), py::arg("mean"), py::arg("rstd"), py::arg("gamma"),
         py::arg("p"), py::arg("seed"), py::arg("offset"), py::arg("need_dres"), py::arg("need_dy"),
         py::arg("want_dy_colsum") = false, py::arg("dh_in") = py::none(), py::arg("post") = false,
         py::arg("dg_acc") = py::none(), py::arg("db_acc") = py::none(), py::arg("dyb_acc") = py::none(),
-        py::arg("part_buf") = py::none(), py::arg("part_acc") = false);
+        py::arg("part_buf") = py::none(), py::arg("part_acc") = false, py::arg("beta") = py::none());
   m.def("colsum_acc", &colsum_acc, "dst += colsum(part) (fp32 partials [rows, cols])");
   m.def("ln_bwd_partials", &ln_bwd_partials, "floats of add_ln_bwd's deferred partial buffer (0: none)");
   m.def("ln_colreduce", &ln_colreduce, "dg/db(/dyb) += column sums of add_ln_bwd partials",

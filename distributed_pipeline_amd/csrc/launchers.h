@@ -64,7 +64,8 @@ bool launch_add_ln_bwd(const uint16_t* dout, const uint16_t* hsave, const float*
                        const float* rstd, const uint16_t* g, uint16_t* dres, uint16_t* dy, float* dyb,
                        float* dg, float* db, int64_t R, int D, float p, uint32_t seed, uint32_t off,
                        hipStream_t s, const uint16_t* dh_in = nullptr, bool post = false,
-                       int zero_mask = 7, float* ws = nullptr, int part_mode = 0);
+                       int zero_mask = 7, float* ws = nullptr, int part_mode = 0,
+                       const uint16_t* beta = nullptr);  // beta: `hsave` is the LN output
 // the deferred second stage of part_mode 1/2 (R = the rows of each summed micro-batch)
 bool launch_ln_colreduce(const float* part, int64_t R, int D, float* dg, float* db, float* dyb, hipStream_t s);
 bool launch_colsum_acc(const float* part, int rows, int cols, float* dst, hipStream_t s);

@@ -111,6 +111,12 @@ __device__ __forceinline__ void dropout_keep(uint32_t seed, uint32_t offset, int
   }
 }
 
+// 1 / gamma for the output-based backward (xhat = (o - b) / gamma, the "memory-efficient"
+// LayerNorm backward).  A column whose bf16 gamma is exactly 0 carries no xhat in its output:
+// its xhat is taken as 0, which leaves that column's dgamma at 0 and drops its xhat * s2 term
+// from dx.  ops/nn.py (_LN_SAVE_OUT, DPA_LN_SAVE_OUT=0 restores the h copy) documents this.
+__device__ __forceinline__ float inv_gamma(float g) { return g != 0.f ? 1.f / g : 0.f; }
+
 template <int VEC>
 __global__ void __launch_bounds__(256) add_ln_fwd_kernel(
     const bf16_t* __restrict__ y, const bf16_t* __restrict__ res, const bf16_t* __restrict__ gamma,
@@ -185,19 +191,30 @@ __global__ void __launch_bounds__(256) add_ln_fwd_kernel(
 // (4 waves per SIMD: the LDS reduction buffer allows 4 blocks per CU); D > 768 keeps
 // 6 x VEC live accumulator/row floats: 4 waves per SIMD up to D = 768, 2-3 up to D = 1024.
 // D >= 1536 takes add_ln_bwd_rowblk_kernel (one row per block) instead.
-template <int VEC, bool POST>
+template <int VEC, bool POST, bool XO>
 __global__ void __launch_bounds__(256, VEC <= 12 ? 4 : VEC <= 16 ? 2 : 1) add_ln_bwd_kernel(
     const bf16_t* __restrict__ dout, const bf16_t* __restrict__ hsave,
     const float* __restrict__ mean_in, const float* __restrict__ rstd_in,
     const bf16_t* __restrict__ gamma, bf16_t* __restrict__ dres, bf16_t* __restrict__ dy,
     float* __restrict__ dyb, float* __restrict__ part_dg, float* __restrict__ part_db, int64_t R,
     float p, uint32_t seed, uint32_t offset, const bf16_t* __restrict__ dh_in, float* __restrict__ part,
-    bool part_acc) {
+    bool part_acc, const bf16_t* __restrict__ beta) {
   constexpr int D = VEC * 64;
   __shared__ float red[4][D];  // reused for dgamma, dbeta, dyb in turn
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   float g[VEC], adg[VEC], adb[VEC], ady[VEC];
   RowIO<VEC>::load(gamma, lane, g);
+  // XO: `hsave` is the LN output o = xhat * g + b (kept alive anyway as the next sublayer's
+  // input), so xhat = (o - b) / g and the forward writes no h copy.  beta and 1 / gamma sit
+  // in LDS (read per row: in registers they would spill the 128-VGPR budget at D = 768)
+  __shared__ float cst[XO ? 2 : 1][XO ? D : 1];
+  if constexpr (XO) {
+    for (int c = threadIdx.x; c < D; c += blockDim.x) {
+      cst[0][c] = bf2f(beta[c]);
+      cst[1][c] = inv_gamma(bf2f(gamma[c]));
+    }
+    __syncthreads();
+  }
 #pragma unroll
   for (int i = 0; i < VEC; ++i) { adg[i] = 0.f; adb[i] = 0.f; ady[i] = 0.f; }
   const float sc = p > 0.f ? 1.f / (1.f - p) : 1.f;
@@ -211,11 +228,20 @@ __global__ void __launch_bounds__(256, VEC <= 12 ? 4 : VEC <= 16 ? 2 : 1) add_ln
 #pragma unroll
       for (int i = 0; i < VEC; ++i) d[i] = keep[i] ? d[i] * sc : 0.f;
     }
-    const float mean = mean_in[row], rstd = rstd_in[row];
+    const float mean = XO ? 0.f : mean_in[row], rstd = rstd_in[row];
+    // opaque zero per row: keeps the loop-invariant LDS reads of cst inside the row loop
+    int zo = 0;
+    if constexpr (XO) asm volatile("v_mov_b32 %0, 0" : "=v"(zo));
     float s1 = 0.f, s2 = 0.f;
 #pragma unroll
     for (int i = 0; i < VEC; ++i) {
-      const float xh = (h[i] - mean) * rstd;
+      float xh;
+      if constexpr (XO) {
+        const int c = RowMap<VEC>::col(lane, i) + zo;
+        xh = (h[i] - cst[0][c]) * cst[1][c];
+      } else {
+        xh = (h[i] - mean) * rstd;
+      }
       adg[i] += d[i] * xh;
       adb[i] += d[i];
       const float gx = d[i] * g[i];
@@ -281,13 +307,13 @@ __global__ void __launch_bounds__(256, VEC <= 12 ? 4 : VEC <= 16 ? 2 : 1) add_ln
 // VGPRs - one wave per SIMD), and the block's column sums need no cross-wave reduction.  The two
 // row sums cross the 4 waves through LDS (double-buffered by row parity: one barrier per row).
 // Column sums always two-stage: part[block][3][D].
-template <int D, bool POST>
+template <int D, bool POST, bool XO>
 __global__ void __launch_bounds__(256) add_ln_bwd_rowblk_kernel(
     const bf16_t* __restrict__ dout, const bf16_t* __restrict__ hsave,
     const float* __restrict__ mean_in, const float* __restrict__ rstd_in,
     const bf16_t* __restrict__ gamma, bf16_t* __restrict__ dres, bf16_t* __restrict__ dy,
     bool want_dyb, int64_t R, float p, uint32_t seed, uint32_t offset, const bf16_t* __restrict__ dh_in,
-    float* __restrict__ part, bool part_acc) {
+    float* __restrict__ part, bool part_acc, const bf16_t* __restrict__ beta) {
   constexpr int VT = D / 256;
   constexpr int CH = VT % 8 == 0 ? 8 : VT % 4 == 0 ? 4 : VT % 2 == 0 ? 2 : 1;
   constexpr int NG = VT / CH;
@@ -352,6 +378,12 @@ __global__ void __launch_bounds__(256) add_ln_bwd_rowblk_kernel(
   };
   float g[VT], adg[VT], adb[VT], ady[VT];
   ld(gamma, g);
+  float bt[XO ? VT : 1], rg[XO ? VT : 1];
+  if constexpr (XO) {
+    ld(beta, bt);
+#pragma unroll
+    for (int i = 0; i < VT; ++i) rg[i] = inv_gamma(g[i]);
+  }
 #pragma unroll
   for (int i = 0; i < VT; ++i) { adg[i] = 0.f; adb[i] = 0.f; ady[i] = 0.f; }
   const float sc = p > 0.f ? 1.f / (1.f - p) : 1.f;
@@ -366,11 +398,12 @@ __global__ void __launch_bounds__(256) add_ln_bwd_rowblk_kernel(
 #pragma unroll
       for (int i = 0; i < VT; ++i) d[i] = keep[i] ? d[i] * sc : 0.f;
     }
-    const float mean = mean_in[row], rstd = rstd_in[row];
+    const float mean = XO ? 0.f : mean_in[row], rstd = rstd_in[row];
     float s1 = 0.f, s2 = 0.f;
 #pragma unroll
     for (int i = 0; i < VT; ++i) {
-      const float xh = (h[i] - mean) * rstd;
+      float xh;
+      if constexpr (XO) xh = (h[i] - bt[i]) * rg[i]; else xh = (h[i] - mean) * rstd;
       adg[i] += d[i] * xh;
       adb[i] += d[i];
       const float gx = d[i] * g[i];
@@ -521,7 +554,7 @@ static void ln_bwd_impl(const uint16_t* dout, const uint16_t* hsave, const float
                         const float* rstd, const uint16_t* g, uint16_t* dres, uint16_t* dy,
                         float* dyb, float* dg, float* db, int64_t R, float p, uint32_t seed,
                         uint32_t off, const uint16_t* dh_in, bool post, int zero_mask, hipStream_t s,
-                        float* ws, int part_mode) {
+                        float* ws, int part_mode, const uint16_t* beta) {
   constexpr int D = VEC * 64;
   const int64_t nb2 = ln_bwd_two_stage_blocks(R, D);
   const bool two_stage = ws != nullptr && nb2 > 0;
@@ -540,28 +573,32 @@ static void ln_bwd_impl(const uint16_t* dout, const uint16_t* hsave, const float
   }
   float* part = two_stage ? ws : nullptr;
   float* const dyb_k = dy ? dyb : nullptr;
+  // beta != nullptr: `hsave` is the LN output (pre-dropout placement only: a post-dropout
+  // output has zeroed elements and cannot be inverted)
+  const bool xo = beta != nullptr && !post;
+  const bf16_t* bt = (const bf16_t*)beta;
   if constexpr (D >= LN_WIDE_D) {
     if (two_stage) {
-      if (post)
-        hipLaunchKernelGGL((add_ln_bwd_rowblk_kernel<D, true>), dim3(nb), dim3(256), 0, s, (const bf16_t*)dout,
-                           (const bf16_t*)hsave, mean, rstd, (const bf16_t*)g, (bf16_t*)dres, (bf16_t*)dy,
-                           dyb_k != nullptr, R, p, seed, off, (const bf16_t*)dh_in, part, pacc);
-      else
-        hipLaunchKernelGGL((add_ln_bwd_rowblk_kernel<D, false>), dim3(nb), dim3(256), 0, s, (const bf16_t*)dout,
-                           (const bf16_t*)hsave, mean, rstd, (const bf16_t*)g, (bf16_t*)dres, (bf16_t*)dy,
-                           dyb_k != nullptr, R, p, seed, off, (const bf16_t*)dh_in, part, pacc);
+#define DPA_LN_ROWBLK(P, X)                                                                                 \
+  hipLaunchKernelGGL((add_ln_bwd_rowblk_kernel<D, P, X>), dim3(nb), dim3(256), 0, s, (const bf16_t*)dout, \
+                     (const bf16_t*)hsave, mean, rstd, (const bf16_t*)g, (bf16_t*)dres, (bf16_t*)dy,      \
+                     dyb_k != nullptr, R, p, seed, off, (const bf16_t*)dh_in, part, pacc, bt)
+      if (post) DPA_LN_ROWBLK(true, false);
+      else if (xo) DPA_LN_ROWBLK(false, true);
+      else DPA_LN_ROWBLK(false, false);
+#undef DPA_LN_ROWBLK
       if (reduce) ln_colreduce_launch(part, nb, D, dg, db, dyb_k, s);
       return;
     }
   }
-  if (post)
-    hipLaunchKernelGGL((add_ln_bwd_kernel<VEC, true>), dim3(nb), dim3(256), 0, s, (const bf16_t*)dout,
-                       (const bf16_t*)hsave, mean, rstd, (const bf16_t*)g, (bf16_t*)dres, (bf16_t*)dy, dyb_k, dg,
-                       db, R, p, seed, off, (const bf16_t*)dh_in, part, pacc);
-  else
-    hipLaunchKernelGGL((add_ln_bwd_kernel<VEC, false>), dim3(nb), dim3(256), 0, s, (const bf16_t*)dout,
-                       (const bf16_t*)hsave, mean, rstd, (const bf16_t*)g, (bf16_t*)dres, (bf16_t*)dy, dyb_k, dg,
-                       db, R, p, seed, off, (const bf16_t*)dh_in, part, pacc);
+#define DPA_LN_BWD(P, X)                                                                                     \
+  hipLaunchKernelGGL((add_ln_bwd_kernel<VEC, P, X>), dim3(nb), dim3(256), 0, s, (const bf16_t*)dout,         \
+                     (const bf16_t*)hsave, mean, rstd, (const bf16_t*)g, (bf16_t*)dres, (bf16_t*)dy, dyb_k, dg, \
+                     db, R, p, seed, off, (const bf16_t*)dh_in, part, pacc, bt)
+  if (post) DPA_LN_BWD(true, false);
+  else if (xo) DPA_LN_BWD(false, true);
+  else DPA_LN_BWD(false, false);
+#undef DPA_LN_BWD
   if (two_stage && reduce) ln_colreduce_launch(part, nb, D, dg, db, dyb_k, s);
 }
 
@@ -587,9 +624,10 @@ bool launch_add_ln_bwd(const uint16_t* dout, const uint16_t* hsave, const float*
                        const float* rstd, const uint16_t* g, uint16_t* dres, uint16_t* dy, float* dyb,
                        float* dg, float* db, int64_t R, int D, float p, uint32_t seed, uint32_t off,
                        hipStream_t s, const uint16_t* dh_in, bool post, int zero_mask, float* ws,
-                       int part_mode) {
+                       int part_mode, const uint16_t* beta) {
+  if (beta && post) return false;  // a post-dropout output cannot be inverted
   DPA_LN_DISPATCH(D, ln_bwd_impl, dout, hsave, mean, rstd, g, dres, dy, dyb, dg, db, R, p, seed,
-                  off, dh_in, post, zero_mask, s, ws, part_mode)
+                  off, dh_in, post, zero_mask, s, ws, part_mode, beta)
   return true;
 }
 
