@@ -69,7 +69,11 @@ def test_add_ln_bwd_from_output(R, D, p):
     assert e_got.max().item() <= 2 * e_ref.max().item() + 1e-2, (e_got.max().item(), e_ref.max().item())
     assert e_got.mean().item() <= 1.5 * e_ref.mean().item() + 1e-4, (e_got.mean().item(), e_ref.mean().item())
     assert torch.equal(got[1] == 0, ref[1] == 0)  # dy: same dropout mask
-    torch.testing.assert_close(got[1].float(), ref[1].float(), rtol=3e-2, atol=3e-2)
+    dy_ref = h.grad * (ref[1] != 0).float() / (1 - p)
+    e_got = (got[1].float() - dy_ref).abs()
+    e_ref = (ref[1].float() - dy_ref).abs()
+    assert e_got.max().item() <= 2 * e_ref.max().item() + 1e-2, (e_got.max().item(), e_ref.max().item())
+    assert e_got.mean().item() <= 1.5 * e_ref.mean().item() + 1e-4, (e_got.mean().item(), e_ref.mean().item())
     torch.testing.assert_close(got[2], gf.grad, rtol=1e-2, atol=1e-2 * gf.grad.abs().max().item())
     torch.testing.assert_close(got[3], bf.grad, rtol=1e-2, atol=1e-2 * bf.grad.abs().max().item())
     torch.testing.assert_close(got[4], ref[4], rtol=1e-2, atol=1e-2 * ref[4].abs().max().item())
