@@ -184,7 +184,7 @@ static std::vector<at::Tensor> add_ln_fwd(const at::Tensor& y, c10::optional<at:
                                           const at::Tensor& g, const at::Tensor& b, double p,
                                           double eps, int64_t seed, int64_t offset,
                                           c10::optional<at::Tensor> pos, c10::optional<at::Tensor> temb,
-                                          int64_t L, bool post, bool save_h) {
+                                          int64_t L, bool post, bool save_h, bool h_guard) {
   CHECK_DEV(y); CHECK_BF16(y); CHECK_CONTIG(y); CHECK_BF16(g); CHECK_BF16(b);
   TORCH_CHECK(y.dim() == 2, "y must be [R, D]");
   const int64_t R = y.size(0);
@@ -210,7 +210,9 @@ static std::vector<at::Tensor> add_ln_fwd(const at::Tensor& y, c10::optional<at:
     tp = bf_ptr(*temb);
   }
   const c10::DeviceGuard guard(y.device());
-  // save_h = false: no bf16 copy of h (the backward reconstructs xhat from the output)
+  // save_h = false: no bf16 copy of h.  h_guard: the copy is written only for a gamma with
+  // some |gamma| < 0.125 (norm.hip LN_XO_GMIN) - add_ln_bwd(beta=, hcopy=) reads it then and
+  // reconstructs xhat from the output otherwise
   at::Tensor out = at::empty_like(y), hs = save_h ? at::empty_like(y) : at::Tensor();
   auto f32 = y.options().dtype(at::kFloat);
   at::Tensor mean = at::empty({R}, f32), rstd = at::empty({R}, f32);
@@ -219,7 +221,8 @@ static std::vector<at::Tensor> add_ln_fwd(const at::Tensor& y, c10::optional<at:
                                    save_h ? reinterpret_cast<uint16_t*>(hs.data_ptr()) : nullptr,
                                    mean.data_ptr<float>(),
                                    rstd.data_ptr<float>(), R, D, (float)p, (float)eps,
-                                   (uint32_t)seed, (uint32_t)offset, cur_stream(), pp, tp, (int)L, post);
+                                   (uint32_t)seed, (uint32_t)offset, cur_stream(), pp, tp, (int)L, post,
+                                   save_h && h_guard);
   TORCH_CHECK(ok, "add_ln_fwd: unsupported hidden size ", D);
   return {out, hs, mean, rstd};
 }
@@ -231,7 +234,8 @@ static std::vector<at::Tensor> add_ln_bwd(const at::Tensor& dout, const at::Tens
                                           bool want_dyb, c10::optional<at::Tensor> dh_in, bool post,
                                           c10::optional<at::Tensor> dg_acc, c10::optional<at::Tensor> db_acc,
                                           c10::optional<at::Tensor> dyb_acc, c10::optional<at::Tensor> part_buf,
-                                          bool part_acc, c10::optional<at::Tensor> beta) {
+                                          bool part_acc, c10::optional<at::Tensor> beta,
+                                          c10::optional<at::Tensor> hcopy) {
   CHECK_DEV(dout); CHECK_BF16(dout); CHECK_CONTIG(dout); CHECK_BF16(hs); CHECK_CONTIG(hs);
   TORCH_CHECK(hs.sizes() == dout.sizes(), "add_ln_bwd: hsave/out shape");
   // beta given: `hs` is the LN output (forward with save_h=false), xhat = (out - beta) / gamma
@@ -239,8 +243,12 @@ static std::vector<at::Tensor> add_ln_bwd(const at::Tensor& dout, const at::Tens
   if (beta.has_value() && beta->defined()) {
     CHECK_BF16((*beta)); CHECK_CONTIG((*beta));
     TORCH_CHECK(beta->numel() == dout.size(1) && !post, "add_ln_bwd: beta [D], pre-dropout placement only");
+    TORCH_CHECK(hcopy.has_value() && hcopy->defined() && hcopy->sizes() == dout.sizes(),
+                "add_ln_bwd: beta needs hcopy (the forward's guarded h copy)");
+    CHECK_BF16((*hcopy)); CHECK_CONTIG((*hcopy));
     btp = bf_ptr(*beta);
   }
+  const uint16_t* hcp = btp ? bf_ptr(*hcopy) : nullptr;
   const uint16_t* dhp = nullptr;
   if (dh_in.has_value() && dh_in->defined()) {
     CHECK_BF16((*dh_in)); CHECK_CONTIG((*dh_in));
@@ -290,7 +298,7 @@ static std::vector<at::Tensor> add_ln_bwd(const at::Tensor& dout, const at::Tens
       need_dy ? reinterpret_cast<uint16_t*>(dy.data_ptr()) : nullptr,
       dyb.defined() ? dyb.data_ptr<float>() : nullptr,
       dg.data_ptr<float>(), db.data_ptr<float>(), R, D, (float)p, (uint32_t)seed, (uint32_t)offset,
-      cur_stream(), dhp, post, zero_mask, wsn > 0 ? ws.data_ptr<float>() : nullptr, part_mode, btp);
+      cur_stream(), dhp, post, zero_mask, wsn > 0 ? ws.data_ptr<float>() : nullptr, part_mode, btp, hcp);
   TORCH_CHECK(ok, "add_ln_bwd: unsupported hidden size ", D);
   return {dres, dy, ext_g ? at::Tensor() : dg, ext_b ? at::Tensor() : db, ext_y ? at::Tensor() : dyb};
 }
@@ -852,13 +860,14 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         "LN(dropout(y [+pos] [+temb]) + res) (post: dropout(LN(...))) -> (out, hsave, mean, rstd)",
         py::arg("y"), py::arg("res"), py::arg("gamma"), py::arg("beta"), py::arg("p"), py::arg("eps"),
         py::arg("seed"), py::arg("offset"), py::arg("pos") = py::none(), py::arg("temb") = py::none(),
-        py::arg("L") = 1, py::arg("post") = false, py::arg("save_h") = true);
+        py::arg("L") = 1, py::arg("post") = false, py::arg("save_h") = true, py::arg("h_guard") = false);
   m.def("add_ln_bwd", &add_ln_bwd, "backward of add_ln_fwd -> (dres, dy, dgamma, dbeta, colsum(dy))",
         py::arg("dout"), py::arg("hsave"), py::arg("mean"), py::arg("rstd"), py::arg("gamma"),
         py::arg("p"), py::arg("seed"), py::arg("offset"), py::arg("need_dres"), py::arg("need_dy"),
         py::arg("want_dy_colsum") = false, py::arg("dh_in") = py::none(), py::arg("post") = false,
         py::arg("dg_acc") = py::none(), py::arg("db_acc") = py::none(), py::arg("dyb_acc") = py::none(),
-        py::arg("part_buf") = py::none(), py::arg("part_acc") = false, py::arg("beta") = py::none());
+        py::arg("part_buf") = py::none(), py::arg("part_acc") = false, py::arg("beta") = py::none(),
+        py::arg("hcopy") = py::none());
   m.def("colsum_acc", &colsum_acc, "dst += colsum(part) (fp32 partials [rows, cols])");
   m.def("ln_bwd_partials", &ln_bwd_partials, "floats of add_ln_bwd's deferred partial buffer (0: none)");
   m.def("ln_colreduce", &ln_colreduce, "dg/db(/dyb) += column sums of add_ln_bwd partials",

@@ -57,7 +57,7 @@ bool launch_add_ln_fwd(const uint16_t* y, const uint16_t* res, const uint16_t* g
                        uint16_t* out, uint16_t* hsave, float* mean, float* rstd, int64_t R, int D,
                        float p, float eps, uint32_t seed, uint32_t off, hipStream_t s,
                        const uint16_t* pos = nullptr, const uint16_t* temb = nullptr, int L = 1,
-                       bool post = false);
+                       bool post = false, bool hguard = false);  // hguard: write hsave only if some |gamma| is small
 int ln_bwd_blocks(int64_t R);
 // dyb (nullable): column sums of dy (the bias gradient of the layer producing y)
 bool launch_add_ln_bwd(const uint16_t* dout, const uint16_t* hsave, const float* mean,
@@ -65,7 +65,8 @@ bool launch_add_ln_bwd(const uint16_t* dout, const uint16_t* hsave, const float*
                        float* dg, float* db, int64_t R, int D, float p, uint32_t seed, uint32_t off,
                        hipStream_t s, const uint16_t* dh_in = nullptr, bool post = false,
                        int zero_mask = 7, float* ws = nullptr, int part_mode = 0,
-                       const uint16_t* beta = nullptr);  // beta: `hsave` is the LN output
+                       const uint16_t* beta = nullptr,    // beta: `hsave` is the LN output ...
+                       const uint16_t* hcopy = nullptr);  // ... and hcopy the guarded h copy
 // the deferred second stage of part_mode 1/2 (R = the rows of each summed micro-batch)
 bool launch_ln_colreduce(const float* part, int64_t R, int D, float* dg, float* db, float* dyb, hipStream_t s);
 bool launch_colsum_acc(const float* part, int rows, int cols, float* dst, hipStream_t s);

@@ -112,10 +112,14 @@ __device__ __forceinline__ void dropout_keep(uint32_t seed, uint32_t offset, int
 }
 
 // 1 / gamma for the output-based backward (xhat = (o - b) / gamma, the "memory-efficient"
-// LayerNorm backward).  A column whose bf16 gamma is exactly 0 carries no xhat in its output:
-// its xhat is taken as 0, which leaves that column's dgamma at 0 and drops its xhat * s2 term
-// from dx.  ops/nn.py (_LN_SAVE_OUT, DPA_LN_SAVE_OUT=0 restores the h copy) documents this.
+// LayerNorm backward; used only when every |gamma| >= LN_XO_GMIN, so never 0 there).
 __device__ __forceinline__ float inv_gamma(float g) { return g != 0.f ? 1.f / g : 0.f; }
+// Guard of the output-based backward: (o - b) / gamma amplifies the bf16 rounding of o by
+// 1 / |gamma|, so a LayerNorm with any |gamma| below this keeps the exact h-copy path: its
+// forward writes the h copy (hguard) and its backward reads it.  Both kernels evaluate the
+// same predicate on the same gamma (the optimizer runs after the backward), so no flag
+// travels between them and nothing syncs with the host.
+constexpr float LN_XO_GMIN = 0.125f;
 
 template <int VEC>
 __global__ void __launch_bounds__(256) add_ln_fwd_kernel(
@@ -123,7 +127,7 @@ __global__ void __launch_bounds__(256) add_ln_fwd_kernel(
     const bf16_t* __restrict__ beta, bf16_t* __restrict__ out, bf16_t* __restrict__ hsave,
     float* __restrict__ mean_out, float* __restrict__ rstd_out, int64_t R, float p, float eps,
     uint32_t seed, uint32_t offset, const bf16_t* __restrict__ pos, const bf16_t* __restrict__ temb,
-    int L, int post) {
+    int L, int post, int hguard) {
   constexpr int D = VEC * 64;
   const int lane = threadIdx.x & 63;
   const int64_t row = (int64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
@@ -158,7 +162,18 @@ __global__ void __launch_bounds__(256) add_ln_fwd_kernel(
   // round h to bf16 first so the backward (which reloads the bf16 copy) is consistent
 #pragma unroll
   for (int i = 0; i < VEC; ++i) h[i] = bf2f(f2bf(h[i]));
-  if (hsave) RowIO<VEC>::store(hsave + row * D, lane, h);
+  float g[VEC], b[VEC], o[VEC];
+  RowIO<VEC>::load(gamma, lane, g);
+  RowIO<VEC>::load(beta, lane, b);
+  bool write_h = hsave != nullptr;
+  if (write_h && hguard) {
+    // output-based backward unless some |gamma| is small (the row holds all of gamma)
+    bool small = false;
+#pragma unroll
+    for (int i = 0; i < VEC; ++i) small |= fabsf(g[i]) < LN_XO_GMIN;
+    write_h = __builtin_amdgcn_ballot_w64(small) != 0;
+  }
+  if (write_h) RowIO<VEC>::store(hsave + row * D, lane, h);
   float s = 0.f;
 #pragma unroll
   for (int i = 0; i < VEC; ++i) s += h[i];
@@ -167,9 +182,6 @@ __global__ void __launch_bounds__(256) add_ln_fwd_kernel(
 #pragma unroll
   for (int i = 0; i < VEC; ++i) { const float d = h[i] - mean; v += d * d; }
   const float rstd = rsqrtf(wave_sum(v) * (1.f / D) + eps);
-  float g[VEC], b[VEC], o[VEC];
-  RowIO<VEC>::load(gamma, lane, g);
-  RowIO<VEC>::load(beta, lane, b);
 #pragma unroll
   for (int i = 0; i < VEC; ++i) o[i] = (h[i] - mean) * rstd * g[i] + b[i];
   if (p > 0.f && post) {
@@ -198,7 +210,7 @@ __global__ void __launch_bounds__(256, VEC <= 12 ? 4 : VEC <= 16 ? 2 : 1) add_ln
     const bf16_t* __restrict__ gamma, bf16_t* __restrict__ dres, bf16_t* __restrict__ dy,
     float* __restrict__ dyb, float* __restrict__ part_dg, float* __restrict__ part_db, int64_t R,
     float p, uint32_t seed, uint32_t offset, const bf16_t* __restrict__ dh_in, float* __restrict__ part,
-    bool part_acc, const bf16_t* __restrict__ beta) {
+    bool part_acc, const bf16_t* __restrict__ beta, const bf16_t* __restrict__ hcopy) {
   constexpr int D = VEC * 64;
   __shared__ float red[4][D];  // reused for dgamma, dbeta, dyb in turn
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
@@ -208,19 +220,25 @@ __global__ void __launch_bounds__(256, VEC <= 12 ? 4 : VEC <= 16 ? 2 : 1) add_ln
   // input), so xhat = (o - b) / g and the forward writes no h copy.  beta and 1 / gamma sit
   // in LDS (read per row: in registers they would spill the 128-VGPR budget at D = 768)
   __shared__ float cst[XO ? 2 : 1][XO ? D : 1];
+  bool xo = false;  // wave-uniform: every wave holds all of gamma
   if constexpr (XO) {
+    bool small = false;
+#pragma unroll
+    for (int i = 0; i < VEC; ++i) small |= fabsf(g[i]) < LN_XO_GMIN;
+    xo = __builtin_amdgcn_ballot_w64(small) == 0;
     for (int c = threadIdx.x; c < D; c += blockDim.x) {
       cst[0][c] = bf2f(beta[c]);
       cst[1][c] = inv_gamma(bf2f(gamma[c]));
     }
     __syncthreads();
   }
+  const bf16_t* const hsrc = XO && !xo ? hcopy : hsave;
 #pragma unroll
   for (int i = 0; i < VEC; ++i) { adg[i] = 0.f; adb[i] = 0.f; ady[i] = 0.f; }
   const float sc = p > 0.f ? 1.f / (1.f - p) : 1.f;
   for (int64_t row = (int64_t)blockIdx.x * 4 + w; row < R; row += (int64_t)gridDim.x * 4) {
     float h[VEC], d[VEC];
-    RowIO<VEC>::load(hsave + row * D, lane, h);
+    RowIO<VEC>::load(hsrc + row * D, lane, h);
     RowIO<VEC>::load(dout + row * D, lane, d);
     if (POST && p > 0.f) {
       bool keep[VEC];
@@ -228,7 +246,7 @@ __global__ void __launch_bounds__(256, VEC <= 12 ? 4 : VEC <= 16 ? 2 : 1) add_ln
 #pragma unroll
       for (int i = 0; i < VEC; ++i) d[i] = keep[i] ? d[i] * sc : 0.f;
     }
-    const float mean = XO ? 0.f : mean_in[row], rstd = rstd_in[row];
+    const float mean = XO && xo ? 0.f : mean_in[row], rstd = rstd_in[row];
     // opaque zero per row: keeps the loop-invariant LDS reads of cst inside the row loop
     int zo = 0;
     if constexpr (XO) asm volatile("v_mov_b32 %0, 0" : "=v"(zo));
@@ -236,7 +254,7 @@ __global__ void __launch_bounds__(256, VEC <= 12 ? 4 : VEC <= 16 ? 2 : 1) add_ln
 #pragma unroll
     for (int i = 0; i < VEC; ++i) {
       float xh;
-      if constexpr (XO) {
+      if (XO && xo) {
         const int c = RowMap<VEC>::col(lane, i) + zo;
         xh = (h[i] - cst[0][c]) * cst[1][c];
       } else {
@@ -313,7 +331,8 @@ __global__ void __launch_bounds__(256) add_ln_bwd_rowblk_kernel(
     const float* __restrict__ mean_in, const float* __restrict__ rstd_in,
     const bf16_t* __restrict__ gamma, bf16_t* __restrict__ dres, bf16_t* __restrict__ dy,
     bool want_dyb, int64_t R, float p, uint32_t seed, uint32_t offset, const bf16_t* __restrict__ dh_in,
-    float* __restrict__ part, bool part_acc, const bf16_t* __restrict__ beta) {
+    float* __restrict__ part, bool part_acc, const bf16_t* __restrict__ beta,
+    const bf16_t* __restrict__ hcopy) {
   constexpr int VT = D / 256;
   constexpr int CH = VT % 8 == 0 ? 8 : VT % 4 == 0 ? 4 : VT % 2 == 0 ? 2 : 1;
   constexpr int NG = VT / CH;
@@ -379,18 +398,30 @@ __global__ void __launch_bounds__(256) add_ln_bwd_rowblk_kernel(
   float g[VT], adg[VT], adb[VT], ady[VT];
   ld(gamma, g);
   float bt[XO ? VT : 1], rg[XO ? VT : 1];
+  __shared__ int nsmall;
+  bool xo = false;  // block-uniform (the threads hold different columns of gamma)
   if constexpr (XO) {
     ld(beta, bt);
+    bool small = false;
 #pragma unroll
-    for (int i = 0; i < VT; ++i) rg[i] = inv_gamma(g[i]);
+    for (int i = 0; i < VT; ++i) {
+      rg[i] = inv_gamma(g[i]);
+      small |= fabsf(g[i]) < LN_XO_GMIN;
+    }
+    if (t == 0) nsmall = 0;
+    __syncthreads();
+    if (small) nsmall = 1;
+    __syncthreads();
+    xo = nsmall == 0;
   }
+  const bf16_t* const hsrc = XO && !xo ? hcopy : hsave;
 #pragma unroll
   for (int i = 0; i < VT; ++i) { adg[i] = 0.f; adb[i] = 0.f; ady[i] = 0.f; }
   const float sc = p > 0.f ? 1.f / (1.f - p) : 1.f;
   int par = 0;
   for (int64_t row = blockIdx.x; row < R; row += gridDim.x, par ^= 1) {
     float h[VT], d[VT];
-    ld(hsave + row * D, h);
+    ld(hsrc + row * D, h);
     ld(dout + row * D, d);
     if (POST && p > 0.f) {
       bool keep[VT];
@@ -398,12 +429,12 @@ __global__ void __launch_bounds__(256) add_ln_bwd_rowblk_kernel(
 #pragma unroll
       for (int i = 0; i < VT; ++i) d[i] = keep[i] ? d[i] * sc : 0.f;
     }
-    const float mean = XO ? 0.f : mean_in[row], rstd = rstd_in[row];
+    const float mean = mean_in[row], rstd = rstd_in[row];
     float s1 = 0.f, s2 = 0.f;
 #pragma unroll
     for (int i = 0; i < VT; ++i) {
       float xh;
-      if constexpr (XO) xh = (h[i] - bt[i]) * rg[i]; else xh = (h[i] - mean) * rstd;
+      if (XO && xo) xh = (h[i] - bt[i]) * rg[i]; else xh = (h[i] - mean) * rstd;
       adg[i] += d[i] * xh;
       adb[i] += d[i];
       const float gx = d[i] * g[i];
@@ -495,21 +526,21 @@ template <int VEC>
 static void ln_fwd_impl(const uint16_t* y, const uint16_t* res, const uint16_t* g, const uint16_t* b,
                         uint16_t* out, uint16_t* hsave, float* mean, float* rstd, int64_t R, float p,
                         float eps, uint32_t seed, uint32_t off, const uint16_t* pos, const uint16_t* temb,
-                        int L, bool post, hipStream_t s) {
+                        int L, bool post, bool hguard, hipStream_t s) {
   const unsigned grid = (unsigned)((R + 3) / 4);
   hipLaunchKernelGGL(add_ln_fwd_kernel<VEC>, dim3(grid), dim3(256), 0, s, (const bf16_t*)y,
                      (const bf16_t*)res, (const bf16_t*)g, (const bf16_t*)b, (bf16_t*)out,
                      (bf16_t*)hsave, mean, rstd, R, p, eps, seed, off, (const bf16_t*)pos,
-                     (const bf16_t*)temb, L < 1 ? 1 : L, post ? 1 : 0);
+                     (const bf16_t*)temb, L < 1 ? 1 : L, post ? 1 : 0, hguard ? 1 : 0);
 }
 
 bool launch_add_ln_fwd(const uint16_t* y, const uint16_t* res, const uint16_t* g, const uint16_t* b,
                        uint16_t* out, uint16_t* hsave, float* mean, float* rstd, int64_t R, int D,
                        float p, float eps, uint32_t seed, uint32_t off, hipStream_t s, const uint16_t* pos,
-                       const uint16_t* temb, int L, bool post) {
+                       const uint16_t* temb, int L, bool post, bool hguard) {
   if ((pos || temb) && (L < 1 || R % L)) return false;
   DPA_LN_DISPATCH(D, ln_fwd_impl, y, res, g, b, out, hsave, mean, rstd, R, p, eps, seed, off, pos, temb, L,
-                  post, s)
+                  post, hguard, s)
   return true;
 }
 
@@ -554,7 +585,7 @@ static void ln_bwd_impl(const uint16_t* dout, const uint16_t* hsave, const float
                         const float* rstd, const uint16_t* g, uint16_t* dres, uint16_t* dy,
                         float* dyb, float* dg, float* db, int64_t R, float p, uint32_t seed,
                         uint32_t off, const uint16_t* dh_in, bool post, int zero_mask, hipStream_t s,
-                        float* ws, int part_mode, const uint16_t* beta) {
+                        float* ws, int part_mode, const uint16_t* beta, const uint16_t* hcopy) {
   constexpr int D = VEC * 64;
   const int64_t nb2 = ln_bwd_two_stage_blocks(R, D);
   const bool two_stage = ws != nullptr && nb2 > 0;
@@ -575,14 +606,15 @@ static void ln_bwd_impl(const uint16_t* dout, const uint16_t* hsave, const float
   float* const dyb_k = dy ? dyb : nullptr;
   // beta != nullptr: `hsave` is the LN output (pre-dropout placement only: a post-dropout
   // output has zeroed elements and cannot be inverted)
-  const bool xo = beta != nullptr && !post;
+  const bool xo = beta != nullptr && hcopy != nullptr && !post;
   const bf16_t* bt = (const bf16_t*)beta;
   if constexpr (D >= LN_WIDE_D) {
     if (two_stage) {
 #define DPA_LN_ROWBLK(P, X)                                                                                 \
   hipLaunchKernelGGL((add_ln_bwd_rowblk_kernel<D, P, X>), dim3(nb), dim3(256), 0, s, (const bf16_t*)dout, \
                      (const bf16_t*)hsave, mean, rstd, (const bf16_t*)g, (bf16_t*)dres, (bf16_t*)dy,      \
-                     dyb_k != nullptr, R, p, seed, off, (const bf16_t*)dh_in, part, pacc, bt)
+                     dyb_k != nullptr, R, p, seed, off, (const bf16_t*)dh_in, part, pacc, bt,    \
+                     (const bf16_t*)hcopy)
       if (post) DPA_LN_ROWBLK(true, false);
       else if (xo) DPA_LN_ROWBLK(false, true);
       else DPA_LN_ROWBLK(false, false);
@@ -594,7 +626,7 @@ static void ln_bwd_impl(const uint16_t* dout, const uint16_t* hsave, const float
 #define DPA_LN_BWD(P, X)                                                                                     \
   hipLaunchKernelGGL((add_ln_bwd_kernel<VEC, P, X>), dim3(nb), dim3(256), 0, s, (const bf16_t*)dout,         \
                      (const bf16_t*)hsave, mean, rstd, (const bf16_t*)g, (bf16_t*)dres, (bf16_t*)dy, dyb_k, dg, \
-                     db, R, p, seed, off, (const bf16_t*)dh_in, part, pacc, bt)
+                     db, R, p, seed, off, (const bf16_t*)dh_in, part, pacc, bt, (const bf16_t*)hcopy)
   if (post) DPA_LN_BWD(true, false);
   else if (xo) DPA_LN_BWD(false, true);
   else DPA_LN_BWD(false, false);
@@ -624,10 +656,10 @@ bool launch_add_ln_bwd(const uint16_t* dout, const uint16_t* hsave, const float*
                        const float* rstd, const uint16_t* g, uint16_t* dres, uint16_t* dy, float* dyb,
                        float* dg, float* db, int64_t R, int D, float p, uint32_t seed, uint32_t off,
                        hipStream_t s, const uint16_t* dh_in, bool post, int zero_mask, float* ws,
-                       int part_mode, const uint16_t* beta) {
-  if (beta && post) return false;  // a post-dropout output cannot be inverted
+                       int part_mode, const uint16_t* beta, const uint16_t* hcopy) {
+  if (beta && (post || !hcopy)) return false;  // a post-dropout output cannot be inverted
   DPA_LN_DISPATCH(D, ln_bwd_impl, dout, hsave, mean, rstd, g, dres, dy, dyb, dg, db, R, p, seed,
-                  off, dh_in, post, zero_mask, s, ws, part_mode, beta)
+                  off, dh_in, post, zero_mask, s, ws, part_mode, beta, hcopy)
   return true;
 }
 

@@ -135,9 +135,10 @@ _QKV_HEAD_MAJOR = os.environ.get("DPA_QKV_HEAD_MAJOR", "1") != "0"
 _SAVE_ACT_DERIV = os.environ.get("DPA_SAVE_ACT_DERIV", "1") != "0"
 # post-LN sublayers: the LayerNorm backward reconstructs xhat = (out - beta) / gamma from the
 # sublayer's output - which the next sublayer keeps alive anyway as its input - instead of
-# the forward writing a bf16 copy of h (one [T, D] store less per sublayer, and that much less
-# activation memory).  A column whose bf16 gamma is exactly 0 gets xhat = 0 (norm.hip
-# inv_gamma).  DPA_LN_SAVE_OUT=0: the forward saves h as before.
+# the forward writing a bf16 copy of h (one [T, D] store less per sublayer).  Guarded: a
+# LayerNorm with any |gamma| < 0.125 (where 1 / gamma would amplify out's bf16 rounding) keeps
+# the exact h-copy path - both kernels test the same gamma on the device, no host sync
+# (norm.hip LN_XO_GMIN).  DPA_LN_SAVE_OUT=0: always the h copy.
 _LN_SAVE_OUT = os.environ.get("DPA_LN_SAVE_OUT", "1") != "0"
 
 
@@ -624,12 +625,10 @@ class _MLPLNFn(torch.autograd.Function):
         x2 = x.reshape(-1, shp[-1])
         y, h, z1, cfg = _mlp_fwd(x2, w1_16, b1_16, w2_16, b2_16, act)
         out, hsave, mean, rstd = get_ext().add_ln_fwd(y, x2, lw16, lb16, float(p), float(eps), seed,
-                                                      off, save_h=not _LN_SAVE_OUT)
+                                                      off, h_guard=_LN_SAVE_OUT)
         del y
-        if _LN_SAVE_OUT:
-            hsave = out
-        ctx.save_for_backward(x2, w1_16, w2_16, h, z1, hsave, mean, rstd, lw16,
-                              lb16 if _LN_SAVE_OUT else None)
+        ctx.save_for_backward(x2, w1_16, w2_16, h, z1, out if _LN_SAVE_OUT else hsave, mean, rstd, lw16,
+                              lb16 if _LN_SAVE_OUT else None, hsave if _LN_SAVE_OUT else None)
         ctx.params = (w1, b1, w2, b2)
         ctx.ln_params = (lw, lb)
         ctx.cfg = cfg
@@ -639,7 +638,7 @@ class _MLPLNFn(torch.autograd.Function):
 
     @staticmethod
     def backward(ctx, dout):
-        x2, w1_16, w2_16, h, z1, hsave, mean, rstd, lw16, lb16 = ctx.saved_tensors
+        x2, w1_16, w2_16, h, z1, hsave, mean, rstd, lw16, lb16, hcopy = ctx.saved_tensors
         p, seed, off = ctx.ln
         need_dx = ctx.needs_input_grad[0]
         lw, lb = ctx.ln_params
@@ -651,7 +650,7 @@ class _MLPLNFn(torch.autograd.Function):
                       if gb2 is not None else (None, False))
         dres, dy, dlw, dlb, dyb = get_ext().add_ln_bwd(
             d2, hsave, mean, rstd, lw16, float(p), seed, off, need_dx, True, True, dg_acc=dg, db_acc=dbl,
-            dyb_acc=gb2, part_buf=part, part_acc=pacc, beta=lb16)
+            dyb_acc=gb2, part_buf=part, part_acc=pacc, beta=lb16, hcopy=hcopy)
         if b2 is not None and dyb is None:
             dyb = _ACCUMULATED  # fc2's bias gradient went onto b2.grad in the LN kernel
         dx, dw1, db1, dw2, db2 = _mlp_bwd(dy, x2, w1_16, w2_16, h, z1, ctx.params, ctx.cfg, need_dx,
@@ -693,12 +692,10 @@ class _AttnLNFn(torch.autograd.Function):
         ro = _route(o2, wo16.shape[0], "none")
         y, _, _ = _lin_fwd(o2, wo16, bo16, "none", ro)
         out, hsave, mean, rstd = get_ext().add_ln_fwd(y, x2, lw16, lb16, float(p), float(eps), seed_l,
-                                                      off_l, save_h=not _LN_SAVE_OUT)
+                                                      off_l, h_guard=_LN_SAVE_OUT)
         del y
-        if _LN_SAVE_OUT:
-            hsave = out
-        ctx.save_for_backward(x2, qkv3, o, lse, wq16, wo16, hsave, mean, rstd, lw16,
-                              lb16 if _LN_SAVE_OUT else None)
+        ctx.save_for_backward(x2, qkv3, o, lse, wq16, wo16, out if _LN_SAVE_OUT else hsave, mean, rstd,
+                              lw16, lb16 if _LN_SAVE_OUT else None, hsave if _LN_SAVE_OUT else None)
         ctx.params = (wq, bq, wo, bo)
         ctx.ln_params = (lw, lb)
         ctx.cfg = (heads, p_attn, seed_a, off_a, p, seed_l, off_l, rq, ro, bool(hm))
@@ -707,7 +704,7 @@ class _AttnLNFn(torch.autograd.Function):
 
     @staticmethod
     def backward(ctx, dout):
-        x2, qkv3, o, lse, wq16, wo16, hsave, mean, rstd, lw16, lb16 = ctx.saved_tensors
+        x2, qkv3, o, lse, wq16, wo16, hsave, mean, rstd, lw16, lb16, hcopy = ctx.saved_tensors
         wq, bq, wo, bo = ctx.params
         heads, p_attn, seed_a, off_a, p, seed_l, off_l, rq, ro, hm = ctx.cfg
         need_dx = ctx.needs_input_grad[0]
@@ -719,7 +716,7 @@ class _AttnLNFn(torch.autograd.Function):
                       if gbo is not None else (None, False))
         dres, dy, dlw, dlb, dyb = ext.add_ln_bwd(
             d2, hsave, mean, rstd, lw16, float(p), seed_l, off_l, need_dx, True, True, dg_acc=dg, db_acc=dbl,
-            dyb_acc=gbo, part_buf=part, part_acc=pacc, beta=lb16)
+            dyb_acc=gbo, part_buf=part, part_acc=pacc, beta=lb16, hcopy=hcopy)
         if bo is not None and dyb is None:
             dyb = _ACCUMULATED  # the out projection's bias gradient went onto bo.grad
         # out projection
