@@ -54,7 +54,7 @@ def parse():
     ap.add_argument("--ref-warmup", type=int, default=2,
                     help="untimed reference-schedule steps first (its two extra HIP streams grow their own "
                          "allocator pools in the first steps)")
-    ap.add_argument("--ref-steps", type=int, default=3,
+    ap.add_argument("--ref-steps", type=int, default=8,
                     help="also time this many steps of the reference 32 x 64 schedule (0 = skip)")
     ap.add_argument("--ref-windows", type=int, default=1,
                     help="time the reference schedule in this many back-to-back windows of --ref-steps "
@@ -175,10 +175,12 @@ def main():
         one_step()
     sync()
     elapsed = time.perf_counter() - t0
+    rank_ms = [elapsed / a.steps * 1e3] * 2  # [min, max] over ranks of this rank's ms/step
     if world > 1:
-        t = torch.tensor([elapsed], dtype=torch.float64, device=dev if dev.type == "cuda" else "cpu")
+        t = torch.tensor([elapsed, -elapsed], dtype=torch.float64, device=dev if dev.type == "cuda" else "cpu")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
+        elapsed = float(t[0].item())
+        rank_ms = [-float(t[1].item()) / a.steps * 1e3, elapsed / a.steps * 1e3]
 
     exec_used = loop.exec_microbatch
 
@@ -293,8 +295,20 @@ def main():
         out["config"]["comm"] = ("reducer-owned RCCL communicator, priority %d stream" % nat.stream_priority()
                                  if nat is not None and nat.direct() else
                                  ("c10d process group" if world > 1 else "none (world 1)"))
+    # evidence of what the job ran on: the backend's world size, the ranks of the communicator
+    # the gradient buckets are reduced over (the reducer-owned RCCL communicator's
+    # ncclCommCount in direct mode), and the spread of per-rank step times
+    out["ranks"] = {"backend": dist.get_backend() if world > 1 else None,
+                    "backend_world_size": dist.get_world_size() if world > 1 else 1,
+                    "data_plane_comm_ranks": (loop.ddp_model.comm_ranks()
+                                              if engine == "native" else world),
+                    "rank_ms_per_step_min": round(rank_ms[0], 3),
+                    "rank_ms_per_step_max": round(rank_ms[1], 3)}
     if dev.type == "cuda":  # HBM headroom of the fused schedule (288 GB per MI355X)
         out["peak_hbm_gb"] = round(torch.cuda.max_memory_allocated(dev) / 2**30, 1)
+        free, total = torch.cuda.mem_get_info(dev)
+        out["hbm_free_gb"] = round(free / 2**30, 1)  # device-wide free now (RCCL buffers excluded)
+        out["hbm_total_gb"] = round(total / 2**30, 1)
     if rank == 0:
         out["topology"] = topology()
     if rank == 0:

@@ -247,6 +247,14 @@ class BucketReducer {
     finalize();
   }
 
+  // ranks of the reducer-owned RCCL communicator (ncclCommCount), -1 without one
+  int64_t comm_size() const {
+    if (!rcomm_) return -1;
+    int n = 0;
+    DPA_RCCL_CHECK(ncclCommCount(rcomm_, &n));
+    return n;
+  }
+
   int64_t num_buckets() const { return (int64_t)launched_.size(); }
   int64_t next_bucket() const { return next_; }
   std::vector<int64_t> pending() const {
@@ -468,6 +476,7 @@ void register_comm(pybind11::module& m) {
       .def("finalize", &BucketReducer::finalize, pybind11::call_guard<pybind11::gil_scoped_release>())
       .def("reduce_all", &BucketReducer::reduce_all, pybind11::call_guard<pybind11::gil_scoped_release>())
       .def("num_buckets", &BucketReducer::num_buckets)
+      .def("comm_size", &BucketReducer::comm_size)
       .def("next_bucket", &BucketReducer::next_bucket)
       .def("pending", &BucketReducer::pending);
 }

@@ -269,6 +269,16 @@ class _WgradDeferral:
         for e in self.bias_sites.values():
             self._bias_reduce(e)
 
+    def release_retired(self, stream):
+        """Free the replaced column-sum buffers once ``stream`` has joined every stream that
+        could still use them (the trainer calls this after the overlapped schedule's joins):
+        ``record_stream`` keeps the allocator from reusing a block before the work queued on
+        ``stream`` so far - which follows all of it - has run."""
+        for b in self._retired:
+            if stream is not None and b.is_cuda:
+                b.record_stream(stream)
+        self._retired = []
+
     def drop(self):
         """Forget held operands (an abandoned backward whose gradients are discarded)."""
         self.pending = {}

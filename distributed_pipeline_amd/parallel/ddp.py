@@ -32,8 +32,8 @@ implements the same protocol for the single-GPU multi-rank test transport.
   :meth:`average_gradients` if a plain torch optimizer consumes the grads.
 * Startup: one flat broadcast of all parameters from rank 0 plus a shape
   checksum all-reduce (replaces DDP's per-tensor broadcast, SURVEY X-4).
-* HIP-graph mode: when backward runs inside a captured graph no Python hook
-  fires; :meth:`finalize` then launches every bucket after the replay.
+* Hook-free backward (e.g. a replayed HIP graph, where no Python hook fires):
+  :meth:`reduce_all_now` launches every bucket after it.
 * Unused parameters: a bucket whose hooks have not all fired by ``finalize()`` is
   launched there, after backward, without overlap (torch DDP raises instead).  The
   first armed step records which hooks fired and warns once, naming the unused
@@ -442,6 +442,35 @@ class DDPEngine(nn.Module):
                                "gradients were not reduced; the optimizer step was refused). "
                                "Ranks drifted apart by more than the kernel's 20 s bound - "
                                "unset DPA_IPC_ALLREDUCE to use RCCL, which blocks instead.")
+
+    def comm_ranks(self):
+        """Ranks of the communicator the data plane reduces over: the reducer-owned RCCL
+        communicator's ``ncclCommCount`` in direct mode, else the process group's size
+        (1 when not distributed).  ``bench.py`` reports it as evidence that RCCL saw N ranks."""
+        if not self.distributed:
+            return 1
+        if self._native is not None and self._native.direct():
+            return int(self._native.comm_size())
+        return dist.get_world_size(self.pg)
+
+    def warmup_comm(self):
+        """One reduction of every bucket (of zeroed gradients) on the data plane and one
+        c10d all-reduce of the largest bucket's size, so that RCCL's lazily allocated
+        channel buffers - of the reducer-owned communicator and of the process group's -
+        exist before the trainer sizes its executed micro-batch against free HBM
+        (``TrainLoop._settle_exec_microbatch``).  Leaves the gradients zero."""
+        if not self.distributed:
+            return
+        self.zero_grad()
+        self.reduce_all_now()
+        dev = self.space.grad_flat.device
+        if dist.get_backend(self.pg) != "nccl":
+            dev = torch.device("cpu")
+        big = max(b.end - b.start for b in self.buckets)
+        dist.all_reduce(torch.zeros(big, dtype=torch.float32, device=dev), group=self.pg)
+        if dev.type == "cuda":
+            torch.cuda.synchronize(dev)
+        self.zero_grad()
 
     def reduce_all_now(self):
         """Graph mode: backward ran without hooks; reduce every bucket now."""

@@ -17,6 +17,7 @@
 
 #include "gemm256.hip"
 #include "gemm_pp.hip"
+#include "gemm4w.hip"
 
 namespace dpa {
 int device_cu_count() {
@@ -316,6 +317,43 @@ int main(int argc, char** argv) {
       CK(hipFree(Z2));
       hipLaunchKernelGGL(fill_rand, dim3(4096), dim3(256), 0, 0, Z, maxC, 4u, 1.f);
       CK(hipDeviceSynchronize());
+    }
+    for (auto& v : pv) time_it(v, s, 2);
+    for (int r = 0; r < rounds; ++r)
+      for (auto& v : pv) v.ms.push_back(time_it(v, s, iters));
+    for (auto& v : pv) {
+      std::sort(v.ms.begin(), v.ms.end());
+      const float med = v.ms[v.ms.size() / 2];
+      printf("%-32s median %.4f ms  min %.4f ms  %.1f TF/s\n", v.name.c_str(), med, v.ms[0], v.flop / med / 1e9);
+    }
+    return 0;
+  }
+
+  if (argc > 2 && std::string(argv[2]) == "4w") {
+    // one wave per SIMD (gemm4w.hip) vs the two-wave 8-phase template, main loop only (no
+    // epilogue stores), one tile per workgroup in both (non-persistent)
+    std::vector<Variant> pv;
+    for (const Shape& sh : shapes) {
+      const int K = sh.K, N = sh.N;
+      const double fl = 2.0 * T * K * N;
+      const std::string nm = sh.name;
+      pv.push_back({nm + "/g256_nostore", [=](hipStream_t st) {
+                      hipLaunchKernelGGL((dpa::g256::gemm256_kernel<false, false, dpa::g256::EPI_NONE>),
+                                         dim3((T / 256) * (N / 256)), dim3(512), 0, st, (const dpa::bf16_t*)A,
+                                         (int64_t)K, (const dpa::bf16_t*)B, (int64_t)K, T, N, K / 64, K / 64, 1,
+                                         (dpa::bf16_t*)C, (int64_t)N, nullptr, nullptr, 0, nullptr, nullptr);
+                    }, fl, {}});
+      pv.push_back({nm + "/4w_nostore", [=](hipStream_t st) {
+                      dpa::launch_gemm4w(A, B, C, T, N, K, false, st);
+                    }, fl, {}});
+      pv.push_back({nm + "/fwd_gp", [=](hipStream_t st) {
+                      dpa::launch_gemmp_nt(A, B, nullptr, C, nullptr, T, N, K, 0, ncu, st);
+                    }, fl, {}});
+    }
+    for (const Shape& sh : shapes) {
+      dpa::launch_gemm4w(A, B, C, T, sh.N, sh.K, true, s);
+      CK(hipStreamSynchronize(s));
+      printf("check %s 4w relerr %.3e\n", sh.name, check(A, B, false, C, T, sh.N, sh.K));
     }
     for (auto& v : pv) time_it(v, s, 2);
     for (int r = 0; r < rounds; ++r)

@@ -363,6 +363,11 @@ class TrainLoop:
                     # take them on EVERY rank here, so a reference-style callback that
                     # reads trainer.ema_params on rank 0 alone cannot hang the others.
                     snap = self.ema_params if self._ema_is_collective() else None
+                    # ZeRO-1 with the bf16 shadow all-gather leaves the fp32 master stale
+                    # outside this rank's shards: gather it (a collective, every rank) so a
+                    # callback reading trainer.model / master_params sees the current weights
+                    if hasattr(self.ddp_model, "materialize_master"):
+                        self.ddp_model.materialize_master()
                     if dist_util.get_rank() == 0:
                         self._ema_snapshot = snap
                         try:
@@ -486,10 +491,16 @@ class TrainLoop:
             if not self._exec_settled:
                 self._settle_exec_microbatch(batch)
             return self._forward_backward(batch)
+        reserve = None if self._exec_settled else self._hbm_reserve()
         while True:
             snap = self._log_snapshot()
             try:
-                return self._forward_backward(batch)
+                out = self._forward_backward(batch)
+                if reserve is not None:
+                    del reserve
+                    torch.cuda.empty_cache()
+                self._exec_settled = True
+                return out
             except torch.cuda.OutOfMemoryError:
                 # auto executed micro-batch (one rank): retry the whole step at half the
                 # size; the gradient buffer is zeroed again and the failed try's logged
@@ -502,8 +513,16 @@ class TrainLoop:
                 torch.cuda.empty_cache()
 
     def _shrink_exec_microbatch(self):
-        smaller = max(self.microbatch, (self.exec_microbatch // 2) // self.microbatch * self.microbatch)
-        if smaller == self.exec_microbatch:
+        """Next smaller executed micro-batch: one more chunk per step (balanced chunks, e.g.
+        DiffuSeq-XL's 32 micro-batches as 2 x 1024 -> 3 x ~704 -> 4 x 512), doubling the
+        chunk count past 8 chunks."""
+        mb = self.microbatch
+        nmicro = -(-self.batch_size // mb)
+        cur = -(-self.exec_microbatch // mb)
+        chunks = -(-nmicro // cur)
+        nxt = chunks + 1 if chunks < 8 else chunks * 2
+        smaller = max(mb, min(cur - 1, -(-nmicro // nxt)) * mb)
+        if smaller >= self.exec_microbatch:
             return False
         logger.log(f"exec_microbatch {self.exec_microbatch} does not fit: retrying with {smaller}")
         self.exec_microbatch = smaller
@@ -516,9 +535,15 @@ class TrainLoop:
         then the ranks take the MIN.  A rank that cannot fit even ``microbatch`` reports
         0, so every rank raises together instead of hanging in a collective."""
         import torch.distributed as dist
+        # RCCL allocates its channel buffers lazily, outside torch's caching allocator: run
+        # the data plane's and the process group's first collectives BEFORE probing, so the
+        # probe sizes the executed micro-batch against what they leave free
+        if hasattr(self.ddp_model, "warmup_comm"):
+            self.ddp_model.warmup_comm()
         snap = self._log_snapshot()
         self._probing = True
         ok = True
+        reserve = self._hbm_reserve()
         try:
             with self.ddp_model.no_sync():
                 while True:
@@ -533,9 +558,10 @@ class TrainLoop:
         finally:
             self._probing = False
             self._log_restore(snap)
+            del reserve
         self._zero_grad()
         if torch.cuda.is_available():
-            torch.cuda.empty_cache()
+            torch.cuda.empty_cache()  # hands the probe's (and the reserve's) blocks back to the driver
         dev = dist_util.dev() if dist.get_backend() == "nccl" else torch.device("cpu")
         t = torch.tensor([self.exec_microbatch if ok else 0], dtype=torch.int64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MIN)
@@ -547,6 +573,21 @@ class TrainLoop:
             logger.log(f"exec_microbatch: rank-agreed {agreed} (this rank fit {self.exec_microbatch})")
         self.exec_microbatch = agreed
         self._exec_settled = True
+
+    def _hbm_reserve(self):
+        """HBM held back while the executed micro-batch is probed (``DPA_HBM_RESERVE_GB``;
+        default 8 GB at world > 1, 0 on one rank): what the settled size leaves free for
+        RCCL's later allocations and allocator fragmentation.  Returns the holding tensor."""
+        if not torch.cuda.is_available() or self.device.type != "cuda":
+            return None
+        env = os.environ.get("DPA_HBM_RESERVE_GB", "").strip()
+        gb = float(env) if env else (8.0 if dist_util.get_world_size() > 1 else 0.0)
+        if gb <= 0:
+            return None
+        try:
+            return torch.empty(int(gb * (1 << 30)), dtype=torch.uint8, device=self.device)
+        except torch.cuda.OutOfMemoryError:
+            return None
 
     @staticmethod
     def _log_snapshot():
@@ -714,7 +755,10 @@ class TrainLoop:
             if defer.stream is not None:
                 cur.wait_stream(defer.stream)
             defer.stream = None
-        cur.wait_stream(side)
+            # also on failure: a retry's zero_grad on this stream must follow every kernel
+            # the abandoned attempt queued on the side stream (it adds into the flat grads)
+            cur.wait_stream(side)
+            defer.release_retired(cur)
         # the buffered loss terms of the side stream's chunks are read on this stream now
         for _, t, w, vals in self._loss_log_buf or ():
             for x in (t, w, *vals):
@@ -1132,7 +1176,3 @@ class LMTrainLoop(TrainLoop):
     def backward_from_losses(self, losses):
         (losses["loss"] * self.loss_scale).mean().backward()
 
-
-@contextlib.contextmanager
-def nullcontext():
-    yield
