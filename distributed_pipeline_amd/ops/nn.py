@@ -147,6 +147,38 @@ def _gemm_shape_ok(x2, n_out):
             and x2.shape[0] % 128 == 0 and n_out % 128 == 0 and x2.shape[1] % 128 == 0)
 
 
+# Small token counts (the time-embedding MLP runs on [B, 128] rows: B = 64 in the reference
+# 32 x 64 schedule) are padded with zero rows to a multiple of 128 so the native MFMA GEMMs
+# take them instead of hipBLASLt.  Zero rows add nothing to the weight / bias gradients
+# (their output gradient is zero) and are sliced off the outputs and the input gradient.
+_PAD_ROWS = 128
+_PAD_MAX_T = 8192
+PAD_STATS = {"padded": 0}
+
+
+def _pad_rows(x2, n_outs):
+    """x2 zero-padded to a multiple of 128 rows when that makes the native GEMMs eligible
+    (else x2 itself), and the original row count."""
+    T = x2.shape[0]
+    if (T % _PAD_ROWS == 0 or T > _PAD_MAX_T or GEMM_MODE == "blas" or not x2.is_cuda
+            or x2.dtype != torch.bfloat16 or x2.shape[1] % 128 or any(n % 128 for n in n_outs)
+            or not native_ok(x2, kernel="gemm_nt")):
+        return x2, T
+    Tp = -(-T // _PAD_ROWS) * _PAD_ROWS
+    PAD_STATS["padded"] += 1
+    xp = x2.new_zeros(Tp, x2.shape[1])
+    xp[:T].copy_(x2)
+    return xp, T
+
+
+def _pad_grad(dy2, Tp):
+    if dy2.shape[0] == Tp:
+        return dy2
+    dp = dy2.new_zeros(Tp, dy2.shape[1])
+    dp[:dy2.shape[0]].copy_(dy2)
+    return dp
+
+
 def _route(x2, n_out, act):
     """-> (native_fwd, native_dgrad, native_wgrad)"""
     if GEMM_MODE == "blas" or not _gemm_shape_ok(x2, n_out):
@@ -464,6 +496,23 @@ def _grad_acc(p):
     return g
 
 
+def _into_grad(p, g):
+    """Add a parameter gradient in place into ``p.grad`` when that is a flat fp32 buffer view
+    (native DDP engine) and return None to autograd, else return ``g``.  Nothing then reaches
+    the parameter's AccumulateGrad node: in the overlapped micro-batch schedule the backwards
+    alternate between two HIP streams while each AccumulateGrad node keeps the stream it was
+    created on, so a materialised gradient would make autograd order the two streams against
+    each other (torch's "AccumulateGrad node's stream does not match" warning) - the add runs
+    on the backward's own stream instead."""
+    if g is None or p is None or g is _ACCUMULATED:
+        return g
+    acc = _grad_acc(p)
+    if acc is None:
+        return g
+    acc.add_(g.reshape(acc.shape))
+    return None
+
+
 def _lin_param_grads(w, b, dz, x2, native, db=None):
     """(dW, db) of one Linear from its output-side gradient dz [T, N] and input x2.
 
@@ -473,16 +522,17 @@ def _lin_param_grads(w, b, dz, x2, native, db=None):
     reduced it, else summed here."""
     if db is _ACCUMULATED:
         dw = _accumulate_wgrad(w, dz, x2, None)[0] if native else _mm_fp32(dz.t(), x2)
-        return dw, None
+        return _into_grad(w, dw), None
     if native:
         if db is not None:
             dw, _ = _accumulate_wgrad(w, dz, x2, None)
-            return dw, db
-        return _accumulate_wgrad(w, dz, x2, b)
+            return _into_grad(w, dw), _into_grad(b, db)
+        dw, db = _accumulate_wgrad(w, dz, x2, b)
+        return _into_grad(w, dw), _into_grad(b, db)
     dw = _mm_fp32(dz.t(), x2)
     if b is not None and db is None:
         db = dz.float().sum(0)
-    return dw, db
+    return _into_grad(w, dw), _into_grad(b, db)
 
 
 def _dgrad(dz, w16, native):
@@ -501,7 +551,7 @@ class _LinearFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, w, b, w16, b16, act):
         shp = x.shape
-        x2 = x.reshape(-1, shp[-1])
+        x2, T = _pad_rows(x.reshape(-1, shp[-1]), (w16.shape[0],))
         route = _route(x2, w16.shape[0], act)
         y, z, zact = _lin_fwd(x2, w16, b16, act, route)
         ctx.save_for_backward(x2, w16, z, y if act == "tanh" else None)
@@ -509,13 +559,14 @@ class _LinearFn(torch.autograd.Function):
         ctx.act = zact
         ctx.route = route
         ctx.shp = shp
-        return y.reshape(*shp[:-1], w16.shape[0])
+        ctx.T = T
+        return y[:T].reshape(*shp[:-1], w16.shape[0])
 
     @staticmethod
     def backward(ctx, dy):
         x2, w16, z, y = ctx.saved_tensors
         w, b = ctx.params
-        dy2 = dy.reshape(-1, dy.shape[-1]).contiguous()
+        dy2 = _pad_grad(dy.reshape(-1, dy.shape[-1]).contiguous(), x2.shape[0])
         _, nat_dgrad, nat_wgrad = ctx.route
         db = _take_db(dy2) if (b is not None and ctx.act == "none") else None
         if ctx.act != "none" or (b is not None and db is None and not nat_wgrad):
@@ -523,7 +574,7 @@ class _LinearFn(torch.autograd.Function):
             dz, db = _bias_act_bwd(dy2, z, y, ctx.act, b is not None)
         else:
             dz = dy2
-        dx = _dgrad(dz, w16, nat_dgrad).reshape(ctx.shp) if ctx.needs_input_grad[0] else None
+        dx = _dgrad(dz, w16, nat_dgrad)[:ctx.T].reshape(ctx.shp) if ctx.needs_input_grad[0] else None
         dw, db = _lin_param_grads(w, b, dz, x2, nat_wgrad, db)
         return dx, dw, db, None, None, None
 
@@ -601,22 +652,23 @@ class _MLPFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, w1, b1, w2, b2, w1_16, b1_16, w2_16, b2_16, act):
         shp = x.shape
-        x2 = x.reshape(-1, shp[-1])
+        x2, T = _pad_rows(x.reshape(-1, shp[-1]), (w1_16.shape[0], w2_16.shape[0]))
         y, h, z1, cfg = _mlp_fwd(x2, w1_16, b1_16, w2_16, b2_16, act)
         ctx.save_for_backward(x2, w1_16, w2_16, h, z1)
         ctx.params = (w1, b1, w2, b2)
         ctx.cfg = cfg
         ctx.shp = shp
-        return y.reshape(*shp[:-1], w2_16.shape[0])
+        ctx.T = T
+        return y[:T].reshape(*shp[:-1], w2_16.shape[0])
 
     @staticmethod
     def backward(ctx, dy):
         x2, w1_16, w2_16, h, z1 = ctx.saved_tensors
-        dy2 = dy.reshape(-1, dy.shape[-1]).contiguous()
+        dy2 = _pad_grad(dy.reshape(-1, dy.shape[-1]).contiguous(), x2.shape[0])
         dx, dw1, db1, dw2, db2 = _mlp_bwd(dy2, x2, w1_16, w2_16, h, z1, ctx.params, ctx.cfg,
                                           ctx.needs_input_grad[0])
         if dx is not None:
-            dx = dx.reshape(ctx.shp)
+            dx = dx[:ctx.T].reshape(ctx.shp)
         return dx, dw1, db1, dw2, db2, None, None, None, None, None
 
 
@@ -667,7 +719,7 @@ class _MLPLNFn(torch.autograd.Function):
                                           db2=dyb, dx_acc=dres)
         if dx is not None:
             dx = dx.reshape(ctx.shp)
-        return (dx, dw1, db1, dw2, db2, dlw, dlb) + (None,) * 11
+        return (dx, dw1, db1, dw2, db2, _into_grad(lw, dlw), _into_grad(lb, dlb)) + (None,) * 11
 
 
 class _AttnLNFn(torch.autograd.Function):
@@ -746,7 +798,7 @@ class _AttnLNFn(torch.autograd.Function):
         dwq, dbq = _lin_param_grads(wq, bq, dz, x2, rq[2], dbq)
         if dx is not None:
             dx = dx.reshape(ctx.shp)
-        return (dx, dwq, dbq, dwo, dbo, dlw, dlb) + (None,) * 14
+        return (dx, dwq, dbq, dwo, dbo, _into_grad(lw, dlw), _into_grad(lb, dlb)) + (None,) * 14
 
 
 def _ln_block_ok(x, *lins):
@@ -827,7 +879,7 @@ class _AddLNFn(torch.autograd.Function):
                                                      dg_acc=_grad_acc(w), db_acc=_grad_acc(b))
         if dy is not None:
             _offer_db(dy, dyb)
-        return dy, (dres if has_res else None), dw, db, None, None, None, None, None, None
+        return dy, (dres if has_res else None), _into_grad(w, dw), _into_grad(b, db), None, None, None, None, None, None
 
 
 class _AddLNExFn(torch.autograd.Function):
@@ -1049,6 +1101,7 @@ class _LinearXentFn(torch.autograd.Function):
             loss, lse = ext.lxent_fwd(x, w16, b16, target)
         ctx.save_for_backward(x, w16, b16, target, lse)
         ctx.has_b = b is not None
+        ctx.wb = (w, b)
         return loss
 
     @staticmethod
@@ -1061,7 +1114,8 @@ class _LinearXentFn(torch.autograd.Function):
                                          ctx.has_b and ctx.needs_input_grad[2])
         if dxu is not None:
             dx = dxu.mul_(g.unsqueeze(1)).to(x.dtype)
-        return dx, dw, db, None, None, None
+        w, b = ctx.wb
+        return dx, _into_grad(w, dw), _into_grad(b, db), None, None, None
 
 
 def _pad_vocab(w16, b16, mult=256):
@@ -1105,6 +1159,7 @@ class _ChunkedLinearXentFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, w, b, w16, b16, target, chunk):
         ext = get_ext()
+        ctx.wb = (w, b)
         N0, V = x.shape[0], w16.shape[0]
         N = (N0 + 255) // 256 * 256
         if N != N0:  # token rows padded to the GEMM tile (zero rows, ignored targets)
@@ -1184,7 +1239,8 @@ class _ChunkedLinearXentFn(torch.autograd.Function):
         dw = dwp[:V] if need_dw else None
         if dx is not None and N != N0:
             dx = dx[:N0]
-        return dx, dw, db, None, None, None, None
+        w, b = ctx.wb
+        return dx, _into_grad(w, dw), _into_grad(b, db), None, None, None, None
 
 
 # wide-E CE: kept logit chunks become softmax - onehot in the forward's row pass
@@ -1230,18 +1286,23 @@ class _EmbFn(torch.autograd.Function):
     def forward(ctx, ids, w, w16):
         ctx.save_for_backward(ids)
         ctx.n = w.shape[0]
+        ctx.w = w
         return F.embedding(ids, w16)
 
     @staticmethod
     def backward(ctx, dy):
         (ids,) = ctx.saved_tensors
-        dw = torch.zeros(ctx.n, dy.shape[-1], dtype=torch.float32, device=dy.device)
         if native_ok(dy, kernel="emb_grad") and dy.shape[-1] in (128, 256, 768, 1024, 2048):
-            # sorted segment sum on the device (csrc/diffusion.hip), no ATen index_add
+            # sorted segment sum on the device (csrc/diffusion.hip), no ATen index_add; its
+            # atomics add straight onto the flat fp32 .grad view when there is one
+            acc = _grad_acc(ctx.w)
+            dw = acc if acc is not None else torch.zeros(ctx.n, dy.shape[-1], dtype=torch.float32,
+                                                         device=dy.device)
             get_ext().emb_grad(ids.contiguous(), dy.contiguous(), dw)
-        else:
-            dw.index_add_(0, ids.reshape(-1), dy.reshape(-1, dy.shape[-1]).float())
-        return None, dw, None
+            return None, (None if acc is not None else dw), None
+        dw = torch.zeros(ctx.n, dy.shape[-1], dtype=torch.float32, device=dy.device)
+        dw.index_add_(0, ids.reshape(-1), dy.reshape(-1, dy.shape[-1]).float())
+        return None, _into_grad(ctx.w, dw), None
 
 
 def embedding(ids, weight, dtype):

@@ -188,6 +188,39 @@ def test_fused_mlp_matches_reference():
             _close(a, p.grad)
 
 
+@pytest.mark.parametrize("B", [64, 1, 200])
+def test_small_token_count_padded_to_native(B):
+    """The time-embedding MLP at the reference micro-batch (B = 64 rows of 128) and a Linear
+    at odd small row counts run on the native GEMMs with zero-padded rows (no hipBLASLt):
+    outputs, input gradients and parameter gradients equal the fp32 reference."""
+    from distributed_pipeline_amd.models.layers import MLP, Linear
+    from distributed_pipeline_amd.ops import nn as nn_ops
+    torch.manual_seed(1)
+    m = MLP(128, 512, 768, "silu", init_std=0.05).cuda()
+    lin = Linear(768, 256, act="tanh").cuda()
+    for mod in (m, lin):
+        for p in mod.parameters():
+            p.grad = torch.zeros_like(p)
+    x = torch.randn(B, 128, device="cuda", requires_grad=True)
+    before = nn_ops.PAD_STATS["padded"]
+    y = lin(m(x.bfloat16()))
+    assert nn_ops.PAD_STATS["padded"] >= before + 2, "small-T GEMMs did not take the padded native path"
+    g = torch.randn_like(y)
+    y.backward(g)
+    grads = [p.grad.clone() for mod in (m, lin) for p in mod.parameters()]
+    xg = x.grad.clone()
+    for mod in (m, lin):
+        for p in mod.parameters():
+            p.grad = None
+    x.grad = None
+    yr = lin(m(x))  # fp32 reference path
+    yr.backward(g.float())
+    _close(y, yr.detach())
+    _close(xg, x.grad)
+    for a, p in zip(grads, [p for mod in (m, lin) for p in mod.parameters()]):
+        _close(a, p.grad)
+
+
 def _dact_ref(a, act):
     if act == 1:
         return 0.5 * (1 + torch.erf(a / 2 ** 0.5)) + a * torch.exp(-0.5 * a * a) / (2 * torch.pi) ** 0.5
