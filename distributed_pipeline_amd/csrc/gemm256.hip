@@ -628,7 +628,13 @@ __device__ __forceinline__ float bf_hi(uint32_t w) { return __uint_as_float(w & 
 // rows, column-major inside a group (GM x NT tiles share GM A panels and NT B panels).
 template <int POL>
 __device__ __forceinline__ void st_out(bf16_t* p, const uint4& v) {
-  if constexpr (POL & 1) {
+  if constexpr (POL & 4) {
+    // write-through: the line is not allocated in the XCD's L2, which keeps the operand
+    // panels the next tiles read resident (s_nop 1: the data registers must not be
+    // overwritten before the store has read them - hipcc pads nothing inside an asm)
+    const u32x4_v x = {v.x, v.y, v.z, v.w};
+    asm volatile("global_store_dwordx4 %0, %1, off sc1\n\ts_nop 1" ::"v"(p), "v"(x) : "memory");
+  } else if constexpr (POL & 1) {
     const u32x4_v x = {v.x, v.y, v.z, v.w};
     __builtin_nontemporal_store(x, reinterpret_cast<u32x4_v*>(p));
   } else {

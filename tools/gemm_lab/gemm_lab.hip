@@ -18,6 +18,7 @@
 #include "gemm256.hip"
 #include "gemm_pp.hip"
 #include "gemm4w.hip"
+#include "gemm4p.hip"
 
 namespace dpa {
 int device_cu_count() {
@@ -312,6 +313,88 @@ int main(int argc, char** argv) {
       gps<false, 6, 1, 1, 8, 8, 3>(A, K, B, K, T, N, K, C2, bias, Z2, nullptr, ncu, q, s);
       CK(hipStreamSynchronize(s));
       printf("check stagger gelu y maxdiff %.3e d maxdiff %.3e\n", maxdiff(C, C2, (int64_t)T * N),
+             maxdiff(Z, Z2, (int64_t)T * N));
+      CK(hipFree(C2));
+      CK(hipFree(Z2));
+      hipLaunchKernelGGL(fill_rand, dim3(4096), dim3(256), 0, 0, Z, maxC, 4u, 1.f);
+      CK(hipDeviceSynchronize());
+    }
+    for (auto& v : pv) time_it(v, s, 2);
+    for (int r = 0; r < rounds; ++r)
+      for (auto& v : pv) v.ms.push_back(time_it(v, s, iters));
+    for (auto& v : pv) {
+      std::sort(v.ms.begin(), v.ms.end());
+      const float med = v.ms[v.ms.size() / 2];
+      printf("%-32s median %.4f ms  min %.4f ms  %.1f TF/s\n", v.name.c_str(), med, v.ms[0], v.flop / med / 1e9);
+    }
+    return 0;
+  }
+
+  if (argc > 2 && std::string(argv[2]) == "4p") {
+    // persistent one-wave-per-SIMD 256 x 128 kernel with the epilogue inside the next tile's
+    // main loop (gemm4p.hip) vs the production persistent 8-wave kernel (gemmp_kernel)
+    std::vector<Variant> pv;
+    for (const Shape& sh : shapes) {
+      const int K = sh.K, N = sh.N;
+      const double fl = 2.0 * T * K * N;
+      const std::string nm = sh.name;
+      pv.push_back({nm + "/gp_bias", [=](hipStream_t st) {
+                      dpa::launch_gemmp_nt(A, B, bias, C, nullptr, T, N, K, 0, ncu, st);
+                    }, fl, {}});
+      pv.push_back({nm + "/gp_bias_sc1", [=](hipStream_t st) {
+                      gp<false, 0, 0, 4, 1>(A, K, B, K, T, N, K, C, bias, nullptr, nullptr, ncu, st);
+                    }, fl, {}});
+      pv.push_back({nm + "/4p_bias", [=](hipStream_t st) {
+                      dpa::launch_gemm4p<0, 0>(A, B, bias, C, nullptr, T, N, K, ncu, st);
+                    }, fl, {}});
+      pv.push_back({nm + "/4p_nostore", [=](hipStream_t st) {
+                      dpa::launch_gemm4p<-1, 0>(A, B, bias, C, nullptr, T, N, K, ncu, st);
+                    }, fl, {}});
+      // data gradient dx[T][K] = dy[T][N] W[N][K] (B transposed reads), plain and write-through stores
+      pv.push_back({nm + "/gp_dgrad", [=](hipStream_t st) {
+                      gp<true, 0, 0, 0, 1>(A, N, B, K, T, K, N, C, nullptr, nullptr, nullptr, ncu, st);
+                    }, fl, {}});
+      pv.push_back({nm + "/gp_dgrad_sc1", [=](hipStream_t st) {
+                      gp<true, 0, 0, 4, 1>(A, N, B, K, T, K, N, C, nullptr, nullptr, nullptr, ncu, st);
+                    }, fl, {}});
+      if (nm == "ffn_out") {
+        pv.push_back({nm + "/gp_dgrad_dact_db", [=](hipStream_t st) {
+                        gp<true, 4, 4, 1, 8>(A, 768, B, 3072, T, 3072, 768, C, nullptr, Z, CP, ncu, st);
+                      }, fl, {}});
+        pv.push_back({nm + "/gp_dgrad_dact_db_sc1", [=](hipStream_t st) {
+                        gp<true, 4, 4, 4, 8>(A, 768, B, 3072, T, 3072, 768, C, nullptr, Z, CP, ncu, st);
+                      }, fl, {}});
+      }
+      if (nm == "ffn_in") {
+        pv.push_back({nm + "/gp_gelu_d", [=](hipStream_t st) {
+                        dpa::launch_gemmp_nt(A, B, bias, C, Z, T, N, K, 1, ncu, st, true);
+                      }, fl, {}});
+        pv.push_back({nm + "/gp_gelu_d_sc1", [=](hipStream_t st) {
+                        gp<false, 6, 1, 4, 8>(A, K, B, K, T, N, K, C, bias, Z, nullptr, ncu, st);
+                      }, fl, {}});
+        pv.push_back({nm + "/4p_gelu_d", [=](hipStream_t st) {
+                        dpa::launch_gemm4p<6, 1>(A, B, bias, C, Z, T, N, K, ncu, st);
+                      }, fl, {}});
+      }
+    }
+    for (const Shape& sh : shapes) {
+      dpa::launch_gemm4p<0, 0>(A, B, nullptr, C, nullptr, T, sh.N, sh.K, ncu, s);
+      CK(hipStreamSynchronize(s));
+      printf("check %s 4p relerr %.3e\n", sh.name, check(A, B, false, C, T, sh.N, sh.K));
+    }
+    {  // bias and GELU epilogues vs the production kernel's (same accumulation order)
+      const int K = 768, N = 3072;
+      uint16_t *C2, *Z2;
+      CK(hipMalloc(&C2, (size_t)T * N * 2));
+      CK(hipMalloc(&Z2, (size_t)T * N * 2));
+      dpa::launch_gemmp_nt(A, B, bias, C, nullptr, T, N, K, 0, ncu, s);
+      dpa::launch_gemm4p<0, 0>(A, B, bias, C2, nullptr, T, N, K, ncu, s);
+      CK(hipStreamSynchronize(s));
+      printf("check 4p bias vs gp maxdiff %.3e\n", maxdiff(C, C2, (int64_t)T * N));
+      dpa::launch_gemmp_nt(A, B, bias, C, Z, T, N, K, 1, ncu, s, true);
+      dpa::launch_gemm4p<6, 1>(A, B, bias, C2, Z2, T, N, K, ncu, s);
+      CK(hipStreamSynchronize(s));
+      printf("check 4p gelu vs gp y maxdiff %.3e d maxdiff %.3e\n", maxdiff(C, C2, (int64_t)T * N),
              maxdiff(Z, Z2, (int64_t)T * N));
       CK(hipFree(C2));
       CK(hipFree(Z2));
