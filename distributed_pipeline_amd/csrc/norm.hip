@@ -114,12 +114,19 @@ __device__ __forceinline__ void dropout_keep(uint32_t seed, uint32_t offset, int
 // 1 / gamma for the output-based backward (xhat = (o - b) / gamma, the "memory-efficient"
 // LayerNorm backward; used only when every |gamma| >= LN_XO_GMIN, so never 0 there).
 __device__ __forceinline__ float inv_gamma(float g) { return g != 0.f ? 1.f / g : 0.f; }
-// Guard of the output-based backward: (o - b) / gamma amplifies the bf16 rounding of o by
-// 1 / |gamma|, so a LayerNorm with any |gamma| below this keeps the exact h-copy path: its
-// forward writes the h copy (hguard) and its backward reads it.  Both kernels evaluate the
-// same predicate on the same gamma (the optimizer runs after the backward), so no flag
-// travels between them and nothing syncs with the host.
+// Guard of the output-based backward.  o = xhat * g + b is rounded to bf16 (relative error
+// e of |o|), so xhat = (o - b) / g carries an absolute error e * (|xhat| + |b| / |g|), against
+// e * (|xhat| + |mean| * rstd) for the h copy: the reconstruction is as exact as the h copy
+// only while |b| / |g| stays O(1) and g is not tiny.  A LayerNorm with any column where
+// |g| < LN_XO_GMIN or |b| > LN_XO_BRATIO * |g| keeps the exact h-copy path: its forward writes
+// the h copy (hguard) and its backward reads it.  Both kernels evaluate the same predicate on
+// the same gamma and beta (the optimizer runs after the backward), so no flag travels between
+// them and nothing syncs with the host.
 constexpr float LN_XO_GMIN = 0.125f;
+constexpr float LN_XO_BRATIO = 1.0f;
+__device__ __forceinline__ bool xo_unsafe(float g, float b) {
+  return fabsf(g) < LN_XO_GMIN || fabsf(b) > LN_XO_BRATIO * fabsf(g);
+}
 
 template <int VEC>
 __global__ void __launch_bounds__(256) add_ln_fwd_kernel(
@@ -170,7 +177,7 @@ __global__ void __launch_bounds__(256) add_ln_fwd_kernel(
     // output-based backward unless some |gamma| is small (the row holds all of gamma)
     bool small = false;
 #pragma unroll
-    for (int i = 0; i < VEC; ++i) small |= fabsf(g[i]) < LN_XO_GMIN;
+    for (int i = 0; i < VEC; ++i) small |= xo_unsafe(g[i], b[i]);
     write_h = __builtin_amdgcn_ballot_w64(small) != 0;
   }
   if (write_h) RowIO<VEC>::store(hsave + row * D, lane, h);
@@ -222,9 +229,11 @@ __global__ void __launch_bounds__(256, VEC <= 12 ? 4 : VEC <= 16 ? 2 : 1) add_ln
   __shared__ float cst[XO ? 2 : 1][XO ? D : 1];
   bool xo = false;  // wave-uniform: every wave holds all of gamma
   if constexpr (XO) {
+    float bb[VEC];
+    RowIO<VEC>::load(beta, lane, bb);
     bool small = false;
 #pragma unroll
-    for (int i = 0; i < VEC; ++i) small |= fabsf(g[i]) < LN_XO_GMIN;
+    for (int i = 0; i < VEC; ++i) small |= xo_unsafe(g[i], bb[i]);
     xo = __builtin_amdgcn_ballot_w64(small) == 0;
     for (int c = threadIdx.x; c < D; c += blockDim.x) {
       cst[0][c] = bf2f(beta[c]);
@@ -406,7 +415,7 @@ __global__ void __launch_bounds__(256) add_ln_bwd_rowblk_kernel(
 #pragma unroll
     for (int i = 0; i < VT; ++i) {
       rg[i] = inv_gamma(g[i]);
-      small |= fabsf(g[i]) < LN_XO_GMIN;
+      small |= xo_unsafe(g[i], bt[i]);
     }
     if (t == 0) nsmall = 0;
     __syncthreads();

@@ -136,9 +136,10 @@ _SAVE_ACT_DERIV = os.environ.get("DPA_SAVE_ACT_DERIV", "1") != "0"
 # post-LN sublayers: the LayerNorm backward reconstructs xhat = (out - beta) / gamma from the
 # sublayer's output - which the next sublayer keeps alive anyway as its input - instead of
 # the forward writing a bf16 copy of h (one [T, D] store less per sublayer).  Guarded: a
-# LayerNorm with any |gamma| < 0.125 (where 1 / gamma would amplify out's bf16 rounding) keeps
-# the exact h-copy path - both kernels test the same gamma on the device, no host sync
-# (norm.hip LN_XO_GMIN).  DPA_LN_SAVE_OUT=0: always the h copy.
+# LayerNorm with any column where |gamma| < 0.125 or |beta| > |gamma| (where the
+# reconstruction would amplify out's bf16 rounding) keeps the exact h-copy path - both kernels
+# test the same gamma / beta on the device, no host sync (norm.hip xo_unsafe).
+# DPA_LN_SAVE_OUT=0: always the h copy.
 _LN_SAVE_OUT = os.environ.get("DPA_LN_SAVE_OUT", "1") != "0"
 
 

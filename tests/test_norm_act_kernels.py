@@ -52,7 +52,7 @@ def test_add_ln_bwd_from_output(R, D, p):
     y = torch.randn(R, D, device="cuda").bfloat16()
     r = torch.randn(R, D, device="cuda").bfloat16()
     g = (1 + 0.1 * torch.randn(D, device="cuda")).clamp(min=0.6).bfloat16()
-    b = (0.2 * torch.randn(D, device="cuda")).bfloat16()
+    b = (0.2 * torch.randn(D, device="cuda")).clamp(-0.5, 0.5).bfloat16()  # |b| < |g|: unguarded
     out, hs, mean, rstd = ext.add_ln_fwd(y, r, g, b, p, 1e-12, 3, 9)
     hc = torch.full_like(hs, float("nan"))  # the guarded copy must stay unwritten and unread
     out2, hs2, mean2, rstd2 = ext.add_ln_fwd(y, r, g, b, p, 1e-12, 3, 9, h_guard=True)
@@ -73,7 +73,8 @@ def test_add_ln_bwd_from_output(R, D, p):
         assert e_got.mean().item() <= 1.5 * e_ref.mean().item() + 1e-4, (k, e_got.mean().item(), e_ref.mean().item())
     for k, want in ((2, gf.grad), (3, bf.grad), (4, ref[4])):
         torch.testing.assert_close(got[k], want, rtol=1e-2, atol=1e-2 * want.abs().max().item())
-    # guard: a small gamma entry -> the h copy is written and read, results == h-copy kernels
+    # guard: a small gamma entry, or a column with |beta| > |gamma|, -> the h copy is written
+    # and read, results == h-copy kernels
     gs = g.clone()
     gs[5] = 0.01
     out3, hs3, mean3, rstd3 = ext.add_ln_fwd(y, r, gs, b, p, 1e-12, 3, 9)
@@ -88,6 +89,43 @@ def test_add_ln_bwd_from_output(R, D, p):
             torch.testing.assert_close(a.float(), e.float(), rtol=8e-3, atol=1e-3 * e.float().abs().max().item())
         else:
             torch.testing.assert_close(a, e, rtol=1e-4, atol=1e-4 * e.abs().max().item())
+    bs = b.clone()
+    bs[7] = 1.5 * g[7].float()
+    _, hgb, _, _ = ext.add_ln_fwd(y, r, g, bs, p, 1e-12, 3, 9, h_guard=True)
+    _, hsb, _, _ = ext.add_ln_fwd(y, r, g, bs, p, 1e-12, 3, 9)
+    assert torch.equal(hgb, hsb), "a |beta| > |gamma| column must keep the h copy"
+
+
+@pytest.mark.parametrize("gmin", [0.13, 0.25, 0.5])
+@pytest.mark.parametrize("bscale", [0.1, 0.5, 2.0])
+def test_add_ln_bwd_from_output_guard_region(gmin, bscale):
+    """The output-based backward (or its guard) over gamma spreads down to min |gamma| in
+    {0.13, 0.25, 0.5} and realistic-to-large beta: every combination must be as accurate as
+    the h-copy backward against the fp32 LayerNorm of the same bf16 h (the guard sends the
+    columns / layers where (out - beta) / gamma would amplify out's rounding to the h copy)."""
+    ext = _ext()
+    torch.manual_seed(1)
+    R, D, p = 4096, 768, 0.1
+    y = torch.randn(R, D, device="cuda").bfloat16()
+    r = torch.randn(R, D, device="cuda").bfloat16()
+    g = (gmin + (1.5 - gmin) * torch.rand(D, device="cuda"))
+    g = (g * torch.where(torch.rand(D, device="cuda") < 0.5, -1.0, 1.0)).bfloat16()
+    b = (bscale * torch.randn(D, device="cuda")).bfloat16()
+    out, hs, mean, rstd = ext.add_ln_fwd(y, r, g, b, p, 1e-12, 5, 2)
+    _, hg, _, _ = ext.add_ln_fwd(y, r, g, b, p, 1e-12, 5, 2, h_guard=True)
+    dout = torch.randn(R, D, device="cuda").bfloat16()
+    ref = ext.add_ln_bwd(dout, hs, mean, rstd, g, p, 5, 2, True, True, True)
+    got = ext.add_ln_bwd(dout, out, mean, rstd, g, p, 5, 2, True, True, True, beta=b, hcopy=hg)
+    h = hs.float().requires_grad_(True)
+    gf = g.float().requires_grad_(True)
+    bf = b.float().requires_grad_(True)
+    torch.nn.functional.layer_norm(h, (D,), gf, bf, 1e-12).backward(dout.float())
+    for k, want in ((0, h.grad), (2, gf.grad)):
+        e_got = (got[k].float() - want).abs()
+        e_ref = (ref[k].float() - want).abs()
+        assert e_got.max().item() <= 2 * e_ref.max().item() + 1e-2 * want.abs().max().item(), (
+            k, e_got.max().item(), e_ref.max().item())
+        assert e_got.mean().item() <= 1.5 * e_ref.mean().item() + 1e-4, (k, e_got.mean().item(), e_ref.mean().item())
 
 
 @pytest.mark.parametrize("R,D", [(2048, 768), (2048, 2048), (70000, 2048), (512, 128)])
