@@ -74,6 +74,12 @@ def bucket_members(numels, cap_mb, first_mb):
     space exists (the sharded engine pads the space at these bucket ends)."""
     groups, cur, off, cur_start, limit = [], [], 0, 0, first_mb * _MiB
     for i, n in enumerate(numels):
+        if cur and n * 4 > cap_mb * _MiB:
+            # a parameter larger than a whole bucket (GPT-2's tied 50257 x 768 embedding,
+            # 154 MB) gets a bucket of its own: the parameters before it are not held back
+            # until its gradient - complete only after the embedding backward - is ready
+            groups.append(cur)
+            cur, cur_start, limit = [], off, cap_mb * _MiB
         cur.append(i)
         off = (off + n + ALIGN - 1) // ALIGN * ALIGN
         if (off - cur_start) * 4 >= limit or i == len(numels) - 1:
@@ -90,6 +96,10 @@ def plan_buckets(space, cap_mb, first_mb):
     cur_start, cur_params = 0, []
     limit = first_mb * _MiB
     for i, p in enumerate(layout):
+        if cur_params and p.numel() * 4 > cap_mb * _MiB:  # own bucket (see bucket_members)
+            buckets.append((cur_start, starts[i], cur_params))
+            cur_start, cur_params = starts[i], []
+            limit = cap_mb * _MiB
         cur_params.append(p)
         end = starts[i + 1]
         if (end - cur_start) * 4 >= limit or i == len(layout) - 1:

@@ -31,11 +31,22 @@ def test_bucket_plan_partition(sizes, cap_kb, first_kb):
             off = space.offsets[id(p)]
             assert s <= off and off + p.numel() <= e
     # a bucket closes as soon as it reaches its limit: dropping its last parameter
-    # would leave it under the limit (first bucket: first_mb, then cap_mb)
+    # would leave it under the limit (first bucket: first_mb, then cap_mb) - or early, when
+    # the next parameter alone exceeds cap_mb (that one gets a bucket of its own)
     for i, (s, e, ps) in enumerate(buckets[:-1]):
         limit = (first if i == 0 else cap) * _MiB
         last_off = space.offsets[id(ps[-1])]
         assert (last_off - s) * 4 < limit
+        nxt = buckets[i + 1][2][0]
+        if (e - s) * 4 < limit:
+            assert nxt.numel() * 4 > cap * _MiB
+    for s, e, ps in buckets:
+        if any(p.numel() * 4 > cap * _MiB for p in ps[1:]):
+            raise AssertionError("an oversized parameter shares a bucket with earlier ones")
+    # the planner the sharded engine uses before the flat space exists agrees
+    from distributed_pipeline_amd.parallel.ddp import bucket_members
+    idx = {id(p): i for i, p in enumerate(space.layout)}
+    assert bucket_members([p.numel() for p in space.layout], cap, first) == [[idx[id(p)] for p in b[2]] for b in buckets]
 
 
 @settings(max_examples=30, deadline=None)

@@ -20,13 +20,7 @@
 #include "gemm4w.hip"
 #include "gemm4p.hip"
 
-namespace dpa {
-int device_cu_count() {
-  int n = 0;
-  (void)hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, 0);
-  return n;
-}
-}  // namespace dpa
+#include "gemm.hip"  // 128 x 128 kernels (and device_cu_count)
 
 
 #define CK(x)                                                                      \
@@ -318,6 +312,45 @@ int main(int argc, char** argv) {
       CK(hipFree(Z2));
       hipLaunchKernelGGL(fill_rand, dim3(4096), dim3(256), 0, 0, Z, maxC, 4u, 1.f);
       CK(hipDeviceSynchronize());
+    }
+    for (auto& v : pv) time_it(v, s, 2);
+    for (int r = 0; r < rounds; ++r)
+      for (auto& v : pv) v.ms.push_back(time_it(v, s, iters));
+    for (auto& v : pv) {
+      std::sort(v.ms.begin(), v.ms.end());
+      const float med = v.ms[v.ms.size() / 2];
+      printf("%-32s median %.4f ms  min %.4f ms  %.1f TF/s\n", v.name.c_str(), med, v.ms[0], v.flop / med / 1e9);
+    }
+    return 0;
+  }
+
+  if (argc > 2 && std::string(argv[2]) == "small") {
+    // reference-schedule micro-batch (64 x 128 = 8192 tokens): persistent 256 x 256 tiles
+    // (96-384 tiles for 256 CUs) vs the 128 x 128 kernel (4x the tiles)
+    const int Ts = 8192;
+    std::vector<Variant> pv;
+    for (const Shape& sh : shapes) {
+      const int K = sh.K, N = sh.N;
+      const double fl = 2.0 * Ts * K * N;
+      const std::string nm = sh.name;
+      pv.push_back({nm + "/fwd_gp256", [=](hipStream_t st) {
+                      dpa::launch_gemmp_nt(A, B, bias, C, nullptr, Ts, N, K, 0, ncu, st);
+                    }, fl, {}});
+      pv.push_back({nm + "/fwd_t128", [=](hipStream_t st) {
+                      hipLaunchKernelGGL((dpa::gemm_kernel<false, false, dpa::EPI_BIAS_ACT>), dim3((Ts / 128) * (N / 128)),
+                                         dim3(256), 0, st, (const dpa::bf16_t*)A, (int64_t)K, (const dpa::bf16_t*)B,
+                                         (int64_t)K, Ts, N, K, K, 1, (dpa::bf16_t*)C, (int64_t)N, nullptr,
+                                         (const dpa::bf16_t*)bias, 0, nullptr, nullptr);
+                    }, fl, {}});
+      pv.push_back({nm + "/dgrad_gp256", [=](hipStream_t st) {
+                      dpa::launch_gemmp_nn(A, B, C, nullptr, 0, Ts, N, K, ncu, st, nullptr);
+                    }, fl, {}});
+      pv.push_back({nm + "/dgrad_t128", [=](hipStream_t st) {
+                      hipLaunchKernelGGL((dpa::gemm_kernel<false, true, dpa::EPI_BF16>), dim3((Ts / 128) * (K / 128)),
+                                         dim3(256), 0, st, (const dpa::bf16_t*)A, (int64_t)N, (const dpa::bf16_t*)B,
+                                         (int64_t)K, Ts, K, N, N, 1, (dpa::bf16_t*)C, (int64_t)K, nullptr, nullptr, 0,
+                                         nullptr, nullptr);
+                    }, fl, {}});
     }
     for (auto& v : pv) time_it(v, s, 2);
     for (int r = 0; r < rounds; ++r)
