@@ -56,6 +56,8 @@ def parse():
                          "allocator pools in the first steps)")
     ap.add_argument("--ref-steps", type=int, default=8,
                     help="also time this many steps of the reference 32 x 64 schedule (0 = skip)")
+    ap.add_argument("--ref-graph", type=int, default=1,
+                    help="run the reference schedule as a replayed HIP graph (TrainLoop cuda_graph; 0 = eager)")
     ap.add_argument("--ref-windows", type=int, default=1,
                     help="time the reference schedule in this many back-to-back windows of --ref-steps "
                          "(the mean over all is reported, each window under windows_ms)")
@@ -206,7 +208,9 @@ def main():
         # all but the last (same model, optimizer state and process)
         loop._exec_auto = False
         loop.exec_microbatch = a.microbatch
-        for _ in range(max(1, a.ref_warmup)):  # warm the small-shape kernels and stream pools
+        loop.cuda_graph = bool(a.ref_graph) and dev.type == "cuda"
+        # (graph mode: two eager steps, then the capture + first replay - all untimed)
+        for _ in range(max(3 if loop.cuda_graph else 1, a.ref_warmup)):
             one_step()
         diag = []
         if a.ref_windows > 1:  # per-window diagnostics: allocator growth and Python GC time
@@ -240,6 +244,7 @@ def main():
         wins = [win() for _ in range(max(1, a.ref_windows))]
         e, n_ref = sum(wins), a.ref_steps * len(wins)
         ref_sched = {"exec_microbatch": a.microbatch, "steps": n_ref,
+                     "hip_graph": loop._graph is not None,
                      "ms_per_step": round(e / n_ref * 1e3, 3),
                      "value": round(n_ref / e * world, 4)}
         if len(wins) > 1:

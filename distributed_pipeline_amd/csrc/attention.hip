@@ -45,7 +45,7 @@ __device__ __forceinline__ DropCfg make_drop(float p, uint32_t seed, uint32_t of
   d.on = p > 0.f;
   d.thr16 = (uint32_t)(p * 65536.f + 0.5f);
   d.scale = d.on ? 1.f / (1.f - p) : 1.f;
-  d.seedmix = lowbias32(seed ^ lowbias32(offset * 0xC2B2AE3Du ^ (bh * 0x27D4EB2Fu)));
+  d.seedmix = lowbias32(seed ^ lowbias32((offset + rng_base()) * 0xC2B2AE3Du ^ (bh * 0x27D4EB2Fu)));
   return d;
 }
 
@@ -1018,5 +1018,7 @@ void launch_colpart_reduce(const float* colpart, float* db, int R, int H, int D,
   hipLaunchKernelGGL(colpart_reduce_d_kernel, dim3(3 * H * (D / 64), nch), dim3(256), 0, s, colpart, db, R, H,
                      D, rchunk);
 }
+
+DPA_RNG_BASE_EXPORT(attention)
 
 }  // namespace dpa

@@ -51,7 +51,7 @@ __device__ __forceinline__ DropCfg make_drop(float p, uint32_t seed, uint32_t of
   d.on = p > 0.f;
   d.thr16 = (uint32_t)(p * 65536.f + 0.5f);
   d.scale = d.on ? 1.f / (1.f - p) : 1.f;
-  d.seedmix = lowbias32(seed ^ lowbias32(offset * 0xC2B2AE3Du ^ (bh * 0x27D4EB2Fu)));
+  d.seedmix = lowbias32(seed ^ lowbias32((offset + rng_base()) * 0xC2B2AE3Du ^ (bh * 0x27D4EB2Fu)));
   return d;
 }
 __device__ __forceinline__ uint32_t drop_hash(const DropCfg& d, int q, int key) {
@@ -1265,5 +1265,7 @@ bool launch_attn128_bwd(const uint16_t* qkv, const uint16_t* out, const uint16_t
   }
   return true;
 }
+
+DPA_RNG_BASE_EXPORT(attention128)
 
 }  // namespace dpa

@@ -834,6 +834,17 @@ static std::vector<at::Tensor> diff_loss_bwd(const at::Tensor& xs, const at::Ten
   return {d_out, d_xs};
 }
 
+// Bump the device-side Philox offset base of every kernel translation unit that draws noise
+// or dropout (common.h g_rng_base): a replayed HIP graph's baked offsets + the base = fresh
+// numbers per replay.  Stream-ordered on the current stream.
+static void rng_base_add(int64_t d) {
+  const auto s = cur_stream();
+  dpa::rng_base_add_attention((uint32_t)d, s);
+  dpa::rng_base_add_attention128((uint32_t)d, s);
+  dpa::rng_base_add_diffusion((uint32_t)d, s);
+  dpa::rng_base_add_norm((uint32_t)d, s);
+}
+
 static at::Tensor timestep_emb(const at::Tensor& ts, int64_t dim, double max_period) {
   CHECK_DEV(ts); CHECK_F32(ts); CHECK_CONTIG(ts);
   TORCH_CHECK(ts.dim() == 1 && dim > 0, "timesteps [B]");
@@ -917,5 +928,6 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("emb_qsample_bwd", &emb_qsample_bwd, "scatter-add of the q_sample gradients into dW (fp32)");
   m.def("diff_loss_fwd", &diff_loss_fwd, "DiffuSeq per-sample (mse, tT) losses");
   m.def("diff_loss_bwd", &diff_loss_bwd, "backward of diff_loss_fwd -> (d_out, d_x_start)");
+  m.def("rng_base_add", &rng_base_add, "advance the device-side Philox offset base (graph replays)");
   m.def("timestep_emb", &timestep_emb, "sinusoidal timestep embedding [cos | sin] -> bf16");
 }

@@ -37,6 +37,22 @@ __device__ __forceinline__ bf16_t f2bf(float f) {
   return __builtin_bit_cast(bf16_t, (__bf16)f);
 }
 
+// ---- device-side base of the in-kernel Philox offsets -----------------------
+// Every kernel that draws noise or dropout adds g_rng_base to the offset its launch passes; it
+// is 0 in eager runs.  A replayed HIP graph bakes its launches' offsets, so the trainer bumps
+// the base once per replay (rng_base_add, a one-thread kernel) and every replay draws fresh
+// numbers.  Internal linkage: one copy per translation unit, so each TU that draws numbers
+// exports its own rng_base_add_<tu> (DPA_RNG_BASE_EXPORT) and bindings.cpp bumps them all.
+static __device__ uint32_t g_rng_base;
+static __global__ void rng_base_add_kernel(uint32_t d) {
+  if (threadIdx.x == 0) g_rng_base += d;
+}
+__device__ __forceinline__ uint32_t rng_base() { return g_rng_base; }
+#define DPA_RNG_BASE_EXPORT(NAME)                                          \
+  void rng_base_add_##NAME(uint32_t d, hipStream_t s) {                    \
+    hipLaunchKernelGGL(rng_base_add_kernel, dim3(1), dim3(64), 0, s, d);   \
+  }
+
 // ---- wave64 reductions ----------------------------------------------------
 __device__ __forceinline__ float wave_sum(float v) {
 #pragma unroll

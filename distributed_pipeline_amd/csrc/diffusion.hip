@@ -32,7 +32,7 @@ namespace dpa {
 __device__ __forceinline__ void normal4(uint32_t seed, uint32_t stream, uint32_t offset,
                                         uint64_t grp, float out[4]) {
   uint32_t r[4];
-  philox4(seed, 0x2545F491u ^ stream, (uint32_t)grp, (uint32_t)(grp >> 32), offset, stream, r);
+  philox4(seed, 0x2545F491u ^ stream, (uint32_t)grp, (uint32_t)(grp >> 32), offset + rng_base(), stream, r);
 #pragma unroll
   for (int k = 0; k < 2; ++k) {
     // u1 in (0, 1]: never log(0)
@@ -387,5 +387,7 @@ void launch_timestep_emb(const float* ts, int B, int dim, float max_period, uint
   hipLaunchKernelGGL(timestep_emb_kernel, dim3(grid_cap((int64_t)B * dim, 1024)), dim3(256), 0, s, ts,
                      B, dim, logf(max_period), (bf16_t*)out);
 }
+
+DPA_RNG_BASE_EXPORT(diffusion)
 
 }  // namespace dpa

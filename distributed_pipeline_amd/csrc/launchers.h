@@ -182,5 +182,11 @@ bool launch_gemmp_nn(const uint16_t* dy, const uint16_t* W, uint16_t* dx, const 
 bool launch_gemmp_nn_acc(const uint16_t* dy, const uint16_t* W, uint16_t* dx, int T, int N, int K, int ncu,
                          hipStream_t s);
 int device_cu_count();
+// bump the device-side Philox offset base of each translation unit that draws numbers
+// (common.h g_rng_base: graph replays)
+void rng_base_add_attention(uint32_t d, hipStream_t s);
+void rng_base_add_attention128(uint32_t d, hipStream_t s);
+void rng_base_add_diffusion(uint32_t d, hipStream_t s);
+void rng_base_add_norm(uint32_t d, hipStream_t s);
 
 }  // namespace dpa

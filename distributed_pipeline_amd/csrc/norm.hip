@@ -94,7 +94,7 @@ __device__ __forceinline__ void dropout_keep(uint32_t seed, uint32_t offset, int
     for (int c = 0; c < VEC / 4; ++c) {
       const int col = M::col(ln, 4 * c);
       uint32_t r[4];
-      philox4(seed, 0x5bd1e995u, (uint32_t)row, (uint32_t)(row >> 32) ^ (uint32_t)(col >> 2), offset,
+      philox4(seed, 0x5bd1e995u, (uint32_t)row, (uint32_t)(row >> 32) ^ (uint32_t)(col >> 2), offset + rng_base(),
               0xdeadbeefu, r);
 #pragma unroll
       for (int k = 0; k < 4; ++k) keep[4 * c + k] = r[k] >= thr;
@@ -104,7 +104,7 @@ __device__ __forceinline__ void dropout_keep(uint32_t seed, uint32_t offset, int
     for (int i = 0; i < VEC; ++i) {
       const int col = M::col(ln, i);
       uint32_t r[4];
-      philox4(seed, 0x5bd1e995u, (uint32_t)row, (uint32_t)(row >> 32) ^ (uint32_t)(col >> 2), offset,
+      philox4(seed, 0x5bd1e995u, (uint32_t)row, (uint32_t)(row >> 32) ^ (uint32_t)(col >> 2), offset + rng_base(),
               0xdeadbeefu, r);
       keep[i] = r[col & 3] >= thr;
     }
@@ -393,7 +393,7 @@ __global__ void __launch_bounds__(256) add_ln_bwd_rowblk_kernel(
       const int c = col(i);  // pairs never straddle a 4-column Philox block (c even)
       uint32_t r[4];
       if (CH >= 4 && (i % 4) != 0) continue;
-      philox4(seed, 0x5bd1e995u, (uint32_t)row, (uint32_t)(row >> 32) ^ (uint32_t)(c >> 2), offset,
+      philox4(seed, 0x5bd1e995u, (uint32_t)row, (uint32_t)(row >> 32) ^ (uint32_t)(c >> 2), offset + rng_base(),
               0xdeadbeefu, r);
       if constexpr (CH >= 4) {
 #pragma unroll
@@ -671,5 +671,7 @@ bool launch_add_ln_bwd(const uint16_t* dout, const uint16_t* hsave, const float*
                   off, dh_in, post, zero_mask, s, ws, part_mode, beta, hcopy)
   return true;
 }
+
+DPA_RNG_BASE_EXPORT(norm)
 
 }  // namespace dpa

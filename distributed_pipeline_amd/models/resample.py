@@ -32,6 +32,8 @@ class ScheduleSampler:
 
 
 class UniformSampler(ScheduleSampler):
+    graph_safe = True  # device-side draw from the default CUDA generator (graph-capturable)
+
     def weights(self):
         return np.ones([self.num_timesteps])
 
@@ -41,6 +43,8 @@ class UniformSampler(ScheduleSampler):
 
 
 class FixSampler(ScheduleSampler):
+    graph_safe = True
+
     def weights(self):
         w = np.zeros([self.num_timesteps])
         w[-1] = 1.0

@@ -978,21 +978,36 @@ def residual_layernorm(h, x, weight, bias, p=0.0, eps=1e-5, training=True, pos=N
 
 
 class RNG:
-    """Device-resident (seed, offset) for the in-kernel Philox streams.
+    """(seed, offset) of the in-kernel Philox streams.
 
-    Kernels read nothing from the host per call: the offset is a python int
-    that advances per call site, so eager runs get fresh randomness.  Graph
-    capture uses ``graph_safe_offsets``: offsets are baked in but combined with
-    a device counter bumped once per replay.
-    """
+    Eager runs: the offset is a host counter that advances per call site, so every launch
+    draws fresh numbers.  HIP-graph replays (utils/trainer.py graph mode): the offsets are
+    baked into the captured launches, and every kernel adds a device-side base
+    (csrc/common.h ``g_rng_base``, 0 in eager runs).  ``graph_begin`` sets the base so a
+    replay of a graph captured at offsets [r0, r0 + span) draws [counter, counter + span) -
+    exactly what an eager step would have drawn next - and ``graph_end`` resets it to 0."""
     seed = 1234
     counter = 0
+    _dev_base = 0
 
     @classmethod
     def next(cls, n=1):
         off = cls.counter
         cls.counter += n
         return cls.seed, off
+
+    @classmethod
+    def graph_begin(cls, r0, span):
+        d = (cls.counter - r0) & 0xFFFFFFFF
+        get_ext().rng_base_add(d)
+        cls._dev_base = d
+        cls.counter += span
+
+    @classmethod
+    def graph_end(cls):
+        if cls._dev_base:
+            get_ext().rng_base_add((-cls._dev_base) & 0xFFFFFFFF)
+            cls._dev_base = 0
 
 
 def add_dropout_layernorm(y, residual, weight, bias, p=0.0, eps=1e-12, training=True):

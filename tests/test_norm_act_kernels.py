@@ -120,12 +120,16 @@ def test_add_ln_bwd_from_output_guard_region(gmin, bscale):
     gf = g.float().requires_grad_(True)
     bf = b.float().requires_grad_(True)
     torch.nn.functional.layer_norm(h, (D,), gf, bf, 1e-12).backward(dout.float())
-    for k, want in ((0, h.grad), (2, gf.grad)):
-        e_got = (got[k].float() - want).abs()
-        e_ref = (ref[k].float() - want).abs()
-        assert e_got.max().item() <= 2 * e_ref.max().item() + 1e-2 * want.abs().max().item(), (
-            k, e_got.max().item(), e_ref.max().item())
-        assert e_got.mean().item() <= 1.5 * e_ref.mean().item() + 1e-4, (k, e_got.mean().item(), e_ref.mean().item())
+    # dx: within the h-copy backward's own bf16 error
+    e_got = (got[0].float() - h.grad).abs()
+    e_ref = (ref[0].float() - h.grad).abs()
+    assert e_got.max().item() <= 2 * e_ref.max().item() + 1e-2 * h.grad.abs().max().item(), (
+        e_got.max().item(), e_ref.max().item())
+    assert e_got.mean().item() <= 1.5 * e_ref.mean().item() + 1e-4, (e_got.mean().item(), e_ref.mean().item())
+    # dgamma / dbeta: sums over 4096 rows of dout x xhat, where the output-based xhat carries
+    # out's bf16 rounding (the h copy's rounding is inside the reference): bf16-level agreement
+    for k, want in ((2, gf.grad), (3, bf.grad)):
+        torch.testing.assert_close(got[k], want, rtol=1e-2, atol=1e-2 * want.abs().max().item())
 
 
 @pytest.mark.parametrize("R,D", [(2048, 768), (2048, 2048), (70000, 2048), (512, 128)])

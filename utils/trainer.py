@@ -144,6 +144,7 @@ class TrainLoop:
             save_rng_state=True,
             flops_per_sample=None,
             peak_tflops=None,
+            cuda_graph=False,
     ):
         self.model = model
         self.data = data
@@ -209,6 +210,13 @@ class TrainLoop:
         self.flops_per_sample = flops_per_sample
         self.peak_tflops = float(peak_tflops or os.environ.get("DPA_PEAK_TFLOPS", 2500.0))
         self._profile_window = _parse_window(profile_steps)
+        # HIP-graph mode (native engine, fixed executed micro-batch): after two eager steps the
+        # whole forward/backward of a step - every micro-batch, all streams - is captured once
+        # and replayed; DPA_CUDA_GRAPH=1 turns it on as well
+        self.cuda_graph = (bool(cuda_graph) or os.environ.get("DPA_CUDA_GRAPH", "0") == "1")
+        self._graph = None
+        self._graph_eager_steps = 0
+        self._graph_capturing = False
         self._profiler = None
         self._tp = None  # (wall time, step) at the start of the throughput window
         self._tokens_per_sample = None
@@ -463,7 +471,7 @@ class TrainLoop:
         size = size or self.microbatch
         micro_batch = self._slice_to_device(total_batch, start_index, size)
         last_batch = (start_index + size) >= self.get_batch_length(total_batch)
-        if last_batch or not self.use_ddp:
+        if (last_batch or not self.use_ddp) and not self._graph_capturing:
             losses = self.compute_losses(micro_batch)
         else:
             with self.ddp_model.no_sync():
@@ -480,6 +488,8 @@ class TrainLoop:
         self.model.train(was_training)
 
     def forward_backward(self, batch):
+        if self._graph_ok(batch):
+            return self._forward_backward_graphed(batch)
         if not self._exec_auto or self.exec_microbatch <= self.microbatch:
             return self._forward_backward(batch)
         if self.use_ddp and (dist_util.get_world_size() > 1 or self.engine_kind != "native"):
@@ -511,6 +521,73 @@ class TrainLoop:
                 if self.use_ddp and hasattr(self.ddp_model, "disarm"):
                     self.ddp_model.disarm()
                 torch.cuda.empty_cache()
+
+    # ---- HIP-graph mode ---------------------------------------------------------------
+    def _graph_ok(self, batch):
+        """Graph mode applies to the native engine on a GPU with a fixed executed micro-batch
+        (not the auto size, which may still shrink) and a device-side timestep sampler."""
+        if not self.cuda_graph or self.engine_kind != "native" or self.device.type != "cuda":
+            return False
+        if self._exec_auto or not isinstance(batch, dict) or not getattr(self, "graph_logging", False):
+            return False
+        sampler = getattr(self, "schedule_sampler", None)
+        return sampler is None or getattr(sampler, "graph_safe", False)
+
+    def _forward_backward_graphed(self, batch):
+        """The step's forward/backward as one replayed HIP graph (SURVEY 5.1 / VERDICT r3:
+        the reference 32 x 64 schedule issues ~1,500 launches per micro-batch pair from
+        Python; a replay issues them from the device queue).
+
+        * Two eager steps first (allocator pools, the extension's lazily built state, the
+          deferral buffers), then one capture of ``_forward_backward`` on static copies of the
+          batch tensors, then a replay per step.
+        * Randomness: the in-kernel Philox offsets are baked into the graph, so every replay
+          is bracketed by ``ops.nn.RNG.graph_begin`` / ``graph_end`` (a device-side offset
+          base: the replay draws what an eager step would have drawn next); the timestep
+          sampler draws from torch's default CUDA generator, which graph capture registers
+          (fresh numbers per replay as well).
+        * Loss logging: the captured chunks' loss tensors are static graph outputs; they are
+          logged after each replay.
+        * DDP: nothing is reduced inside the graph (every micro-batch runs under ``no_sync``,
+          no bucket hook fires in a replay); ``reduce_all_now`` reduces every bucket after it.
+        """
+        from distributed_pipeline_amd.ops.nn import RNG
+        if self._graph is None and self._graph_eager_steps < 2:
+            self._graph_eager_steps += 1
+            return self._forward_backward(batch)
+        if self._graph is None:
+            self._capture_step(batch)
+        st = self._graph_state
+        for k, v in batch.items():
+            st["inputs"][k].copy_(v.to(self.device, non_blocking=True), non_blocking=True)
+        RNG.graph_begin(st["rng_r0"], st["rng_span"])
+        self._graph.replay()
+        RNG.graph_end()
+        self._loss_log_buf = list(st["log_buf"])
+        self._flush_loss_log()
+        if self.use_ddp:
+            self.ddp_model.reduce_all_now()
+
+    def _capture_step(self, batch):
+        from distributed_pipeline_amd.ops.nn import RNG
+        st = {"inputs": {k: v.to(self.device).clone() for k, v in batch.items()}}
+        torch.cuda.synchronize(self.device)
+        r0 = RNG.counter
+        g = torch.cuda.CUDAGraph()
+        self._graph_capturing = True
+        self._graph_log_buf = None
+        try:
+            with torch.cuda.graph(g):
+                self._forward_backward(st["inputs"])
+        finally:
+            self._graph_capturing = False
+        st["rng_r0"], st["rng_span"] = r0, RNG.counter - r0
+        RNG.counter = r0  # nothing ran yet: the first replay draws what the capture reserved
+        st["log_buf"] = self._graph_log_buf or []
+        self._graph_log_buf = None
+        self._graph = g
+        self._graph_state = st
+        logger.log(f"HIP graph captured: one step's forward/backward ({st['rng_span']} RNG offsets)")
 
     def _shrink_exec_microbatch(self):
         """Next smaller executed micro-batch: one more chunk per step (balanced chunks, e.g.
@@ -614,6 +691,8 @@ class TrainLoop:
         starts = list(range(0, n, self.exec_microbatch))
         if self._overlap_ok(len(starts)):
             return self._forward_backward_overlapped(batch, starts, n)
+        if self._graph_capturing:
+            self._loss_log_buf = []  # logged after each replay (static graph outputs)
         for i in starts:
             with self._range("forward"):
                 losses = self._common_forward(batch, i, self.exec_microbatch)
@@ -621,6 +700,8 @@ class TrainLoop:
             self.loss_scale = self._chunk_loss_scale(i, min(n, i + self.exec_microbatch), n)
             with self._range("backward"):
                 self.backward_from_losses(losses)
+        if self._graph_capturing:
+            self._graph_log_buf, self._loss_log_buf = self._loss_log_buf, None
 
     # ---- overlapped micro-batch schedule (several executed chunks per step) ----------
     def _overlap_ok(self, nchunks):
@@ -736,7 +817,7 @@ class TrainLoop:
                             st.wait_stream(defer.stream)  # every earlier weight gradient is in
                     else:
                         defer.active = defer.depth > 1
-                    if last and self.use_ddp:
+                    if last and self.use_ddp and not self._graph_capturing:
                         self.ddp_model.arm_for_backward()
                     self.loss_scale = self._chunk_loss_scale(starts[k], min(n, starts[k] + self.exec_microbatch), n)
                     t0 = time.perf_counter()
@@ -763,6 +844,9 @@ class TrainLoop:
         for _, t, w, vals in self._loss_log_buf or ():
             for x in (t, w, *vals):
                 x.record_stream(cur)
+        if self._graph_capturing:  # logged after each replay (static graph outputs)
+            self._graph_log_buf, self._loss_log_buf = self._loss_log_buf, None
+            return
         self._flush_loss_log()
 
     def _chunk_loss_scale(self, start, end, n):
@@ -1058,6 +1142,7 @@ class DiffusionTrainLoop(TrainLoop):
     term exactly like DiffuSeq's ``log_loss_dict`` but with device-side
     accumulation (no per-sample host copies).
     """
+    graph_logging = True  # log_loss_dict buffers (graph mode logs each replay's outputs)
     supports_microbatch_fusion = True
 
     def __init__(self, *, diffusion, schedule_sampler, **kwargs):
