@@ -161,8 +161,15 @@ class BucketReducer {
 
   // Called at forward time when gradient synchronisation is enabled (torch-DDP
   // semantics: the no_sync decision is taken when the graph is built).
-  void arm() {
+  //
+  // ``stream``: the stream the armed backward produces its gradients on (0: the current
+  // stream at launch time).  The grad-ready hooks do NOT run on it reliably: autograd
+  // runs a leaf's AccumulateGrad - and its hook - on the stream of the forward that
+  // first used the leaf, which in the overlapped micro-batch schedule is often the
+  // other stream; an event recorded there would not follow the gradient kernels.
+  void arm(int64_t stream = 0) {
     std::lock_guard<std::mutex> g(mu_);
+    arm_stream_ = reinterpret_cast<hipStream_t>(stream);
     pending_ = size_;
     std::fill(launched_.begin(), launched_.end(), false);
     for (auto& w : work_) w.reset();
@@ -243,7 +250,7 @@ class BucketReducer {
 
   // Reduce every bucket now (graph mode: backward ran without hooks).
   void reduce_all() {
-    arm();
+    arm(0);
     finalize();
   }
 
@@ -367,8 +374,8 @@ class BucketReducer {
 
   void launch_direct(int b) {
     const int64_t n = bounds_[b + 1] - bounds_[b];
-    // the grad-ready point: everything the compute stream queued so far
-    DPA_HIP_CHECK(hipEventRecord(ready_[b], compute_stream()));
+    // the grad-ready point: everything the backward's stream queued so far
+    DPA_HIP_CHECK(hipEventRecord(ready_[b], arm_stream_ ? arm_stream_ : compute_stream()));
     DPA_HIP_CHECK(hipStreamWaitEvent(cs_, ready_[b], 0));
     float* g = grad_.data_ptr<float>() + bounds_[b];
     void* buf = g;
@@ -442,6 +449,7 @@ class BucketReducer {
   uint32_t ipc_epoch_ = 0;
   IpcPeers peers_{};
   hipStream_t cs_ = nullptr;
+  hipStream_t arm_stream_ = nullptr;  // the armed backward's stream (arm()), null: current
   std::vector<hipEvent_t> ready_;
   hipEvent_t done_ = nullptr;
   std::mutex mu_;
@@ -460,7 +468,7 @@ void register_comm(pybind11::module& m) {
            pybind11::arg("shard_out") = pybind11::none(),
            pybind11::arg("shard_offsets") = std::vector<int64_t>(),
            pybind11::arg("rccl_uid") = std::string(), pybind11::arg("rank") = 0, pybind11::arg("world") = 1)
-      .def("arm", &BucketReducer::arm)
+      .def("arm", &BucketReducer::arm, pybind11::arg("stream") = 0)
       .def("disarm", &BucketReducer::disarm, pybind11::call_guard<pybind11::gil_scoped_release>())
       .def("armed", &BucketReducer::armed)
       .def("direct", &BucketReducer::direct)

@@ -20,8 +20,9 @@ implements the same protocol for the single-GPU multi-rank test transport.
   even when a fused wgrad GEMM accumulated the gradient in place and returned
   None); the bucket whose counter hits zero is all-reduced asynchronously.  On
   RCCL the C++ reducer owns its communicator and a highest-priority HIP stream:
-  an event recorded on the compute stream at the grad-ready point orders the
-  bucket's all-reduce after its gradient kernels, and finalize() makes the
+  an event recorded at the grad-ready point on the stream the backward was ARMED on
+  (not the hook's stream: autograd runs a leaf's hook on the stream of the forward
+  that first used it) orders the bucket's all-reduce after its gradient kernels, and finalize() makes the
   compute stream wait on the comm stream (no host synchronisation).  Buckets are
   launched in order so every rank issues collectives in the same sequence.
 * ``no_sync()`` has torch-DDP semantics: the decision is taken at *forward*
@@ -143,6 +144,7 @@ class DDPEngine(nn.Module):
         self.reduce_dtype = reduce_dtype
         self._sync_enabled = True
         self._armed = False
+        self._arm_stream = None      # the armed backward's stream (see _arm)
         self._next_launch = 0
         self.bucket_cap_mb, self.first_bucket_mb = bucket_cap_mb, first_bucket_mb
         self.buckets = [_Bucket(i, s, e, ps) for i, (s, e, ps) in
@@ -260,15 +262,28 @@ class DDPEngine(nn.Module):
         self.wait_shadow()
         if self.distributed and torch.is_grad_enabled() and self.training:
             self._armed = self._sync_enabled
-            if self._native is not None:
-                self._native.arm() if self._armed else self._native.disarm()
-            elif self._armed:
-                for b in self.buckets:
-                    b.pending = len(b.params)
-                    b.work = None
-                    b.launched = False
-                self._next_launch = 0
+            if self._armed:
+                self._arm()
+            elif self._native is not None:
+                self._native.disarm()
         return self.module(*args, **kwargs)
+
+    def _arm(self):
+        """Arm for a backward that produces its gradients on the CURRENT stream.  The
+        bucket launches are ordered after that stream, not after whatever stream a hook
+        happens to run on: autograd runs a leaf's AccumulateGrad (and its post-accumulate
+        hook) on the stream of the forward that first used the leaf, which in the
+        overlapped micro-batch schedule is often the other stream."""
+        cuda = self.space.device.type == "cuda"
+        self._arm_stream = torch.cuda.current_stream(self.space.device) if cuda else None
+        if self._native is not None:
+            self._native.arm(self._arm_stream.cuda_stream if cuda else 0)
+            return
+        for b in self.buckets:
+            b.pending = len(b.params)
+            b.work = None
+            b.launched = False
+        self._next_launch = 0
 
     def arm_for_backward(self):
         """Arm the reducer for the next backward regardless of how the forward ran: the
@@ -278,14 +293,7 @@ class DDPEngine(nn.Module):
         if not self.distributed:
             return
         self._armed = True
-        if self._native is not None:
-            self._native.arm()
-        else:
-            for b in self.buckets:
-                b.pending = len(b.params)
-                b.work = None
-                b.launched = False
-            self._next_launch = 0
+        self._arm()
 
     def disarm(self):
         """Abandon a partially run backward (e.g. an out-of-memory retry): no bucket of
@@ -322,7 +330,11 @@ class DDPEngine(nn.Module):
             b = self._bucket_of[id(p)]
             b.pending -= 1
             if b.pending == 0:
-                self._launch_ready_in_order()
+                if self._arm_stream is not None:
+                    with torch.cuda.stream(self._arm_stream):
+                        self._launch_ready_in_order()
+                else:
+                    self._launch_ready_in_order()
         return hook
 
     def _launch_ready_in_order(self):
