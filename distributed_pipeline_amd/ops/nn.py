@@ -139,8 +139,11 @@ _SAVE_ACT_DERIV = os.environ.get("DPA_SAVE_ACT_DERIV", "1") != "0"
 # LayerNorm with any column where |gamma| < 0.125 or |beta| > |gamma| (where the
 # reconstruction would amplify out's bf16 rounding) keeps the exact h-copy path - both kernels
 # test the same gamma / beta on the device, no host sync (norm.hip xo_unsafe).
-# DPA_LN_SAVE_OUT=0: always the h copy.
-_LN_SAVE_OUT = os.environ.get("DPA_LN_SAVE_OUT", "1") != "0"
+# Opt-in (DPA_LN_SAVE_OUT=1): measured 1.9-2.0 ms/step SLOWER than the h copy on the headline
+# (6 interleaved runs, 167.1-167.2 vs 165.2-165.4 ms: profiles/ln_save_out_ab_r4.txt) - the
+# guarded forward still writes the h copy and the backward's extra gamma/beta reads and
+# reconstruction cost more than the saved store - so the default is the h copy.
+_LN_SAVE_OUT = os.environ.get("DPA_LN_SAVE_OUT", "0") == "1"
 
 
 def _gemm_shape_ok(x2, n_out):
