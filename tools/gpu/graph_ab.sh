@@ -3,6 +3,7 @@
 # DiffuSeq-XL (auto executed micro-batch) for the HBM headroom after settling.
 set -o pipefail
 mkdir -p gpurun_out/gab
+timeout -k 10 400 python -u -m pytest -x -v --timeout 300 --timeout-method thread tests/test_overlap_multirank_gpu.py tests/test_graph_gpu.py > gpurun_out/gab/tests.log 2>&1 || exit $?
 run() {  # name "ENV=V ..." "bench args"
   env $2 timeout -k 10 300 python -u bench.py --steps 2 --warmup 1 --ref-steps 8 --ref-windows 2 $3 \
     --json-out gpurun_out/gab/$1.json > gpurun_out/gab/$1.log 2>&1 || return $?
