@@ -314,6 +314,12 @@ def main():
         free, total = torch.cuda.mem_get_info(dev)
         out["hbm_free_gb"] = round(free / 2**30, 1)  # device-wide free now (RCCL buffers excluded)
         out["hbm_total_gb"] = round(total / 2**30, 1)
+        # headroom at the step's peak: what the caching allocator never had to reserve (RCCL's
+        # lazily allocated buffers live there), and how often it freed its cache and retried
+        # a failed hipMalloc (steps thrashing at the edge of HBM)
+        ms = torch.cuda.memory_stats(dev)
+        out["hbm_headroom_at_peak_gb"] = round((total - torch.cuda.max_memory_reserved(dev)) / 2**30, 1)
+        out["alloc_retries"] = int(ms.get("num_alloc_retries", 0))
     if rank == 0:
         out["topology"] = topology()
     if rank == 0:
