@@ -73,6 +73,9 @@ def parse():
     ap.add_argument("--data-workers", type=int, default=2)
     ap.add_argument("--log-interval", type=int, default=20)
     ap.add_argument("--json-out", default=None)
+    ap.add_argument("--comm-probe", type=int, default=1,
+                    help="N > 1: after the timed runs, time the full gradient reduction and the "
+                         "process group's all-reduce at 3 sizes (reported under comm_probe)")
     return ap.parse_args()
 
 
@@ -99,6 +102,46 @@ def topology():
         hops = [l.get("num_hops") for l in links if isinstance(l, dict) and "num_hops" in l]
         out.append({"gpu": gpu, "link_types": kinds, "peers": len(links), "max_hops": max(hops) if hops else None})
     return out or None
+
+
+def comm_probe(loop, engine, dev, sync):
+    """After the timed runs (N > 1): the data plane's full gradient reduction
+    with this run's bucket plan (``DDPEngine.reduce_all_now``: every bucket, back to back,
+    nothing to overlap with - the cost a step hides under its backward) and the process
+    group's all-reduce bus bandwidth at three bucket sizes.  Times are the max over ranks."""
+    import torch
+    import torch.distributed as dist
+
+    def timed(fn, iters):
+        fn()
+        sync()
+        t = time.perf_counter()
+        for _ in range(iters):
+            fn()
+        sync()
+        e = torch.tensor([(time.perf_counter() - t) / iters], dtype=torch.float64,
+                         device=dev if dev.type == "cuda" else "cpu")
+        dist.all_reduce(e, op=dist.ReduceOp.MAX)
+        return float(e.item())
+
+    world = dist.get_world_size()
+    res = {}
+    if engine == "native":
+        eng = loop.ddp_model
+        nbytes = eng.space.grad_flat.numel() * 4
+        sec = timed(eng.reduce_all_now, 3)
+        res["grad_reduce_all"] = {"mb": round(nbytes / 2**20, 1), "ms": round(sec * 1e3, 3),
+                                  "busbw_GBps": round(nbytes / sec / 1e9 * 2 * (world - 1) / world, 1),
+                                  "buckets": len(eng.buckets)}
+        eng.zero_grad()
+    sizes = (4, 32, 128) if dev.type == "cuda" else (1, 4)
+    res["pg_allreduce"] = []
+    for mb in sizes:
+        x = torch.ones(mb * (1 << 18), dtype=torch.float32, device=dev if dev.type == "cuda" else "cpu")
+        sec = timed(lambda: dist.all_reduce(x), 5)
+        res["pg_allreduce"].append({"mb": mb, "us": round(sec * 1e6, 1),
+                                    "busbw_GBps": round(mb * 2**20 / sec / 1e9 * 2 * (world - 1) / world, 1)})
+    return res
 
 
 def main():
@@ -309,6 +352,8 @@ def main():
                                               if engine == "native" else world),
                     "rank_ms_per_step_min": round(rank_ms[0], 3),
                     "rank_ms_per_step_max": round(rank_ms[1], 3)}
+    if world > 1 and a.comm_probe:
+        out["comm_probe"] = comm_probe(loop, engine, dev, sync)
     if dev.type == "cuda":  # HBM headroom of the fused schedule (288 GB per MI355X)
         out["peak_hbm_gb"] = round(torch.cuda.max_memory_allocated(dev) / 2**30, 1)
         free, total = torch.cuda.mem_get_info(dev)

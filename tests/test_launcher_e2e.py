@@ -86,3 +86,8 @@ def test_bench_contract_two_ranks_gloo():
     assert abs(d["ms_per_step"] - 1e3 / d["optimizer_steps_per_sec"]) < 1e-2 * d["ms_per_step"]
     # the BASELINE metric / ratio belong to the headline config only
     assert d["vs_baseline"] is None and "tiny" in d["metric"]
+    # rank evidence and the post-run comm probe (N > 1)
+    assert d["ranks"]["backend_world_size"] == 2 and d["ranks"]["data_plane_comm_ranks"] == 2
+    cp = d["comm_probe"]
+    assert cp["grad_reduce_all"]["ms"] > 0 and cp["grad_reduce_all"]["buckets"] >= 1
+    assert [r["mb"] for r in cp["pg_allreduce"]] == [1, 4] and all(r["busbw_GBps"] > 0 for r in cp["pg_allreduce"])
