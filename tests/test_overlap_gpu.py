@@ -63,16 +63,17 @@ def test_overlapped_schedule_matches_sequential():
         assert abs(a - b) <= 1e-4 * abs(a)
 
 
+@pytest.mark.parametrize("overlap", [True, False])
 @pytest.mark.parametrize("depth", [2, 4])
-def test_deferred_wgrad_matches_sequential(depth):
+def test_deferred_wgrad_matches_sequential(depth, overlap):
     """Weight-gradient deferral (ops/nn.py _WgradDeferral): the held (dy, x) operands of
-    ``depth`` micro-batches run as one multi-segment split-K GEMM.  Same fp32 sum in another
-    order: gradients within fp32 rounding of the sequential loop's, and the multi-segment
-    launch must actually have run."""
+    ``depth`` micro-batches run as one multi-segment split-K GEMM, in the overlapped schedule
+    and in the one-stream sequential one.  Same fp32 sum in another order: gradients within
+    fp32 rounding of the sequential loop's, and the multi-segment launch must actually have run."""
     from distributed_pipeline_amd.ops.nn import WGRAD_DEFER
     g0, p0, l0 = _loop(False)
     before = dict(WGRAD_DEFER.stats)
-    g1, p1, l1 = _loop(True, defer=depth)
+    g1, p1, l1 = _loop(overlap, defer=depth)
     assert WGRAD_DEFER.stats["multi_launches"] > before["multi_launches"]
     assert not WGRAD_DEFER.pending
     # the LayerNorm / dact-bias column sums of the un-armed micro-batches were deferred too

@@ -693,26 +693,52 @@ class TrainLoop:
             return self._forward_backward_overlapped(batch, starts, n)
         if self._graph_capturing:
             self._loss_log_buf = []  # logged after each replay (static graph outputs)
-        for i in starts:
-            with self._range("forward"):
-                losses = self._common_forward(batch, i, self.exec_microbatch)
-            self.log_loss_dict(mode="train", losses=losses)
-            self.loss_scale = self._chunk_loss_scale(i, min(n, i + self.exec_microbatch), n)
-            with self._range("backward"):
-                self.backward_from_losses(losses)
+        # weight-gradient deferral on the one stream (tile-starved chunks only, as the overlap;
+        # the last chunk's backward - the DDP-armed one - runs after a flush)
+        defer = None
+        if len(starts) > 1 and self.defer_wgrad > 1 and self._tile_starved():
+            from distributed_pipeline_amd.ops import nn as nn_ops
+            defer = nn_ops.WGRAD_DEFER
+            defer.depth, defer.stream, defer.cur = self.defer_wgrad, None, torch.cuda.current_stream()
+        try:
+            for k, i in enumerate(starts):
+                with self._range("forward"):
+                    losses = self._common_forward(batch, i, self.exec_microbatch)
+                self.log_loss_dict(mode="train", losses=losses)
+                self.loss_scale = self._chunk_loss_scale(i, min(n, i + self.exec_microbatch), n)
+                if defer is not None:
+                    defer.active = k < len(starts) - 1
+                    if not defer.active:
+                        defer.flush()
+                with self._range("backward"):
+                    self.backward_from_losses(losses)
+        except BaseException:
+            if defer is not None:
+                defer.drop()
+            raise
+        finally:
+            if defer is not None:
+                defer.active, defer.cur = False, None
+                defer.release_retired(torch.cuda.current_stream())
         if self._graph_capturing:
             self._graph_log_buf, self._loss_log_buf = self._loss_log_buf, None
 
     # ---- overlapped micro-batch schedule (several executed chunks per step) ----------
-    def _overlap_ok(self, nchunks):
-        # only tile-starved chunks gain from a second stream: at <= 64K tokens a 768-wide GEMM
-        # has <= 768 output tiles (3 rounds of 256 CUs); larger chunks (DiffuSeq-XL's 1024-sample
-        # chunks) fill the chip alone, and overlapping two of them doubles the live activations
-        # (DPA_OVERLAP_MAX_TOKENS overrides)
+    def _tile_starved(self):
+        # at <= 64K tokens a 768-wide GEMM has <= 768 output tiles (3 rounds of 256 CUs); larger
+        # chunks (DiffuSeq-XL's 1024-sample chunks) fill the chip alone, and overlapping or
+        # deferring them doubles live memory (DPA_OVERLAP_MAX_TOKENS overrides)
         toks = self.exec_microbatch * (self._tokens_per_sample or 1)
         max_toks = int(os.environ.get("DPA_OVERLAP_MAX_TOKENS", "65536"))
-        return (nchunks > 1 and self.overlap_microbatches and not self._probing
-                and self.engine_kind == "native" and self.device.type == "cuda" and toks <= max_toks)
+        return (not self._probing and self.engine_kind == "native" and self.device.type == "cuda"
+                and toks <= max_toks)
+
+    def _overlap_ok(self, nchunks):
+        # only tile-starved chunks gain from a second stream; under HIP-graph capture the
+        # overlap is optional (DPA_GRAPH_OVERLAP=0: the captured step runs on one stream)
+        if self._graph_capturing and os.environ.get("DPA_GRAPH_OVERLAP", "1") == "0":
+            return False
+        return nchunks > 1 and self.overlap_microbatches and self._tile_starved()
 
     def _chunk_state(self):
         """Per-chunk hook state (``_last_*`` attributes set by compute_losses and read by
