@@ -56,8 +56,9 @@ def parse():
                          "allocator pools in the first steps)")
     ap.add_argument("--ref-steps", type=int, default=8,
                     help="also time this many steps of the reference 32 x 64 schedule (0 = skip)")
-    ap.add_argument("--ref-graph", type=int, default=1,
-                    help="run the reference schedule as a replayed HIP graph (TrainLoop cuda_graph; 0 = eager)")
+    ap.add_argument("--ref-graph", type=int, default=0,
+                    help="run the reference schedule as a replayed HIP graph (TrainLoop cuda_graph; 0 = eager: "
+                         "the replay measured 249-251 vs 228-229 ms/step eager, profiles/ref_schedule_graph_ab_r4.txt)")
     ap.add_argument("--ref-windows", type=int, default=1,
                     help="time the reference schedule in this many back-to-back windows of --ref-steps "
                          "(the mean over all is reported, each window under windows_ms)")
