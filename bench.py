@@ -354,7 +354,10 @@ def main():
                     "rank_ms_per_step_min": round(rank_ms[0], 3),
                     "rank_ms_per_step_max": round(rank_ms[1], 3)}
     if world > 1 and a.comm_probe:
-        out["comm_probe"] = comm_probe(loop, engine, dev, sync)
+        try:  # diagnostics only: never cost the measured line
+            out["comm_probe"] = comm_probe(loop, engine, dev, sync)
+        except Exception as e:  # noqa: BLE001
+            out["comm_probe"] = {"error": f"{type(e).__name__}: {e}"[:300]}
     if dev.type == "cuda":  # HBM headroom of the fused schedule (288 GB per MI355X)
         out["peak_hbm_gb"] = round(torch.cuda.max_memory_allocated(dev) / 2**30, 1)
         free, total = torch.cuda.mem_get_info(dev)
