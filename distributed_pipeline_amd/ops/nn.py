@@ -1199,6 +1199,11 @@ class _ChunkedLinearXentFn(torch.autograd.Function):
         # a single split-K GEMM over all N tokens
         kept_is_grad = keep and _XENT_ROWS_FUSED
         allg = torch.empty(N, wp.shape[0], dtype=x.dtype, device=x.device) if keep else None
+        if kept_is_grad:
+            # kept chunks: sized for the 256 MB Infinity Cache, so the row pass reads the
+            # logits the GEMM has just written from the MALL instead of HBM (the backward's
+            # GEMMs run over all N tokens at once, so small chunks cost them nothing)
+            chunk = min(chunk, max(256, (_XENT_FWD_CHUNK_BYTES // (wp.shape[0] * 2)) // 256 * 256))
         for s in range(0, N, chunk):
             e = min(N, s + chunk)
             lg = _chunk_logits(x[s:e], wp, bp, allg[s:e] if allg is not None else None)
@@ -1235,7 +1240,17 @@ class _ChunkedLinearXentFn(torch.autograd.Function):
         db = torch.zeros(V, dtype=torch.float32, device=x.device) if need_db else None
         allg, ctx.allg = ctx.allg, None
         unscaled = allg is not None and ctx.kept_is_grad
-        for s in range(0, N, ctx.chunk):
+        if unscaled:
+            # kept softmax - onehot for all N tokens: dx = diag(g) (G Wp) as ONE data-gradient
+            # GEMM (a per-chunk GEMM has only chunk/256 x 3 output tiles at E = 768)
+            if need_dx:
+                ext.gemm_nn_into(allg, wp, dx)
+                dx.mul_(g_all[:, None])
+            if need_db:
+                for s in range(0, N, ctx.chunk):
+                    e = min(N, s + ctx.chunk)
+                    db.add_(g_all[s:e] @ allg[s:e, :V].float())
+        for s in range(0, N if not unscaled else 0, ctx.chunk):
             e = min(N, s + ctx.chunk)
             # a kept chunk is a row slice of allg: it is freed with the whole buffer at
             # the end of the backward, not per chunk
@@ -1275,6 +1290,8 @@ _XENT_CHUNK_BYTES = int(os.environ.get("DPA_XENT_CHUNK_MB", "2048")) << 20
 # logits kept from the forward for the backward (bytes; GPT-2 small at 128 x 1024 tokens
 # needs 13 GB): above this the backward recomputes each chunk
 _XENT_KEEP_BYTES = int(os.environ.get("DPA_XENT_KEEP_GB", "24")) << 30
+# forward chunk when the logits are kept (softmax - onehot in place): MALL-resident
+_XENT_FWD_CHUNK_BYTES = int(os.environ.get("DPA_XENT_FWD_CHUNK_MB", "128")) << 20
 
 
 def linear_cross_entropy(x, weight, bias, target):
