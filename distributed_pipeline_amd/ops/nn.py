@@ -1240,7 +1240,8 @@ class _ChunkedLinearXentFn(torch.autograd.Function):
         db = torch.zeros(V, dtype=torch.float32, device=x.device) if need_db else None
         allg, ctx.allg = ctx.allg, None
         unscaled = allg is not None and ctx.kept_is_grad
-        if unscaled:
+        all_n = unscaled and _XENT_DX_ALL
+        if all_n:
             # kept softmax - onehot for all N tokens: dx = diag(g) (G Wp) as ONE data-gradient
             # GEMM (a per-chunk GEMM has only chunk/256 x 3 output tiles at E = 768)
             if need_dx:
@@ -1250,7 +1251,7 @@ class _ChunkedLinearXentFn(torch.autograd.Function):
                 for s in range(0, N, ctx.chunk):
                     e = min(N, s + ctx.chunk)
                     db.add_(g_all[s:e] @ allg[s:e, :V].float())
-        for s in range(0, N if not unscaled else 0, ctx.chunk):
+        for s in range(0, N if not all_n else 0, ctx.chunk):
             e = min(N, s + ctx.chunk)
             # a kept chunk is a row slice of allg: it is freed with the whole buffer at
             # the end of the backward, not per chunk
@@ -1290,6 +1291,8 @@ _XENT_CHUNK_BYTES = int(os.environ.get("DPA_XENT_CHUNK_MB", "2048")) << 20
 # logits kept from the forward for the backward (bytes; GPT-2 small at 128 x 1024 tokens
 # needs 13 GB): above this the backward recomputes each chunk
 _XENT_KEEP_BYTES = int(os.environ.get("DPA_XENT_KEEP_GB", "24")) << 30
+# kept logits: the backward's dx as one GEMM over all tokens (DPA_XENT_DX_ALL=0: per chunk)
+_XENT_DX_ALL = os.environ.get("DPA_XENT_DX_ALL", "1") != "0"
 # forward chunk when the logits are kept (softmax - onehot in place): MALL-resident
 _XENT_FWD_CHUNK_BYTES = int(os.environ.get("DPA_XENT_FWD_CHUNK_MB", "128")) << 20
 
