@@ -76,7 +76,7 @@ def parse():
     ap.add_argument("--json-out", default=None)
     ap.add_argument("--comm-probe", type=int, default=1,
                     help="N > 1: after the timed runs, time the full gradient reduction and the "
-                         "process group's all-reduce at 3 sizes (reported under comm_probe)")
+                         "process group's all-reduce at 1-128 MB (reported under comm_probe)")
     return ap.parse_args()
 
 
@@ -109,7 +109,8 @@ def comm_probe(loop, engine, dev, sync):
     """After the timed runs (N > 1): the data plane's full gradient reduction
     with this run's bucket plan (``DDPEngine.reduce_all_now``: every bucket, back to back,
     nothing to overlap with - the cost a step hides under its backward) and the process
-    group's all-reduce bus bandwidth at three bucket sizes.  Times are the max over ranks."""
+    group's all-reduce bus bandwidth at bucket sizes 1-128 MB (the data behind the 4 MiB first
+    bucket / 32 MiB buckets), and the NCCL_* / RCCL_* environment.  Times are the max over ranks."""
     import torch
     import torch.distributed as dist
 
@@ -135,13 +136,15 @@ def comm_probe(loop, engine, dev, sync):
                                   "busbw_GBps": round(nbytes / sec / 1e9 * 2 * (world - 1) / world, 1),
                                   "buckets": len(eng.buckets)}
         eng.zero_grad()
-    sizes = (4, 32, 128) if dev.type == "cuda" else (1, 4)
+    sizes = (1, 4, 16, 32, 64, 128) if dev.type == "cuda" else (1, 4)
     res["pg_allreduce"] = []
     for mb in sizes:
         x = torch.ones(mb * (1 << 18), dtype=torch.float32, device=dev if dev.type == "cuda" else "cpu")
         sec = timed(lambda: dist.all_reduce(x), 5)
         res["pg_allreduce"].append({"mb": mb, "us": round(sec * 1e6, 1),
                                     "busbw_GBps": round(mb * 2**20 / sec / 1e9 * 2 * (world - 1) / world, 1)})
+    # the RCCL knobs this run saw (none set = RCCL's own topology-derived defaults)
+    res["rccl_env"] = {k: v for k, v in os.environ.items() if k.startswith(("NCCL_", "RCCL_"))}
     return res
 
 
