@@ -24,6 +24,7 @@
 //   through LDS and written as whole 128-byte rows of the packed dqkv.
 // Dropout bits: the same per-(query, key-pair) hash as attention.hip.
 #include <cstdlib>
+#include <utility>
 
 #include "common.h"
 #include "launchers.h"
@@ -169,7 +170,10 @@ __device__ __forceinline__ void dma_img(char* img, const bf16_t* src, int64_t ld
   for (int i = 0; i < 4; ++i) {
     const int pc = w * 4 + i;
     const int row = pc * 8 + (lane >> 3), phys = lane & 7;
-    const bf16_t* g = src + (int64_t)row * ld + ((phys ^ ((row >> 1) & 7)) << 3);
+    // 32-bit lane offset (row < 128, ld < 2^24: one full-rate 24-bit multiply) on the uniform
+    // base, not a 64-bit product per piece
+    const uint32_t off = __umul24((uint32_t)row, (uint32_t)ld) + (uint32_t)((phys ^ ((row >> 1) & 7)) << 3);
+    const bf16_t* g = src + off;
     __builtin_amdgcn_global_load_lds((glob_void*)g, (lds_void*)(img + pc * 1024), 16, 0, 0);
   }
 }
@@ -288,13 +292,16 @@ __global__ void __launch_bounds__(256, 2) attn128_fwd_kernel(const bf16_t* __res
     o[0] = zero16();
     o[1] = zero16();
     const float fk = dc.on ? inv_l * dc.scale : inv_l;
+    // key pair of register 2j of tile t: t * 16 + (j & 1) + 4 (j >> 1) + 2 hf
+    const uint32_t hq = (uint32_t)q * 0x9E3779B1u, hk0 = (uint32_t)(2 * hf) * 0x85EBCA77u;
 #pragma unroll
     for (int t = 0; t < 4; ++t) {
       if (dc.on) {
         // one hash per key pair (registers 2j, 2j + 1 are keys 2m, 2m + 1), as one batch
         uint32_t hh[8];
 #pragma unroll
-        for (int j = 0; j < 8; ++j) hh[j] = drop_hash(dc, q, t * 32 + acc_row(2 * j, hf));
+        for (int j = 0; j < 8; ++j)  // drop_hash(dc, q, t * 32 + acc_row(2 j, hf)), per-lane terms hoisted
+          hh[j] = mix32(dc.seedmix ^ hq ^ (hk0 + (uint32_t)(t * 16 + (j & 1) + 4 * (j >> 1)) * 0x85EBCA77u));
 #pragma unroll
         for (int i = 0; i < 16; ++i) acc[t][i] = keep_from(dc, hh[i >> 1], i & 1) ? acc[t][i] * fk : 0.f;
       } else {
@@ -435,54 +442,64 @@ __device__ __forceinline__ void bwd_dkv_step(f32x16 (&dv)[2], f32x16 (&dk)[2], c
   dk[DT] = mfma32(sf, tq, dk[DT]);
 }
 
-template <int T, int G>
+// Per-lane dropout hash terms of one item: hq = (4 hf + (key & 1)) * C_Q and hk = (key >> 1) * C_K.
+// The query of a hash is T*32 + 8G + 2j + 4hf + (key & 1) with T, G, j compile-time, so its
+// product with C_Q is hq plus an immediate (mod 2^32): no quarter-rate v_mul_lo_u32 per hash.
+struct HashTerms {
+  uint32_t hq, hk;
+  int par;
+};
+
+template <int T, int G, bool DROP>
 __device__ __forceinline__ void bwd_pds(f32x16& sacc, f32x16& dpacc, uint32_t base,
-                                        const BwdBases& B, const DropCfg& dc, int key, int hf) {
+                                        const BwdBases& B, const DropCfg& dc, const HashTerms& ht) {
   const f32x4 lv = rdf4o<T * 128 + G * 32>(base + B.stat);
   const f32x4 dl = rdf4o<T * 128 + G * 32 + 512>(base + B.stat);
   lgkm0();
   // keys key and key^1 sit on adjacent lanes and need the same (query, key pair)
   // hashes: each lane computes two of the four and swaps for the rest (DPP)
   uint32_t hh[4];
-  if (dc.on) {
-    const int par = key & 1;
+  if constexpr (DROP) {
 #pragma unroll
     for (int j = 0; j < 2; ++j) {
-      const uint32_t mine = drop_hash(dc, T * 32 + 8 * G + 4 * hf + 2 * j + par, key);
+      constexpr uint32_t CQ = 0x9E3779B1u;
+      const uint32_t qt = ht.hq + (uint32_t)(T * 32 + 8 * G + 2 * j) * CQ;
+      const uint32_t mine = mix32(dc.seedmix ^ qt ^ ht.hk);
       const uint32_t other = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)mine, 0xB1, 0xF, 0xF, true);
-      hh[2 * j] = par ? other : mine;
-      hh[2 * j + 1] = par ? mine : other;
+      hh[2 * j] = ht.par ? other : mine;
+      hh[2 * j + 1] = ht.par ? mine : other;
     }
   }
 #pragma unroll
   for (int r = 0; r < 4; ++r) {
     const int i = 4 * G + r;
     const float pr = fexp2(fmaf(sacc[i], ATT_C, -lv[r]));
-    float pd = pr, dpd = dpacc[i];
-    if (dc.on) {
-      const bool kp = keep_from(dc, hh[r], key);
-      pd = kp ? pr * dc.scale : 0.f;
-      dpd = kp ? dpd * dc.scale : 0.f;
+    if constexpr (DROP) {
+      // one select per score: the kept-and-scaled multiplier serves P and dP
+      const float m = keep_from(dc, hh[r], ht.par) ? dc.scale : 0.f;
+      sacc[i] = pr * m;
+      dpacc[i] = pr * fmaf(dpacc[i], m, -dl[r]);
+    } else {
+      sacc[i] = pr;
+      dpacc[i] = pr * (dpacc[i] - dl[r]);
     }
-    sacc[i] = pd;
-    dpacc[i] = pr * (dpd - dl[r]);
   }
 }
 
-template <int T>
+template <int T, bool DROP>
 __device__ __forceinline__ void bwd_tile(f32x16 (&dv)[2], f32x16 (&dk)[2], uint4 (&dsb)[2],
                                          uint32_t base, const BwdBases& B, uint32_t kbase,
-                                         const bf16x8 (&vf)[4], const DropCfg& dc, int key, int hf) {
+                                         const bf16x8 (&vf)[4], const DropCfg& dc, const HashTerms& ht) {
   f32x16 sacc = zero16(), dpacc = zero16();
   bwd_sdp_step<T, 0>(sacc, dpacc, base, B, kbase, vf);
   bwd_sdp_step<T, 1>(sacc, dpacc, base, B, kbase, vf);
   bwd_sdp_step<T, 2>(sacc, dpacc, base, B, kbase, vf);
   bwd_sdp_step<T, 3>(sacc, dpacc, base, B, kbase, vf);
   // P, dS on this lane's query rows 32T + 8g + 4h + r (statistics read per group g)
-  bwd_pds<T, 0>(sacc, dpacc, base, B, dc, key, hf);
-  bwd_pds<T, 1>(sacc, dpacc, base, B, dc, key, hf);
-  bwd_pds<T, 2>(sacc, dpacc, base, B, dc, key, hf);
-  bwd_pds<T, 3>(sacc, dpacc, base, B, dc, key, hf);
+  bwd_pds<T, 0, DROP>(sacc, dpacc, base, B, dc, ht);
+  bwd_pds<T, 1, DROP>(sacc, dpacc, base, B, dc, ht);
+  bwd_pds<T, 2, DROP>(sacc, dpacc, base, B, dc, ht);
+  bwd_pds<T, 3, DROP>(sacc, dpacc, base, B, dc, ht);
   {
     const bf16x8 pf = acc_to_frag(sacc, 0), sf = acc_to_frag(dpacc, 0);
     dsb[0] = __builtin_bit_cast(uint4, sf);
@@ -509,20 +526,31 @@ __device__ __forceinline__ void bwd_dq_step(f32x16 (&dq)[2], uint32_t base, cons
   dq[1] = mfma32(af, b1, dq[1]);
 }
 
-template <int X, int DT>
-__device__ __forceinline__ void bwd_stage_out(const f32x16& acc, float scale, uint32_t a) {
-#pragma unroll
-  for (int i = 0; i < 16; ++i) {
-    // row 32w + 4h + (i&3) + 8(i>>2), column DT*32 + (lane&31): all but the lane part immediate
-    switch (i) {
-#define DPA_ST(I) case I: wr16o<X * IMG + ((I & 3) + 8 * (I >> 2)) * 128 + DT * 64>(a, f2bf(acc[I] * scale)); break;
-      DPA_ST(0) DPA_ST(1) DPA_ST(2) DPA_ST(3) DPA_ST(4) DPA_ST(5) DPA_ST(6) DPA_ST(7)
-      DPA_ST(8) DPA_ST(9) DPA_ST(10) DPA_ST(11) DPA_ST(12) DPA_ST(13) DPA_ST(14) DPA_ST(15)
-#undef DPA_ST
-    }
-  }
+// One b16 LDS write per register (converting registers in pairs and writing the high half
+// with ds_write_b16_d16_hi saves 48 conversions per item but made the compiler allocate 256
+// VGPRs and spill).  Row of register i: 32w + 4h + (i&3) + 8(i>>2), column DT*32 + (lane&31): all but the lane
+// part immediate.
+template <int X, int DT, int M>
+__device__ __forceinline__ void bwd_stage_pair(const f32x16& acc, float scale, uint32_t a) {
+  constexpr int I0 = 2 * M, I1 = 2 * M + 1;
+  wr16o<X * IMG + ((I0 & 3) + 8 * (I0 >> 2)) * 128 + DT * 64>(a, f2bf(acc[I0] * scale));
+  wr16o<X * IMG + ((I1 & 3) + 8 * (I1 >> 2)) * 128 + DT * 64>(a, f2bf(acc[I1] * scale));
 }
 
+template <int X, int DT, int... M>
+__device__ __forceinline__ void bwd_stage_out_seq(const f32x16& acc, float scale, uint32_t a,
+                                                  std::integer_sequence<int, M...>) {
+  (bwd_stage_pair<X, DT, M>(acc, scale, a), ...);
+}
+
+template <int X, int DT>
+__device__ __forceinline__ void bwd_stage_out(const f32x16& acc, float scale, uint32_t a) {
+  bwd_stage_out_seq<X, DT>(acc, scale, a, std::make_integer_sequence<int, 8>{});
+}
+
+// DROP: attention dropout on (p > 0), a template parameter so the per-score dropout work
+// carries no wave-uniform branch (~130 scalar branches and their exec bookkeeping per item)
+template <bool DROP>
 __global__ void __launch_bounds__(256, 2) attn128_bwd_kernel(
     const bf16_t* __restrict__ qkv, const bf16_t* __restrict__ out, const bf16_t* __restrict__ dout,
     const float* __restrict__ lse, bf16_t* __restrict__ dqkv, float* __restrict__ colpart, int B,
@@ -555,13 +583,14 @@ __global__ void __launch_bounds__(256, 2) attn128_bwd_kernel(
     dma_img(smem + I_K, qb + lay.sw, lay.ld, w, lane);
     uint4 opf[4];
     {
-      const bf16_t* orow = out + ((int64_t)b * L + (tid >> 1)) * ldo + (int64_t)hd * HD + (tid & 1) * 32;
+      const bf16_t* orow = out + ((int64_t)b * L * ldo + (int64_t)hd * HD) +
+                           (__umul24((uint32_t)(tid >> 1), (uint32_t)ldo) + (uint32_t)(tid & 1) * 32);
 #pragma unroll
       for (int c = 0; c < 4; ++c) opf[c] = *reinterpret_cast<const uint4*>(orow + c * 8);
     }
     bf16x8 vf[4];
     {
-      const bf16_t* vrow = qb + (int64_t)key * lay.ld + 2 * lay.sw;
+      const bf16_t* vrow = (qb + 2 * lay.sw) + __umul24((uint32_t)key, (uint32_t)lay.ld);
 #pragma unroll
       for (int s = 0; s < 4; ++s) vf[s] = ld_frag(vrow + 16 * s + 8 * hf);
     }
@@ -590,14 +619,18 @@ __global__ void __launch_bounds__(256, 2) attn128_bwd_kernel(
     barrier();
 
     const DropCfg dc = make_drop(p, seed, offset, (uint32_t)item);
+    HashTerms ht;
+    ht.par = key & 1;
+    ht.hq = (uint32_t)(4 * hf + ht.par) * 0x9E3779B1u;
+    ht.hk = (uint32_t)(key >> 1) * 0x85EBCA77u;
     const uint32_t kbase = base + kb * 128;
     f32x16 dk[2], dv[2];
     uint4 dsb[4][2];  // dS as bf16 (the exact A-operand packing), 8 registers per tile
     dk[0] = zero16(); dk[1] = zero16(); dv[0] = zero16(); dv[1] = zero16();
-    bwd_tile<0>(dv, dk, dsb[0], base, BB, kbase, vf, dc, key, hf);
-    bwd_tile<1>(dv, dk, dsb[1], base, BB, kbase, vf, dc, key, hf);
-    bwd_tile<2>(dv, dk, dsb[2], base, BB, kbase, vf, dc, key, hf);
-    bwd_tile<3>(dv, dk, dsb[3], base, BB, kbase, vf, dc, key, hf);
+    bwd_tile<0, DROP>(dv, dk, dsb[0], base, BB, kbase, vf, dc, ht);
+    bwd_tile<1, DROP>(dv, dk, dsb[1], base, BB, kbase, vf, dc, ht);
+    bwd_tile<2, DROP>(dv, dk, dsb[2], base, BB, kbase, vf, dc, ht);
+    bwd_tile<3, DROP>(dv, dk, dsb[3], base, BB, kbase, vf, dc, ht);
     // dS^T -> LDS over Q + dO (dead once every wave is here): [128 keys][128 q], 256-B rows
     barrier();
     {
@@ -631,6 +664,10 @@ __global__ void __launch_bounds__(256, 2) attn128_bwd_kernel(
     bf16_t* gb = dqkv + (int64_t)b * L * ld + (int64_t)hd * HD;
     const uint32_t ca = base + BB.cpy;
     const int crow = tid >> 3, cch = tid & 7;
+    // this thread's row segment once; the 12 stores add wave-uniform offsets (no per-store
+    // 64-bit multiply of the row index by ld)
+    const uint32_t roff = __umul24((uint32_t)crow, (uint32_t)ld) + (uint32_t)cch * 8;
+    const int64_t s32 = 32 * ld, sq = (int64_t)H * HD;
     // Column sums of the bf16 dQ/dK/dV this item writes (the qkv bias gradient,
     // so the wgrad GEMM needs no column-sum pass): each thread sums its 4 rows.
     float cs[3][8];
@@ -638,8 +675,7 @@ __global__ void __launch_bounds__(256, 2) attn128_bwd_kernel(
   {                                                                                       \
     const bf16x8 v = rd128o<(C >> 2) * IMG + (C & 3) * 4096>(ca);                         \
     lgkm0();                                                                              \
-    *reinterpret_cast<bf16x8*>(gb + (int64_t)(crow + 32 * (C & 3)) * ld +                 \
-                               (int64_t)(C >> 2) * H * HD + cch * 8) = v;                \
+    *reinterpret_cast<bf16x8*>((gb + ((C & 3) * s32 + (C >> 2) * sq)) + roff) = v;         \
     _Pragma("unroll") for (int j = 0; j < 8; ++j) {                                       \
       const float f = __uint_as_float((uint32_t)(uint16_t)v[j] << 16);                    \
       cs[C >> 2][j] = (C & 3) ? cs[C >> 2][j] + f : f;                                    \
@@ -794,6 +830,8 @@ __global__ void __launch_bounds__(256, 1) attn128_fwd_d128_kernel(const bf16_t* 
     l += __shfl_xor(l, 32, 64);
     const float inv_l = 1.f / l;
     const float fk = dc.on ? inv_l * dc.scale : inv_l;
+    // key pair of register 2j of tile t: t * 16 + (j & 1) + 4 (j >> 1) + 2 hf
+    const uint32_t hq = (uint32_t)q * 0x9E3779B1u, hk0 = (uint32_t)(2 * hf) * 0x85EBCA77u;
     f32x16 o[4];
 #pragma unroll
     for (int dt = 0; dt < 4; ++dt) o[dt] = zero16();
@@ -802,7 +840,8 @@ __global__ void __launch_bounds__(256, 1) attn128_fwd_d128_kernel(const bf16_t* 
       if (dc.on) {
         uint32_t hh[8];  // one hash per key pair, as a batch
 #pragma unroll
-        for (int j = 0; j < 8; ++j) hh[j] = drop_hash(dc, q, t * 32 + acc_row(2 * j, hf));
+        for (int j = 0; j < 8; ++j)  // drop_hash(dc, q, t * 32 + acc_row(2 j, hf)), per-lane terms hoisted
+          hh[j] = mix32(dc.seedmix ^ hq ^ (hk0 + (uint32_t)(t * 16 + (j & 1) + 4 * (j >> 1)) * 0x85EBCA77u));
 #pragma unroll
         for (int i = 0; i < 16; ++i) acc[t][i] = keep_from(dc, hh[i >> 1], i & 1) ? acc[t][i] * fk : 0.f;
       } else {
@@ -1109,14 +1148,14 @@ __global__ void __launch_bounds__(256, 1) attn128_bwd_kv_d128_kernel(
         for (int r = 0; r < 4; ++r) {
           const int i = 4 * G + r;
           const float pr = fexp2(fmaf(sacc[i], ATT_C2, -lv[r] * 1.4426950408889634f));
-          float pd = pr, dpd = dpacc[i];
-          if (dc.on) {
-            const bool kp = keep_from(dc, hh[r], key);
-            pd = kp ? pr * dc.scale : 0.f;
-            dpd = kp ? dpd * dc.scale : 0.f;
+          if (dc.on) {  // one select per score (see bwd_pds)
+            const float m = keep_from(dc, hh[r], key) ? dc.scale : 0.f;
+            sacc[i] = pr * m;
+            dpacc[i] = pr * fmaf(dpacc[i], m, -dl[r]);
+          } else {
+            sacc[i] = pr;
+            dpacc[i] = pr * (dpacc[i] - dl[r]);
           }
-          sacc[i] = pd;
-          dpacc[i] = pr * (dpd - dl[r]);
         }
       }
 #pragma unroll
@@ -1254,9 +1293,14 @@ bool launch_attn128_bwd(const uint16_t* qkv, const uint16_t* out, const uint16_t
   if (Lq != a128::L || causal || (!a128::enabled() && !head_major)) return false;
   const int items = B * H, slots = 2 * a128::num_cus();
   const int grid = items < slots ? items : slots;
-  hipLaunchKernelGGL(a128::attn128_bwd_kernel, dim3(grid), dim3(256), 0, s, (const bf16_t*)qkv,
-                     (const bf16_t*)out, (const bf16_t*)dout, lse, (bf16_t*)dqkv,
-                     dbias ? colpart : nullptr, B, H, p, seed, offset, head_major ? 1 : 0);
+  if (p > 0.f)
+    hipLaunchKernelGGL(a128::attn128_bwd_kernel<true>, dim3(grid), dim3(256), 0, s, (const bf16_t*)qkv,
+                       (const bf16_t*)out, (const bf16_t*)dout, lse, (bf16_t*)dqkv,
+                       dbias ? colpart : nullptr, B, H, p, seed, offset, head_major ? 1 : 0);
+  else
+    hipLaunchKernelGGL(a128::attn128_bwd_kernel<false>, dim3(grid), dim3(256), 0, s, (const bf16_t*)qkv,
+                       (const bf16_t*)out, (const bf16_t*)dout, lse, (bf16_t*)dqkv,
+                       dbias ? colpart : nullptr, B, H, p, seed, offset, head_major ? 1 : 0);
   if (dbias) {
     const int bchunk = 64, nch = (B + bchunk - 1) / bchunk;
     if (!db_accumulate) hipMemsetAsync(dbias, 0, sizeof(float) * 3 * H * a128::HD, s);

@@ -501,14 +501,19 @@ class TrainLoop:
             if not self._exec_settled:
                 self._settle_exec_microbatch(batch)
             return self._forward_backward(batch)
-        reserve = None if self._exec_settled else self._hbm_reserve()
+        if not self._exec_settled:
+            self._reset_hbm_peak()
         while True:
             snap = self._log_snapshot()
             try:
                 out = self._forward_backward(batch)
-                if reserve is not None:
-                    del reserve
-                    torch.cuda.empty_cache()
+                if not self._exec_settled and not self._hbm_headroom_ok() and self._shrink_exec_microbatch():
+                    # the step fit, but its peak left less HBM than the reserve free (at the
+                    # edge the caching allocator thrashes - DiffuSeq-XL ran 2x slower with
+                    # 0.9 GB left): redo it one chunk smaller (gradients re-zeroed, logs restored)
+                    self._log_restore(snap)
+                    self._reset_hbm_peak()
+                    continue
                 self._exec_settled = True
                 return out
             except torch.cuda.OutOfMemoryError:
@@ -620,22 +625,27 @@ class TrainLoop:
         snap = self._log_snapshot()
         self._probing = True
         ok = True
-        reserve = self._hbm_reserve()
+        self._reset_hbm_peak()
         try:
             with self.ddp_model.no_sync():
                 while True:
                     try:
                         self._forward_backward(batch)
-                        break
+                        if self._hbm_headroom_ok():
+                            break
+                        # fits, but leaves less than the reserve free at its peak
+                        if not self._shrink_exec_microbatch():
+                            break
+                        self._reset_hbm_peak()
                     except torch.cuda.OutOfMemoryError:
                         torch.cuda.empty_cache()
+                        self._reset_hbm_peak()
                         if not self._shrink_exec_microbatch():
                             ok = False
                             break
         finally:
             self._probing = False
             self._log_restore(snap)
-            del reserve
         self._zero_grad()
         if torch.cuda.is_available():
             torch.cuda.empty_cache()  # hands the probe's (and the reserve's) blocks back to the driver
@@ -651,20 +661,34 @@ class TrainLoop:
         self.exec_microbatch = agreed
         self._exec_settled = True
 
-    def _hbm_reserve(self):
-        """HBM held back while the executed micro-batch is probed (``DPA_HBM_RESERVE_GB``;
-        default 8 GB at world > 1, 0 on one rank): what the settled size leaves free for
-        RCCL's later allocations and allocator fragmentation.  Returns the holding tensor."""
-        if not torch.cuda.is_available() or self.device.type != "cuda":
-            return None
+    def _hbm_reserve_gb(self):
+        """HBM the settled executed micro-batch must leave free at its peak
+        (``DPA_HBM_RESERVE_GB``, default 8 GB): room for RCCL's lazily allocated buffers and
+        for allocator fragmentation.  DiffuSeq-XL at 1024-sample chunks peaks within 1 GB of
+        the 288 GB and thrashes the caching allocator (2x step time when anything else takes
+        memory); 704-sample chunks cost 0.5% and leave 104 GB (profiles/xl_hbm_headroom_r4.txt)."""
         env = os.environ.get("DPA_HBM_RESERVE_GB", "").strip()
-        gb = float(env) if env else (8.0 if dist_util.get_world_size() > 1 else 0.0)
+        return float(env) if env else 8.0
+
+    def _reset_hbm_peak(self):
+        if torch.cuda.is_available() and self.device.type == "cuda":
+            torch.cuda.empty_cache()  # cached blocks of a larger earlier try are not this one's peak
+            torch.cuda.reset_peak_memory_stats(self.device)
+
+    def _hbm_headroom_ok(self):
+        """Did the step just run leave at least the reserve unreserved at its peak?"""
+        if not torch.cuda.is_available() or self.device.type != "cuda":
+            return True
+        gb = self._hbm_reserve_gb()
         if gb <= 0:
-            return None
-        try:
-            return torch.empty(int(gb * (1 << 30)), dtype=torch.uint8, device=self.device)
-        except torch.cuda.OutOfMemoryError:
-            return None
+            return True
+        total = torch.cuda.get_device_properties(self.device).total_memory
+        head = total - torch.cuda.max_memory_reserved(self.device)
+        if head >= gb * (1 << 30):
+            return True
+        logger.log(f"exec_microbatch {self.exec_microbatch}: {head / 2**30:.1f} GB HBM left at the "
+                   f"step's peak, under the {gb:g} GB reserve")
+        return False
 
     @staticmethod
     def _log_snapshot():
