@@ -307,7 +307,9 @@ __global__ void __launch_bounds__(256) attn_fwd_kernel(const bf16_t* __restrict_
 // exp2(m_old - m_new).  O's rows live on accumulator registers, not lanes, so a
 // register's factor is fetched from the lane that owns that query (one
 // ds_bpermute per register per tile).  K is read once instead of twice.
-template <int D, bool CAUSAL>
+// DROP (attention dropout on, p > 0) is a template parameter in the single-pass forward and
+// both backward kernels: the per-score dropout work then carries no wave-uniform branch.
+template <int D, bool CAUSAL, bool DROP>
 __global__ void __launch_bounds__(256, D == 64 ? 2 : 1) attn_fwd_online_kernel(const bf16_t* __restrict__ qkv,
                                                              bf16_t* __restrict__ out,
                                                              float* __restrict__ lse, int L, int H,
@@ -412,7 +414,7 @@ __global__ void __launch_bounds__(256, D == 64 ? 2 : 1) attn_fwd_online_kernel(c
             add += pr;
             acc[t][i] = pr;
           }
-          if (dc.on) {  // hashes as an independent batch after the exps (ILP), then the keep selects
+          if constexpr (DROP) {  // hashes as an independent batch after the exps (ILP), then the keep selects
             uint32_t hh[8];
 #pragma unroll
             for (int j = 0; j < 8; ++j) hh[j] = drop_hash_t(dc, qterm, kt0 + (uint32_t)(acc_off(2 * j) >> 1) * DROP_CK);
@@ -589,7 +591,7 @@ __device__ __forceinline__ int64_t colpart_slot(const AttnItem& it0, int L, int 
   return ((int64_t)it0.b * NI + it0.t) * H + it0.hd;
 }
 
-template <int D, bool CAUSAL>
+template <int D, bool CAUSAL, bool DROP>
 __global__ void __launch_bounds__(256, D == 64 ? 2 : 1) attn_bwd_kv_kernel(
     const bf16_t* __restrict__ qkv, const bf16_t* __restrict__ dout, const float* __restrict__ lse,
     const float* __restrict__ delta, bf16_t* __restrict__ dqkv, int L, int H, float p,
@@ -664,7 +666,7 @@ __global__ void __launch_bounds__(256, D == 64 ? 2 : 1) attn_bwd_kv_kernel(
         // each lane of an adjacent pair computes every other one and takes the rest from
         // its neighbour (DPP quad_perm [1,0,3,2]) - half the quarter-rate multiplies
         uint32_t hh[16];
-        if (dc.on) {
+        if constexpr (DROP) {
           const int par = lane & 1;
           const uint32_t kt = (uint32_t)(key >> 1) * DROP_CK;
           const uint32_t qt0 = (uint32_t)(q0 + qt * 32 + 4 * hf + par) * DROP_CQ;
@@ -692,14 +694,13 @@ __global__ void __launch_bounds__(256, D == 64 ? 2 : 1) attn_bwd_kv_kernel(
         for (int i = 0; i < 16; ++i) {
           const int r = qt * 32 + acc_row(i, hf);
           const float pr = sacc[i];
-          float pd = pr, dpd = dpacc[i];
-          if (dc.on) {
-            const bool kp = keep_from(dc, hh[i], key);
-            pd = kp ? pr * dc.scale : 0.f;
-            dpd = kp ? dpd * dc.scale : 0.f;
+          if constexpr (DROP) {  // one select per score: the kept-and-scaled multiplier serves P and dP
+            const float m = keep_from(dc, hh[i], key) ? dc.scale : 0.f;
+            sacc[i] = pr * m;
+            dpacc[i] = pr * fmaf(dpacc[i], m, -s_del[r]);
+          } else {
+            dpacc[i] = pr * (dpacc[i] - s_del[r]);
           }
-          sacc[i] = pd;
-          dpacc[i] = pr * (dpd - s_del[r]);
         }
 #pragma unroll
         for (int s = 0; s < 2; ++s) {
@@ -719,17 +720,23 @@ __global__ void __launch_bounds__(256, D == 64 ? 2 : 1) attn_bwd_kv_kernel(
     }
     __syncthreads();
   }
+  {
+    // per-lane 32-bit offset once (rows 4 hf + c of the wave's 32 keys); the per-register
+    // row steps are wave-uniform, and full 32-key blocks need no row guard
+    bf16_t* const kvb = dqkv + ((int64_t)b * L + kbase) * ld + (int64_t)hd * D + (int64_t)H * D;
+    const uint32_t lo = __umul24((uint32_t)(4 * hf), (uint32_t)ld) + (uint32_t)(lane & 31);
+    const bool full = kbase + 32 <= L;
 #pragma unroll
-  for (int dt = 0; dt < D / 32; ++dt)
+    for (int dt = 0; dt < D / 32; ++dt)
 #pragma unroll
-    for (int i = 0; i < 16; ++i) {
-      const int kk = kbase + acc_row(i, hf);
-      if (kk < L) {
-        bf16_t* base = dqkv + ((int64_t)b * L + kk) * ld + (int64_t)hd * D + dt * 32 + (lane & 31);
-        base[(int64_t)H * D] = f2bf(dk[dt][i] * rsqrt_d<D>());
-        base[2LL * H * D] = f2bf(dv[dt][i]);
+      for (int i = 0; i < 16; ++i) {
+        if (full || kbase + acc_row(i, hf) < L) {
+          bf16_t* base = (kvb + ((int64_t)((i & 3) + 8 * (i >> 2)) * ld + dt * 32)) + lo;
+          base[0] = f2bf(dk[dt][i] * rsqrt_d<D>());
+          base[(int64_t)H * D] = f2bf(dv[dt][i]);
+        }
       }
-    }
+  }
   if (colpart) {  // k and v bias-gradient partials of this block's keys
     float* cp = colpart + colpart_slot(it0, L, H, CAUSAL) * (3 * D);
     auto ok = [&](int i) { return kbase + acc_row(i, hf) < L; };
@@ -747,7 +754,7 @@ __global__ void __launch_bounds__(256, D == 64 ? 2 : 1) attn_bwd_kv_kernel(
 //   dQ += dS K with dS^T fed as the A operand and K read transposed.
 // No atomics: each workgroup owns its queries' dQ rows completely.
 // ---------------------------------------------------------------------------
-template <int D, bool CAUSAL>
+template <int D, bool CAUSAL, bool DROP>
 __global__ void __launch_bounds__(256, D == 64 ? 2 : 1) attn_bwd_q_kernel(
     const bf16_t* __restrict__ qkv, const bf16_t* __restrict__ dout, const float* __restrict__ lse,
     float* __restrict__ delta, bf16_t* __restrict__ dqkv, int L, int H, float p,
@@ -830,7 +837,7 @@ __global__ void __launch_bounds__(256, D == 64 ? 2 : 1) attn_bwd_q_kernel(
         const uint32_t kt0 = (uint32_t)((kv0 + t * 32 + 4 * hf) >> 1) * DROP_CK;
         // dropout hashes first, one per key pair, as an independent batch (ILP)
         uint32_t hh[8];
-        if (dc.on) {
+        if constexpr (DROP) {
 #pragma unroll
           for (int j = 0; j < 8; ++j) hh[j] = drop_hash_t(dc, qterm, kt0 + (uint32_t)(acc_off(2 * j) >> 1) * DROP_CK);
         }
@@ -848,7 +855,7 @@ __global__ void __launch_bounds__(256, D == 64 ? 2 : 1) attn_bwd_q_kernel(
         for (int i = 0; i < 16; ++i) {
           const float pr = sacc[i];
           float dpd = dpacc[i];
-          if (dc.on) dpd = keep_from(dc, hh[i >> 1], i & 1) ? dpd * dc.scale : 0.f;
+          if constexpr (DROP) dpd = keep_from(dc, hh[i >> 1], i & 1) ? dpd * dc.scale : 0.f;
           sacc[i] = pr * (dpd - dlt);
         }
 #pragma unroll
@@ -866,13 +873,17 @@ __global__ void __launch_bounds__(256, D == 64 ? 2 : 1) attn_bwd_q_kernel(
     }
     __syncthreads();
   }
+  {
+    bf16_t* const qob = dqkv + ((int64_t)b * L + qbase) * ld + (int64_t)hd * D;
+    const uint32_t lo = __umul24((uint32_t)(4 * hf), (uint32_t)ld) + (uint32_t)(lane & 31);
+    const bool full = qbase + 32 <= L;
 #pragma unroll
-  for (int dt = 0; dt < D / 32; ++dt)
+    for (int dt = 0; dt < D / 32; ++dt)
 #pragma unroll
-    for (int i = 0; i < 16; ++i) {
-      const int qq = qbase + acc_row(i, hf);
-      if (qq < L) dqkv[((int64_t)b * L + qq) * ld + (int64_t)hd * D + dt * 32 + (lane & 31)] = f2bf(dq[dt][i] * rsqrt_d<D>());
-    }
+      for (int i = 0; i < 16; ++i)
+        if (full || qbase + acc_row(i, hf) < L)
+          ((qob + ((int64_t)((i & 3) + 8 * (i >> 2)) * ld + dt * 32)) + lo)[0] = f2bf(dq[dt][i] * rsqrt_d<D>());
+  }
   if (colpart) {  // q bias-gradient partials of this block's queries
     float* cp = colpart + colpart_slot(it0, L, H, CAUSAL) * (3 * D);
     block_colsum<D>(dq, rsqrt_d<D>(), [&](int i) { return qbase + acc_row(i, hf) < L; }, cred, cp, pass > 0, w,
@@ -899,12 +910,16 @@ static void attn_fwd_general(const uint16_t* qkv, uint16_t* out, float* lse, int
                          (bf16_t*)out, lse, L, H, p, seed, offset);
     return;
   }
-  if (causal)
-    hipLaunchKernelGGL((attn_fwd_online_kernel<D, true>), grid, dim3(256), 0, s, (const bf16_t*)qkv,
-                       (bf16_t*)out, lse, L, H, p, seed, offset);
-  else
-    hipLaunchKernelGGL((attn_fwd_online_kernel<D, false>), grid, dim3(256), 0, s, (const bf16_t*)qkv,
-                       (bf16_t*)out, lse, L, H, p, seed, offset);
+#define DPA_FWD_ONLINE(C, DR)                                                                      \
+  hipLaunchKernelGGL((attn_fwd_online_kernel<D, C, DR>), grid, dim3(256), 0, s, (const bf16_t*)qkv, \
+                     (bf16_t*)out, lse, L, H, p, seed, offset)
+  const bool drop = p > 0.f;
+  if (causal) {
+    if (drop) DPA_FWD_ONLINE(true, true); else DPA_FWD_ONLINE(true, false);
+  } else {
+    if (drop) DPA_FWD_ONLINE(false, true); else DPA_FWD_ONLINE(false, false);
+  }
+#undef DPA_FWD_ONLINE
 }
 
 bool launch_attn_fwd(const uint16_t* qkv, uint16_t* out, float* lse, int B, int L, int H, int D,
@@ -942,19 +957,22 @@ static void attn_bwd_general(const uint16_t* qkv, const uint16_t* out, const uin
   // dQ kernel first: it forms delta = rowsum(dO * O) in-kernel and publishes it for the
   // dK/dV kernel (no separate delta pass over O and dO)
   dim3 grid(attn_grid(B, L, H, causal));  // attn_item() layout
+#define DPA_BWD(C, DR)                                                                            \
+  do {                                                                                            \
+    hipLaunchKernelGGL((attn_bwd_q_kernel<D, C, DR>), grid, dim3(256), 0, s, (const bf16_t*)qkv,  \
+                       (const bf16_t*)dout, lse, delta, (bf16_t*)dqkv, L, H, p, seed, offset,     \
+                       (const bf16_t*)out, colpart);                                              \
+    hipLaunchKernelGGL((attn_bwd_kv_kernel<D, C, DR>), grid, dim3(256), 0, s, (const bf16_t*)qkv, \
+                       (const bf16_t*)dout, lse, delta, (bf16_t*)dqkv, L, H, p, seed, offset,     \
+                       colpart);                                                                  \
+  } while (0)
+  const bool drop = p > 0.f;
   if (causal) {
-    hipLaunchKernelGGL((attn_bwd_q_kernel<D, true>), grid, dim3(256), 0, s, (const bf16_t*)qkv,
-                       (const bf16_t*)dout, lse, delta, (bf16_t*)dqkv, L, H, p, seed, offset,
-                       (const bf16_t*)out, colpart);
-    hipLaunchKernelGGL((attn_bwd_kv_kernel<D, true>), grid, dim3(256), 0, s, (const bf16_t*)qkv,
-                       (const bf16_t*)dout, lse, delta, (bf16_t*)dqkv, L, H, p, seed, offset, colpart);
+    if (drop) DPA_BWD(true, true); else DPA_BWD(true, false);
   } else {
-    hipLaunchKernelGGL((attn_bwd_q_kernel<D, false>), grid, dim3(256), 0, s, (const bf16_t*)qkv,
-                       (const bf16_t*)dout, lse, delta, (bf16_t*)dqkv, L, H, p, seed, offset,
-                       (const bf16_t*)out, colpart);
-    hipLaunchKernelGGL((attn_bwd_kv_kernel<D, false>), grid, dim3(256), 0, s, (const bf16_t*)qkv,
-                       (const bf16_t*)dout, lse, delta, (bf16_t*)dqkv, L, H, p, seed, offset, colpart);
+    if (drop) DPA_BWD(false, true); else DPA_BWD(false, false);
   }
+#undef DPA_BWD
 }
 
 bool launch_attn_bwd(const uint16_t* qkv, const uint16_t* out, const uint16_t* dout, const float* lse,
