@@ -56,6 +56,11 @@ __device__ __forceinline__ bool keep_from(const DropCfg& d, uint32_t h, int key)
   const uint32_t r = (key & 1) ? (h >> 16) : (h & 0xffffu);
   return r >= d.thr16;
 }
+// keep_from for a per-lane key parity (sh = 16 for an even key, 0 for odd): one shift and one
+// compare instead of extracting and selecting a 16-bit half
+__device__ __forceinline__ bool keep_sh(const DropCfg& d, uint32_t h, uint32_t sh) {
+  return (h << sh) >= (d.thr16 << 16);
+}
 __device__ __forceinline__ bool keep_bit(const DropCfg& d, int q, int key) {
   return keep_from(d, drop_hash(d, q, key), key);
 }
@@ -695,7 +700,7 @@ __global__ void __launch_bounds__(256, D == 64 ? 2 : 1) attn_bwd_kv_kernel(
           const int r = qt * 32 + acc_row(i, hf);
           const float pr = sacc[i];
           if constexpr (DROP) {  // one select per score: the kept-and-scaled multiplier serves P and dP
-            const float m = keep_from(dc, hh[i], key) ? dc.scale : 0.f;
+            const float m = keep_sh(dc, hh[i], (key & 1) ? 0u : 16u) ? dc.scale : 0.f;
             sacc[i] = pr * m;
             dpacc[i] = pr * fmaf(dpacc[i], m, -s_del[r]);
           } else {

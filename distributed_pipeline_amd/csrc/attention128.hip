@@ -62,6 +62,11 @@ __device__ __forceinline__ bool keep_from(const DropCfg& d, uint32_t h, int key)
   const uint32_t r = (key & 1) ? (h >> 16) : (h & 0xffffu);
   return r >= d.thr16;
 }
+// keep_from for a per-lane key parity: sh = 16 (even key: low half) or 0 (odd key: high half);
+// (h << sh) >= thr16 << 16 is the same test in two ops instead of four (no select of halves)
+__device__ __forceinline__ bool keep_sh(const DropCfg& d, uint32_t h, uint32_t sh) {
+  return (h << sh) >= (d.thr16 << 16);
+}
 __device__ __forceinline__ bool keep_bit(const DropCfg& d, int q, int key) {
   return keep_from(d, drop_hash(d, q, key), key);
 }
@@ -446,7 +451,7 @@ __device__ __forceinline__ void bwd_dkv_step(f32x16 (&dv)[2], f32x16 (&dk)[2], c
 // The query of a hash is T*32 + 8G + 2j + 4hf + (key & 1) with T, G, j compile-time, so its
 // product with C_Q is hq plus an immediate (mod 2^32): no quarter-rate v_mul_lo_u32 per hash.
 struct HashTerms {
-  uint32_t hq, hk;
+  uint32_t hq, hk, sh;  // sh: keep_sh shift of this lane's key parity
   int par;
 };
 
@@ -476,12 +481,14 @@ __device__ __forceinline__ void bwd_pds(f32x16& sacc, f32x16& dpacc, uint32_t ba
     const float pr = fexp2(fmaf(sacc[i], ATT_C, -lv[r]));
     if constexpr (DROP) {
       // one select per score: the kept-and-scaled multiplier serves P and dP
-      const float m = keep_from(dc, hh[r], ht.par) ? dc.scale : 0.f;
+      const float m = keep_sh(dc, hh[r], ht.sh) ? dc.scale : 0.f;
       sacc[i] = pr * m;
       dpacc[i] = pr * fmaf(dpacc[i], m, -dl[r]);
     } else {
+      // no dropout: dS carries the 1/sqrt(64) gradient scale (exact in bf16, a power of two)
+      // in the same FMA, so dQ / dK need no scaling pass; dl is delta / 8 here
       sacc[i] = pr;
-      dpacc[i] = pr * (dpacc[i] - dl[r]);
+      dpacc[i] = pr * fmaf(dpacc[i], 0.125f, -dl[r]);
     }
   }
 }
@@ -613,7 +620,7 @@ __global__ void __launch_bounds__(256, 2) attn128_bwd_kernel(
         }
       }
       s += __shfl_xor(s, 1, 64);
-      if (half == 0) wr_b32(base + BWD_STATS + 512 + row * 4, __float_as_uint(s));
+      if (half == 0) wr_b32(base + BWD_STATS + 512 + row * 4, __float_as_uint(DROP ? s : s * 0.125f));
       if (tid < L) wr_b32(base + BWD_STATS + tid * 4, __float_as_uint(lpf * LOG2Ef));
     }
     barrier();
@@ -621,6 +628,7 @@ __global__ void __launch_bounds__(256, 2) attn128_bwd_kernel(
     const DropCfg dc = make_drop(p, seed, offset, (uint32_t)item);
     HashTerms ht;
     ht.par = key & 1;
+    ht.sh = ht.par ? 0u : 16u;
     ht.hq = (uint32_t)(4 * hf + ht.par) * 0x9E3779B1u;
     ht.hk = (uint32_t)(key >> 1) * 0x85EBCA77u;
     const uint32_t kbase = base + kb * 128;
@@ -657,8 +665,9 @@ __global__ void __launch_bounds__(256, 2) attn128_bwd_kernel(
     // stage dQ (rows = queries of wave w), dK, dV (rows = keys of wave w), unswizzled
     barrier();
     const uint32_t oa = base + BB.ost;
-    bwd_stage_out<0, 0>(dq[0], 0.125f, oa); bwd_stage_out<0, 1>(dq[1], 0.125f, oa);
-    bwd_stage_out<1, 0>(dk[0], 0.125f, oa); bwd_stage_out<1, 1>(dk[1], 0.125f, oa);
+    constexpr float gs = DROP ? 0.125f : 1.f;  // without dropout dS already carried the 1/8
+    bwd_stage_out<0, 0>(dq[0], gs, oa); bwd_stage_out<0, 1>(dq[1], gs, oa);
+    bwd_stage_out<1, 0>(dk[0], gs, oa); bwd_stage_out<1, 1>(dk[1], gs, oa);
     bwd_stage_out<2, 0>(dv[0], 1.f, oa);    bwd_stage_out<2, 1>(dv[1], 1.f, oa);
     barrier();
     bf16_t* gb = dqkv + (int64_t)b * L * ld + (int64_t)hd * HD;
@@ -1149,7 +1158,7 @@ __global__ void __launch_bounds__(256, 1) attn128_bwd_kv_d128_kernel(
           const int i = 4 * G + r;
           const float pr = fexp2(fmaf(sacc[i], ATT_C2, -lv[r] * 1.4426950408889634f));
           if (dc.on) {  // one select per score (see bwd_pds)
-            const float m = keep_from(dc, hh[r], key) ? dc.scale : 0.f;
+            const float m = keep_sh(dc, hh[r], (key & 1) ? 0u : 16u) ? dc.scale : 0.f;
             sacc[i] = pr * m;
             dpacc[i] = pr * fmaf(dpacc[i], m, -dl[r]);
           } else {
