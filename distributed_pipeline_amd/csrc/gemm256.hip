@@ -239,7 +239,7 @@ __device__ __forceinline__ int opaque(int x) {
 // XS / extra (persistent kernel): `extra` = XS stores of the previous tile were
 // issued between this tile's prologue DMA and its first iteration, so the waits
 // of phases 0-3 of that iteration leave them in flight.
-template <int P, bool A_TR, bool B_TR, bool CS, bool SWAP = false, int XS = 0>
+template <int P, bool A_TR, bool B_TR, bool CS, bool SWAP = false, int XS = 0, int DRAIN = 0>
 __device__ __forceinline__ void phase(f32x4 (&acc)[2][2][4][2], bf16x8 (&fa)[4][2],
                                       bf16x8 (&fb0)[2][2], bf16x8 (&fb1)[2][2], float& cs,
                                       const Operand<A_TR>& opA, const Operand<B_TR>& opB,
@@ -280,7 +280,7 @@ __device__ __forceinline__ void phase(f32x4 (&acc)[2][2][4][2], bf16x8 (&fa)[4][
       wait_vm<8>();
     }
   } else {
-    wait_vm<0>();
+    wait_vm<DRAIN>();  // DRAIN: ops issued after the last DMA that may stay in flight
   }
   // 3. barrier, retire reads, 16 MFMAs on one quadrant, barrier
   barrier();
@@ -623,6 +623,13 @@ __device__ __forceinline__ int lds_read_b32_sync(uint32_t addr) {
 __device__ __forceinline__ float bf_lo(uint32_t w) { return __uint_as_float(w << 16); }
 __device__ __forceinline__ float bf_hi(uint32_t w) { return __uint_as_float(w & 0xffff0000u); }
 
+// Early issue of the DACT epilogue's first aux rounds inside the last K-iteration
+// (DPA_GEMM_EARLY_AUX at compile time; 1 = on)
+#ifndef DPA_GEMM_EARLY_AUX
+#define DPA_GEMM_EARLY_AUX 1
+#endif
+constexpr int PEARLY_AUX = DPA_GEMM_EARLY_AUX;
+
 // Lab knobs (tools/gemm_lab; the library uses the defaults): POL bit 0 = non-temporal
 // epilogue stores, bit 1 = non-temporal aux loads; GM > 1 walks tiles in groups of GM tile
 // rows, column-major inside a group (GM x NT tiles share GM A panels and NT B panels).
@@ -918,7 +925,13 @@ __global__ void __launch_bounds__(512) gemmp_kernel(const bf16_t* __restrict__ A
       phase<6, false, B_TR, false, true>(acc, fa, fb0, fb1, cs, opA, opB, smem, csa, 0, more, false, grp);
       phase<7, false, B_TR, false, true>(acc, fa, fb0, fb1, cs, opA, opB, smem, csa, 0, more, false, grp);
     }
-    for (int it = 1; it < niter; ++it) {
+    // the epilogue's activation-backward operand (EPI 3/4/5) of rounds 0 and 1: issued in the
+    // last K-iteration once its DMA is out (phases 2-7 then leave these 4 loads in flight),
+    // so their HBM latency hides under that iteration's MFMAs instead of the epilogue's first
+    // rounds (niter == 1: issued after the main loop as before)
+    uint4 aux[2][2];
+    constexpr bool EARLY_AUX = DACT && (PEARLY_AUX != 0);
+    for (int it = 1; it < niter - (EARLY_AUX ? 1 : 0); ++it) {
       const int te = 2 * it;
       const bool more = it + 1 < niter;
       phase<0, false, B_TR, false, true>(acc, fa, fb0, fb1, cs, opA, opB, smem, csa, te, more, false, grp);
@@ -930,6 +943,28 @@ __global__ void __launch_bounds__(512) gemmp_kernel(const bf16_t* __restrict__ A
       phase<6, false, B_TR, false, true>(acc, fa, fb0, fb1, cs, opA, opB, smem, csa, te, more, false, grp);
       phase<7, false, B_TR, false, true>(acc, fa, fb0, fb1, cs, opA, opB, smem, csa, te, more, false, grp);
     }
+    bool aux_issued = false;
+    if constexpr (EARLY_AUX) {
+      if (niter > 1) {  // the peeled last iteration
+        const int te = 2 * (niter - 1);
+        phase<0, false, B_TR, false, true>(acc, fa, fb0, fb1, cs, opA, opB, smem, csa, te, false, false, grp);
+        phase<1, false, B_TR, false, true>(acc, fa, fb0, fb1, cs, opA, opB, smem, csa, te, false, false, grp);
+        {
+          const int ln = opaque(lane_id());
+#pragma unroll
+          for (int ro = 0; ro < 2; ++ro)
+#pragma unroll
+            for (int k = 0; k < 2; ++k) aux[ro][k] = ld_aux<POL>(Zout + row_off(tile, ro, k, ln));
+        }
+        aux_issued = true;
+        phase<2, false, B_TR, false, true, 0, 4>(acc, fa, fb0, fb1, cs, opA, opB, smem, csa, te, false, false, grp);
+        phase<3, false, B_TR, false, true, 0, 4>(acc, fa, fb0, fb1, cs, opA, opB, smem, csa, te, false, false, grp);
+        phase<4, false, B_TR, false, true, 0, 4>(acc, fa, fb0, fb1, cs, opA, opB, smem, csa, te, false, false, grp);
+        phase<5, false, B_TR, false, true, 0, 4>(acc, fa, fb0, fb1, cs, opA, opB, smem, csa, te, false, false, grp);
+        phase<6, false, B_TR, false, true, 0, 4>(acc, fa, fb0, fb1, cs, opA, opB, smem, csa, te, false, false, grp);
+        phase<7, false, B_TR, false, true, 0, 4>(acc, fa, fb0, fb1, cs, opA, opB, smem, csa, te, false, false, grp);
+      }
+    }
     if (dyn && w == 0) {
       // every wave's main loop ended in vmcnt(0): the claim has landed
       const int i = __builtin_amdgcn_readfirstlane(claimed);
@@ -938,8 +973,7 @@ __global__ void __launch_bounds__(512) gemmp_kernel(const bf16_t* __restrict__ A
     if (grp == 0) barrier();  // re-align the groups: every wave's LDS reads are retired
     const int next = dyn ? __builtin_amdgcn_readfirstlane(lds_read_b32_sync(sbase + P_NEXT_OFF)) : tile + G;
     const bool has_next = next < ntiles;
-    uint4 aux[2][2];
-    if constexpr (DACT) {
+    if (DACT && !aux_issued) {
       // activation-backward operand of rounds 0 and 1 (row-major, full lines), issued
       // before the next tile's prologue DMA so that waiting for it leaves the DMA in flight
       const int ln = opaque(lane_id());

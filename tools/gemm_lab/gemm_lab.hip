@@ -363,6 +363,38 @@ int main(int argc, char** argv) {
     return 0;
   }
 
+  if (argc > 2 && std::string(argv[2]) == "aux") {
+    // epilogues that read an aux operand (EPI 5 residual-accumulating dgrad, EPI 4 dact dgrad
+    // with bias column sums) vs the plain dgrad: build with -DDPA_GEMM_EARLY_AUX=0 / 1 to
+    // compare the aux loads issued in the last K-iteration against after the main loop
+    std::vector<Variant> pv;
+    for (const Shape& sh : shapes) {
+      const int K = sh.K, N = sh.N;
+      const double fl = 2.0 * T * K * N;
+      const std::string nm = sh.name;
+      pv.push_back({nm + "/gp_dgrad", [=](hipStream_t st) {
+                      gp<true, 0, 0, 0, 1>(A, N, B, K, T, K, N, C, nullptr, nullptr, nullptr, ncu, st);
+                    }, fl, {}});
+      pv.push_back({nm + "/gp_dgrad_res", [=](hipStream_t st) {
+                      gp<true, 5, 0, 0, 1>(A, N, B, K, T, K, N, C, nullptr, Z, nullptr, ncu, st);
+                    }, fl, {}});
+      if (nm == "ffn_out")
+        pv.push_back({nm + "/gp_dgrad_dact_db", [=](hipStream_t st) {
+                        gp<true, 4, 4, 1, 8>(A, 768, B, 3072, T, 3072, 768, C, nullptr, Z, CP, ncu, st);
+                      }, fl, {}});
+    }
+    printf("DPA_GEMM_EARLY_AUX=%d\n", DPA_GEMM_EARLY_AUX);
+    for (auto& v : pv) time_it(v, s, 2);
+    for (int r = 0; r < rounds; ++r)
+      for (auto& v : pv) v.ms.push_back(time_it(v, s, iters));
+    for (auto& v : pv) {
+      std::sort(v.ms.begin(), v.ms.end());
+      const float med = v.ms[v.ms.size() / 2];
+      printf("%-32s median %.4f ms  min %.4f ms  %.1f TF/s\n", v.name.c_str(), med, v.ms[0], v.flop / med / 1e9);
+    }
+    return 0;
+  }
+
   if (argc > 2 && std::string(argv[2]) == "4p") {
     // persistent one-wave-per-SIMD 256 x 128 kernel with the epilogue inside the next tile's
     // main loop (gemm4p.hip) vs the production persistent 8-wave kernel (gemmp_kernel)
