@@ -191,3 +191,55 @@ def test_numa_helpers(tmp_path):
     assert sorted(len(x) for x in parts) == [2, 2, 3, 3]
     assert set().union(*parts) == set(range(10))
     assert dist_util.bind_cpus_to_gpu(0, mode="off") is None
+
+
+def test_exec_microbatch_shrinks_for_hbm_headroom(tmp_path):
+    """One rank, auto executed micro-batch: a step that fits but leaves less HBM than the
+    reserve at its peak (``TrainLoop._hbm_headroom_ok``) is redone one chunk smaller - the
+    gradient of the redone step equals the reference sum of micro-batch gradients (nothing of
+    the first try remains) and the logged loss is that of the redone step only."""
+    from basic_utils import logger
+    from utils.trainer import TrainLoop
+
+    logger.configure(dir=str(tmp_path), format_strs=[])
+    torch.manual_seed(0)
+    model = torch.nn.Sequential(torch.nn.Linear(6, 16), torch.nn.Tanh(), torch.nn.Linear(16, 1))
+
+    class Loop(TrainLoop):
+        supports_microbatch_fusion = True
+
+        def compute_losses(self, mb):
+            self.chunks.append(mb["x"].shape[0])
+            out = self.ddp_model(mb["x"]).squeeze(-1)
+            return {"loss": (out - mb["y"]) ** 2}
+
+        def backward_from_losses(self, losses):
+            (losses["loss"] * self.loss_scale).mean().backward()
+
+        def _hbm_headroom_ok(self):  # "too little left" above 4 samples per chunk
+            return self.exec_microbatch <= 4
+
+    g = torch.Generator().manual_seed(1)
+    batch = {"x": torch.randn(8, 6, generator=g), "y": torch.randn(8, generator=g)}
+    loop = Loop(model=model, data=iter([batch] * 4), batch_size=8, microbatch=2, lr=1e-3,
+                ema_rate="0.9", log_interval=10, save_interval=10 ** 9, resume_checkpoint="",
+                learning_steps=0, checkpoint_path="", ddp_engine="native", precision="fp32",
+                exec_microbatch=0)
+    loop.chunks = []
+    loop.exec_microbatch = 8
+    loop.forward_backward(batch)
+    # 8 (one chunk) fits but is refused for headroom; the next size is two balanced chunks of 4
+    assert loop._exec_settled and loop.exec_microbatch == 4
+    assert loop.chunks[-2:] == [4, 4]
+    grads = loop.ddp_model.space.grad_flat.clone()
+    ref = torch.zeros_like(grads)
+    for p in model.parameters():
+        p.grad = None
+    for i in range(0, 8, 2):
+        out = model(batch["x"][i:i + 2]).squeeze(-1)
+        ((out - batch["y"][i:i + 2]) ** 2).mean().backward()
+    space = loop.ddp_model.space
+    for p in model.parameters():
+        o, e = space.range_of(p)
+        ref[o:e] = p.grad.reshape(-1)
+    torch.testing.assert_close(grads, ref, rtol=1e-5, atol=1e-6)
