@@ -1200,9 +1200,8 @@ class _ChunkedLinearXentFn(torch.autograd.Function):
         kept_is_grad = keep and _XENT_ROWS_FUSED
         allg = torch.empty(N, wp.shape[0], dtype=x.dtype, device=x.device) if keep else None
         if kept_is_grad:
-            # kept chunks: sized for the 256 MB Infinity Cache, so the row pass reads the
-            # logits the GEMM has just written from the MALL instead of HBM (the backward's
-            # GEMMs run over all N tokens at once, so small chunks cost them nothing)
+            # kept chunks (DPA_XENT_FWD_CHUNK_MB): the backward's GEMMs run over all N tokens at
+            # once, so the forward chunk size is free
             chunk = min(chunk, max(256, (_XENT_FWD_CHUNK_BYTES // (wp.shape[0] * 2)) // 256 * 256))
         for s in range(0, N, chunk):
             e = min(N, s + chunk)
@@ -1293,8 +1292,10 @@ _XENT_CHUNK_BYTES = int(os.environ.get("DPA_XENT_CHUNK_MB", "2048")) << 20
 _XENT_KEEP_BYTES = int(os.environ.get("DPA_XENT_KEEP_GB", "24")) << 30
 # kept logits: the backward's dx as one GEMM over all tokens (DPA_XENT_DX_ALL=0: per chunk)
 _XENT_DX_ALL = os.environ.get("DPA_XENT_DX_ALL", "1") != "0"
-# forward chunk when the logits are kept (softmax - onehot in place): MALL-resident
-_XENT_FWD_CHUNK_BYTES = int(os.environ.get("DPA_XENT_FWD_CHUNK_MB", "128")) << 20
+# forward chunk when the logits are kept (softmax - onehot in place).  128 MB chunks (resident
+# in the 256 MB Infinity Cache) did not speed the row pass up (profiles/gpt2_head_ab_r4.txt) and
+# cost ~200 small loss/lse copies per GPT-2 step, so the default keeps the 2 GB chunks
+_XENT_FWD_CHUNK_BYTES = int(os.environ.get("DPA_XENT_FWD_CHUNK_MB", "2048")) << 20
 
 
 def linear_cross_entropy(x, weight, bias, target):
