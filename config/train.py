@@ -127,9 +127,9 @@ class PerfSettings(S):
         = _(True, "With several executed micro-batches per step (e.g. exec_microbatch=-1), run micro-batch "
                   "k+1's forward on a second HIP stream while k's backward runs (bitwise-identical gradients).")
     defer_wgrad: int \
-        = _(4, "With several executed micro-batches per step: hold each Linear's weight-gradient operands for "
+        = _(8, "With several executed micro-batches per step: hold each Linear's weight-gradient operands for "
                "this many micro-batches and run them as one multi-segment split-K GEMM (same fp32 sum; "
-               "0/1 = off, at most 4).")
+               "0/1 = off, at most 8).")
     shard_data: bool \
         = _(False, "Give each rank a disjoint shard of the data (DistributedSampler-style).")
     log_cross_rank_mean: bool \

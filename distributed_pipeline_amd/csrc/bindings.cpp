@@ -621,7 +621,7 @@ static bool gemm_wgrad_multi(const std::vector<at::Tensor>& dys, const std::vect
                              c10::optional<at::Tensor> db) {
   TORCH_CHECK(!dys.empty() && dys.size() == xs.size(), "gemm_wgrad_multi: segment lists");
   const int nseg = (int)dys.size();
-  if (nseg > 4) return false;
+  if (nseg > 8) return false;  // g256::WG_MAXSEG
   CHECK_F32(dW); CHECK_CONTIG(dW);
   const int T = (int)dys[0].size(0), N = (int)dys[0].size(1), K = (int)xs[0].size(1);
   std::vector<const uint16_t*> dp(nseg), xp(nseg);

@@ -296,7 +296,7 @@ __device__ __forceinline__ void phase(f32x4 (&acc)[2][2][4][2], bf16x8 (&fa)[4][
 
 // Token segments of a multi-segment weight gradient: dW += sum_s dy_s^T x_s, every segment
 // ktiles_total K-tiles long (the reference schedule's deferred micro-batch pairs).
-constexpr int WG_MAXSEG = 4;
+constexpr int WG_MAXSEG = 8;
 struct WgSegs {
   const bf16_t* a[WG_MAXSEG];
   const bf16_t* b[WG_MAXSEG];

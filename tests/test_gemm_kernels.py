@@ -64,7 +64,7 @@ def test_gemm_wgrad_accumulates(T, N, K, tile):
     _close(db, refb, 1e-3)
 
 
-@pytest.mark.parametrize("nseg", [2, 3, 4])
+@pytest.mark.parametrize("nseg", [2, 3, 4, 8])
 @pytest.mark.parametrize("T,N,K", [(8192, 768, 768), (8192, 2304, 768), (2048, 768, 3072), (256, 256, 512)])
 def test_gemm_wgrad_multi_segment(T, N, K, nseg):
     """One multi-segment split-K launch == the sum of per-segment weight gradients."""

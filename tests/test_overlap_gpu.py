@@ -64,7 +64,7 @@ def test_overlapped_schedule_matches_sequential():
 
 
 @pytest.mark.parametrize("overlap", [True, False])
-@pytest.mark.parametrize("depth", [2, 4])
+@pytest.mark.parametrize("depth", [2, 4, 8])
 def test_deferred_wgrad_matches_sequential(depth, overlap):
     """Weight-gradient deferral (ops/nn.py _WgradDeferral): the held (dy, x) operands of
     ``depth`` micro-batches run as one multi-segment split-K GEMM, in the overlapped schedule

@@ -133,7 +133,7 @@ class TrainLoop:
             shard_optimizer=False,
             exec_microbatch=0,
             overlap_microbatches=True,
-            defer_wgrad=4,
+            defer_wgrad=8,
             log_cross_rank_mean=False,
             # ---- observability / robustness (all optional) ----
             nan_guard="off",
@@ -190,7 +190,7 @@ class TrainLoop:
                                      and os.environ.get("DPA_OVERLAP_MB", "1") != "0")
         # ...and hold each Linear's weight-gradient operands for defer_wgrad micro-batches, run as
         # one multi-segment split-K GEMM (ops/nn.py _WgradDeferral; DPA_DEFER_WGRAD overrides)
-        self.defer_wgrad = max(0, min(4, int(os.environ.get("DPA_DEFER_WGRAD", defer_wgrad))))
+        self.defer_wgrad = max(0, min(8, int(os.environ.get("DPA_DEFER_WGRAD", defer_wgrad))))
         # host seconds spent enqueueing the overlapped schedule's forwards / backwards (the
         # reference schedule's 32 micro-batches per step can be host-bound)
         self.host_time = {"fwd": 0.0, "bwd": 0.0}
