@@ -210,9 +210,35 @@ __device__ __forceinline__ QkvLayout qkv_layout(int H, int hmaj) {
   return q;
 }
 
+// ---- immediate-offset LDS access (per-lane base VGPR + compile-time offset) --
+template <int IMM>
+__device__ __forceinline__ bf16x8 rd128o(uint32_t a) {
+  bf16x8 f;
+  asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(f) : "v"(a), "i"(IMM));
+  return f;
+}
+template <int IMM>
+__device__ __forceinline__ f32x4 rdf4o(uint32_t a) {
+  f32x4 f;
+  asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(f) : "v"(a), "i"(IMM));
+  return f;
+}
+template <int IMM>
+__device__ __forceinline__ bf16x4 rdtro(uint32_t a) {
+  bf16x4 f;
+  asm volatile("ds_read_b64_tr_b16 %0, %1 offset:%2" : "=v"(f) : "v"(a), "i"(IMM));
+  return f;
+}
+template <int IMM>
+__device__ __forceinline__ void wr16o(uint32_t a, uint16_t v) {
+  asm volatile("ds_write_b16 %0, %1 offset:%2" ::"v"(a), "v"((uint32_t)v), "i"(IMM) : "memory");
+}
+
 // ============================================================================
 // forward
 // ============================================================================
+// DROP: attention dropout on (p > 0) at compile time (no per-score wave-uniform branch).
+template <bool DROP>
 __global__ void __launch_bounds__(256, 2) attn128_fwd_kernel(const bf16_t* __restrict__ qkv,
                                                             bf16_t* __restrict__ out,
                                                             float* __restrict__ lse, int B, int H,
@@ -259,34 +285,51 @@ __global__ void __launch_bounds__(256, 2) attn128_fwd_kernel(const bf16_t* __res
     const int b = item / H, hd = item - b * H;
     const DropCfg dc = make_drop(p, seed, offset, (uint32_t)item);
     const int q = w * 32 + (lane & 31);
+    // per-lane LDS fragment bases, derived once per item through an opaque zero (hoisted out of
+    // the item loop they would stay live across it); every read is base + immediate
+    uint32_t z0;
+    asm volatile("v_mov_b32 %0, 0" : "=v"(z0));
+    const int ln = lane + (int)z0;
+    uint32_t rb[4], tp;
+    {
+      const int r = ln & 31, sw_r = (r >> 1) & 7, h = ln >> 5;
+#pragma unroll
+      for (int s = 0; s < 4; ++s) rb[s] = (uint32_t)(r * 128 + (((2 * s + h) ^ sw_r) << 4));
+      // transposed V fragment rows r0 + 4h + qq (+8), r0 % 16 == 0: swizzle (2h + qq/2); the
+      // second column block is +64 bytes, the +8 rows' read +1024 + (1 - dt) * 64
+      const int g = ln >> 4, li = ln & 15, qq = li >> 2, pp = li & 3;
+      const int cp = 2 * (g & 1) + (pp >> 1), e = (pp & 1) * 8;
+      tp = (uint32_t)((4 * h + qq) * 128 + ((cp ^ ((2 * h + (qq >> 1)) & 7)) << 4) + e);
+    }
 
     // S^T (keys in registers, query on the lane)
     f32x16 acc[4];
-#pragma unroll
-    for (int t = 0; t < 4; ++t) {
-      bf16x8 kf[4];
-#pragma unroll
-      for (int s = 0; s < 4; ++s) kf[s] = frag_r(ki, t * 32, s, lane);
-      lgkm0();
-      acc[t] = zero16();
-#pragma unroll
-      for (int s = 0; s < 4; ++s) acc[t] = mfma32(kf[s], qf[s], acc[t]);
-    }
+#define DPA_FWD_S(T)                                                            \
+  {                                                                            \
+    bf16x8 kf[4];                                                              \
+    kf[0] = rd128o<T * 4096>(ki + rb[0]);                                      \
+    kf[1] = rd128o<T * 4096>(ki + rb[1]);                                      \
+    kf[2] = rd128o<T * 4096>(ki + rb[2]);                                      \
+    kf[3] = rd128o<T * 4096>(ki + rb[3]);                                      \
+    lgkm0();                                                                   \
+    acc[T] = zero16();                                                         \
+    for (int s = 0; s < 4; ++s) acc[T] = mfma32(kf[s], qf[s], acc[T]);         \
+  }
+    DPA_FWD_S(0) DPA_FWD_S(1) DPA_FWD_S(2) DPA_FWD_S(3)
+#undef DPA_FWD_S
+    // max over the raw scores, the softmax scale folded into the exp's FMA
     float m = -INFINITY;
 #pragma unroll
     for (int t = 0; t < 4; ++t)
 #pragma unroll
-      for (int i = 0; i < 16; ++i) {
-        acc[t][i] *= ATT_C;
-        m = fmaxf(m, acc[t][i]);
-      }
-    m = fmaxf(m, __shfl_xor(m, 32, 64));
+      for (int i = 0; i < 16; ++i) m = fmaxf(m, acc[t][i]);
+    m = fmaxf(m, __shfl_xor(m, 32, 64)) * ATT_C;
     float l = 0.f;
 #pragma unroll
     for (int t = 0; t < 4; ++t)
 #pragma unroll
       for (int i = 0; i < 16; ++i) {
-        const float e = fexp2(acc[t][i] - m);
+        const float e = fexp2(fmaf(acc[t][i], ATT_C, -m));
         acc[t][i] = e;
         l += e;
       }
@@ -296,12 +339,22 @@ __global__ void __launch_bounds__(256, 2) attn128_fwd_kernel(const bf16_t* __res
     f32x16 o[2];
     o[0] = zero16();
     o[1] = zero16();
-    const float fk = dc.on ? inv_l * dc.scale : inv_l;
+    const float fk = DROP ? inv_l * dc.scale : inv_l;
     // key pair of register 2j of tile t: t * 16 + (j & 1) + 4 (j >> 1) + 2 hf
     const uint32_t hq = (uint32_t)q * 0x9E3779B1u, hk0 = (uint32_t)(2 * hf) * 0x85EBCA77u;
+#define DPA_FWD_PV(T, S)                                                                            \
+  {                                                                                                \
+    const bf16x8 af = acc_to_frag(acc[T], S);                                                      \
+    constexpr int R0 = (T * 32 + 16 * S) * 128;                                                    \
+    const bf16x8 v0 = cat44(rdtro<IMG + R0>(ki + tp), rdtro<IMG + R0 + 1024 + 64>(ki + tp));       \
+    const bf16x8 v1 = cat44(rdtro<IMG + R0 + 64>(ki + tp), rdtro<IMG + R0 + 1024>(ki + tp));       \
+    lgkm0();                                                                                       \
+    o[0] = mfma32(af, v0, o[0]);                                                                   \
+    o[1] = mfma32(af, v1, o[1]);                                                                   \
+  }
 #pragma unroll
     for (int t = 0; t < 4; ++t) {
-      if (dc.on) {
+      if constexpr (DROP) {
         // one hash per key pair (registers 2j, 2j + 1 are keys 2m, 2m + 1), as one batch
         uint32_t hh[8];
 #pragma unroll
@@ -313,35 +366,36 @@ __global__ void __launch_bounds__(256, 2) attn128_fwd_kernel(const bf16_t* __res
 #pragma unroll
         for (int i = 0; i < 16; ++i) acc[t][i] *= fk;
       }
-#pragma unroll
-      for (int s = 0; s < 2; ++s) {
-        const bf16x8 af = acc_to_frag(acc[t], s);
-        bf16x8 vf[2];
-#pragma unroll
-        for (int dt = 0; dt < 2; ++dt) vf[dt] = frag_tp(vi, t * 32 + 16 * s, dt * 32, lane);
-        lgkm0();
-#pragma unroll
-        for (int dt = 0; dt < 2; ++dt) o[dt] = mfma32(af, vf[dt], o[dt]);
-      }
     }
-    // stage O (rows = queries) in the K image (dead: every wave passed its S^T)
+    DPA_FWD_PV(0, 0) DPA_FWD_PV(0, 1) DPA_FWD_PV(1, 0) DPA_FWD_PV(1, 1)
+    DPA_FWD_PV(2, 0) DPA_FWD_PV(2, 1) DPA_FWD_PV(3, 0) DPA_FWD_PV(3, 1)
+#undef DPA_FWD_PV
+    // stage O (rows = queries) unswizzled in the K image (dead: every wave passed its S^T):
+    // row 32w + 4h + (i&3) + 8(i>>2), column dt*32 + (lane&31) - all but the lane part immediate
     barrier();
     const uint32_t qi = ki;
-#pragma unroll
-    for (int dt = 0; dt < 2; ++dt)
-#pragma unroll
-      for (int i = 0; i < 16; ++i) {
-        const int row = w * 32 + acc_row(i, hf), col = dt * 32 + (lane & 31);
-        wr_b16(qi + off_r(row, col >> 3) + (col & 7) * 2, f2bf(o[dt][i]));
-      }
+    {
+      const uint32_t ost = qi + (uint32_t)((32 * w + 4 * hf) * 128 + (ln & 31) * 2);
+#define DPA_FWD_ST(I)                                                        \
+  wr16o<((I & 3) + 8 * (I >> 2)) * 128>(ost, f2bf(o[0][I]));                 \
+  wr16o<((I & 3) + 8 * (I >> 2)) * 128 + 64>(ost, f2bf(o[1][I]));
+      DPA_FWD_ST(0) DPA_FWD_ST(1) DPA_FWD_ST(2) DPA_FWD_ST(3) DPA_FWD_ST(4) DPA_FWD_ST(5)
+      DPA_FWD_ST(6) DPA_FWD_ST(7) DPA_FWD_ST(8) DPA_FWD_ST(9) DPA_FWD_ST(10) DPA_FWD_ST(11)
+      DPA_FWD_ST(12) DPA_FWD_ST(13) DPA_FWD_ST(14) DPA_FWD_ST(15)
+#undef DPA_FWD_ST
+    }
     barrier();
     bf16_t* ob = out + (int64_t)b * L * ldo + (int64_t)hd * HD;
-#pragma unroll
-    for (int c = 0; c < 4; ++c) {
-      const int idx = tid + c * 256, row = idx >> 3, ch = idx & 7;
-      const bf16x8 v = rd128(qi + off_r(row, ch));
+    {
+      const uint32_t cpy = qi + (uint32_t)((tid >> 3) * 128 + (tid & 7) * 16);
+      const bf16x8 c0 = rd128o<0>(cpy), c1 = rd128o<4096>(cpy), c2 = rd128o<8192>(cpy), c3 = rd128o<12288>(cpy);
       lgkm0();
-      *reinterpret_cast<bf16x8*>(ob + (int64_t)row * ldo + ch * 8) = v;
+      bf16_t* orow = ob + __umul24((uint32_t)(tid >> 3), (uint32_t)ldo) + (tid & 7) * 8;
+      const int64_t r32 = 32 * ldo;
+      *reinterpret_cast<bf16x8*>(orow) = c0;
+      *reinterpret_cast<bf16x8*>(orow + r32) = c1;
+      *reinterpret_cast<bf16x8*>(orow + 2 * r32) = c2;
+      *reinterpret_cast<bf16x8*>(orow + 3 * r32) = c3;
     }
   }
 }
@@ -349,30 +403,6 @@ __global__ void __launch_bounds__(256, 2) attn128_fwd_kernel(const bf16_t* __res
 // ============================================================================
 // backward
 // ============================================================================
-// ---- immediate-offset LDS access (per-lane base VGPR + compile-time offset) --
-template <int IMM>
-__device__ __forceinline__ bf16x8 rd128o(uint32_t a) {
-  bf16x8 f;
-  asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(f) : "v"(a), "i"(IMM));
-  return f;
-}
-template <int IMM>
-__device__ __forceinline__ f32x4 rdf4o(uint32_t a) {
-  f32x4 f;
-  asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(f) : "v"(a), "i"(IMM));
-  return f;
-}
-template <int IMM>
-__device__ __forceinline__ bf16x4 rdtro(uint32_t a) {
-  bf16x4 f;
-  asm volatile("ds_read_b64_tr_b16 %0, %1 offset:%2" : "=v"(f) : "v"(a), "i"(IMM));
-  return f;
-}
-template <int IMM>
-__device__ __forceinline__ void wr16o(uint32_t a, uint16_t v) {
-  asm volatile("ds_write_b16 %0, %1 offset:%2" ::"v"(a), "v"((uint32_t)v), "i"(IMM) : "memory");
-}
-
 // LDS (one stage per workgroup, two workgroups per CU so that one's loads
 // overlap the other's math): Q, dO, K images; then lse2[128], delta[128].  V never
 // goes through LDS: each wave needs only its 32 keys' V rows (fragment registers).
@@ -1259,8 +1289,12 @@ bool launch_attn128_fwd(const uint16_t* qkv, uint16_t* out, float* lse, int B, i
   if (Lq != a128::L || causal || (!a128::enabled() && !head_major)) return false;
   const int items = B * H, slots = 2 * a128::num_cus();
   const int grid = items < slots ? items : slots;
-  hipLaunchKernelGGL(a128::attn128_fwd_kernel, dim3(grid), dim3(256), 0, s, (const bf16_t*)qkv,
-                     (bf16_t*)out, lse, B, H, p, seed, offset, head_major ? 1 : 0);
+  if (p > 0.f)
+    hipLaunchKernelGGL(a128::attn128_fwd_kernel<true>, dim3(grid), dim3(256), 0, s, (const bf16_t*)qkv,
+                       (bf16_t*)out, lse, B, H, p, seed, offset, head_major ? 1 : 0);
+  else
+    hipLaunchKernelGGL(a128::attn128_fwd_kernel<false>, dim3(grid), dim3(256), 0, s, (const bf16_t*)qkv,
+                       (bf16_t*)out, lse, B, H, p, seed, offset, head_major ? 1 : 0);
   return true;
 }
 
