@@ -146,10 +146,15 @@ static std::vector<at::Tensor> lxent_fwd_dx(const at::Tensor& x, const at::Tenso
   return {loss, lse, dxu};
 }
 
+static void emb_grad(const at::Tensor& ids, const at::Tensor& dy, at::Tensor& dW);
+
+// onehot_scatter: the dW kernel leaves out the target one-hot (softmax only) and it is added
+// here as dW[t] -= g x_t, db[t] -= g over the valid targets, by the sorted segment-sum scatter
+// of the embedding backward - a compare, subtract and select less per logit in the kernel
 static std::vector<at::Tensor> lxent_bwd(const at::Tensor& dloss, const at::Tensor& x,
                                          const at::Tensor& W, c10::optional<at::Tensor> b,
                                          const at::Tensor& tgt, const at::Tensor& lse, bool need_dx,
-                                         bool need_dw, bool need_db) {
+                                         bool need_dw, bool need_db, bool onehot_scatter) {
   check_lxent(x, W, b, tgt);
   CHECK_F32(dloss); CHECK_F32(lse); CHECK_CONTIG(dloss); CHECK_CONTIG(lse);
   const c10::DeviceGuard guard(x.device());
@@ -169,11 +174,18 @@ static std::vector<at::Tensor> lxent_bwd(const at::Tensor& dloss, const at::Tens
   if (need_dw || need_db) {
     dW = at::zeros({V, E}, f32);
     if (need_db) db = at::zeros({V}, f32);
+    const bool scatter = onehot_scatter && need_dw && (E == 128 || E == 256);
     if (N > 0)
       dpa::launch_lxent_dw(bf_ptr(x), bf_ptr(W), opt_bf_ptr(b), tgt.data_ptr<int64_t>(),
                            lse.data_ptr<float>(), dloss.data_ptr<float>(), N, V, E,
                            dW.data_ptr<float>(), need_db ? db.data_ptr<float>() : nullptr,
-                           cur_stream());
+                           cur_stream(), !scatter);
+    if (scatter && N > 0) {
+      const at::Tensor valid = tgt.ge(0).logical_and(tgt.lt(V));
+      const at::Tensor ng = at::where(valid, dloss.neg(), at::zeros({}, dloss.options()));
+      emb_grad(tgt, x.to(at::kFloat).mul_(ng.unsqueeze(1)), dW);  // ids outside [0, V) are skipped
+      if (need_db) db.index_add_(0, tgt.clamp(0, V - 1), ng);
+    }
     if (!need_dw) dW = at::Tensor();
   }
   return {dx, dW, db};
@@ -918,7 +930,10 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("lxent_fwd", &lxent_fwd, "fused linear + cross-entropy forward -> (loss, lse)");
   m.def("lxent_fwd_dx", &lxent_fwd_dx,
         "fused linear-CE forward + unscaled input gradient -> (loss, lse, dxu fp32 [N, E])");
-  m.def("lxent_bwd", &lxent_bwd, "fused linear + cross-entropy backward -> (dx, dW fp32, db fp32)");
+  m.def("lxent_bwd", &lxent_bwd, "fused linear + cross-entropy backward -> (dx, dW fp32, db fp32)",
+        pybind11::arg("dloss"), pybind11::arg("x"), pybind11::arg("W"), pybind11::arg("b"), pybind11::arg("tgt"),
+        pybind11::arg("lse"), pybind11::arg("need_dx"), pybind11::arg("need_dw"), pybind11::arg("need_db"),
+        pybind11::arg("onehot_scatter") = false);
   m.def("xent_rows_fwd", &xent_rows_fwd, "row softmax-CE over bf16 logits [R, ld] -> (loss, lse)");
   m.def("xent_rows_bwd_", &xent_rows_bwd_, "in place: logits -> dloss * (softmax - onehot)");
   m.def("xent_rows_fwd_grad_", &xent_rows_fwd_grad_,

@@ -50,7 +50,7 @@ void launch_lxent_dx(const uint16_t* x, const uint16_t* W, const uint16_t* b, co
                      float* dx_acc, hipStream_t s);
 void launch_lxent_dw(const uint16_t* x, const uint16_t* W, const uint16_t* b, const int64_t* tgt,
                      const float* lse, const float* dloss, int N, int V, int E, float* dW, float* db,
-                     hipStream_t s);
+                     hipStream_t s, bool onehot = true);
 
 // ---- norm.hip (fused dropout + residual + LayerNorm) ---------------------------
 bool launch_add_ln_fwd(const uint16_t* y, const uint16_t* res, const uint16_t* g, const uint16_t* b,

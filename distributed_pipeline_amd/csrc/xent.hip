@@ -488,7 +488,10 @@ __global__ void __launch_bounds__(256) lxent_fwd_dx_combine_kernel(
 // ---------------------------------------------------------------------------
 // Backward: dW (+ db)
 // ---------------------------------------------------------------------------
-template <int E>
+// ONEHOT: subtract the target's one-hot inside the kernel (a compare, subtract and select per
+// logit); false: the caller adds dW[target] -= g x and db[target] -= g as a sorted scatter
+// (bindings.cpp lxent_bwd), which leaves the per-logit work at exp, scale and column sum.
+template <int E, bool ONEHOT = true>
 __global__ void __launch_bounds__(512) lxent_dw_kernel(
     const bf16_t* __restrict__ x, const bf16_t* __restrict__ W, const bf16_t* __restrict__ bias,
     const int64_t* __restrict__ target, const float* __restrict__ lse, const float* __restrict__ dloss,
@@ -578,7 +581,7 @@ __global__ void __launch_bounds__(512) lxent_dw_kernel(
         for (int r = 0; r < 4; ++r) {
           const int i = 4 * g4 + r;
           const float gp = g4v[r] * fexp2(fmaf(acc[i], LOG2E, -l4[r]));
-          const float d = (tgs[r] == v) ? gp - g4v[r] : gp;
+          const float d = (ONEHOT && tgs[r] == v) ? gp - g4v[r] : gp;
           acc[i] = d;
           dbs += d;
         }
@@ -757,18 +760,21 @@ void launch_lxent_dx(const uint16_t* x, const uint16_t* W, const uint16_t* b, co
 
 void launch_lxent_dw(const uint16_t* x, const uint16_t* W, const uint16_t* b, const int64_t* tgt,
                      const float* lse, const float* dloss, int N, int V, int E, float* dW, float* db,
-                     hipStream_t s) {
+                     hipStream_t s, bool onehot) {
   const int vb = (V + 255) / 256;
   const int tchunks = (N + 63) / 64;
   const int TS = pick_splits(vb, tchunks, 960);
   const int tps = ((tchunks + TS - 1) / TS) * 64;
   const int TSx = (N + tps - 1) / tps;
-  if (E == 128)
-    hipLaunchKernelGGL(lxent_dw_kernel<128>, dim3(vb, TSx), dim3(512), 0, s, (const bf16_t*)x,
-                       (const bf16_t*)W, (const bf16_t*)b, tgt, lse, dloss, N, V, tps, dW, db);
-  else
-    hipLaunchKernelGGL(lxent_dw_kernel<256>, dim3(vb, TSx), dim3(512), 0, s, (const bf16_t*)x,
-                       (const bf16_t*)W, (const bf16_t*)b, tgt, lse, dloss, N, V, tps, dW, db);
+#define DPA_LXDW(EE, OH)                                                                                \
+  hipLaunchKernelGGL((lxent_dw_kernel<EE, OH>), dim3(vb, TSx), dim3(512), 0, s, (const bf16_t*)x,        \
+                     (const bf16_t*)W, (const bf16_t*)b, tgt, lse, dloss, N, V, tps, dW, db)
+  if (E == 128) {
+    if (onehot) DPA_LXDW(128, true); else DPA_LXDW(128, false);
+  } else {
+    if (onehot) DPA_LXDW(256, true); else DPA_LXDW(256, false);
+  }
+#undef DPA_LXDW
 }
 
 }  // namespace dpa

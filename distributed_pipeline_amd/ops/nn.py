@@ -1130,7 +1130,7 @@ class _LinearXentFn(torch.autograd.Function):
         g = dloss.contiguous().float()
         need_dx = ctx.needs_input_grad[0] and dxu is None
         dx, dw, db = get_ext().lxent_bwd(g, x, w16, b16, target, lse, need_dx, ctx.needs_input_grad[1],
-                                         ctx.has_b and ctx.needs_input_grad[2])
+                                         ctx.has_b and ctx.needs_input_grad[2], _XENT_ONEHOT_SCATTER)
         if dxu is not None:
             dx = dxu.mul_(g.unsqueeze(1)).to(x.dtype)
         w, b = ctx.wb
@@ -1280,6 +1280,10 @@ class _ChunkedLinearXentFn(torch.autograd.Function):
 # wide-E CE: kept logit chunks become softmax - onehot in the forward's row pass
 # (DPA_XENT_ROWS_FUSED=0: forward statistics only, separate backward row pass)
 _XENT_ROWS_FUSED = os.environ.get("DPA_XENT_ROWS_FUSED", "1") != "0"
+
+# fused CE backward: the weight-gradient kernel computes softmax only and the target one-hot
+# goes in as a sorted scatter (DPA_XENT_ONEHOT_SCATTER=0: in the kernel, per logit)
+_XENT_ONEHOT_SCATTER = os.environ.get("DPA_XENT_ONEHOT_SCATTER", "1") != "0"
 
 # fused CE: forward also emits the unscaled input gradient (DPA_XENT_FUSED_DX=0: separate dx pass)
 _XENT_FUSED_DX = os.environ.get("DPA_XENT_FUSED_DX", "1") != "0"
