@@ -1281,9 +1281,10 @@ class _ChunkedLinearXentFn(torch.autograd.Function):
 # (DPA_XENT_ROWS_FUSED=0: forward statistics only, separate backward row pass)
 _XENT_ROWS_FUSED = os.environ.get("DPA_XENT_ROWS_FUSED", "1") != "0"
 
-# fused CE backward: the weight-gradient kernel computes softmax only and the target one-hot
-# goes in as a sorted scatter (DPA_XENT_ONEHOT_SCATTER=0: in the kernel, per logit)
-_XENT_ONEHOT_SCATTER = os.environ.get("DPA_XENT_ONEHOT_SCATTER", "1") != "0"
+# fused CE backward, DPA_XENT_ONEHOT_SCATTER=1: the weight-gradient kernel computes softmax only
+# and the target one-hot goes in as a sorted scatter. Off by default: the kernel saves 0.35
+# ms/step but the scatter and the bias index_add cost 1.7 (profiles/xent_onehot_scatter_ab_r4.txt)
+_XENT_ONEHOT_SCATTER = os.environ.get("DPA_XENT_ONEHOT_SCATTER", "0") == "1"
 
 # fused CE: forward also emits the unscaled input gradient (DPA_XENT_FUSED_DX=0: separate dx pass)
 _XENT_FUSED_DX = os.environ.get("DPA_XENT_FUSED_DX", "1") != "0"

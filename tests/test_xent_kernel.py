@@ -48,6 +48,11 @@ def test_lxent_fwd_bwd(N, V, E, with_bias):
     torch.testing.assert_close(dW, Wr.grad, rtol=2e-2, atol=1e-2 * Wr.grad.abs().max().item())
     if with_bias:
         torch.testing.assert_close(db, br.grad, rtol=2e-2, atol=1e-2 * br.grad.abs().max().item())
+    # the opt-in form: softmax-only weight-gradient kernel + sorted one-hot scatter
+    _, dW2, db2 = ext.lxent_bwd(g, x, W, b, tgt, lse, False, True, with_bias, onehot_scatter=True)
+    torch.testing.assert_close(dW2, Wr.grad, rtol=2e-2, atol=1e-2 * Wr.grad.abs().max().item())
+    if with_bias:
+        torch.testing.assert_close(db2, br.grad, rtol=2e-2, atol=1e-2 * br.grad.abs().max().item())
 
 
 def test_linear_cross_entropy_autograd_matches_torch():

@@ -1247,9 +1247,9 @@ class DiffusionTrainLoop(TrainLoop):
         vals = torch.stack([(entries[0][2][i] if len(entries) == 1 else torch.cat([e[2][i] for e in entries]))
                             .float() * (w if k == "loss" else 1.0) for i, k in enumerate(keys)])
         q = (4 * t // T).clamp_(0, 3)
-        onehot = torch.nn.functional.one_hot(q, 4).float()                    # [N, 4]
-        qsum = vals @ onehot                                                    # [K, 4]
-        qcnt = onehot.sum(0)                                                    # [4]
+        # bucket sums by scatter (a [K,N]x[N,4] matmul here was the schedule's one library GEMM)
+        qsum = vals.new_zeros(len(keys), 4).index_add_(1, q, vals)             # [K, 4]
+        qcnt = vals.new_zeros(4).index_add_(0, q, torch.ones_like(vals[0]))    # [4]
         n = len(entries)
         means = vals.view(len(keys), n, -1).mean(2).sum(1)                     # sum of chunk means
         for i, k in enumerate(keys):
