@@ -67,8 +67,10 @@ def parse():
     ap.add_argument("--model", default="diffuseq")
     ap.add_argument("--reference-equivalent", action="store_true")
     ap.add_argument("--precision", default=None)
-    ap.add_argument("--bucket-cap-mb", type=float, default=32.0)
-    ap.add_argument("--first-bucket-mb", type=float, default=4.0)
+    # 0 = measured at startup on the job's process group (parallel/ddp.py tune_bucket_sizes);
+    # world 1 has no reduction and keeps 32 / 4
+    ap.add_argument("--bucket-cap-mb", type=float, default=0.0)
+    ap.add_argument("--first-bucket-mb", type=float, default=0.0)
     ap.add_argument("--zero1", type=int, default=0, help="ZeRO-1 sharded optimizer (N > 1)")
     ap.add_argument("--grad-wire", default="fp32", choices=["fp32", "bf16"])
     ap.add_argument("--data-workers", type=int, default=2)
@@ -343,6 +345,10 @@ def main():
     }
     if engine == "native":
         out["config"]["bucket_mb"] = loop.ddp_model.bucket_sizes_mb()
+        if loop.ddp_model.bucket_tune is not None:
+            out["config"]["bucket_tune"] = {"cap_mb": loop.ddp_model.bucket_cap_mb,
+                                            "first_mb": loop.ddp_model.first_bucket_mb,
+                                            "sweep": loop.ddp_model.bucket_tune}
         nat = getattr(loop.ddp_model, "_native", None)
         out["config"]["comm"] = ("reducer-owned RCCL communicator, priority %d stream" % nat.stream_priority()
                                  if nat is not None and nat.direct() else

@@ -14,7 +14,9 @@ implements the same protocol for the single-GPU multi-rank test transport.
 * Bucket sizes are chosen for point-to-point xGMI rings, not NVSwitch: a small
   first bucket (default 4 MiB) so RCCL starts while backward is still deep in
   the network, then ~32 MiB buckets - large enough to saturate a ring's links,
-  small enough to overlap.  (reference: ``bucket_cap_mb=128``.)
+  small enough to overlap.  (reference: ``bucket_cap_mb=128``.)  ``bucket_cap_mb <= 0``
+  measures them instead (:func:`tune_bucket_sizes`: an all-reduce bandwidth sweep on the
+  job's own process group at startup, the same decision on every rank).
 * Readiness: a post-accumulate-grad hook per parameter decrements its bucket's
   pending counter (autograd runs it once per backward per leaf, after all uses,
   even when a fused wgrad GEMM accumulated the gradient in place and returned
@@ -110,6 +112,52 @@ def plan_buckets(space, cap_mb, first_mb):
     return buckets
 
 
+def tune_bucket_sizes(numel, *, process_group=None, device=None, sizes_mb=(2, 4, 8, 16, 32, 64, 128),
+                      min_buckets=4, frac=0.9, iters=5):
+    """Bucket sizes MEASURED on this job's links (``bucket_cap_mb <= 0``): the
+    all-reduce bus bandwidth of the process group at each size in ``sizes_mb``, timed on every
+    rank and MAX-reduced so all ranks take the same decision.  The cap is the smallest size
+    within ``frac`` of the best bandwidth (a bigger bucket only delays the first launch and the
+    overlap), at most 1/``min_buckets`` of the gradients (so the reduction still overlaps the
+    backward); the first bucket is the smallest size within half the best bandwidth, at most
+    the cap.  On point-to-point xGMI the knee sits where one ring step's payload stops being
+    latency-bound, which depends on the ring count RCCL picks - hence measured, not assumed.
+    Returns ``(cap_mb, first_mb, table)``; ``(32, 4, None)`` without a multi-rank group."""
+    import time
+    if not (dist.is_available() and dist.is_initialized()) or dist.get_world_size(process_group) < 2:
+        return 32.0, 4.0, None
+    world = dist.get_world_size(process_group)
+    backend = dist.get_backend(process_group)
+    dev = device if (backend == "nccl" and device is not None and device.type == "cuda") else torch.device("cpu")
+    grad_mb = numel * 4 / _MiB
+    sizes = [mb for mb in sizes_mb if mb <= max(sizes_mb[0], grad_mb)]
+    times = []
+    for mb in sizes:
+        x = torch.ones(int(mb * _MiB) // 4, dtype=torch.float32, device=dev)
+        dist.all_reduce(x, group=process_group)  # warm: channel / buffer setup outside the timing
+        if dev.type == "cuda":
+            torch.cuda.synchronize(dev)
+        t = time.perf_counter()
+        for _ in range(iters):
+            dist.all_reduce(x, group=process_group)
+        if dev.type == "cuda":
+            torch.cuda.synchronize(dev)
+        times.append((time.perf_counter() - t) / iters)
+        del x
+    tt = torch.tensor(times, dtype=torch.float64, device=dev)
+    dist.all_reduce(tt, op=dist.ReduceOp.MAX, group=process_group)
+    times = tt.tolist()
+    bw = [mb * _MiB * 2 * (world - 1) / world / t / 1e9 for mb, t in zip(sizes, times)]
+    best = max(bw)
+    limit = max(sizes[0], grad_mb / min_buckets)
+    ok = [mb for mb, b in zip(sizes, bw) if b >= frac * best and mb <= limit]
+    cap = float(ok[0] if ok else max([mb for mb in sizes if mb <= limit] or [sizes[0]]))
+    half = [mb for mb, b in zip(sizes, bw) if b >= 0.5 * best and mb <= cap]
+    first = float(half[0] if half else sizes[0])
+    table = [{"mb": mb, "us": round(t * 1e6, 1), "busbw_GBps": round(b, 1)} for mb, t, b in zip(sizes, times, bw)]
+    return cap, first, table
+
+
 class _Bucket:
     __slots__ = ("index", "start", "end", "params", "pending", "work", "launched")
 
@@ -128,6 +176,15 @@ class DDPEngine(nn.Module):
         self.module = module
         self.pg = process_group
         self.distributed = dist.is_available() and dist.is_initialized()
+        self.bucket_tune = None
+        if bucket_cap_mb is None or bucket_cap_mb <= 0:  # "auto": measured on this job's links
+            dev = device if device is not None else next(module.parameters()).device
+            numel = sum(p.numel() for p in module.parameters() if p.requires_grad)
+            bucket_cap_mb, tuned_first, self.bucket_tune = tune_bucket_sizes(
+                numel, process_group=process_group, device=torch.device(dev))
+            if first_bucket_mb is None or first_bucket_mb <= 0:
+                first_bucket_mb = tuned_first
+            first_bucket_mb = min(first_bucket_mb, bucket_cap_mb)
         self.world_size = dist.get_world_size(self.pg) if self.distributed else 1
         self.rank = dist.get_rank(self.pg) if self.distributed else 0
         # (world 1 keeps the sharded machinery - one shard - so it can be exercised alone)
