@@ -664,30 +664,45 @@ static void check_i64(const at::Tensor& t, const char* name) {
               " must be a contiguous int64 HIP tensor");
 }
 
-static std::vector<at::Tensor> xent_rows_fwd(const at::Tensor& lg, int64_t V, const at::Tensor& tgt) {
+// (loss, lse) outputs: the caller's [R] fp32 slices when given (a chunk of the whole
+// batch's vectors: no per-chunk copy), else fresh tensors
+static std::pair<at::Tensor, at::Tensor> xent_rows_outs(const at::Tensor& lg, const c10::optional<at::Tensor>& loss_out,
+                                                        const c10::optional<at::Tensor>& lse_out) {
+  auto f32 = lg.options().dtype(at::kFloat);
+  at::Tensor loss = loss_out.has_value() ? *loss_out : at::empty({lg.size(0)}, f32);
+  at::Tensor lse = lse_out.has_value() ? *lse_out : at::empty({lg.size(0)}, f32);
+  for (const at::Tensor* t : {&loss, &lse})
+    TORCH_CHECK(t->is_cuda() && t->scalar_type() == at::kFloat && t->is_contiguous() && t->numel() == lg.size(0),
+                "loss / lse outputs must be contiguous fp32 [R] HIP tensors");
+  return {loss, lse};
+}
+
+static std::vector<at::Tensor> xent_rows_fwd(const at::Tensor& lg, int64_t V, const at::Tensor& tgt,
+                                             const c10::optional<at::Tensor>& loss_out,
+                                             const c10::optional<at::Tensor>& lse_out) {
   CHECK_DEV(lg); CHECK_BF16(lg); CHECK_CONTIG(lg); CHECK_ALIGNED(lg);
   check_i64(tgt, "target");
   TORCH_CHECK(lg.dim() == 2 && lg.size(1) % 8 == 0 && V > 0 && V <= lg.size(1),
               "logits [R, ld] with ld % 8 == 0 and V <= ld");
   TORCH_CHECK(tgt.numel() == lg.size(0), "target [R]");
   const c10::DeviceGuard guard(lg.device());
-  auto f32 = lg.options().dtype(at::kFloat);
-  at::Tensor loss = at::empty({lg.size(0)}, f32), lse = at::empty({lg.size(0)}, f32);
+  auto [loss, lse] = xent_rows_outs(lg, loss_out, lse_out);
   dpa::launch_xent_rows_fwd(bf_ptr(lg), lg.size(1), (int)V, tgt.data_ptr<int64_t>(), lg.size(0),
                             loss.data_ptr<float>(), lse.data_ptr<float>(), cur_stream());
   return {loss, lse};
 }
 
 // in place: logits -> softmax - onehot (unscaled); returns (loss, lse) (empty list if refused)
-static std::vector<at::Tensor> xent_rows_fwd_grad_(at::Tensor& lg, int64_t V, const at::Tensor& tgt) {
+static std::vector<at::Tensor> xent_rows_fwd_grad_(at::Tensor& lg, int64_t V, const at::Tensor& tgt,
+                                                   const c10::optional<at::Tensor>& loss_out,
+                                                   const c10::optional<at::Tensor>& lse_out) {
   CHECK_DEV(lg); CHECK_BF16(lg); CHECK_CONTIG(lg); CHECK_ALIGNED(lg);
   check_i64(tgt, "target");
   TORCH_CHECK(lg.dim() == 2 && lg.size(1) % 8 == 0 && V > 0 && V <= lg.size(1),
               "logits [R, ld] with ld % 8 == 0 and V <= ld");
   TORCH_CHECK(tgt.numel() == lg.size(0), "target [R]");
   const c10::DeviceGuard guard(lg.device());
-  auto f32 = lg.options().dtype(at::kFloat);
-  at::Tensor loss = at::empty({lg.size(0)}, f32), lse = at::empty({lg.size(0)}, f32);
+  auto [loss, lse] = xent_rows_outs(lg, loss_out, lse_out);
   if (!dpa::launch_xent_rows_fwd_grad(reinterpret_cast<uint16_t*>(lg.data_ptr()), lg.size(1), (int)V,
                                       tgt.data_ptr<int64_t>(), lg.size(0), loss.data_ptr<float>(),
                                       lse.data_ptr<float>(), cur_stream()))
@@ -934,10 +949,14 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         pybind11::arg("dloss"), pybind11::arg("x"), pybind11::arg("W"), pybind11::arg("b"), pybind11::arg("tgt"),
         pybind11::arg("lse"), pybind11::arg("need_dx"), pybind11::arg("need_dw"), pybind11::arg("need_db"),
         pybind11::arg("onehot_scatter") = false);
-  m.def("xent_rows_fwd", &xent_rows_fwd, "row softmax-CE over bf16 logits [R, ld] -> (loss, lse)");
+  m.def("xent_rows_fwd", &xent_rows_fwd, "row softmax-CE over bf16 logits [R, ld] -> (loss, lse)",
+        pybind11::arg("lg"), pybind11::arg("V"), pybind11::arg("tgt"), pybind11::arg("loss_out") = pybind11::none(),
+        pybind11::arg("lse_out") = pybind11::none());
   m.def("xent_rows_bwd_", &xent_rows_bwd_, "in place: logits -> dloss * (softmax - onehot)");
   m.def("xent_rows_fwd_grad_", &xent_rows_fwd_grad_,
-        "in place: logits -> softmax - onehot (unscaled), returns (loss, lse) or [] if the row is too long");
+        "in place: logits -> softmax - onehot (unscaled), returns (loss, lse) or [] if the row is too long",
+        pybind11::arg("lg"), pybind11::arg("V"), pybind11::arg("tgt"), pybind11::arg("loss_out") = pybind11::none(),
+        pybind11::arg("lse_out") = pybind11::none());
   m.def("emb_qsample_fwd", &emb_qsample_fwd,
         "DiffuSeq embedding gather + x_start noise + masked q_sample -> (x_start, x_start bf16, x_t bf16)");
   m.def("emb_qsample_bwd", &emb_qsample_bwd, "scatter-add of the q_sample gradients into dW (fp32)");

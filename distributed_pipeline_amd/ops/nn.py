@@ -1206,14 +1206,12 @@ class _ChunkedLinearXentFn(torch.autograd.Function):
         for s in range(0, N, chunk):
             e = min(N, s + chunk)
             lg = _chunk_logits(x[s:e], wp, bp, allg[s:e] if allg is not None else None)
+            # the row kernels write this chunk's slices of loss / lse directly
             if kept_is_grad:
-                res = ext.xent_rows_fwd_grad_(lg, V, target[s:e])
+                res = ext.xent_rows_fwd_grad_(lg, V, target[s:e], loss[s:e], lse[s:e])
                 assert res, "xent_rows_fwd_grad_ refused the row length"
-                l_c, lse_c = res
             else:
-                l_c, lse_c = ext.xent_rows_fwd(lg, V, target[s:e])
-            loss[s:e].copy_(l_c)
-            lse[s:e].copy_(lse_c)
+                ext.xent_rows_fwd(lg, V, target[s:e], loss[s:e], lse[s:e])
         ctx.allg = allg
         ctx.kept_is_grad = kept_is_grad
         ctx.save_for_backward(x, w16, b16, target, lse, wp, bp)
