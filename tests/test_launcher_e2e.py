@@ -91,3 +91,7 @@ def test_bench_contract_two_ranks_gloo():
     cp = d["comm_probe"]
     assert cp["grad_reduce_all"]["ms"] > 0 and cp["grad_reduce_all"]["buckets"] >= 1
     assert [r["mb"] for r in cp["pg_allreduce"]] == [1, 4] and all(r["busbw_GBps"] > 0 for r in cp["pg_allreduce"])
+    # bucket sizes measured at startup (bench default bucket_cap_mb=0): the cap is a swept size
+    bt = d["config"]["bucket_tune"]
+    assert bt["cap_mb"] in [r["mb"] for r in bt["sweep"]] and bt["first_mb"] <= bt["cap_mb"]
+    assert all(r["busbw_GBps"] > 0 for r in bt["sweep"])
