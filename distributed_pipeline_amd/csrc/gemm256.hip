@@ -1221,7 +1221,10 @@ static WgradPlan wgrad_plan(int T, int N, int K, int nseg = 1) {
         best_p = WgradPlan{s_eff, kps, w == 1};
       }
     }
-    if (wgs > 4 * ncu) break;
+    // search up to 8 rounds of workgroups: a large tile count (GPT-2's 591-tile LM-head
+    // weight gradient) needs 3 splits (1773 workgroups: 6.9 rounds) to avoid a 60%-empty last
+    // round, past the 4-round cap this search used to stop at
+    if (wgs > 8 * ncu) break;
   }
   return best_p;
 }
