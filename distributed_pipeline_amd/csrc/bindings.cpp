@@ -1,6 +1,7 @@
 // Python bindings of the gfx950 kernels (torch tensors -> raw launchers).
 // Every op launches on the *current* HIP stream of the tensor's device, so it
 // composes with torch's stream semantics and with HIP-graph capture.
+#include <cstdlib>
 #include <torch/extension.h>
 #include <ATen/hip/impl/HIPStreamMasqueradingAsCUDA.h>
 #include <c10/core/DeviceGuard.h>
@@ -618,6 +619,33 @@ static void gemm_wgrad(const at::Tensor& dy, const at::Tensor& x, at::Tensor& dW
     dbp = db->data_ptr<float>();
   }
   const c10::DeviceGuard guard(dy.device());
+  // A 128-wide side (DiffuSeq's 128 <-> 768 up / down projections) is not a 256 x 256 tile
+  // shape: the 128-tile kernel then merges its ~170 token splits with device-scope fp32
+  // atomics, which run at the memory side (0.39 ms for a 0.05 TFLOP gradient).  Zero-padding
+  // that side to 256 (a [T, 256] copy) runs it on the 256 x 256 split-K kernel with its
+  // workspace merge instead; the padded half of the result is discarded
+  // (DPA_WGRAD_PAD=0: the 128-tile kernel).
+  static const bool pad_ok = [] {
+    const char* e = std::getenv("DPA_WGRAD_PAD");
+    return !e || std::atoi(e) != 0;
+  }();
+  const int Np = (N + 255) / 256 * 256, Kp = (K + 255) / 256 * 256;
+  if (pad_ok && (Np != N || Kp != K) && N % 64 == 0 && K % 64 == 0 && T % 256 == 0 && T >= 256 &&
+      (int64_t)Np * Kp <= 2 * (int64_t)N * K) {
+    at::Tensor dyp = Np == N ? dy : at::constant_pad_nd(dy, {0, Np - N});
+    at::Tensor xp = Kp == K ? x : at::constant_pad_nd(x, {0, Kp - K});
+    at::Tensor dWp = at::zeros({Np, Kp}, dW.options());
+    at::Tensor dbp2 = dbp ? at::zeros({Np}, dW.options()) : at::Tensor();
+    const int64_t wsp = dpa::gemm256_wgrad_workspace_floats(T, Np, Kp);
+    at::Tensor wsb = at::empty({wsp}, dW.options());
+    if (dpa::launch_gemm256_wgrad(bf_ptr(dyp), bf_ptr(xp), dWp.data_ptr<float>(),
+                                  dbp ? dbp2.data_ptr<float>() : nullptr, T, Np, Kp, cur_stream(),
+                                  wsp ? wsb.data_ptr<float>() : nullptr)) {
+      dW.add_(dWp.narrow(0, 0, N).narrow(1, 0, K));
+      if (dbp) db->add_(dbp2.narrow(0, 0, N));
+      return;
+    }
+  }
   // split-K merge workspace (stream-ordered caching-allocator block, freed after the launch)
   const int64_t wsn = dpa::gemm256_wgrad_workspace_floats(T, N, K);
   at::Tensor ws = at::empty({wsn}, dW.options());

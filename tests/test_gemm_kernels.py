@@ -50,7 +50,9 @@ def test_gemm_nn_dgrad(T, N, K, tile):
 
 
 @pytest.mark.parametrize("T,N,K", [(128, 128, 128), (4096, 768, 768), (8192, 2304, 768), (1024, 768, 3072),
-                                   (640, 256, 256), (256, 512, 768), (32768, 768, 3072)])
+                                   (640, 256, 256), (256, 512, 768), (32768, 768, 3072),
+                                   # a 128-wide side: zero-padded onto the 256 x 256 split-K kernel
+                                   (32768, 768, 128), (8192, 128, 768), (512, 384, 128)])
 def test_gemm_wgrad_accumulates(T, N, K, tile):
     torch.manual_seed(0)
     dy = torch.randn(T, N, device="cuda").bfloat16()
