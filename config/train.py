@@ -110,9 +110,9 @@ class PerfSettings(S):
     ddp_engine: Choice("native", "torch") \
         = _("native", "native = flat-bucket RCCL engine (+fused optimizer); torch = torch DDP + torch AdamW (reference-equivalent).")
     ddp_bucket_cap_mb: float \
-        = _(32.0, "All-reduce bucket size (MiB) for the native engine; 0 = measured at startup on the job's process group (all-reduce bandwidth sweep).")
+        = _(0.0, "All-reduce bucket size (MiB) for the native engine; 0 (default) = measured at startup on the job's process group (all-reduce bandwidth sweep; 32 at world 1).")
     ddp_first_bucket_mb: float \
-        = _(4.0, "First (last-layer) bucket size (MiB) so communication starts early; 0 = measured (with ddp_bucket_cap_mb=0).")
+        = _(0.0, "First (last-layer) bucket size (MiB) so communication starts early; 0 (default) = measured (4 at world 1).")
     grad_reduce_dtype: Choice("fp32", "bf16") \
         = _("fp32", "Dtype on the wire for the gradient all-reduce.")
     shard_optimizer: bool \
