@@ -728,7 +728,9 @@ class TrainLoop:
             for k, i in enumerate(starts):
                 with self._range("forward"):
                     losses = self._common_forward(batch, i, self.exec_microbatch)
-                self.log_loss_dict(mode="train", losses=losses)
+                join = getattr(getattr(self, "diffusion", None), "join_side", None)
+                if join is None:
+                    self.log_loss_dict(mode="train", losses=losses)
                 self.loss_scale = self._chunk_loss_scale(i, min(n, i + self.exec_microbatch), n)
                 if defer is not None:
                     defer.active = k < len(starts) - 1
@@ -736,6 +738,10 @@ class TrainLoop:
                         defer.flush()
                 with self._range("backward"):
                     self.backward_from_losses(losses)
+                if join is not None:
+                    # a side-stream term (the logged nll) overlaps the backward: log after it
+                    join()
+                    self.log_loss_dict(mode="train", losses=losses)
         except BaseException:
             if defer is not None:
                 defer.drop()
@@ -1260,6 +1266,9 @@ class DiffusionTrainLoop(TrainLoop):
         buf, self._loss_log_buf = self._loss_log_buf, None
         if not buf:
             return
+        join = getattr(getattr(self, "diffusion", None), "join_side", None)
+        if join is not None:
+            join()  # buffered terms may come from a side stream (DPA_NLL_SIDE)
         groups = {}
         for keys, t, w, vals in buf:  # equal chunk sizes batch together (the usual case)
             groups.setdefault((keys, t.shape[0]), []).append((t, w, vals))
