@@ -58,13 +58,21 @@ __device__ __forceinline__ f32x2 phi_cdf2(f32x2 z, f32x2& e) {
   return sg * 0.5f + 0.5f;
 }
 
+// tanh(z) = 1 - 2 / (exp(2z) + 1): one v_exp and one v_rcp (the libm tanhf is a branchy
+// polynomial); exp overflow gives 1, underflow -1; absolute error ~1e-7.  Below |z| = 2^-8
+// that absolute error would be a visible relative one, and tanh(z) = z to 5e-6 there.
+__device__ __forceinline__ float tanh_fast(float z) {
+  const float t = 1.f - 2.f * __builtin_amdgcn_rcpf(fexp2(z * 2.8853900817779268f) + 1.f);
+  return fabsf(z) < 0.00390625f ? z : t;
+}
+
 template <int ACT>
 __device__ __forceinline__ f32x2 act2(f32x2 z) {
   if constexpr (ACT == 1) {
     f32x2 e;
     return z * phi_cdf2(z, e);
   } else if constexpr (ACT == 2) {
-    return f32x2{tanhf(z.x), tanhf(z.y)};
+    return f32x2{tanh_fast(z.x), tanh_fast(z.y)};
   } else if constexpr (ACT == 3) {
     const f32x2 d = {1.f + fexp(-z.x), 1.f + fexp(-z.y)};
     return z * f32x2{__builtin_amdgcn_rcpf(d.x), __builtin_amdgcn_rcpf(d.y)};
@@ -82,7 +90,7 @@ __device__ __forceinline__ f32x2 act_dact2(f32x2 z, f32x2& d) {
     d = z * 0.39894228040143268f * e + c;
     return z * c;
   } else if constexpr (ACT == 2) {
-    const f32x2 y = {tanhf(z.x), tanhf(z.y)};
+    const f32x2 y = {tanh_fast(z.x), tanh_fast(z.y)};
     d = 1.f - y * y;
     return y;
   } else if constexpr (ACT == 3) {
@@ -119,7 +127,7 @@ __device__ __forceinline__ f32x2 dact2(f32x2 a) {
 __device__ __forceinline__ float act_apply(float z, int act) {
   switch (act) {
     case 1: return gelu_f(z);
-    case 2: return tanhf(z);
+    case 2: return tanh_fast(z);
     case 3: return z * __builtin_amdgcn_rcpf(1.f + fexp(-z));
     default: return z;
   }
