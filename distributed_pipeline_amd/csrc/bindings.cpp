@@ -321,6 +321,25 @@ static std::vector<at::Tensor> add_ln_bwd(const at::Tensor& dout, const at::Tens
 static int64_t ln_bwd_partials(int64_t R, int64_t D) { return dpa::ln_bwd_ws_floats(R, (int)D); }
 
 // dg += colsum, db += colsum (, dyb += colsum) of partials accumulated by add_ln_bwd(part_buf=...)
+// (dpos [L][H] fp32 or empty, dtemb [B][H] fp32 or empty) of d [B * L][H] bf16 in one read;
+// empty list if the shape is not supported
+static std::vector<at::Tensor> seq_pos_sums(const at::Tensor& d, int64_t L, bool need_pos, bool need_temb) {
+  CHECK_DEV(d); CHECK_BF16(d); CHECK_CONTIG(d);
+  TORCH_CHECK(d.dim() == 2 && L > 0 && d.size(0) % L == 0, "d [B * L, H]");
+  const int64_t B = d.size(0) / L, H = d.size(1);
+  const c10::DeviceGuard guard(d.device());
+  auto f32 = d.options().dtype(at::kFloat);
+  at::Tensor dpos = need_pos ? at::zeros({L, H}, f32) : at::Tensor();
+  at::Tensor dtemb = need_temb ? at::empty({B, H}, f32) : at::Tensor();
+  at::Tensor part = need_pos ? at::empty({(int64_t)dpa::seq_pos_groups((int)B) * L * H}, f32) : at::Tensor();
+  if (!dpa::launch_seq_pos_sums(reinterpret_cast<const uint16_t*>(d.data_ptr()), (int)B, (int)L, (int)H,
+                                need_pos ? dpos.data_ptr<float>() : nullptr,
+                                need_temb ? dtemb.data_ptr<float>() : nullptr,
+                                need_pos ? part.data_ptr<float>() : nullptr, cur_stream()))
+    return {};
+  return {dpos, dtemb};
+}
+
 static void ln_colreduce(const at::Tensor& part, int64_t R, int64_t D, at::Tensor& dg, at::Tensor& db,
                          c10::optional<at::Tensor> dyb) {
   CHECK_DEV(part); CHECK_F32(part); CHECK_CONTIG(part); CHECK_F32(dg); CHECK_F32(db);
@@ -977,6 +996,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         pybind11::arg("dloss"), pybind11::arg("x"), pybind11::arg("W"), pybind11::arg("b"), pybind11::arg("tgt"),
         pybind11::arg("lse"), pybind11::arg("need_dx"), pybind11::arg("need_dw"), pybind11::arg("need_db"),
         pybind11::arg("onehot_scatter") = false);
+  m.def("seq_pos_sums", &seq_pos_sums, "(sum over b, sum over l) of a [B*L, H] bf16 gradient in one read",
+        pybind11::arg("d"), pybind11::arg("L"), pybind11::arg("need_pos"), pybind11::arg("need_temb"));
   m.def("xent_rows_fwd", &xent_rows_fwd, "row softmax-CE over bf16 logits [R, ld] -> (loss, lse)",
         pybind11::arg("lg"), pybind11::arg("V"), pybind11::arg("tgt"), pybind11::arg("loss_out") = pybind11::none(),
         pybind11::arg("lse_out") = pybind11::none());

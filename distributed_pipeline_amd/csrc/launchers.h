@@ -69,6 +69,11 @@ bool launch_add_ln_bwd(const uint16_t* dout, const uint16_t* hsave, const float*
                        const uint16_t* hcopy = nullptr);  // ... and hcopy the guarded h copy
 // the deferred second stage of part_mode 1/2 (R = the rows of each summed micro-batch)
 bool launch_ln_colreduce(const float* part, int64_t R, int D, float* dg, float* db, float* dyb, hipStream_t s);
+// dpos[L][H] (zeroed; += sum over b) and dtemb[B][H] (= sum over l) of a [B][L][H] bf16 gradient in
+// one read; part: seq_pos_groups(B) * L * H floats of workspace.  L in {64, 128, 256}, H % 64 == 0.
+int seq_pos_groups(int B);
+bool launch_seq_pos_sums(const uint16_t* d, int B, int L, int H, float* dpos, float* dtemb, float* part,
+                         hipStream_t s);
 bool launch_colsum_acc(const float* part, int rows, int cols, float* dst, hipStream_t s);
 // fp32 workspace (floats) the small-R two-stage column sums of launch_add_ln_bwd use (0: none)
 int64_t ln_bwd_ws_floats(int64_t R, int D);

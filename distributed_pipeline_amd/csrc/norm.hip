@@ -661,6 +661,62 @@ bool launch_colsum_acc(const float* part, int rows, int cols, float* dst, hipStr
   return true;
 }
 
+// Position- and sequence-sums of a [B][L][H] bf16 gradient in ONE read (the DiffuSeq input
+// block's position-embedding and time-embedding gradients; two ATen reductions read it twice):
+//   dtemb[b][h] = sum_l d[b][l][h]      (written here)
+//   part[g][l][h] = sum_{b in group g} d[b][l][h]   (summed over g by colsum_acc afterwards)
+// Workgroup = 16 sequences x 64 columns; thread (c, q) sums rows l = q + 4k of column c, so a
+// wave reads 64 contiguous columns of one row; LQ = L / 4 position partials live in registers.
+template <int LQ>
+__global__ void __launch_bounds__(256) seq_pos_partial_kernel(const bf16_t* __restrict__ d, int B, int H,
+                                                              float* __restrict__ dtemb,
+                                                              float* __restrict__ part) {
+  constexpr int L = 4 * LQ, BG = 16;
+  __shared__ float red[4][64];
+  const int c = blockIdx.y * 64 + (threadIdx.x & 63), q = threadIdx.x >> 6;
+  const int g = blockIdx.x, b0 = g * BG;
+  float pacc[LQ];
+#pragma unroll
+  for (int k = 0; k < LQ; ++k) pacc[k] = 0.f;
+  for (int bi = 0; bi < BG && b0 + bi < B; ++bi) {
+    const bf16_t* row = d + ((int64_t)(b0 + bi) * L + q) * H + c;
+    float sb = 0.f;
+#pragma unroll
+    for (int k = 0; k < LQ; ++k) {
+      const float v = bf2f(row[(int64_t)k * 4 * H]);
+      pacc[k] += v;
+      sb += v;
+    }
+    red[q][threadIdx.x & 63] = sb;
+    __syncthreads();
+    if (q == 0 && dtemb)
+      dtemb[(int64_t)(b0 + bi) * H + c] = red[0][threadIdx.x] + red[1][threadIdx.x] + red[2][threadIdx.x] +
+                                          red[3][threadIdx.x];
+    __syncthreads();
+  }
+  if (part) {
+    float* pg = part + (int64_t)g * L * H + c;
+#pragma unroll
+    for (int k = 0; k < LQ; ++k) pg[(int64_t)(q + 4 * k) * H] = pacc[k];
+  }
+}
+
+int seq_pos_groups(int B) { return (B + 15) / 16; }
+
+bool launch_seq_pos_sums(const uint16_t* d, int B, int L, int H, float* dpos, float* dtemb, float* part,
+                         hipStream_t s) {
+  if (H % 64 || B <= 0 || (L != 64 && L != 128 && L != 256)) return false;
+  const dim3 grid((unsigned)seq_pos_groups(B), (unsigned)(H / 64));
+  float* pp = dpos ? part : nullptr;
+  switch (L) {
+    case 64: hipLaunchKernelGGL(seq_pos_partial_kernel<16>, grid, dim3(256), 0, s, (const bf16_t*)d, B, H, dtemb, pp); break;
+    case 128: hipLaunchKernelGGL(seq_pos_partial_kernel<32>, grid, dim3(256), 0, s, (const bf16_t*)d, B, H, dtemb, pp); break;
+    default: hipLaunchKernelGGL(seq_pos_partial_kernel<64>, grid, dim3(256), 0, s, (const bf16_t*)d, B, H, dtemb, pp); break;
+  }
+  if (dpos) launch_colsum_acc(part, seq_pos_groups(B), L * H, dpos, s);  // dpos (zeroed) += sum_g part[g]
+  return true;
+}
+
 bool launch_add_ln_bwd(const uint16_t* dout, const uint16_t* hsave, const float* mean,
                        const float* rstd, const uint16_t* g, uint16_t* dres, uint16_t* dy, float* dyb,
                        float* dg, float* db, int64_t R, int D, float p, uint32_t seed, uint32_t off,

@@ -929,11 +929,21 @@ class _AddLNExFn(torch.autograd.Function):
         dpos = dtemb = None
         if need_dy:
             H = dy.shape[-1]
-            d3 = dy.view(-1, L, H)
-            if has_pos and ng[2]:
-                dpos = torch.sum(d3, 0, dtype=torch.float32).to(ctx.pt_dtypes[0])
-            if has_temb and ng[3]:
-                dtemb = torch.sum(d3, 1, dtype=torch.float32).to(ctx.pt_dtypes[1])
+            want_p, want_t = bool(has_pos and ng[2]), bool(has_temb and ng[3])
+            # both sums from one read of dy (csrc/norm.hip seq_pos_partial_kernel)
+            sums = (get_ext().seq_pos_sums(dy, int(L), want_p, want_t)
+                    if (want_p or want_t) and hasattr(get_ext(), "seq_pos_sums") else [])
+            if sums:
+                if want_p:
+                    dpos = sums[0].to(ctx.pt_dtypes[0])
+                if want_t:
+                    dtemb = sums[1].to(ctx.pt_dtypes[1])
+            else:
+                d3 = dy.view(-1, L, H)
+                if want_p:
+                    dpos = torch.sum(d3, 0, dtype=torch.float32).to(ctx.pt_dtypes[0])
+                if want_t:
+                    dtemb = torch.sum(d3, 1, dtype=torch.float32).to(ctx.pt_dtypes[1])
         return ((dy if ng[0] else None), (dres if has_res else None), dpos, dtemb, dw, db,
                 None, None, None, None, None, None, None, None)
 

@@ -302,3 +302,17 @@ def test_gpt2_input_embedding_dropout_then_ln():
                                rtol=2e-2, atol=2e-2)
     x.float().sum().backward()
     torch.testing.assert_close(e.grad.float(), keep / (1 - p), rtol=1e-2, atol=1e-2)
+
+
+@pytest.mark.parametrize("B,L,H", [(64, 128, 768), (5, 64, 128), (17, 256, 256)])
+def test_seq_pos_sums_match_torch(B, L, H):
+    """csrc/norm.hip seq_pos_sums: both reductions of the input block's gradient in one read."""
+    from distributed_pipeline_amd.ops._ext import get_ext
+    torch.manual_seed(0)
+    d = torch.randn(B * L, H, device="cuda").bfloat16()
+    dpos, dtemb = get_ext().seq_pos_sums(d, L, True, True)
+    d3 = d.float().view(B, L, H)
+    torch.testing.assert_close(dpos, d3.sum(0), rtol=1e-4, atol=1e-3)
+    torch.testing.assert_close(dtemb, d3.sum(1), rtol=1e-4, atol=1e-3)
+    only_t = get_ext().seq_pos_sums(d, L, False, True)
+    torch.testing.assert_close(only_t[1], d3.sum(1), rtol=1e-4, atol=1e-3)
