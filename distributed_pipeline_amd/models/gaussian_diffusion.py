@@ -195,7 +195,7 @@ class GaussianDiffusion:
         terms = {"mse": mse}
         decoder_nll = self.token_discrete_loss(x_start16, net, input_ids)
         if compute_nll:
-            side = _nll_side_stream(dev)
+            side = _nll_side_stream(dev) if getattr(self, "nll_side_ok", False) else None
             if side is not None and torch.is_grad_enabled():
                 # the logged nll needs nothing from the backward and nothing of it needs the
                 # nll: it runs on a side stream, joined before the step logs (join_side())
@@ -278,13 +278,18 @@ _NLL_SIDE = {}
 def _nll_side_stream(dev):
     """The side stream of the logged nll, or None (DPA_NLL_SIDE=0, CPU, graph capture).
     Overlapping the backward, the forward-only CE sweep over the vocabulary takes CUs while the
-    memory-bound kernels run: 164.9 vs 165.6 ms/step (profiles/nll_side_stream_ab_r4.txt)."""
+    memory-bound kernels run: 164.9 vs 165.6 ms/step (profiles/nll_side_stream_ab_r4.txt).  Only
+    a whole-batch step uses it (the trainer sets ``nll_side_ok``): per 64-sample chunk of the
+    reference schedule it cost 8-10% (222 -> 241-246 ms/step)."""
     import os
-    if (os.environ.get("DPA_NLL_SIDE", "1") != "1" or dev.type != "cuda"
+    if (os.environ.get("DPA_NLL_SIDE", "0") != "1" or dev.type != "cuda"
             or torch.cuda.is_current_stream_capturing()):  # a captured step logs after replay
         return None
     if dev not in _NLL_SIDE:
-        _NLL_SIDE[dev] = torch.cuda.Stream(device=dev)
+        # from the high-priority pool: a stream taken from the default pool shifts which pool
+        # streams (and so which hardware queues) the overlapped schedule's streams get later in
+        # the process - measured 222 -> 240 ms/step on the reference schedule
+        _NLL_SIDE[dev] = torch.cuda.Stream(device=dev, priority=-1)
     return _NLL_SIDE[dev]
 
 
