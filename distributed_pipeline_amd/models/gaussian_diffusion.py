@@ -286,10 +286,9 @@ def _nll_side_stream(dev):
             or torch.cuda.is_current_stream_capturing()):  # a captured step logs after replay
         return None
     if dev not in _NLL_SIDE:
-        # from the high-priority pool: a stream taken from the default pool shifts which pool
-        # streams (and so which hardware queues) the overlapped schedule's streams get later in
-        # the process - measured 222 -> 240 ms/step on the reference schedule
-        _NLL_SIDE[dev] = torch.cuda.Stream(device=dev, priority=-1)
+        # a pool stream: it shifts which pool streams (hardware queues) an overlapped schedule
+        # run later in the process gets (222 -> 240 ms/step; a high-priority stream: 347)
+        _NLL_SIDE[dev] = torch.cuda.Stream(device=dev)
     return _NLL_SIDE[dev]
 
 
