@@ -103,6 +103,9 @@ def setup_dist(backend=None, silent=False):
                               store=dist.PrefixStore(f"dpa/attempt_{attempt}", store))
             if use_gpu:
                 torch.cuda.set_device(dev())
+                # the step's side streams first, before RCCL and torch's stream pool take
+                # the device's hardware queues (distributed_pipeline_amd/runtime/streams.py)
+                claim_stream_plan(dev())
                 if backend == "nccl":
                     kwargs["device_id"] = dev()
                 bind_cpus_to_gpu(int(os.environ["LOCAL_RANK"]))
@@ -127,6 +130,18 @@ def setup_dist(backend=None, silent=False):
     if int(os.getenv("LOCAL_RANK")) == 0 and not silent:
         print("<INFO> torch.distributed is not available, skipping distributed setting..")
     return False
+
+
+def claim_stream_plan(device):
+    """Create ``device``'s stream plan now (hardware queues are handed out in creation order);
+    a no-op without the native package or on CPU."""
+    try:
+        from distributed_pipeline_amd.runtime.streams import StreamPlan
+    except ImportError:  # pragma: no cover
+        return None
+    if torch.device(device).type != "cuda":
+        return None
+    return StreamPlan.for_device(device)
 
 
 def _parse_cpulist(text):

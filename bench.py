@@ -27,7 +27,11 @@ steps/s, samples/s and tokens/s are reported alongside.
 
 ``--reference-equivalent`` runs the reference's configuration instead (fp32,
 torch DistributedDataParallel with bucket_cap_mb=128, torch AdamW, eager
-PyTorch model) - the measured baseline in BASELINE.md.
+PyTorch model) - the measured baseline in BASELINE.md.  ``--stock`` keeps every op
+on stock PyTorch / ATen (hipBLASLt GEMMs, SDPA attention, ATen LayerNorm and CE:
+``use_hip_kernels=False``); with ``--reference-equivalent --precision bf16 --stock``
+that is the like-for-like bf16 baseline (``vs_stock_bf16``), at the reference's
+micro-batch 64 by default or fused with ``--exec-microbatch 0`` (auto).
 """
 import argparse
 import json
@@ -49,8 +53,9 @@ def parse():
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--batch-size", type=int, default=2048)
     ap.add_argument("--microbatch", type=int, default=64)
-    ap.add_argument("--exec-microbatch", type=int, default=0,
-                    help="samples per executed fwd/bwd: 0 = auto (whole batch), -1 = microbatch (reference schedule)")
+    ap.add_argument("--exec-microbatch", type=int, default=None,
+                    help="samples per executed fwd/bwd: 0 = auto (whole batch), -1 = microbatch (reference "
+                         "schedule); default auto, or -1 with --reference-equivalent")
     ap.add_argument("--ref-warmup", type=int, default=2,
                     help="untimed reference-schedule steps first (its two extra HIP streams grow their own "
                          "allocator pools in the first steps)")
@@ -66,6 +71,8 @@ def parse():
     ap.add_argument("--config-name", default="bert-base-uncased")
     ap.add_argument("--model", default="diffuseq")
     ap.add_argument("--reference-equivalent", action="store_true")
+    ap.add_argument("--stock", action="store_true",
+                    help="stock PyTorch ops only (use_hip_kernels=False): the like-for-like baseline")
     ap.add_argument("--precision", default=None)
     # 0 = measured at startup on the job's process group (parallel/ddp.py tune_bucket_sizes);
     # world 1 has no reduction and keeps 32 / 4
@@ -168,18 +175,19 @@ def main():
     dev = dist_util.dev()
     if dev.type == "cuda":
         torch.cuda.set_device(dev)
+        dist_util.claim_stream_plan(dev)  # world 1: before anything else takes a queue
 
     ref = a.reference_equivalent
     precision = a.precision or ("fp32" if ref else "bf16")
     engine = "torch" if ref else "native"
-    exec_mb = -1 if ref else a.exec_microbatch
+    exec_mb = a.exec_microbatch if a.exec_microbatch is not None else (-1 if ref else 0)
 
     logdir = tempfile.mkdtemp(prefix="dpa_bench_")
     logger.configure(dir=logdir, format_strs=["log"] if rank == 0 else [])
     seed_all(102)
     settings = dict(model=a.model, precision=precision, config_name=a.config_name,
                     seq_len=a.seq_len, vocab_size=30522 if a.model != "gpt2" else 50257,
-                    hidden_dim=128, hidden_t_dim=128, dropout=0.1)
+                    hidden_dim=128, hidden_t_dim=128, dropout=0.1, use_hip_kernels=not a.stock)
     model = create_model_from_config(**settings).to(dev)
     n_params = sum(p.numel() for p in model.parameters())
     data = load_data_from_args("train", "synthetic", a.batch_size, deterministic=False, loop=True,
@@ -304,16 +312,20 @@ def main():
     steps_per_s = a.steps / elapsed
     value = steps_per_s * world
     samples_per_s = steps_per_s * a.batch_size * world
-    baseline = None
+    baseline = stock = None
     bpath = os.path.join(HERE, "baseline_measured.json")
     headline = (a.model == "diffuseq" and a.config_name == "bert-base-uncased" and a.seq_len == 128
                 and a.batch_size == 2048 and a.microbatch == 64)
-    if os.path.exists(bpath) and not ref and headline:
+    if os.path.exists(bpath) and not ref and not a.stock and headline:
         with open(bpath) as f:
             b = json.load(f)
         per_gpu = b.get("reference_equivalent_steps_per_sec_per_gpu")
         if per_gpu:
             baseline = per_gpu * world
+        # the best stock-PyTorch bf16 run of the reference's trainer (micro-batch 64 or fused)
+        sb = b.get("stock_bf16_steps_per_sec_per_gpu")
+        if sb:
+            stock = sb * world
     out = {
         # the BASELINE.json metric for the headline config; other configs say what they ran
         "metric": METRIC if headline else (f"train steps/sec (whole node), {a.model}/{a.config_name} "
@@ -327,13 +339,14 @@ def main():
         "higher_is_better": True,
         "scaling": "weak",
         "vs_baseline": round(value / baseline, 3) if baseline else None,
+        "vs_stock_bf16": round(value / stock, 3) if stock else None,
         "dtype": "bf16" if precision == "bf16" else "fp32",
         "data": "synthetic (random token ids, random src/trg split; random-init weights)",
         "config": {"model": "DiffuSeq-base" if a.config_name == "bert-base-uncased" else a.config_name,
                    "global_batch": a.batch_size * world, "per_gpu_batch": a.batch_size,
                    "microbatch": a.microbatch, "exec_microbatch": exec_used,
                    "seq_len": a.seq_len, "parallelism": f"dp{world}",
-                   "engine": engine, "params": n_params},
+                   "engine": engine, "params": n_params, "stock_ops": bool(a.stock)},
         "optimizer_steps_per_sec": round(steps_per_s, 4),
         "samples_per_sec": round(samples_per_s, 1),
         "tokens_per_sec": round(samples_per_s * a.seq_len, 1),
@@ -378,6 +391,12 @@ def main():
         ms = torch.cuda.memory_stats(dev)
         out["hbm_headroom_at_peak_gb"] = round((total - torch.cuda.max_memory_reserved(dev)) / 2**30, 1)
         out["alloc_retries"] = int(ms.get("num_alloc_retries", 0))
+    if dev.type == "cuda":  # the step's stream plan (runtime/streams.py): role -> stream id
+        from distributed_pipeline_amd.runtime.streams import StreamPlan
+        out["streams"] = StreamPlan.for_device(dev).describe()
+        nat = getattr(getattr(loop, "ddp_model", None), "_native", None)
+        if nat is not None and hasattr(nat, "comm_stream") and nat.direct():
+            out["streams"]["handles"]["comm"] = hex(nat.comm_stream())
     if rank == 0:
         out["topology"] = topology()
     if rank == 0:

@@ -10,6 +10,8 @@ Micro-batches are then device slices (views): no per-micro-batch transfers remai
 """
 import torch
 
+from distributed_pipeline_amd.runtime.streams import plan_stream
+
 
 class DevicePrefetcher:
     """Iterator over ``it`` yielding dict batches already resident on ``device``."""
@@ -18,7 +20,7 @@ class DevicePrefetcher:
         self.it = iter(it)
         self.device = torch.device(device)
         self.cuda = self.device.type == "cuda"
-        self.stream = torch.cuda.Stream(self.device) if self.cuda else None
+        self.stream = plan_stream(self.device, "copy") if self.cuda else None
         self._next = self._stage()
 
     def _stage(self):

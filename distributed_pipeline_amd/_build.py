@@ -74,7 +74,7 @@ def build(force=False, jobs=None, debug=False, verbose=True):
     kernels = sorted(glob.glob(os.path.join(CSRC, "*.hip")))
     binding = os.path.join(CSRC, "bindings.cpp")
     # host-side C++ (torch / c10d APIs): compiled with the binding flags
-    host_cpp = sorted(glob.glob(os.path.join(CSRC, "comm", "*.cpp")))
+    host_cpp = sorted(glob.glob(os.path.join(CSRC, "comm", "*.cpp")) + glob.glob(os.path.join(CSRC, "runtime", "*.cpp")))
     opt = ["-O0", "-g"] if debug else ["-O3"]
     common = ["-std=c++17", "-fPIC", "--offload-arch=" + ARCH, "-D__HIP_PLATFORM_AMD__=1",
               "-Wno-unused-result", "-Wno-unused-command-line-argument"] + opt

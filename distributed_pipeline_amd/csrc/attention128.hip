@@ -1346,7 +1346,7 @@ bool launch_attn128_bwd(const uint16_t* qkv, const uint16_t* out, const uint16_t
                        dbias ? colpart : nullptr, B, H, p, seed, offset, head_major ? 1 : 0);
   if (dbias) {
     const int bchunk = 64, nch = (B + bchunk - 1) / bchunk;
-    if (!db_accumulate) hipMemsetAsync(dbias, 0, sizeof(float) * 3 * H * a128::HD, s);
+    if (!db_accumulate) (void)hipMemsetAsync(dbias, 0, sizeof(float) * 3 * H * a128::HD, s);
     hipLaunchKernelGGL(a128::colpart_reduce_kernel, dim3(3 * H, nch), dim3(256), 0, s, colpart,
                        dbias, B, H, bchunk);
   }

@@ -11,7 +11,8 @@
 #include "launchers.h"
 
 namespace dpa {
-void register_comm(pybind11::module& m);  // comm/reducer.cpp
+void register_comm(pybind11::module& m);     // comm/reducer.cpp
+void register_runtime(pybind11::module& m);  // runtime/streams.cpp
 }
 
 #define CHECK_DEV(x) TORCH_CHECK((x).is_cuda(), #x " must be a HIP tensor")
@@ -248,7 +249,7 @@ static std::vector<at::Tensor> add_ln_bwd(const at::Tensor& dout, const at::Tens
                                           c10::optional<at::Tensor> dg_acc, c10::optional<at::Tensor> db_acc,
                                           c10::optional<at::Tensor> dyb_acc, c10::optional<at::Tensor> part_buf,
                                           bool part_acc, c10::optional<at::Tensor> beta,
-                                          c10::optional<at::Tensor> hcopy) {
+                                          c10::optional<at::Tensor> hcopy, bool pair_hash) {
   CHECK_DEV(dout); CHECK_BF16(dout); CHECK_CONTIG(dout); CHECK_BF16(hs); CHECK_CONTIG(hs);
   TORCH_CHECK(hs.sizes() == dout.sizes(), "add_ln_bwd: hsave/out shape");
   // beta given: `hs` is the LN output (forward with save_h=false), xhat = (out - beta) / gamma
@@ -311,7 +312,8 @@ static std::vector<at::Tensor> add_ln_bwd(const at::Tensor& dout, const at::Tens
       need_dy ? reinterpret_cast<uint16_t*>(dy.data_ptr()) : nullptr,
       dyb.defined() ? dyb.data_ptr<float>() : nullptr,
       dg.data_ptr<float>(), db.data_ptr<float>(), R, D, (float)p, (uint32_t)seed, (uint32_t)offset,
-      cur_stream(), dhp, post, zero_mask, wsn > 0 ? ws.data_ptr<float>() : nullptr, part_mode, btp, hcp);
+      cur_stream(), dhp, post, zero_mask, wsn > 0 ? ws.data_ptr<float>() : nullptr, part_mode, btp, hcp,
+      pair_hash);
   TORCH_CHECK(ok, "add_ln_bwd: unsupported hidden size ", D);
   return {dres, dy, ext_g ? at::Tensor() : dg, ext_b ? at::Tensor() : db, ext_y ? at::Tensor() : dyb};
 }
@@ -470,17 +472,27 @@ static std::vector<at::Tensor> attn_bwd(const at::Tensor& dout, const at::Tensor
 }
 
 // ---- GEMMs ---------------------------------------------------------------------------
-static std::tuple<at::Tensor, at::Tensor, bool> gemm_nt(const at::Tensor& x, const at::Tensor& W,
-                                                        c10::optional<at::Tensor> b, int64_t act,
-                                                        bool want_deriv, int64_t head_major_L) {
+// want_deriv: 0 z = pre-activation; 1 z = act'(pre-activation) (bf16) when the persistent kernel
+// runs; 2 z = act' as u8 codes in the persistent kernels' tile-native layout ([T * N] uint8, read
+// back only by gemm_nn_dact(act=5)).  Returns (y, z, mode): the z that was written (0 / 1 / 2).
+static std::tuple<at::Tensor, at::Tensor, int64_t> gemm_nt(const at::Tensor& x, const at::Tensor& W,
+                                                           c10::optional<at::Tensor> b, int64_t act,
+                                                           int64_t want_deriv, int64_t head_major_L) {
   CHECK_DEV(x); CHECK_BF16(x); CHECK_BF16(W); CHECK_CONTIG(x); CHECK_CONTIG(W);
   const int T = (int)x.size(0), K = (int)x.size(1), N = (int)W.size(0);
   TORCH_CHECK(W.size(1) == K, "gemm_nt: W [N, K]");
   const c10::DeviceGuard guard(x.device());
   at::Tensor y = at::empty({T, N}, x.options());
   at::Tensor z;
+  if (want_deriv == 2 && (act == 1 || act == 3) && head_major_L <= 0) {
+    at::Tensor z8 = at::empty({(int64_t)T * N}, x.options().dtype(at::kByte));
+    if (dpa::launch_gemmp_nt(bf_ptr(x), bf_ptr(W), opt_bf_ptr(b), reinterpret_cast<uint16_t*>(y.data_ptr()),
+                             reinterpret_cast<uint16_t*>(z8.data_ptr()), T, N, K, (int)act, dpa::device_cu_count(),
+                             cur_stream(), true, 0, true))
+      return {y, z8, 2};
+  }
   if (act == 1 || act == 3) z = at::empty({T, N}, x.options());
-  bool deriv = want_deriv && z.defined();
+  bool deriv = want_deriv != 0 && z.defined();
   // head_major_L > 0: y stored as [T / L, N / 64, L, 64] (heads of 64 columns; the L = 128
   // attention reads each head contiguously)
   int hm = 0;
@@ -493,7 +505,25 @@ static std::tuple<at::Tensor, at::Tensor, bool> gemm_nt(const at::Tensor& x, con
                                 z.defined() ? reinterpret_cast<uint16_t*>(z.data_ptr()) : nullptr, T, N,
                                 K, (int)act, cur_stream(), &deriv, hm);
   TORCH_CHECK(ok, "gemm_nt: unsupported shape T=", T, " N=", N, " K=", K);
-  return {y, z, deriv};
+  return {y, z, deriv ? 1 : 0};
+}
+
+// h = res + dropout_p(x W^T + b) (post-LN sublayer branch + residual in the GEMM epilogue;
+// pair-hash dropout bits, regenerated by add_ln_bwd(pair_hash=True)); undefined when the shape
+// does not tile for the persistent kernel (the caller composes the old way)
+static at::Tensor gemm_nt_res(const at::Tensor& x, const at::Tensor& W, c10::optional<at::Tensor> b,
+                              const at::Tensor& res, double p, int64_t seed, int64_t offset) {
+  CHECK_DEV(x); CHECK_BF16(x); CHECK_BF16(W); CHECK_CONTIG(x); CHECK_CONTIG(W);
+  CHECK_BF16(res); CHECK_CONTIG(res);
+  const int T = (int)x.size(0), K = (int)x.size(1), N = (int)W.size(0);
+  TORCH_CHECK(W.size(1) == K && res.dim() == 2 && res.size(0) == T && res.size(1) == N, "gemm_nt_res shapes");
+  const c10::DeviceGuard guard(x.device());
+  at::Tensor h = at::empty({T, N}, x.options());
+  if (!dpa::launch_gemmp_nt_res(bf_ptr(x), bf_ptr(W), opt_bf_ptr(b), bf_ptr(res),
+                                reinterpret_cast<uint16_t*>(h.data_ptr()), T, N, K, dpa::device_cu_count(),
+                                cur_stream(), (float)p, (uint32_t)seed, (uint32_t)offset))
+    return at::Tensor();
+  return h;
 }
 
 // y = x . W^T (+ b) into a preallocated row-major [T, N] tensor (a row slice of a larger
@@ -522,7 +552,49 @@ static void gemm_nn_into(const at::Tensor& dy, const at::Tensor& W, at::Tensor& 
   TORCH_CHECK(ok, "gemm_nn_into: unsupported shape T=", T, " N=", N, " K=", K);
 }
 
-// dW[ids[i]] += dy[i] (fp32 accumulate): device sort of the ids, then one wave per run
+// (sorted ids, permutation) with equal ids adjacent: the counting sort of csrc/sort.hip
+// (histogram, scan, wave-aggregated scatter) for vocabularies < 2^17, else at::sort.
+static std::tuple<at::Tensor, at::Tensor> bucket_sort_ids(const at::Tensor& ids, int64_t V) {
+  const at::Tensor flat = ids.reshape({-1}).contiguous();
+  const int64_t n = flat.numel();
+  auto i64 = flat.options().dtype(at::kLong);
+  at::Tensor sorted = at::empty({n}, i64), perm = at::empty({n}, i64);
+  at::Tensor ws = at::empty({dpa::id_sort_workspace_ints((int)std::min<int64_t>(V, 1 << 20))},
+                            flat.options().dtype(at::kInt));
+  if (V < (1 << 17) &&
+      dpa::launch_id_bucket_sort(flat.data_ptr<int64_t>(), n, (int)V, ws.data_ptr<int>(),
+                                 sorted.data_ptr<int64_t>(), perm.data_ptr<int64_t>(), cur_stream()))
+    return {sorted, perm};
+  return at::sort(flat);
+}
+
+static std::vector<at::Tensor> id_sort(const at::Tensor& ids, int64_t V) {
+  CHECK_DEV(ids);
+  TORCH_CHECK(ids.scalar_type() == at::kLong && V > 0, "id_sort: int64 ids, V > 0");
+  const c10::DeviceGuard guard(ids.device());
+  if (ids.numel() == 0) return {ids.reshape({-1}), ids.reshape({-1})};
+  at::Tensor s, p;
+  std::tie(s, p) = bucket_sort_ids(ids, V);
+  return {s, p};
+}
+
+// order of a 0/1 (any nonzero = 1) int64 mask: nonzero entries first, both parts in index order
+static at::Tensor partition01(const at::Tensor& mask) {
+  CHECK_DEV(mask);
+  TORCH_CHECK(mask.scalar_type() == at::kLong, "partition01: int64 mask");
+  const c10::DeviceGuard guard(mask.device());
+  const at::Tensor flat = mask.reshape({-1}).contiguous();
+  const int64_t n = flat.numel();
+  at::Tensor order = at::empty({n}, flat.options());
+  if (n == 0) return order;
+  at::Tensor ws = at::empty({dpa::partition01_workspace_ints(n)}, flat.options().dtype(at::kInt));
+  TORCH_CHECK(dpa::launch_partition01(flat.data_ptr<int64_t>(), n, ws.data_ptr<int>(), order.data_ptr<int64_t>(),
+                                      cur_stream()),
+              "partition01: unsupported size ", n);
+  return order;
+}
+
+// dW[ids[i]] += dy[i] (fp32 accumulate): counting sort of the ids, then one wave per run
 // of equal ids sums its rows in registers and adds once (csrc/diffusion.hip) - the
 // token-embedding backward without ATen's index_add.
 static void emb_grad(const at::Tensor& ids, const at::Tensor& dy, at::Tensor& dW) {
@@ -534,7 +606,7 @@ static void emb_grad(const at::Tensor& ids, const at::Tensor& dy, at::Tensor& dW
   if (NT == 0) return;
   const c10::DeviceGuard guard(dW.device());
   at::Tensor sorted, perm;
-  std::tie(sorted, perm) = at::sort(ids.reshape({-1}));
+  std::tie(sorted, perm) = bucket_sort_ids(ids, dW.size(0));
   const bool b16 = dy.scalar_type() == at::kBFloat16;
   TORCH_CHECK(dpa::launch_emb_grad(sorted.data_ptr<int64_t>(), perm.data_ptr<int64_t>(),
                                    b16 ? nullptr : dy.data_ptr<float>(), b16 ? bf_ptr(dy) : nullptr, NT, (int)E,
@@ -574,10 +646,17 @@ static std::vector<at::Tensor> gemm_nn_dact(const at::Tensor& dy, const at::Tens
                                             const at::Tensor& aux, int64_t act, bool want_db,
                                             c10::optional<at::Tensor> db_acc,
                                             c10::optional<at::Tensor> part_out) {
-  CHECK_DEV(dy); CHECK_BF16(dy); CHECK_BF16(W); CHECK_BF16(aux);
+  CHECK_DEV(dy); CHECK_BF16(dy); CHECK_BF16(W);
   CHECK_CONTIG(dy); CHECK_CONTIG(W); CHECK_CONTIG(aux);
   const int T = (int)dy.size(0), N = (int)dy.size(1), K = (int)W.size(1);
-  TORCH_CHECK(W.size(0) == N && aux.size(0) == T && aux.size(1) == K, "gemm_nn_dact shapes");
+  // act 5: aux = u8 act' codes of gemm_nt(want_deriv=2) ([T * K] bytes, tile-native)
+  if (act == 5) {
+    TORCH_CHECK(aux.scalar_type() == at::kByte && aux.numel() == (int64_t)T * K, "gemm_nn_dact: act 5 aux u8 [T*K]");
+  } else {
+    TORCH_CHECK(aux.scalar_type() == at::kBFloat16 && aux.dim() == 2 && aux.size(0) == T && aux.size(1) == K,
+                "gemm_nn_dact: bf16 aux [T, K]");
+  }
+  TORCH_CHECK(W.size(0) == N, "gemm_nn_dact shapes");
   const c10::DeviceGuard guard(dy.device());
   at::Tensor dz = at::empty({T, K}, dy.options());
   uint16_t* dzp = reinterpret_cast<uint16_t*>(dz.data_ptr());
@@ -598,8 +677,9 @@ static std::vector<at::Tensor> gemm_nn_dact(const at::Tensor& dy, const at::Tens
   } else if (want_db && T % 256 == 0) {
     part = at::empty({(int64_t)(T / 256) * 2, K}, dy.options().dtype(at::kFloat));
   }
-  if (dpa::launch_gemmp_nn(bf_ptr(dy), bf_ptr(W), dzp, bf_ptr(aux), (int)act, T, N, K, dpa::device_cu_count(),
-                           cur_stream(), part.defined() ? part.data_ptr<float>() : nullptr)) {
+  if (dpa::launch_gemmp_nn(bf_ptr(dy), bf_ptr(W), dzp, reinterpret_cast<const uint16_t*>(aux.data_ptr()),
+                           (int)act, T, N, K, dpa::device_cu_count(), cur_stream(),
+                           part.defined() ? part.data_ptr<float>() : nullptr)) {
     if (keep) return {dz, at::Tensor()};
     if (acc) {
       if (!part.defined() || !dpa::launch_colsum_acc(part.data_ptr<float>(), (int)part.size(0), K,
@@ -609,6 +689,7 @@ static std::vector<at::Tensor> gemm_nn_dact(const at::Tensor& dy, const at::Tens
     }
     return {dz, part.defined() ? part.sum(0) : at::Tensor()};
   }
+  TORCH_CHECK(act != 5, "gemm_nn_dact: u8 act' codes need the persistent kernel (shape T=", T, " K=", K, ")");
   // no persistent kernel for this shape: the column sums from dz itself (a kept partial slot
   // gets them in row 0, zeros elsewhere; all zeros when no fused kernel ran either - the
   // caller then computes db itself)
@@ -834,10 +915,10 @@ static void emb_qsample_bwd(const at::Tensor& ids, const at::Tensor& mask, const
   }
   const c10::DeviceGuard guard(dW.device());
   if (n > 0) {
-    // device sort of the token ids -> runs of equal ids summed in registers (one atomic
+    // counting sort of the token ids -> runs of equal ids summed in registers (one atomic
     // per run and column instead of per token and column)
     at::Tensor sorted, perm;
-    if (E == 128 || E == 256) std::tie(sorted, perm) = at::sort(ids.reshape({-1}));
+    if (E == 128 || E == 256) std::tie(sorted, perm) = bucket_sort_ids(ids, dW.size(0));
     dpa::launch_emb_qsample_bwd(ids.data_ptr<int64_t>(), mask.data_ptr<int64_t>(), t.data_ptr<int64_t>(),
                                 sa.data_ptr<float>(), p_xs, p_xs16, p_xt16, p_xt32, B * L, (int)L, (int)E,
                                 (int)dW.size(0), dW.data_ptr<float>(), cur_stream(),
@@ -917,6 +998,7 @@ static void rng_base_add(int64_t d) {
   dpa::rng_base_add_attention128((uint32_t)d, s);
   dpa::rng_base_add_diffusion((uint32_t)d, s);
   dpa::rng_base_add_norm((uint32_t)d, s);
+  dpa::rng_base_add_gemm256((uint32_t)d, s);
 }
 
 static at::Tensor timestep_emb(const at::Tensor& ts, int64_t dim, double max_period) {
@@ -937,6 +1019,7 @@ static bool gemm_supported(int64_t M, int64_t N, int64_t K) {
 PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.doc() = "distributed_pipeline_amd native gfx950 kernels";
   dpa::register_comm(m);
+  dpa::register_runtime(m);
   m.def("sqnorm", &sqnorm, "flat grad L2 norm + clip coefficient (device)");
   m.def("adamw_ema", &adamw_ema, "fused AdamW + EMA + bf16 shadow refresh");
   m.def("ema_update", &ema_update, "flat EMA update");
@@ -952,7 +1035,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("want_dy_colsum") = false, py::arg("dh_in") = py::none(), py::arg("post") = false,
         py::arg("dg_acc") = py::none(), py::arg("db_acc") = py::none(), py::arg("dyb_acc") = py::none(),
         py::arg("part_buf") = py::none(), py::arg("part_acc") = false, py::arg("beta") = py::none(),
-        py::arg("hcopy") = py::none());
+        py::arg("hcopy") = py::none(), py::arg("pair_hash") = false);
   m.def("colsum_acc", &colsum_acc, "dst += colsum(part) (fp32 partials [rows, cols])");
   m.def("ln_bwd_partials", &ln_bwd_partials, "floats of add_ln_bwd's deferred partial buffer (0: none)");
   m.def("ln_colreduce", &ln_colreduce, "dg/db(/dyb) += column sums of add_ln_bwd partials",
@@ -962,6 +1045,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("gemm_nt_into", &gemm_nt_into, "y = x W^T (+b) into a preallocated [T, N] tensor");
   m.def("gemm_nn_into", &gemm_nn_into, "dx = dy W into a preallocated [T, K] tensor");
   m.def("emb_grad", &emb_grad, "dW[ids] += dy (sorted segment sum, fp32)");
+  m.def("id_sort", &id_sort, "counting sort of int64 ids into V + 1 buckets -> (sorted ids, permutation)");
+  m.def("partition01", &partition01, "stable partition order of an int64 0/1 mask (nonzero first)");
   m.def("attn128_supports", &dpa::attn128_supports, "the persistent L = 128 attention covers (L, D, causal)");
   m.def("attn_fwd", &attn_fwd, "fused attention forward (head_dim 64/128) -> (out, lse)", py::arg("qkv"),
         py::arg("heads"), py::arg("p"), py::arg("causal"), py::arg("seed"), py::arg("offset"),
@@ -973,8 +1058,10 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("gemm_nt", &gemm_nt,
         "y = act(x W^T + b) (bf16 MFMA) -> (y, z, z_is_derivative): z is the pre-activation, or "
         "act'(pre-activation) when want_deriv and the persistent kernel ran (backward act code 4)",
-        py::arg("x"), py::arg("W"), py::arg("b"), py::arg("act"), py::arg("want_deriv") = false,
+        py::arg("x"), py::arg("W"), py::arg("b"), py::arg("act"), py::arg("want_deriv") = 0,
         py::arg("head_major_L") = 0);
+  m.def("gemm_nt_res", &gemm_nt_res, "h = res + dropout_p(x W^T + b) in the GEMM epilogue (None: shape not tiled)",
+        py::arg("x"), py::arg("W"), py::arg("b"), py::arg("res"), py::arg("p"), py::arg("seed"), py::arg("offset"));
   m.def("gemm_nn", &gemm_nn, "dx = dy W (bf16 MFMA)");
   m.def("gemm_nn_dact", &gemm_nn_dact,
         "dz = (dy W) * act'(aux) (bf16 MFMA, fused act backward) -> (dz, colsum(dz) fp32 or None)",

@@ -34,6 +34,7 @@
 //   reduced by csrc/ipc_allreduce.hip on the same comm stream - all 7 xGMI links of a
 //   GPU carry traffic at once instead of one ring neighbour's link.
 #include <torch/extension.h>
+#include <ATen/hip/impl/HIPGuardImplMasqueradingAsCUDA.h>
 #include <ATen/hip/impl/HIPStreamMasqueradingAsCUDA.h>
 #include <torch/csrc/distributed/c10d/ProcessGroup.hpp>
 #include <torch/csrc/distributed/c10d/Work.hpp>
@@ -327,6 +328,9 @@ class BucketReducer {
   }
 
   // priority of the reducer's comm stream (direct mode; lower = higher priority)
+  // handle of the data plane's comm stream (0: none - not the direct mode)
+  int64_t comm_stream() const { return (int64_t)reinterpret_cast<uintptr_t>(cs_); }
+
   int64_t stream_priority() const {
     int p = 0;
     if (cs_) (void)hipStreamGetPriority(cs_, &p);
@@ -407,6 +411,12 @@ class BucketReducer {
   }
 
   void launch_pg(int b) {
+    // the process group orders its collective (and the bf16 wire copy below) after the
+    // CURRENT stream: make that the armed backward's stream, not whichever stream autograd
+    // runs this parameter's hook on (in the overlapped schedule often the other one)
+    c10::optional<c10::hip::HIPStreamGuardMasqueradingAsCUDA> guard;
+    if (arm_stream_ && grad_.is_cuda())
+      guard.emplace(c10::hip::getStreamFromExternalMasqueradingAsCUDA(arm_stream_, grad_.device().index()));
     at::Tensor view = slice(grad_, b);
     if (bf16_) {
       at::Tensor wire = slice(comm_, b);
@@ -473,6 +483,7 @@ void register_comm(pybind11::module& m) {
       .def("armed", &BucketReducer::armed)
       .def("direct", &BucketReducer::direct)
       .def("stream_priority", &BucketReducer::stream_priority)
+      .def("comm_stream", &BucketReducer::comm_stream)
       .def("ipc_export", &BucketReducer::ipc_export)
       .def("ipc_open", &BucketReducer::ipc_open)
       .def("ipc_ready", &BucketReducer::ipc_ready)

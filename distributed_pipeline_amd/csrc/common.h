@@ -104,6 +104,41 @@ __device__ __forceinline__ void philox4(uint32_t k0, uint32_t k1, uint32_t c0, u
   out[0] = c0; out[1] = c1; out[2] = c2; out[3] = c3;
 }
 
+// ---- cheap hashes for dropout bits inside matrix-core and memory-bound loops ---------
+// lowbias32: 32-bit avalanche hash (two multiplies).
+__device__ __forceinline__ uint32_t lowbias32(uint32_t x) {
+  x ^= x >> 16; x *= 0x7feb352du; x ^= x >> 15; x *= 0x846ca68bu; x ^= x >> 16;
+  return x;
+}
+
+// One-multiply finaliser for the per-element attention dropout bits (v_mul_lo_u32 is
+// quarter rate, so each multiply dropped saves 12 issue cycles per key pair); keep
+// rate, neighbour correlations and per-row variance match lowbias32 within noise over
+// 1024 x 1024 masks (measured host-side).
+__device__ __forceinline__ uint32_t mix32(uint32_t x) {
+  x ^= x >> 16;
+  x *= 0x7feb352du;
+  x ^= x >> 15;
+  return x;
+}
+
+// Dropout bits of the post-LN sublayers whose residual + dropout run in the producing GEMM's
+// epilogue (gemm256.hip EPI 7) and whose LayerNorm backward regenerates them (norm.hip
+// drop_hash mode): element (row, col) of the [T, D] branch output keeps iff the 16-bit half
+// (col & 1) of pair_hash(row, col) is >= thr16 = round(p * 2^16) - one one-multiply hash per
+// column pair instead of a Philox-7 block per 4 columns (the GEMM epilogue cannot afford
+// Philox: ~38 VALU cycles per element against a ~170-cycle-per-element tile budget).
+__device__ __forceinline__ uint32_t pair_seedmix(uint32_t seed, uint32_t offset) {
+  return lowbias32(seed ^ lowbias32(offset * 0xC2B2AE3Du ^ 0x68E31DA4u));
+}
+__device__ __forceinline__ uint32_t pair_hash(uint32_t seedmix, uint32_t row, uint32_t col) {
+  return mix32(seedmix ^ (row * 0x9E3779B1u) ^ ((col >> 1) * 0x85EBCA77u));
+}
+__device__ __forceinline__ bool pair_keep(uint32_t h, uint32_t col, uint32_t thr16) {
+  return ((col & 1u) ? (h >> 16) : (h & 0xffffu)) >= thr16;
+}
+__host__ __device__ __forceinline__ uint32_t pair_thr16(float p) { return (uint32_t)(p * 65536.f + 0.5f); }
+
 __device__ __forceinline__ float u32_to_unit(uint32_t x) {  // [0,1)
   return (float)(x >> 8) * (1.0f / 16777216.0f);
 }

@@ -563,7 +563,8 @@ template <int EPI>
 struct PEpi {
   // VMEM ops each lane issues after the next tile's prologue DMA: 16 stores (8 rounds x 2),
   // EPI 2 a second 16 (z and y), EPI 3/4 the 12 aux loads of rounds 2..7, EPI 4 two partial stores
-  static constexpr int XS = (EPI == 2 || EPI == 6) ? 32 : (EPI == 3 || EPI == 5) ? 28 : EPI == 4 ? 30 : 16;
+  static constexpr int XS = (EPI == 2 || EPI == 6 || EPI == 8) ? 32 : (EPI == 3 || EPI == 5 || EPI == 7) ? 28
+                            : EPI == 4 ? 30 : 16;
 };
 
 template <int ACT>
@@ -609,6 +610,50 @@ __device__ __forceinline__ uint4 act8(const uint4& u) {
     o[q] = pack_bf2(y.x, y.y);
   }
   return make_uint4(o[0], o[1], o[2], o[3]);
+}
+
+// act'(z) as an 8-bit code (EPI 8 stores it, ACT 5 epilogues read it), two linear segments
+// meeting at code 93 = act' 0.5:
+//   c in [0, 93]:    act' = (c - 19) * 0.5 / 74        -> [-0.1284, 0.5], step 0.0068
+//   c in [93, 255]:  act' = (c + 35) / 256             -> [0.5, 1.1328],  step 2^-8
+// The upper segment's grid IS bf16's grid on [0.5, 1) (and finer on [1, 1.13]), so every act'
+// >= 0.5 is stored exactly as a bf16 act' would be; 0 (code 19) and 1 (code 221) - the
+// saturated regions, most elements of a trained layer - are exact; below 0.5 within 0.0034.
+// Covers gelu' [-0.129, 1.129] (its minimum clamped by 0.0006), silu' [-0.0998, 1.0998] and
+// tanh' [0, 1].  Half the bytes of the bf16 act' the forward writes and the backward reads.
+// The segments are convex / concave at the joint, so the code is the max of the two lines'
+// codes and the value the min of the two lines' values (no compare / select).
+constexpr float Q8_LO_STEP = 0.5f / 74.f;
+__device__ __forceinline__ float q8_code(float d) {
+  const float c = fmaxf(fmaf(d, 148.f, 19.f), fmaf(d, 256.f, -35.f));
+  return __builtin_rintf(__builtin_amdgcn_fmed3f(c, 0.f, 255.f));
+}
+__device__ __forceinline__ float q8_value(float c) {
+  return fminf((c - 19.f) * Q8_LO_STEP, fmaf(c, 1.f / 256.f, 35.f / 256.f));
+}
+
+// 8 bf16 -> act(z) (returned, bf16) and act'(z) as 8 u8 codes (c)
+template <int ACT>
+__device__ __forceinline__ uint4 act_dact8q(const uint4& u, uint2& c) {
+  const uint32_t w[4] = {u.x, u.y, u.z, u.w};
+  uint32_t o[4], cw[2] = {0u, 0u};
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    f32x2 d;
+    const f32x2 y = act_dact2<ACT>(f32x2{__uint_as_float(w[q] << 16), __uint_as_float(w[q] & 0xffff0000u)}, d);
+    o[q] = pack_bf2(y.x, y.y);
+    cw[q >> 1] = __builtin_amdgcn_cvt_pk_u8_f32(q8_code(d.x), (q & 1) * 2, cw[q >> 1]);
+    cw[q >> 1] = __builtin_amdgcn_cvt_pk_u8_f32(q8_code(d.y), (q & 1) * 2 + 1, cw[q >> 1]);
+  }
+  c = make_uint2(cw[0], cw[1]);
+  return make_uint4(o[0], o[1], o[2], o[3]);
+}
+
+// decoded act' of elements 2q, 2q + 1 of an 8-code group
+__device__ __forceinline__ f32x2 q8_pair(const uint4& a, int q) {
+  const uint32_t c = (q >> 1) ? a.y : a.x;
+  const int sh = (q & 1) * 16;
+  return f32x2{q8_value((float)((c >> sh) & 0xffu)), q8_value((float)((c >> (sh + 8)) & 0xffu))};
 }
 
 __device__ __forceinline__ void lds_write_b32(uint32_t addr, int v) {
@@ -657,6 +702,32 @@ __device__ __forceinline__ uint4 ld_aux(const bf16_t* p) {
     return *reinterpret_cast<const uint4*>(p);
   }
 }
+typedef __attribute__((ext_vector_type(2))) unsigned u32x2_v;
+template <int POL>
+__device__ __forceinline__ void st_out8(uint8_t* p, const uint2& v) {
+  if constexpr (POL & 1) {
+    __builtin_nontemporal_store(u32x2_v{v.x, v.y}, reinterpret_cast<u32x2_v*>(p));
+  } else {
+    *reinterpret_cast<uint2*>(p) = v;
+  }
+}
+template <int POL>
+__device__ __forceinline__ uint2 ld_aux8(const uint8_t* p) {
+  if constexpr (POL & 2) {
+    const u32x2_v x = __builtin_nontemporal_load(reinterpret_cast<const u32x2_v*>(p));
+    return make_uint2(x[0], x[1]);
+  } else {
+    return *reinterpret_cast<const uint2*>(p);
+  }
+}
+
+// Epilogue parameters beyond the operands: the residual-dropout epilogue (EPI 7) draws its
+// dropout bits from pair_hash (common.h) with the seed mix of (seed, offset + device base).
+struct EpiArgs {
+  uint32_t seed = 0, offset = 0, thr16 = 0;
+  float scale = 1.f;
+};
+
 template <int GM>
 __device__ __forceinline__ void tile_mn(int t, int NT, int& mt, int& nt) {
   if constexpr (GM <= 1) {
@@ -675,10 +746,13 @@ __global__ void __launch_bounds__(512) gemmp_kernel(const bf16_t* __restrict__ A
                                                     int nk, bf16_t* __restrict__ C, int64_t ldc,
                                                     const bf16_t* __restrict__ bias,
                                                     bf16_t* __restrict__ Zout, float* __restrict__ colpart,
-                                                    int* __restrict__ tile_ctr, int hm) {
+                                                    int* __restrict__ tile_ctr, int hm, EpiArgs ea) {
   __shared__ __attribute__((aligned(1024))) char smem[P_LDS];
   constexpr int XS = PEpi<EPI>::XS;
-  constexpr bool DACT = EPI == 3 || EPI == 4 || EPI == 5;  // epilogues that read aux
+  constexpr bool DACT = EPI == 3 || EPI == 4 || EPI == 5;  // data-gradient epilogues reading aux
+  constexpr bool AUXR = DACT || EPI == 7;                  // epilogues that read aux
+  constexpr bool Q8 = DACT && ACT == 5;                    // aux = act' as tile-native u8 codes
+  static_assert(!(EPI == 8 && ACT == 0), "EPI 8 stores an activation derivative");
   // wave id in an SGPR, lane id re-derived from EXEC wherever needed: nothing
   // lane-dependent has to stay live across the register-full main loop
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -736,6 +810,24 @@ __global__ void __launch_bounds__(512) gemmp_kernel(const bf16_t* __restrict__ A
     }
     return row * ldc + col;
   };
+  // Tile-native byte offset of a u8 act' code group (EPI 8 writes, ACT 5 reads): the 8 codes
+  // of (tile, wave, round, k, lane) are consecutive, so one wave instruction moves 512
+  // contiguous bytes (the row-major u8 layout would give half-line 64-B row segments).  Both
+  // kernels tile the same [T][N] matrix with the same 256 x 256 tiles and wave / lane roles.
+  auto q8_off = [&](int t, int ro, int k, int ln) -> int64_t {
+    int mt, nt;
+    tile_mn<GM>(t, NT, mt, nt);
+    return (((((int64_t)mt * NT + nt) * 8 + w) * 8 + ro) * 2 + k) * 512 + ln * 8;
+  };
+  auto load_aux = [&](int t, int ro, int k, int ln) -> uint4 {
+    if constexpr (Q8) {
+      const uint2 v = ld_aux8<POL>(reinterpret_cast<const uint8_t*>(Zout) + q8_off(t, ro, k, ln));
+      return make_uint4(v.x, v.y, 0u, 0u);
+    } else {
+      return ld_aux<POL>(Zout + row_off(t, ro, k, ln));
+    }
+  };
+  const uint32_t dsm = EPI == 7 ? pair_seedmix(ea.seed, ea.offset + rng_base()) : 0u;
 
   auto epilogue = [&](int t, int slot, uint4 (&aux)[2][2], bool has_next) {
     // lane-derived addressing recomputed here from an opaque lane id: hoisted out of
@@ -789,7 +881,7 @@ __global__ void __launch_bounds__(512) gemmp_kernel(const bf16_t* __restrict__ A
         const int row = k * 8 + rr;
         val[k] = lds_read_b128_sync(stg + row * 128 + ((ch ^ (row & 7)) << 4));
       }
-      if constexpr (DACT) {
+      if constexpr (AUXR) {
         // wait for this round's aux.  Issue order: aux(0) aux(1) [DMA: 13] | r0: wait aux(2)
         // st(0) | r1: wait aux(3) st(1) | ... | r5: wait aux(7) st(5) | r6: wait st(6) | r7: wait
         // st(7); the ops younger than aux(ro) at its wait (2 each; the DMA only when there is
@@ -804,6 +896,13 @@ __global__ void __launch_bounds__(512) gemmp_kernel(const bf16_t* __restrict__ A
         } else {
           wait_vm<4>();
         }
+        uint32_t drow = 0, dcol = 0;
+        if constexpr (EPI == 7) {
+          int mt, nt;
+          tile_mn<GM>(t, NT, mt, nt);
+          drow = (uint32_t)(mt * 256 + qa * 128 + wm * 64 + i * 16 + (ln >> 3));
+          dcol = (uint32_t)(nt * 256 + wn * 64 + (ln & 7) * 8);
+        }
 #pragma unroll
         for (int k = 0; k < 2; ++k) {
           const uint4 a = aux[ro & 1][k];
@@ -812,8 +911,21 @@ __global__ void __launch_bounds__(512) gemmp_kernel(const bf16_t* __restrict__ A
           uint32_t o[4];
 #pragma unroll
           for (int q = 0; q < 4; ++q) {
-            const f32x2 x = f32x2{bf_lo(vw[q]), bf_hi(vw[q])}, a = f32x2{bf_lo(aw[q]), bf_hi(aw[q])};
-            const f32x2 d = EPI == 5 ? x + a : x * dact2<ACT>(a);
+            const f32x2 x = f32x2{bf_lo(vw[q]), bf_hi(vw[q])};
+            f32x2 d;
+            if constexpr (Q8) {
+              d = x * q8_pair(a, q);
+            } else if constexpr (EPI == 7) {
+              // h = residual + dropout(y): y = the bf16 GEMM output (+bias), as a separate
+              // dropout-add pass would see it; the bits are norm.hip's pair-hash mode's
+              const f32x2 r = f32x2{bf_lo(aw[q]), bf_hi(aw[q])};
+              const uint32_t hsh = pair_hash(dsm, drow + k * 8, dcol + 2 * q);
+              const f32x2 m = {(hsh & 0xffffu) >= ea.thr16 ? ea.scale : 0.f, (hsh >> 16) >= ea.thr16 ? ea.scale : 0.f};
+              d = x * m + r;
+            } else {
+              const f32x2 av = f32x2{bf_lo(aw[q]), bf_hi(aw[q])};
+              d = EPI == 5 ? x + av : x * dact2<ACT>(av);
+            }
             o[q] = pack_bf2(d.x, d.y);
             if constexpr (EPI == 4) {
               csum[2 * q] += bf_lo(o[q]);
@@ -825,8 +937,7 @@ __global__ void __launch_bounds__(512) gemmp_kernel(const bf16_t* __restrict__ A
         // this round's aux slot is consumed: prefetch round ro + 2 into it
         if (ro + 2 < 8) {
 #pragma unroll
-          for (int k = 0; k < 2; ++k)
-            aux[ro & 1][k] = ld_aux<POL>(Zout + row_off(t, ro + 2, k, ln));
+          for (int k = 0; k < 2; ++k) aux[ro & 1][k] = load_aux(t, ro + 2, k, ln);
         }
       }
 #pragma unroll
@@ -838,6 +949,11 @@ __global__ void __launch_bounds__(512) gemmp_kernel(const bf16_t* __restrict__ A
           uint4 dv;
           val[k] = act_dact8<ACT>(val[k], dv);
           st_out<POL>(Zout + o, dv);
+        }
+        if constexpr (EPI == 8) {
+          uint2 code;
+          val[k] = act_dact8q<ACT>(val[k], code);
+          st_out8<POL>(reinterpret_cast<uint8_t*>(Zout) + q8_off(t, ro, k, ln), code);
         }
         st_out<POL>(C + o, val[k]);
       }
@@ -885,6 +1001,11 @@ __global__ void __launch_bounds__(512) gemmp_kernel(const bf16_t* __restrict__ A
   // workgroup that starts late (its CU held by a concurrent RCCL kernel) just takes fewer
   // tiles instead of finishing last.  Claimed items form a prefix, so the first claim past
   // ntiles ends the workgroup.
+  // Self-resetting queues: every workgroup of queue x ends with exactly one claim past the
+  // end, then bumps the queue's done counter; the queue's last workgroup (done == qsize - 1:
+  // no claim on the queue can follow) zeroes both counters.  A launch leaves its counters as
+  // it found them, so a HIP graph that bakes the counter address replays correctly whatever
+  // state the host-side slot ring was in at capture.
   const bool dyn = tile_ctr != nullptr && G >= 8;
   int qbase = 0, qsize = 1;
   int* qctr = nullptr;
@@ -892,7 +1013,7 @@ __global__ void __launch_bounds__(512) gemmp_kernel(const bf16_t* __restrict__ A
     const int qg = G >> 3, rg = G & 7, x = blockIdx.x & 7;
     qbase = x < rg ? x * (qg + 1) : rg * (qg + 1) + (x - rg) * qg;
     qsize = x < rg ? qg + 1 : qg;
-    qctr = tile_ctr + x * 16;  // one 64-byte line per queue
+    qctr = tile_ctr + x * 16;  // one 64-byte line per queue: [0] claims, [1] finished workgroups
   }
   int slot = 0;
   bool extra = false;
@@ -930,7 +1051,7 @@ __global__ void __launch_bounds__(512) gemmp_kernel(const bf16_t* __restrict__ A
     // so their HBM latency hides under that iteration's MFMAs instead of the epilogue's first
     // rounds (niter == 1: issued after the main loop as before)
     uint4 aux[2][2];
-    constexpr bool EARLY_AUX = DACT && (PEARLY_AUX != 0);
+    constexpr bool EARLY_AUX = AUXR && (PEARLY_AUX != 0);
     for (int it = 1; it < niter - (EARLY_AUX ? 1 : 0); ++it) {
       const int te = 2 * it;
       const bool more = it + 1 < niter;
@@ -954,7 +1075,7 @@ __global__ void __launch_bounds__(512) gemmp_kernel(const bf16_t* __restrict__ A
 #pragma unroll
           for (int ro = 0; ro < 2; ++ro)
 #pragma unroll
-            for (int k = 0; k < 2; ++k) aux[ro][k] = ld_aux<POL>(Zout + row_off(tile, ro, k, ln));
+            for (int k = 0; k < 2; ++k) aux[ro][k] = load_aux(tile, ro, k, ln);
         }
         aux_issued = true;
         phase<2, false, B_TR, false, true, 0, 4>(acc, fa, fb0, fb1, cs, opA, opB, smem, csa, te, false, false, grp);
@@ -973,18 +1094,27 @@ __global__ void __launch_bounds__(512) gemmp_kernel(const bf16_t* __restrict__ A
     if (grp == 0) barrier();  // re-align the groups: every wave's LDS reads are retired
     const int next = dyn ? __builtin_amdgcn_readfirstlane(lds_read_b32_sync(sbase + P_NEXT_OFF)) : tile + G;
     const bool has_next = next < ntiles;
-    if (DACT && !aux_issued) {
+    if (AUXR && !aux_issued) {
       // activation-backward operand of rounds 0 and 1 (row-major, full lines), issued
       // before the next tile's prologue DMA so that waiting for it leaves the DMA in flight
       const int ln = opaque(lane_id());
 #pragma unroll
       for (int ro = 0; ro < 2; ++ro)
 #pragma unroll
-        for (int k = 0; k < 2; ++k) aux[ro][k] = ld_aux<POL>(Zout + row_off(tile, ro, k, ln));
+        for (int k = 0; k < 2; ++k) aux[ro][k] = load_aux(tile, ro, k, ln);
     }
     if (has_next) prologue(next, slot ^ 1);
     epilogue(tile, slot, aux, has_next);
-    if (!has_next) break;
+    if (!has_next) {
+      if (dyn && w == 0 && lane_id() == 0) {
+        // (vector atomics: the counters are reset through the vector memory path)
+        if (atomicAdd(qctr + 1, 1) == qsize - 1) {
+          atomicExch(qctr, 0);
+          atomicExch(qctr + 1, 0);
+        }
+      }
+      break;
+    }
     zero_acc();
     wait_vm<8 + XS>();  // next tile's K-tile 0 halves landed; this tile's epilogue ops may fly
     barrier();
@@ -1065,9 +1195,10 @@ static int* gemmp_queue(hipStream_t s) {
   if (!g_gemmp_dynamic) return nullptr;
   // one counter buffer per (device, stream): GEMMs on one stream never overlap, but the
   // overlapped micro-batch schedule runs GEMMs on two streams at once
-  // A ring of NSLOT counter sets per (device, stream), zeroed by ONE memset each time the ring
-  // wraps (every earlier launch on the stream has finished by then: stream order) instead of a
-  // memset per launch - the reference schedule issues ~3000 GEMMs per step.
+  // A ring of NSLOT counter sets per (device, stream), zeroed once when created: every launch
+  // leaves its counters zeroed (the kernel's last workgroup per queue resets them), so no
+  // memset runs per launch (the reference schedule issues ~3000 GEMMs per step) and a captured
+  // HIP graph replays with valid counters.
   constexpr int NSLOT = 256, SLOT_INTS = 8 * 16;
   struct Q { int dev; hipStream_t s; int* buf; int cursor; };
   static Q qs[64];
@@ -1078,13 +1209,16 @@ static int* gemmp_queue(hipStream_t s) {
   for (int i = 0; i < nq; ++i)
     if (qs[i].dev == dev && qs[i].s == s) q = &qs[i];
   if (!q) {
+    // a stream first seen while it is being captured (the graph's capture stream) keeps the
+    // static schedule: no allocation inside a capture
+    hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+    if (hipStreamIsCapturing(s, &cs) != hipSuccess || cs != hipStreamCaptureStatusNone) return nullptr;
     int* buf = nullptr;
     if (nq >= 64 || hipMalloc(&buf, (size_t)NSLOT * SLOT_INTS * sizeof(int)) != hipSuccess) return nullptr;
+    if (hipMemsetAsync(buf, 0, (size_t)NSLOT * SLOT_INTS * sizeof(int), s) != hipSuccess) return nullptr;
     qs[nq] = Q{dev, s, buf, 0};
     q = &qs[nq++];
   }
-  if (q->cursor == 0 && hipMemsetAsync(q->buf, 0, (size_t)NSLOT * SLOT_INTS * sizeof(int), s) != hipSuccess)
-    return nullptr;
   int* slot = q->buf + (size_t)q->cursor * SLOT_INTS;
   q->cursor = (q->cursor + 1) % NSLOT;
   return slot;
@@ -1093,13 +1227,13 @@ static int* gemmp_queue(hipStream_t s) {
 template <bool B_TR, int EPI, int ACT, int POL = 0, int GM = 1>
 static void gemmp_launch(const uint16_t* a, int64_t lda, const uint16_t* b, int64_t ldb, int M, int N, int K,
                          uint16_t* c, const uint16_t* bias, uint16_t* z, int ncu, hipStream_t s,
-                         float* colpart, int hm) {
+                         float* colpart, int hm, const g256::EpiArgs& ea) {
   const int tiles = (M / 256) * (N / 256);
   const int grid = persistent_grid(tiles, ncu);
   int* q = (tiles > grid && grid >= 8) ? gemmp_queue(s) : nullptr;
   hipLaunchKernelGGL((g256::gemmp_kernel<B_TR, EPI, ACT, POL, GM>), dim3(grid), dim3(512), 0, s,
                      (const bf16_t*)a, lda, (const bf16_t*)b, ldb, M, N, K / 64, (bf16_t*)c, (int64_t)N,
-                     (const bf16_t*)bias, (bf16_t*)z, colpart, q, hm);
+                     (const bf16_t*)bias, (bf16_t*)z, colpart, q, hm, ea);
 }
 
 // The two GELU-side GEMMs (EPI 6: y and act' stored; EPI 4: times act' plus column sums) of
@@ -1109,28 +1243,34 @@ static void gemmp_launch(const uint16_t* a, int64_t lda, const uint16_t* b, int6
 template <bool B_TR, int EPI, int ACT>
 static void gemmp_go(const uint16_t* a, int64_t lda, const uint16_t* b, int64_t ldb, int M, int N, int K,
                      uint16_t* c, const uint16_t* bias, uint16_t* z, int ncu, hipStream_t s,
-                     float* colpart = nullptr, int hm = 0) {
+                     float* colpart = nullptr, int hm = 0, const g256::EpiArgs& ea = g256::EpiArgs{}) {
   static const bool grouped = [] {
     const char* e = std::getenv("DPA_GEMMP_GROUPED");  // "0": default policy (A/B runs)
     return !(e && e[0] == '0');
   }();
-  if constexpr (EPI == 4 || EPI == 6) {
+  if constexpr (EPI == 4 || EPI == 6 || EPI == 8) {
     if (grouped && (M / 256) % 8 == 0 && N / 256 >= 8) {
-      gemmp_launch<B_TR, EPI, ACT, 1, 8>(a, lda, b, ldb, M, N, K, c, bias, z, ncu, s, colpart, hm);
+      gemmp_launch<B_TR, EPI, ACT, 1, 8>(a, lda, b, ldb, M, N, K, c, bias, z, ncu, s, colpart, hm, ea);
       return;
     }
   }
-  gemmp_launch<B_TR, EPI, ACT>(a, lda, b, ldb, M, N, K, c, bias, z, ncu, s, colpart, hm);
+  gemmp_launch<B_TR, EPI, ACT>(a, lda, b, ldb, M, N, K, c, bias, z, ncu, s, colpart, hm, ea);
 }
 
 // y[T][N] = act(x[T][K] . W[N][K]^T + bias); z (nullable, act != 0) = the pre-activation,
 // or act'(pre-activation) when zderiv (the backward then multiplies: act code 4).
 bool launch_gemmp_nt(const uint16_t* x, const uint16_t* W, const uint16_t* bias, uint16_t* y,
-                     uint16_t* z, int T, int N, int K, int act, int ncu, hipStream_t s, bool zderiv, int hm) {
+                     uint16_t* z, int T, int N, int K, int act, int ncu, hipStream_t s, bool zderiv, int hm,
+                     bool z8) {
   if (!g256_enabled() || T % 256 || N % 256 || K % 128 || K < 128 || act < 0 || act > 3) return false;
   if (hm && (act != 0 || hm < 7 || hm > 30 || (T & ((1 << hm) - 1)) || N % 64)) return false;
+  if (z8 && (act == 0 || z == nullptr || !zderiv)) return false;
   if (act == 0) gemmp_go<false, 0, 0>(x, K, W, K, T, N, K, y, bias, nullptr, ncu, s, nullptr, hm);
-  else if (z != nullptr && zderiv) {
+  else if (z8) {
+    if (act == 1) gemmp_go<false, 8, 1>(x, K, W, K, T, N, K, y, bias, z, ncu, s);
+    else if (act == 2) gemmp_go<false, 8, 2>(x, K, W, K, T, N, K, y, bias, z, ncu, s);
+    else gemmp_go<false, 8, 3>(x, K, W, K, T, N, K, y, bias, z, ncu, s);
+  } else if (z != nullptr && zderiv) {
     if (act == 1) gemmp_go<false, 6, 1>(x, K, W, K, T, N, K, y, bias, z, ncu, s);
     else if (act == 2) gemmp_go<false, 6, 2>(x, K, W, K, T, N, K, y, bias, z, ncu, s);
     else gemmp_go<false, 6, 3>(x, K, W, K, T, N, K, y, bias, z, ncu, s);
@@ -1149,6 +1289,22 @@ bool launch_gemmp_nt(const uint16_t* x, const uint16_t* W, const uint16_t* bias,
 // dx[T][K] = dy[T][N] . W[N][K]  (act != 0: times act'(aux[T][K]); colpart != nullptr:
 // also the per-tile column-sum partials [(T/256)*2][K] of the result)
 // dx[T][K] = dy[T][N] . W[N][K] + dx[T][K]  (in place, bf16)
+// h[T][N] = res[T][N] + dropout_p(x[T][K] . W[N][K]^T + bias): the post-LN sublayer's residual
+// branch folded into the GEMM epilogue (the LayerNorm then reads h alone and writes no h copy);
+// the dropout bits are pair_hash(seed, offset) ones, regenerated by add_ln_bwd's pair-hash mode
+bool launch_gemmp_nt_res(const uint16_t* x, const uint16_t* W, const uint16_t* bias, const uint16_t* res,
+                         uint16_t* h, int T, int N, int K, int ncu, hipStream_t s, float p, uint32_t seed,
+                         uint32_t offset) {
+  if (!g256_enabled() || T % 256 || N % 256 || K % 128 || K < 128 || !(p >= 0.f && p < 1.f)) return false;
+  g256::EpiArgs ea;
+  ea.seed = seed;
+  ea.offset = offset;
+  ea.thr16 = pair_thr16(p);
+  ea.scale = 1.f / (1.f - p);
+  gemmp_go<false, 7, 0>(x, K, W, K, T, N, K, h, bias, const_cast<uint16_t*>(res), ncu, s, nullptr, 0, ea);
+  return true;
+}
+
 bool launch_gemmp_nn_acc(const uint16_t* dy, const uint16_t* W, uint16_t* dx, int T, int N, int K, int ncu,
                          hipStream_t s) {
   if (!g256_enabled() || T % 256 || K % 256 || N % 128 || N < 128) return false;
@@ -1158,11 +1314,14 @@ bool launch_gemmp_nn_acc(const uint16_t* dy, const uint16_t* W, uint16_t* dx, in
 
 bool launch_gemmp_nn(const uint16_t* dy, const uint16_t* W, uint16_t* dx, const uint16_t* aux, int act,
                      int T, int N, int K, int ncu, hipStream_t s, float* colpart) {
-  if (!g256_enabled() || T % 256 || K % 256 || N % 128 || N < 128 || act < 0 || act > 4) return false;
+  if (!g256_enabled() || T % 256 || K % 256 || N % 128 || N < 128 || act < 0 || act > 5) return false;
   uint16_t* ax = const_cast<uint16_t*>(aux);
   if (act == 0 || aux == nullptr) {
     if (colpart) return false;
     gemmp_go<true, 0, 0>(dy, N, W, K, T, K, N, dx, nullptr, nullptr, ncu, s);
+  } else if (act == 5) {  // aux: u8 act' codes in the tile-native layout of an EPI 8 forward
+    if (colpart) gemmp_go<true, 4, 5>(dy, N, W, K, T, K, N, dx, nullptr, ax, ncu, s, colpart);
+    else gemmp_go<true, 3, 5>(dy, N, W, K, T, K, N, dx, nullptr, ax, ncu, s);
   } else if (colpart) {
     if (act == 1) gemmp_go<true, 4, 1>(dy, N, W, K, T, K, N, dx, nullptr, ax, ncu, s, colpart);
     else if (act == 2) gemmp_go<true, 4, 2>(dy, N, W, K, T, K, N, dx, nullptr, ax, ncu, s, colpart);
@@ -1293,5 +1452,7 @@ bool launch_gemm256_wgrad_multi(const uint16_t* const* dys, const uint16_t* cons
   }
   return true;
 }
+
+DPA_RNG_BASE_EXPORT(gemm256)
 
 }  // namespace dpa

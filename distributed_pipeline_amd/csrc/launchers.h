@@ -66,7 +66,8 @@ bool launch_add_ln_bwd(const uint16_t* dout, const uint16_t* hsave, const float*
                        hipStream_t s, const uint16_t* dh_in = nullptr, bool post = false,
                        int zero_mask = 7, float* ws = nullptr, int part_mode = 0,
                        const uint16_t* beta = nullptr,    // beta: `hsave` is the LN output ...
-                       const uint16_t* hcopy = nullptr);  // ... and hcopy the guarded h copy
+                       const uint16_t* hcopy = nullptr,   // ... and hcopy the guarded h copy
+                       bool pair_hash = false);           // dy's dropout bits: common.h pair_hash
 // the deferred second stage of part_mode 1/2 (R = the rows of each summed micro-batch)
 bool launch_ln_colreduce(const float* part, int64_t R, int D, float* dg, float* db, float* dyb, hipStream_t s);
 // dpos[L][H] (zeroed; += sum over b) and dtemb[B][H] (= sum over l) of a [B][L][H] bf16 gradient in
@@ -147,6 +148,16 @@ bool launch_diff_loss_bwd(const float* x_start, const void* out, bool out_bf16, 
 void launch_timestep_emb(const float* ts, int B, int dim, float max_period, uint16_t* out,
                          hipStream_t s);
 
+// ---- sort.hip: counting sort of token ids, stable 0/1 partition ---------------------
+// ids into V + 1 buckets (out-of-range ids -> bucket V); ws: id_sort_workspace_ints(V) ints.
+// Equal ids end up adjacent (order inside a bucket unspecified).  false: V >= 2^17 or n == 0.
+int64_t id_sort_workspace_ints(int V);
+bool launch_id_bucket_sort(const int64_t* ids, int64_t n, int V, int* ws, int64_t* sorted, int64_t* perm,
+                           hipStream_t s);
+// order = indices of the nonzero mask entries, then of the zero ones, each in index order
+int64_t partition01_workspace_ints(int64_t n);
+bool launch_partition01(const int64_t* mask, int64_t n, int* blk_ws, int64_t* order, hipStream_t s);
+
 // ---- gemm.hip (bf16 MFMA GEMMs of Linear layers) ----------------------------------
 bool launch_gemm_nt(const uint16_t* x, const uint16_t* W, const uint16_t* bias, uint16_t* y,
                     uint16_t* z, int T, int N, int K, int act, hipStream_t s,
@@ -179,9 +190,15 @@ bool launch_gemm256_wgrad_multi(const uint16_t* const* dys, const uint16_t* cons
 //       when zderiv (backward act code 4 multiplies by it)
 //   nn: dx[T][K] = dy[T][N] W[N][K] (* act'(aux[T][K]) when aux; act 4: * aux); colpart (nullable, needs
 //       aux): per-tile column-sum partials [(T/256)*2][K] of dx (the bias gradient)
+//       z8 (with zderiv): act'(z) as u8 codes in a tile-native layout ([T * N] bytes; only the
+//       persistent data-gradient kernel reads it: launch_gemmp_nn act 5)
 bool launch_gemmp_nt(const uint16_t* x, const uint16_t* W, const uint16_t* bias, uint16_t* y,
                      uint16_t* z, int T, int N, int K, int act, int ncu, hipStream_t s,
-                     bool zderiv = false, int hm = 0);
+                     bool zderiv = false, int hm = 0, bool z8 = false);
+//   nt_res: h[T][N] = res + dropout_p(x W^T + bias), pair-hash dropout bits (common.h pair_hash)
+bool launch_gemmp_nt_res(const uint16_t* x, const uint16_t* W, const uint16_t* bias, const uint16_t* res,
+                         uint16_t* h, int T, int N, int K, int ncu, hipStream_t s, float p, uint32_t seed,
+                         uint32_t offset);
 bool launch_gemmp_nn(const uint16_t* dy, const uint16_t* W, uint16_t* dx, const uint16_t* aux, int act,
                      int T, int N, int K, int ncu, hipStream_t s, float* colpart);
 bool launch_gemmp_nn_acc(const uint16_t* dy, const uint16_t* W, uint16_t* dx, int T, int N, int K, int ncu,
@@ -193,5 +210,6 @@ void rng_base_add_attention(uint32_t d, hipStream_t s);
 void rng_base_add_attention128(uint32_t d, hipStream_t s);
 void rng_base_add_diffusion(uint32_t d, hipStream_t s);
 void rng_base_add_norm(uint32_t d, hipStream_t s);
+void rng_base_add_gemm256(uint32_t d, hipStream_t s);
 
 }  // namespace dpa

@@ -133,21 +133,4 @@ __device__ __forceinline__ int xcd_remap(int id, int total) {
   return base + (id >> 3);
 }
 
-// Cheap 32-bit hash (lowbias32) for dropout masks inside matrix-core loops.
-__device__ __forceinline__ uint32_t lowbias32(uint32_t x) {
-  x ^= x >> 16; x *= 0x7feb352du; x ^= x >> 15; x *= 0x846ca68bu; x ^= x >> 16;
-  return x;
-}
-
-// One-multiply finaliser for the per-element attention dropout bits (v_mul_lo_u32 is
-// quarter rate, so each multiply dropped saves 12 issue cycles per key pair); keep
-// rate, neighbour correlations and per-row variance match lowbias32 within noise over
-// 1024 x 1024 masks (measured host-side).
-__device__ __forceinline__ uint32_t mix32(uint32_t x) {
-  x ^= x >> 16;
-  x *= 0x7feb352du;
-  x ^= x >> 15;
-  return x;
-}
-
 }  // namespace dpa

@@ -111,6 +111,27 @@ __device__ __forceinline__ void dropout_keep(uint32_t seed, uint32_t offset, int
   }
 }
 
+// keep bits of the pair-hash mode (common.h pair_hash): the post-LN sublayers whose residual +
+// dropout run in the producing GEMM's epilogue (gemm256.hip EPI 7) regenerate them here.
+template <int VEC>
+__device__ __forceinline__ void dropout_keep_pair(uint32_t sm, uint32_t thr16, int64_t row, int ln, bool* keep) {
+  using M = RowMap<VEC>;
+  if constexpr (M::CH % 2 == 0) {
+#pragma unroll
+    for (int i = 0; i < VEC; i += 2) {  // elements i, i + 1 are columns 2j, 2j + 1 of one pair
+      const uint32_t h = pair_hash(sm, (uint32_t)row, (uint32_t)M::col(ln, i));
+      keep[i] = (h & 0xffffu) >= thr16;
+      keep[i + 1] = (h >> 16) >= thr16;
+    }
+  } else {
+#pragma unroll
+    for (int i = 0; i < VEC; ++i) {
+      const uint32_t col = (uint32_t)M::col(ln, i);
+      keep[i] = pair_keep(pair_hash(sm, (uint32_t)row, col), col, thr16);
+    }
+  }
+}
+
 // 1 / gamma for the output-based backward (xhat = (o - b) / gamma, the "memory-efficient"
 // LayerNorm backward; used only when every |gamma| >= LN_XO_GMIN, so never 0 there).
 __device__ __forceinline__ float inv_gamma(float g) { return g != 0.f ? 1.f / g : 0.f; }
@@ -210,7 +231,8 @@ __global__ void __launch_bounds__(256) add_ln_fwd_kernel(
 // (4 waves per SIMD: the LDS reduction buffer allows 4 blocks per CU); D > 768 keeps
 // 6 x VEC live accumulator/row floats: 4 waves per SIMD up to D = 768, 2-3 up to D = 1024.
 // D >= 1536 takes add_ln_bwd_rowblk_kernel (one row per block) instead.
-template <int VEC, bool POST, bool XO>
+// HK: the dy dropout bits come from the pair hash (pre-dropout placement only)
+template <int VEC, bool POST, bool XO, bool HK = false>
 __global__ void __launch_bounds__(256, VEC <= 12 ? 4 : VEC <= 16 ? 2 : 1) add_ln_bwd_kernel(
     const bf16_t* __restrict__ dout, const bf16_t* __restrict__ hsave,
     const float* __restrict__ mean_in, const float* __restrict__ rstd_in,
@@ -245,17 +267,34 @@ __global__ void __launch_bounds__(256, VEC <= 12 ? 4 : VEC <= 16 ? 2 : 1) add_ln
 #pragma unroll
   for (int i = 0; i < VEC; ++i) { adg[i] = 0.f; adb[i] = 0.f; ady[i] = 0.f; }
   const float sc = p > 0.f ? 1.f / (1.f - p) : 1.f;
+  const uint32_t hsm = HK ? pair_seedmix(seed, offset + rng_base()) : 0u, hthr = pair_thr16(p);
   for (int64_t row = (int64_t)blockIdx.x * 4 + w; row < R; row += (int64_t)gridDim.x * 4) {
     float h[VEC], d[VEC];
     RowIO<VEC>::load(hsrc + row * D, lane, h);
     RowIO<VEC>::load(dout + row * D, lane, d);
+    // pair-hash mode: every load of the row issued before any math, the keep bits computed
+    // under their latency (left to itself the scheduler interleaved the cheap hash with the
+    // loads and waited on each: 0.40 vs 0.31 ms per call at 262144 x 768)
+    uint32_t kbits = 0;
+    float mean_h = 0.f, rstd_h = 0.f;
+    if constexpr (HK) {
+      mean_h = mean_in[row];
+      rstd_h = rstd_in[row];
+      __builtin_amdgcn_sched_barrier(0);
+      if (p > 0.f) {
+        bool keep[VEC];
+        dropout_keep_pair<VEC>(hsm, hthr, row, lane, keep);
+#pragma unroll
+        for (int i = 0; i < VEC; ++i) kbits |= keep[i] ? (1u << i) : 0u;
+      }
+    }
     if (POST && p > 0.f) {
       bool keep[VEC];
       dropout_keep<VEC>(seed, offset, row, lane, p, keep);
 #pragma unroll
       for (int i = 0; i < VEC; ++i) d[i] = keep[i] ? d[i] * sc : 0.f;
     }
-    const float mean = XO && xo ? 0.f : mean_in[row], rstd = rstd_in[row];
+    const float mean = HK ? mean_h : (XO && xo ? 0.f : mean_in[row]), rstd = HK ? rstd_h : rstd_in[row];
     // opaque zero per row: keeps the loop-invariant LDS reads of cst inside the row loop
     int zo = 0;
     if constexpr (XO) asm volatile("v_mov_b32 %0, 0" : "=v"(zo));
@@ -290,10 +329,15 @@ __global__ void __launch_bounds__(256, VEC <= 12 ? 4 : VEC <= 16 ? 2 : 1) add_ln
     if (dres) RowIO<VEC>::store(dres + row * D, lane, d);
     if (dy) {
       if (!POST && p > 0.f) {
-        bool keep[VEC];
-        dropout_keep<VEC>(seed, offset, row, lane, p, keep);
+        if constexpr (HK) {
 #pragma unroll
-        for (int i = 0; i < VEC; ++i) d[i] = keep[i] ? d[i] * sc : 0.f;
+          for (int i = 0; i < VEC; ++i) d[i] = ((kbits >> i) & 1u) ? d[i] * sc : 0.f;
+        } else {
+          bool keep[VEC];
+          dropout_keep<VEC>(seed, offset, row, lane, p, keep);
+#pragma unroll
+          for (int i = 0; i < VEC; ++i) d[i] = keep[i] ? d[i] * sc : 0.f;
+        }
       }
       RowIO<VEC>::store(dy + row * D, lane, d);
       if (dyb) {
@@ -334,7 +378,7 @@ __global__ void __launch_bounds__(256, VEC <= 12 ? 4 : VEC <= 16 ? 2 : 1) add_ln
 // VGPRs - one wave per SIMD), and the block's column sums need no cross-wave reduction.  The two
 // row sums cross the 4 waves through LDS (double-buffered by row parity: one barrier per row).
 // Column sums always two-stage: part[block][3][D].
-template <int D, bool POST, bool XO>
+template <int D, bool POST, bool XO, bool HK = false>
 __global__ void __launch_bounds__(256) add_ln_bwd_rowblk_kernel(
     const bf16_t* __restrict__ dout, const bf16_t* __restrict__ hsave,
     const float* __restrict__ mean_in, const float* __restrict__ rstd_in,
@@ -385,8 +429,18 @@ __global__ void __launch_bounds__(256) add_ln_bwd_rowblk_kernel(
       }
     }
   };
-  // same (row, col) -> Philox word map as dropout_keep
+  // same (row, col) -> Philox word map as dropout_keep (HK: the pair hash of dropout_keep_pair)
+  const uint32_t hsm = HK ? pair_seedmix(seed, offset + rng_base()) : 0u, hthr = pair_thr16(p);
   auto keep_mask = [&](int64_t row, bool* keep) {
+    if constexpr (HK) {
+#pragma unroll
+      for (int i = 0; i < VT; i += 2) {  // CH even: elements i, i + 1 are one column pair
+        const uint32_t h = pair_hash(hsm, (uint32_t)row, (uint32_t)col(i));
+        keep[i] = (h & 0xffffu) >= hthr;
+        keep[i + 1] = (h >> 16) >= hthr;
+      }
+      return;
+    }
     const uint32_t thr = (uint32_t)(p * 4294967296.0);
 #pragma unroll
     for (int i = 0; i < VT; i += 2) {
@@ -594,7 +648,7 @@ static void ln_bwd_impl(const uint16_t* dout, const uint16_t* hsave, const float
                         const float* rstd, const uint16_t* g, uint16_t* dres, uint16_t* dy,
                         float* dyb, float* dg, float* db, int64_t R, float p, uint32_t seed,
                         uint32_t off, const uint16_t* dh_in, bool post, int zero_mask, hipStream_t s,
-                        float* ws, int part_mode, const uint16_t* beta, const uint16_t* hcopy) {
+                        float* ws, int part_mode, const uint16_t* beta, const uint16_t* hcopy, bool hk) {
   constexpr int D = VEC * 64;
   const int64_t nb2 = ln_bwd_two_stage_blocks(R, D);
   const bool two_stage = ws != nullptr && nb2 > 0;
@@ -619,26 +673,28 @@ static void ln_bwd_impl(const uint16_t* dout, const uint16_t* hsave, const float
   const bf16_t* bt = (const bf16_t*)beta;
   if constexpr (D >= LN_WIDE_D) {
     if (two_stage) {
-#define DPA_LN_ROWBLK(P, X)                                                                                 \
-  hipLaunchKernelGGL((add_ln_bwd_rowblk_kernel<D, P, X>), dim3(nb), dim3(256), 0, s, (const bf16_t*)dout, \
+#define DPA_LN_ROWBLK(P, X, H)                                                                              \
+  hipLaunchKernelGGL((add_ln_bwd_rowblk_kernel<D, P, X, H>), dim3(nb), dim3(256), 0, s, (const bf16_t*)dout, \
                      (const bf16_t*)hsave, mean, rstd, (const bf16_t*)g, (bf16_t*)dres, (bf16_t*)dy,      \
                      dyb_k != nullptr, R, p, seed, off, (const bf16_t*)dh_in, part, pacc, bt,    \
                      (const bf16_t*)hcopy)
-      if (post) DPA_LN_ROWBLK(true, false);
-      else if (xo) DPA_LN_ROWBLK(false, true);
-      else DPA_LN_ROWBLK(false, false);
+      if (post) DPA_LN_ROWBLK(true, false, false);
+      else if (hk) DPA_LN_ROWBLK(false, false, true);
+      else if (xo) DPA_LN_ROWBLK(false, true, false);
+      else DPA_LN_ROWBLK(false, false, false);
 #undef DPA_LN_ROWBLK
       if (reduce) ln_colreduce_launch(part, nb, D, dg, db, dyb_k, s);
       return;
     }
   }
-#define DPA_LN_BWD(P, X)                                                                                     \
-  hipLaunchKernelGGL((add_ln_bwd_kernel<VEC, P, X>), dim3(nb), dim3(256), 0, s, (const bf16_t*)dout,         \
+#define DPA_LN_BWD(P, X, H)                                                                                  \
+  hipLaunchKernelGGL((add_ln_bwd_kernel<VEC, P, X, H>), dim3(nb), dim3(256), 0, s, (const bf16_t*)dout,      \
                      (const bf16_t*)hsave, mean, rstd, (const bf16_t*)g, (bf16_t*)dres, (bf16_t*)dy, dyb_k, dg, \
                      db, R, p, seed, off, (const bf16_t*)dh_in, part, pacc, bt, (const bf16_t*)hcopy)
-  if (post) DPA_LN_BWD(true, false);
-  else if (xo) DPA_LN_BWD(false, true);
-  else DPA_LN_BWD(false, false);
+  if (post) DPA_LN_BWD(true, false, false);
+  else if (hk) DPA_LN_BWD(false, false, true);
+  else if (xo) DPA_LN_BWD(false, true, false);
+  else DPA_LN_BWD(false, false, false);
 #undef DPA_LN_BWD
   if (two_stage && reduce) ln_colreduce_launch(part, nb, D, dg, db, dyb_k, s);
 }
@@ -721,10 +777,11 @@ bool launch_add_ln_bwd(const uint16_t* dout, const uint16_t* hsave, const float*
                        const float* rstd, const uint16_t* g, uint16_t* dres, uint16_t* dy, float* dyb,
                        float* dg, float* db, int64_t R, int D, float p, uint32_t seed, uint32_t off,
                        hipStream_t s, const uint16_t* dh_in, bool post, int zero_mask, float* ws,
-                       int part_mode, const uint16_t* beta, const uint16_t* hcopy) {
+                       int part_mode, const uint16_t* beta, const uint16_t* hcopy, bool pair_hash) {
   if (beta && (post || !hcopy)) return false;  // a post-dropout output cannot be inverted
+  if (pair_hash && (post || beta)) return false;  // the pair-hash bits are the pre-dropout GEMM epilogue's
   DPA_LN_DISPATCH(D, ln_bwd_impl, dout, hsave, mean, rstd, g, dres, dy, dyb, dg, db, R, p, seed,
-                  off, dh_in, post, zero_mask, s, ws, part_mode, beta, hcopy)
+                  off, dh_in, post, zero_mask, s, ws, part_mode, beta, hcopy, pair_hash)
   return true;
 }
 

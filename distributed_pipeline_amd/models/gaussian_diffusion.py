@@ -260,7 +260,7 @@ class GaussianDiffusion:
             # only masked tokens count (the logged nll): sort them first and mark the rest
             # ignored, so the fused CE kernel skips whole blocks of them (same values)
             fm = mask.reshape(-1)
-            order = torch.argsort(fm, descending=True, stable=True)
+            order = _mask_first_order(fm)
             ids_s = torch.where(fm[order] != 0, input_ids.reshape(-1)[order], -100)
             per_s = net.token_nll(x.reshape(B * L, -1)[order], ids_s)
             per_tok = torch.empty_like(per_s).scatter_(0, order, per_s).view(B, L)
@@ -270,6 +270,17 @@ class GaussianDiffusion:
             m = mask.to(per_tok.dtype)
             return (per_tok * m).sum(-1) / m.sum(-1).clamp_min(1.0)
         return per_tok.mean(-1)
+
+
+def _mask_first_order(fm):
+    """Indices of the nonzero mask entries, then of the zero ones, each in index order: the
+    stable 0/1 partition kernel (csrc/sort.hip, two passes over the mask) on the GPU instead
+    of a general stable argsort."""
+    from ..ops._ext import get_ext
+    ext = get_ext() if fm.is_cuda else None
+    if ext is not None and hasattr(ext, "partition01") and fm.dtype == torch.int64:
+        return ext.partition01(fm)
+    return torch.argsort(fm, descending=True, stable=True)
 
 
 _NLL_SIDE = {}
@@ -286,9 +297,10 @@ def _nll_side_stream(dev):
             or torch.cuda.is_current_stream_capturing()):  # a captured step logs after replay
         return None
     if dev not in _NLL_SIDE:
-        # a pool stream: it shifts which pool streams (hardware queues) an overlapped schedule
-        # run later in the process gets (222 -> 240 ms/step; a high-priority stream: 347)
-        _NLL_SIDE[dev] = torch.cuda.Stream(device=dev)
+        # the stream plan's own queue (a torch pool stream shifted which pool streams - hardware
+        # queues - an overlapped schedule run later in the process got: 222 -> 240 ms/step)
+        from ..runtime.streams import plan_stream
+        _NLL_SIDE[dev] = plan_stream(dev, "nll")
     return _NLL_SIDE[dev]
 
 

@@ -62,8 +62,23 @@ def _mm_fp32(a, b):
 # Linear (+ optional fused activation)
 # --------------------------------------------------------------------------- #
 
-# index = kernel act code; "deriv" (4): the saved operand is already act'(z)
-_ACTS = ("none", "gelu", "tanh", "silu", "deriv")
+# index = kernel act code; "deriv" (4): the saved operand is already act'(z); "deriv8" (5):
+# act'(z) as u8 codes in the persistent GEMM's tile-native layout (see act_q8_decode)
+_ACTS = ("none", "gelu", "tanh", "silu", "deriv", "deriv8")
+
+
+def act_q8_decode(z8, T, N):
+    """[T, N] fp32 act' from the u8 codes of ``gemm_nt(want_deriv=2)``.
+
+    Layout (csrc/gemm256.hip ``q8_off``): byte (((((mt*NT + nt)*8 + w)*8 + ro)*2 + k)*512 + ln*8 + e
+    holds element (mt*256 + qa*128 + wm*64 + i*16 + k*8 + ln//8, nt*256 + wn*64 + (ln%8)*8 + e)
+    with w = 4 wm + wn and ro = 4 qa + i.  Codes (``q8_code``): min((c - 19) * 0.5 / 74,
+    (c + 35) / 256) - the first line below code 93, the second above."""
+    c = z8.view(T // 256, N // 256, 2, 4, 2, 4, 2, 8, 8, 8)  # mt nt wm wn qa i k lr lc e
+    c = c.permute(0, 4, 2, 5, 6, 7, 1, 3, 8, 9).reshape(T, N).float()
+    lo = (c - 19.0) * torch.tensor(0.5 / 74.0, dtype=torch.float32)
+    hi = c * (1.0 / 256.0) + 35.0 / 256.0
+    return torch.minimum(lo, hi)
 
 
 def _act_fwd(z, act):
@@ -85,6 +100,8 @@ def _act_bwd(dy, z, y, act):
     dyf = dy.float()
     if act == "deriv":  # z holds act'(pre-activation), saved by the forward epilogue
         return (dyf * z.float()).to(dy.dtype)
+    if act == "deriv8":  # the same as u8 codes
+        return (dyf * act_q8_decode(z, dy.shape[0], dy.shape[1])).to(dy.dtype)
     if act == "tanh":
         yf = y.float()
         return (dyf * (1.0 - yf * yf)).to(dy.dtype)
@@ -107,6 +124,8 @@ def _bias_act_fwd(z2d, b16, act):
 
 
 def _bias_act_bwd(dy2d, z, y, act, want_db):
+    if act == "deriv8":
+        z, act = act_q8_decode(z, dy2d.shape[0], dy2d.shape[1]).to(dy2d.dtype), "deriv"
     if native_ok(dy2d, kernel="bias_act_bwd") and dy2d.dtype == torch.bfloat16 and dy2d.shape[-1] % 8 == 0:
         zy = z if z is not None else (y if y is not None else dy2d)
         dz, db = get_ext().bias_act_bwd(dy2d, zy, _ACTS.index(act), want_db)
@@ -133,6 +152,13 @@ GEMM_MODE = os.environ.get("DPA_GEMM", "auto")
 _QKV_HEAD_MAJOR = os.environ.get("DPA_QKV_HEAD_MAJOR", "1") != "0"
 # forward GEMM epilogues store act'(z) instead of z for the backward (DPA_SAVE_ACT_DERIV=0: z)
 _SAVE_ACT_DERIV = os.environ.get("DPA_SAVE_ACT_DERIV", "1") != "0"
+# ... and, for the fused MLP (whose backward is the persistent dact GEMM), as 8-bit codes:
+# half the bytes of the largest store / load pair of the step (DPA_ACT_Q8=0: bf16 act')
+_ACT_Q8 = os.environ.get("DPA_ACT_Q8", "1") != "0"
+# post-LN sublayers: residual + dropout of the branch output in the producing GEMM's epilogue
+# (h = x + dropout(y) written once; the LayerNorm reads h alone and writes no h copy)
+# (DPA_RES_FUSE=0: the GEMM writes y and the LayerNorm kernel adds the residual)
+_RES_FUSE = os.environ.get("DPA_RES_FUSE", "1") != "0"
 # post-LN sublayers: the LayerNorm backward reconstructs xhat = (out - beta) / gamma from the
 # sublayer's output - which the next sublayer keeps alive anyway as its input - instead of
 # the forward writing a bf16 copy of h (one [T, D] store less per sublayer).  Guarded: a
@@ -427,19 +453,21 @@ def _accumulate_wgrad(p, dz, x2, bias):
     return dw_out, db_out
 
 
-def _lin_fwd(x2, w16, b16, act, route):
+def _lin_fwd(x2, w16, b16, act, route, q8=False):
     """Forward GEMM (+bias, +activation) of one Linear -> (y, z, zact).
 
     z is what the activation backward needs (gelu/silu; tanh's backward uses y):
     on the persistent kernel act'(pre-activation), computed in the forward epilogue
     together with act (the erf/exp work is shared, and the backward epilogue becomes
     one multiply), else the pre-activation.  zact names the backward rule for z:
-    "deriv" or ``act``."""
+    "deriv", "deriv8" (q8: u8 codes, only for a backward through gemm_nn_dact) or ``act``."""
     if route[0]:
-        y, z, is_d = get_ext().gemm_nt(x2, w16, b16, _ACTS.index(act),
-                                       _SAVE_ACT_DERIV and act in ("gelu", "silu"))
+        want = 0
+        if _SAVE_ACT_DERIV and act in ("gelu", "silu"):
+            want = 2 if (q8 and _ACT_Q8) else 1
+        y, z, mode = get_ext().gemm_nt(x2, w16, b16, _ACTS.index(act), want)
         if act in ("gelu", "silu"):
-            return y, z, ("deriv" if is_d else act)
+            return y, z, ("deriv8" if mode == 2 else "deriv" if mode == 1 else act)
     else:
         if b16 is not None and x2.is_cuda:
             z = torch.addmm(b16, x2, w16.t())  # hipBLASLt bias epilogue
@@ -603,12 +631,25 @@ def _dgrad_acc(dz, w16, native, dx_acc):
     return dx_acc.add_(_dgrad(dz, w16, native))
 
 
-def _mlp_fwd(x2, w1_16, b1_16, w2_16, b2_16, act):
+def _res_gemm(x2, w16, b16, res, route, drop):
+    """h = res + dropout(x2 W^T + b) in the GEMM epilogue (drop = (p, seed, offset)), or None
+    when that path is off or the shape does not tile."""
+    if not (_RES_FUSE and route[0] and drop is not None and res is not None):
+        return None
+    p, seed, off = drop
+    return get_ext().gemm_nt_res(x2, w16, b16, res, float(p), seed, off)
+
+
+def _mlp_fwd(x2, w1_16, b1_16, w2_16, b2_16, act, res=None, drop=None):
+    """-> (y, h, z1, cfg, fused): fused = y is already res + dropout(fc2 output) (_res_gemm)."""
     r1 = _route(x2, w1_16.shape[0], act)
-    h, z1, zact = _lin_fwd(x2, w1_16, b1_16, act, r1)
+    h, z1, zact = _lin_fwd(x2, w1_16, b1_16, act, r1, q8=True)
     r2 = _route(h, w2_16.shape[0], "none")
-    y, _, _ = _lin_fwd(h, w2_16, b2_16, "none", r2)
-    return y, h, z1, (zact, r1, r2)
+    y = _res_gemm(h, w2_16, b2_16, res, r2, drop)
+    fused = y is not None
+    if not fused:
+        y, _, _ = _lin_fwd(h, w2_16, b2_16, "none", r2)
+    return y, h, z1, (zact, r1, r2), fused
 
 
 def _mlp_bwd(dy2, x2, w1_16, w2_16, h, z1, params, cfg, need_dx, db2=None, dx_acc=None):
@@ -636,6 +677,8 @@ def _mlp_bwd(dy2, x2, w1_16, w2_16, h, z1, params, cfg, need_dx, db2=None, dx_ac
             db1 = _ACCUMULATED  # fc1's bias gradient went onto b1.grad (or its deferred slot)
     if dz1 is None:
         db1 = None
+        if act == "deriv8":  # no fused dact GEMM for this shape: decode the codes
+            z1, act = act_q8_decode(z1, dy2.shape[0], w2_16.shape[1]).to(dy2.dtype), "deriv"
         dh = _dgrad(dy2, w2_16, r2[1])
         if act != "none" or b1 is not None:
             # the activation backward reads dh anyway: it also sums db1
@@ -657,7 +700,7 @@ class _MLPFn(torch.autograd.Function):
     def forward(ctx, x, w1, b1, w2, b2, w1_16, b1_16, w2_16, b2_16, act):
         shp = x.shape
         x2, T = _pad_rows(x.reshape(-1, shp[-1]), (w1_16.shape[0], w2_16.shape[0]))
-        y, h, z1, cfg = _mlp_fwd(x2, w1_16, b1_16, w2_16, b2_16, act)
+        y, h, z1, cfg, _ = _mlp_fwd(x2, w1_16, b1_16, w2_16, b2_16, act)
         ctx.save_for_backward(x2, w1_16, w2_16, h, z1)
         ctx.params = (w1, b1, w2, b2)
         ctx.cfg = cfg
@@ -676,6 +719,22 @@ class _MLPFn(torch.autograd.Function):
         return dx, dw1, db1, dw2, db2, None, None, None, None, None
 
 
+def _ln_after_branch(y, x2, lw16, lb16, p, eps, seed, off, fused):
+    """LayerNorm of a post-LN sublayer -> (out, hsave, mean, rstd, xo).
+
+    fused: y already is h = x + dropout(branch) (the GEMM epilogue, pair-hash bits): the kernel
+    reads h alone, and h itself is what the backward keeps.  Otherwise the kernel adds the
+    dropped-out branch and the residual and writes the h copy (or, with DPA_LN_SAVE_OUT, only
+    where the output-based backward is unsafe: xo)."""
+    ext = get_ext()
+    if fused:
+        out, _, mean, rstd = ext.add_ln_fwd(y, None, lw16, lb16, 0.0, float(eps), 0, 0, save_h=False)
+        return out, y, mean, rstd, False
+    out, hsave, mean, rstd = ext.add_ln_fwd(y, x2, lw16, lb16, float(p), float(eps), seed, off,
+                                            h_guard=_LN_SAVE_OUT)
+    return out, hsave, mean, rstd, _LN_SAVE_OUT
+
+
 class _MLPLNFn(torch.autograd.Function):
     """Post-LN FFN sublayer as one op: out = LN(dropout(fc2(act(fc1(x)))) + x).
 
@@ -689,23 +748,22 @@ class _MLPLNFn(torch.autograd.Function):
                 seed, off):
         shp = x.shape
         x2 = x.reshape(-1, shp[-1])
-        y, h, z1, cfg = _mlp_fwd(x2, w1_16, b1_16, w2_16, b2_16, act)
-        out, hsave, mean, rstd = get_ext().add_ln_fwd(y, x2, lw16, lb16, float(p), float(eps), seed,
-                                                      off, h_guard=_LN_SAVE_OUT)
+        y, h, z1, cfg, fused = _mlp_fwd(x2, w1_16, b1_16, w2_16, b2_16, act, res=x2, drop=(p, seed, off))
+        out, hsave, mean, rstd, xo = _ln_after_branch(y, x2, lw16, lb16, p, eps, seed, off, fused)
         del y
-        ctx.save_for_backward(x2, w1_16, w2_16, h, z1, out if _LN_SAVE_OUT else hsave, mean, rstd, lw16,
-                              lb16 if _LN_SAVE_OUT else None, hsave if _LN_SAVE_OUT else None)
+        ctx.save_for_backward(x2, w1_16, w2_16, h, z1, out if xo else hsave, mean, rstd, lw16,
+                              lb16 if xo else None, hsave if xo else None)
         ctx.params = (w1, b1, w2, b2)
         ctx.ln_params = (lw, lb)
         ctx.cfg = cfg
-        ctx.ln = (p, seed, off)
+        ctx.ln = (p, seed, off, fused)
         ctx.shp = shp
         return out.reshape(shp)
 
     @staticmethod
     def backward(ctx, dout):
         x2, w1_16, w2_16, h, z1, hsave, mean, rstd, lw16, lb16, hcopy = ctx.saved_tensors
-        p, seed, off = ctx.ln
+        p, seed, off, fused = ctx.ln
         need_dx = ctx.needs_input_grad[0]
         lw, lb = ctx.ln_params
         b2 = ctx.params[3]
@@ -716,7 +774,7 @@ class _MLPLNFn(torch.autograd.Function):
                       if gb2 is not None else (None, False))
         dres, dy, dlw, dlb, dyb = get_ext().add_ln_bwd(
             d2, hsave, mean, rstd, lw16, float(p), seed, off, need_dx, True, True, dg_acc=dg, db_acc=dbl,
-            dyb_acc=gb2, part_buf=part, part_acc=pacc, beta=lb16, hcopy=hcopy)
+            dyb_acc=gb2, part_buf=part, part_acc=pacc, beta=lb16, hcopy=hcopy, pair_hash=fused)
         if b2 is not None and dyb is None:
             dyb = _ACCUMULATED  # fc2's bias gradient went onto b2.grad in the LN kernel
         dx, dw1, db1, dw2, db2 = _mlp_bwd(dy, x2, w1_16, w2_16, h, z1, ctx.params, ctx.cfg, need_dx,
@@ -756,15 +814,17 @@ class _AttnLNFn(torch.autograd.Function):
         o, lse = ext.attn_fwd(qkv3, heads, float(p_attn), False, seed_a, off_a, bool(hm))
         o2 = o.view(-1, o.shape[-1])
         ro = _route(o2, wo16.shape[0], "none")
-        y, _, _ = _lin_fwd(o2, wo16, bo16, "none", ro)
-        out, hsave, mean, rstd = get_ext().add_ln_fwd(y, x2, lw16, lb16, float(p), float(eps), seed_l,
-                                                      off_l, h_guard=_LN_SAVE_OUT)
+        y = _res_gemm(o2, wo16, bo16, x2, ro, (p, seed_l, off_l))
+        fused = y is not None
+        if not fused:
+            y, _, _ = _lin_fwd(o2, wo16, bo16, "none", ro)
+        out, hsave, mean, rstd, xo = _ln_after_branch(y, x2, lw16, lb16, p, eps, seed_l, off_l, fused)
         del y
-        ctx.save_for_backward(x2, qkv3, o, lse, wq16, wo16, out if _LN_SAVE_OUT else hsave, mean, rstd,
-                              lw16, lb16 if _LN_SAVE_OUT else None, hsave if _LN_SAVE_OUT else None)
+        ctx.save_for_backward(x2, qkv3, o, lse, wq16, wo16, out if xo else hsave, mean, rstd,
+                              lw16, lb16 if xo else None, hsave if xo else None)
         ctx.params = (wq, bq, wo, bo)
         ctx.ln_params = (lw, lb)
-        ctx.cfg = (heads, p_attn, seed_a, off_a, p, seed_l, off_l, rq, ro, bool(hm))
+        ctx.cfg = (heads, p_attn, seed_a, off_a, p, seed_l, off_l, rq, ro, bool(hm), fused)
         ctx.shp = shp
         return out.reshape(shp)
 
@@ -772,7 +832,7 @@ class _AttnLNFn(torch.autograd.Function):
     def backward(ctx, dout):
         x2, qkv3, o, lse, wq16, wo16, hsave, mean, rstd, lw16, lb16, hcopy = ctx.saved_tensors
         wq, bq, wo, bo = ctx.params
-        heads, p_attn, seed_a, off_a, p, seed_l, off_l, rq, ro, hm = ctx.cfg
+        heads, p_attn, seed_a, off_a, p, seed_l, off_l, rq, ro, hm, fused = ctx.cfg
         need_dx = ctx.needs_input_grad[0]
         ext = get_ext()
         lw, lb = ctx.ln_params
@@ -782,7 +842,7 @@ class _AttnLNFn(torch.autograd.Function):
                       if gbo is not None else (None, False))
         dres, dy, dlw, dlb, dyb = ext.add_ln_bwd(
             d2, hsave, mean, rstd, lw16, float(p), seed_l, off_l, need_dx, True, True, dg_acc=dg, db_acc=dbl,
-            dyb_acc=gbo, part_buf=part, part_acc=pacc, beta=lb16, hcopy=hcopy)
+            dyb_acc=gbo, part_buf=part, part_acc=pacc, beta=lb16, hcopy=hcopy, pair_hash=fused)
         if bo is not None and dyb is None:
             dyb = _ACCUMULATED  # the out projection's bias gradient went onto bo.grad
         # out projection

@@ -1,0 +1,92 @@
+"""The step's stream plan: every side stream a training step uses, created once per device in a
+fixed order, each on a hardware queue of its own.
+
+HIP multiplexes a process's streams onto ``GPU_MAX_HW_QUEUES`` (4 on the MI355X boxes) pooled
+HSA queues; torch's pool streams (``torch.cuda.Stream()``) are handed out round-robin from a pool
+of 32 that was spread over those queues when the pool was created.  Which queue a side stream
+got therefore depended on how many pool streams had been taken before it, and two streams on one
+queue serialise: one extra pool stream taken by the logged-nll overlap moved the reference
+schedule's side streams and slowed it from 222 to 240 ms/step (profiles/nll_side_stream_ab_r4.txt).
+
+Here each role gets a stream created with a full CU mask (``stream_create(mode=1)``,
+csrc/runtime/streams.cpp): the CU mask is a queue property, so the runtime gives such a stream an
+HSA queue of its own, never shared with the compute stream, the other roles or torch's pool.
+Roles (reference call sites whose work they carry):
+
+=========  ==========================================================================
+compute    the current stream (not created here): forward, backward, optimizer
+side       second forward/backward stream of the overlapped micro-batch schedule
+           (utils/trainer.py ``_forward_backward_overlapped``; reference trainer.py:216-235)
+wgrad      deferred weight gradients of the un-armed micro-batches (ops/nn.py deferral)
+nll        the logged nll's forward-only vocabulary sweep (models/gaussian_diffusion.py)
+copy       H2D prefetch of the next batch (data/prefetch.py; reference trainer.py:210-213)
+=========  ==========================================================================
+
+The data plane's comm stream is the C++ reducer's own (csrc/comm/reducer.cpp), created on the
+highest-priority queue pool, which the compute stream (normal priority) never uses.
+
+``DPA_STREAM_PLAN=pool`` restores torch pool streams (A/B runs)."""
+import os
+
+import torch
+
+ROLES = ("side", "wgrad", "nll", "copy")
+
+
+class StreamPlan:
+    _plans = {}
+
+    def __init__(self, device, mode=None):
+        self.device = torch.device(device)
+        self.mode = mode or os.environ.get("DPA_STREAM_PLAN", "ordered")
+        self.streams = {}
+        if self.device.type != "cuda":
+            return
+        ext = None
+        if self.mode in ("ordered", "cumask"):
+            from ..ops._ext import get_ext
+            ext = get_ext()
+            if ext is None or not hasattr(ext, "stream_create"):
+                self.mode = "pool"
+        with torch.cuda.device(self.device):
+            for role in ROLES:  # fixed creation order
+                if self.mode == "ordered" and role == "copy":
+                    s = self.streams["nll"]  # 4 queues: the brief H2D prefetch shares the nll queue
+                elif self.mode in ("ordered", "cumask"):
+                    s = torch.cuda.ExternalStream(ext.stream_create(1 if self.mode == "cumask" else 0, 0),
+                                                  device=self.device)
+                else:
+                    s = torch.cuda.Stream(device=self.device)
+                self.streams[role] = s
+
+    @classmethod
+    def for_device(cls, device):
+        """The process-wide plan of ``device`` (created on first use, never destroyed)."""
+        device = torch.device(device)
+        if device.type == "cuda" and device.index is None:
+            device = torch.device("cuda", torch.cuda.current_device())
+        key = (device.type, device.index)
+        if key not in cls._plans:
+            cls._plans[key] = cls(device)
+        return cls._plans[key]
+
+    @staticmethod
+    def roles():
+        return ROLES
+
+    def get(self, role):
+        """The stream of ``role`` (None on CPU)."""
+        if role not in ROLES:
+            raise KeyError(role)
+        return self.streams.get(role)
+
+    def describe(self):
+        return {"mode": self.mode, "roles": list(ROLES),
+                "handles": {r: hex(s.cuda_stream) for r, s in self.streams.items()}}
+
+
+def plan_stream(device, role):
+    """Shorthand: the stream of ``role`` in ``device``'s plan (None on CPU)."""
+    if torch.device(device).type != "cuda":
+        return None
+    return StreamPlan.for_device(device).get(role)

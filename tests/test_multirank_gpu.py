@@ -2,6 +2,7 @@
 engine's bucket hooks, comm ordering and no_sync on real GPU streams, with the
 bf16 kernels in the loop.  (RCCL itself needs distinct GPUs; its path is the
 same engine code with backend "nccl".)"""
+import contextlib
 import os
 
 import pytest
@@ -184,3 +185,82 @@ def test_zero1_reduce_scatter_over_rccl_single_rank(wire):
     p.join(timeout=60)
     assert p.exitcode == 0
     torch.testing.assert_close(torch.from_numpy(sharded), torch.from_numpy(plain), rtol=1e-6, atol=1e-7)
+
+
+def _rccl_overlap_worker(port, comm, q):
+    """W = 1 over RCCL, the trainer's overlapped 4 x 64 schedule with weight-gradient deferral
+    and a bf16 wire: the buckets are packed / reduced from hooks that autograd runs on either of
+    two streams while the deferred weight gradients join before the armed last backward."""
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), DPA_REDUCER_COMM=comm)
+    torch.cuda.set_device(0)
+    dist.init_process_group("nccl", rank=0, world_size=1, device_id=torch.device("cuda:0"))
+    try:
+        from basic_utils import logger
+        from distributed_pipeline_amd.ops.nn import RNG
+        from utils.initialization import create_diffusion_from_config, create_model_from_config
+        from utils.trainer import DiffusionTrainLoop
+        logger.configure(dir="/tmp/dpa_rccl_overlap", format_strs=[])
+        torch.manual_seed(1234)
+        model = create_model_from_config(model="diffuseq", precision="bf16", config_name="tiny",
+                                         hidden_size=256, num_layers=2, num_heads=4, intermediate_size=1024,
+                                         vocab_size=3000, seq_len=128, hidden_dim=128, hidden_t_dim=128,
+                                         dropout=0.1).cuda()
+        diffusion, sampler = create_diffusion_from_config(diffusion_steps=100)
+        g = torch.Generator().manual_seed(7)
+        B, L = 256, 128
+        batch = {"input_ids": torch.randint(1000, 3000, (B, L), generator=g).cuda(),
+                 "input_mask": torch.cat([torch.zeros(B, 32, dtype=torch.long),
+                                          torch.ones(B, L - 32, dtype=torch.long)], 1).cuda()}
+        loop = DiffusionTrainLoop(diffusion=diffusion, schedule_sampler=sampler, model=model, data=iter([batch]),
+                                  batch_size=B, microbatch=64, lr=1e-4, ema_rate="0.9999", log_interval=1,
+                                  save_interval=10 ** 9, resume_checkpoint="", learning_steps=1,
+                                  checkpoint_path="/tmp/dpa_rccl_overlap", ddp_engine="native", precision="bf16",
+                                  exec_microbatch=-1, overlap_microbatches=True, defer_wgrad=4,
+                                  device_prefetch=False, bucket_cap_mb=1.0, first_bucket_mb=0.25,
+                                  grad_reduce_dtype="bf16")
+        eng = loop.ddp_model
+
+        def run(reduce):
+            eng.zero_grad()
+            torch.manual_seed(99)
+            RNG.counter = 0  # same noise / dropout / timesteps in both runs
+            loop.use_ddp = reduce
+            with (contextlib.nullcontext() if reduce else eng.no_sync()):
+                loop.forward_backward(batch)
+            launched = eng._native.next_bucket() if (reduce and eng._native is not None) else -1
+            if reduce:
+                eng.finalize()
+            torch.cuda.synchronize()
+            return eng.space.grad_flat.clone(), launched
+
+        local, _ = run(False)       # nothing armed: the local sum of the 4 micro-batches
+        reduced, launched = run(True)   # the armed last backward: every bucket over the bf16 wire
+        q.put((eng._native is not None, eng._native.direct() if eng._native is not None else False,
+               len(eng.buckets), launched, local.cpu().numpy(), reduced.cpu().numpy()))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("comm", ["direct", "pg"])
+def test_native_reducer_overlapped_schedule_bf16_wire_single_rank(comm):
+    """W = 1 RCCL, the overlapped micro-batch schedule, deferred weight gradients, bf16 wire:
+    the reduced gradient equals the local no-reduction gradient to bf16 rounding.  The one
+    single-rank configuration where a bucket packed before its last gradient contribution
+    (a mis-ordered arm / hook stream) shows: that element would miss part of its
+    sum.  ``pg``: collectives through the c10d process group, ordered on the armed stream."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    p = ctx.Process(target=_rccl_overlap_worker, args=(find_free_port(), comm, q))
+    p.start()
+    native, direct, nb, launched, local, reduced = q.get(timeout=300)
+    p.join(timeout=60)
+    assert p.exitcode == 0
+    assert native and direct == (comm == "direct"), (native, direct)
+    assert nb > 3 and launched == nb, (launched, nb)
+    local, reduced = torch.from_numpy(local), torch.from_numpy(reduced)
+    assert local.abs().sum() > 0
+    # the bf16 wire rounds every element once: within 2^-8 relative of the local sum
+    # (plus the fp32 atomic-order noise of two backward runs)
+    tol = 2.0 ** -8 * local.abs() + 1e-6 * local.abs().max()
+    bad = ((reduced - local).abs() > tol).float().mean().item()
+    assert bad < 1e-3, bad

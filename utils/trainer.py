@@ -33,6 +33,7 @@ import torch
 from torch.optim import AdamW
 
 from basic_utils import dist_util, logger
+from distributed_pipeline_amd.runtime.streams import plan_stream
 
 
 def _exists(path):
@@ -225,6 +226,7 @@ class TrainLoop:
 
         self._load_and_sync_parameters()
         self.device = next(self.model.parameters()).device
+        dist_util.claim_stream_plan(self.device)  # no-op if setup_dist / the caller made it
         if device_prefetch and self.device.type == "cuda" and self.data is not None:
             from data.prefetch import DevicePrefetcher
             self.data = DevicePrefetcher(self.data, self.device)  # SURVEY K-2
@@ -794,7 +796,7 @@ class TrainLoop:
         grad-ready events are recorded where the gradients are produced."""
         cur = torch.cuda.current_stream()
         if getattr(self, "_side_stream", None) is None:
-            self._side_stream = torch.cuda.Stream(device=self.device)
+            self._side_stream = plan_stream(self.device, "side")
         side = self._side_stream
         side.wait_stream(cur)  # batch copies / last step's optimizer update
         nch = len(starts)
@@ -854,7 +856,7 @@ class TrainLoop:
         # backward chain (DPA_WGRAD_SIDE_STREAM=0: on the backward's own stream)
         if os.environ.get("DPA_WGRAD_SIDE_STREAM", "1") != "0":
             if getattr(self, "_wgrad_stream", None) is None:
-                self._wgrad_stream = torch.cuda.Stream(device=self.device)
+                self._wgrad_stream = plan_stream(self.device, "wgrad")
             defer.stream = self._wgrad_stream
         else:
             defer.stream = None
