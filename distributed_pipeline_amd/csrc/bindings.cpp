@@ -153,10 +153,14 @@ static void emb_grad(const at::Tensor& ids, const at::Tensor& dy, at::Tensor& dW
 // onehot_scatter: the dW kernel leaves out the target one-hot (softmax only) and it is added
 // here as dW[t] -= g x_t, db[t] -= g over the valid targets, by the sorted segment-sum scatter
 // of the embedding backward - a compare, subtract and select less per logit in the kernel
+// dw_acc / db_acc: fp32 buffers of W's / b's shape (the parameters' flat .grad views) the kernel
+// accumulates into directly (its split-token partials are fp32 atomics anyway); the matching
+// results are then undefined - no zero-filled scratch and no autograd-side add per call
 static std::vector<at::Tensor> lxent_bwd(const at::Tensor& dloss, const at::Tensor& x,
                                          const at::Tensor& W, c10::optional<at::Tensor> b,
                                          const at::Tensor& tgt, const at::Tensor& lse, bool need_dx,
-                                         bool need_dw, bool need_db, bool onehot_scatter) {
+                                         bool need_dw, bool need_db, bool onehot_scatter,
+                                         c10::optional<at::Tensor> dw_acc, c10::optional<at::Tensor> db_acc) {
   check_lxent(x, W, b, tgt);
   CHECK_F32(dloss); CHECK_F32(lse); CHECK_CONTIG(dloss); CHECK_CONTIG(lse);
   const c10::DeviceGuard guard(x.device());
@@ -173,9 +177,14 @@ static std::vector<at::Tensor> lxent_bwd(const at::Tensor& dloss, const at::Tens
                            reinterpret_cast<uint16_t*>(dx.data_ptr()),
                            acc.defined() ? acc.data_ptr<float>() : nullptr, cur_stream());
   }
+  auto acc_ok = [&](const c10::optional<at::Tensor>& t, int64_t numel) {
+    return t.has_value() && t->defined() && t->scalar_type() == at::kFloat && t->is_contiguous() &&
+           t->numel() == numel && t->device() == x.device();
+  };
+  const bool ext_w = need_dw && acc_ok(dw_acc, (int64_t)V * E), ext_b = need_db && acc_ok(db_acc, V);
   if (need_dw || need_db) {
-    dW = at::zeros({V, E}, f32);
-    if (need_db) db = at::zeros({V}, f32);
+    dW = ext_w ? *dw_acc : at::zeros({V, E}, f32);
+    if (need_db) db = ext_b ? *db_acc : at::zeros({V}, f32);
     const bool scatter = onehot_scatter && need_dw && (E == 128 || E == 256);
     if (N > 0)
       dpa::launch_lxent_dw(bf_ptr(x), bf_ptr(W), opt_bf_ptr(b), tgt.data_ptr<int64_t>(),
@@ -188,7 +197,8 @@ static std::vector<at::Tensor> lxent_bwd(const at::Tensor& dloss, const at::Tens
       emb_grad(tgt, x.to(at::kFloat).mul_(ng.unsqueeze(1)), dW);  // ids outside [0, V) are skipped
       if (need_db) db.index_add_(0, tgt.clamp(0, V - 1), ng);
     }
-    if (!need_dw) dW = at::Tensor();
+    if (!need_dw || ext_w) dW = at::Tensor();
+    if (ext_b) db = at::Tensor();
   }
   return {dx, dW, db};
 }
@@ -1082,7 +1092,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("lxent_bwd", &lxent_bwd, "fused linear + cross-entropy backward -> (dx, dW fp32, db fp32)",
         pybind11::arg("dloss"), pybind11::arg("x"), pybind11::arg("W"), pybind11::arg("b"), pybind11::arg("tgt"),
         pybind11::arg("lse"), pybind11::arg("need_dx"), pybind11::arg("need_dw"), pybind11::arg("need_db"),
-        pybind11::arg("onehot_scatter") = false);
+        pybind11::arg("onehot_scatter") = false, pybind11::arg("dw_acc") = pybind11::none(),
+        pybind11::arg("db_acc") = pybind11::none());
   m.def("seq_pos_sums", &seq_pos_sums, "(sum over b, sum over l) of a [B*L, H] bf16 gradient in one read",
         pybind11::arg("d"), pybind11::arg("L"), pybind11::arg("need_pos"), pybind11::arg("need_temb"));
   m.def("xent_rows_fwd", &xent_rows_fwd, "row softmax-CE over bf16 logits [R, ld] -> (loss, lse)",

@@ -97,6 +97,50 @@ static int64_t ipc_allreduce_sim(std::vector<at::Tensor> ts, int64_t mode, int64
   return err.item<int>();
 }
 
+// The reducer's issue pattern on one device: steps x buckets of different sizes through ONE
+// staging buffer of 2 x cap floats per rank (cap = the largest bucket), the epoch advancing
+// per bucket across steps (so the parity half alternates bucket to bucket) and one-shot /
+// two-shot chosen per bucket exactly as BucketReducer::launch_direct does.  buckets[b][r] is
+// rank r's slice of bucket b; each bucket is all-reduced `steps` times in bucket order.
+static int64_t ipc_allreduce_sim_buckets(std::vector<std::vector<at::Tensor>> buckets, int64_t steps) {
+  TORCH_CHECK(!buckets.empty() && steps >= 1, "buckets and steps");
+  const int W = (int)buckets[0].size();
+  TORCH_CHECK(W >= 1 && W <= IPC_MAXW, "1..8 simulated ranks");
+  int64_t cap = 0;
+  for (auto& b : buckets) {
+    TORCH_CHECK((int)b.size() == W, "every bucket has one tensor per rank");
+    for (auto& t : b)
+      TORCH_CHECK(t.is_cuda() && t.scalar_type() == at::kFloat && t.is_contiguous() && t.numel() == b[0].numel(),
+                  "equal-size contiguous fp32 device tensors per bucket");
+    cap = std::max<int64_t>(cap, b[0].numel());
+    TORCH_CHECK((int64_t)ipc_allreduce_blocks(b[0].numel(), W, true) * W <= 1024,
+                "ipc_allreduce_sim_buckets: bucket too large to co-schedule its simulated ranks");
+  }
+  const c10::DeviceGuard guard(buckets[0][0].device());
+  auto opt = buckets[0][0].options();
+  at::Tensor stage = at::zeros({W, 2 * cap}, opt);
+  at::Tensor flags = at::zeros({W, IPC_FLAG_WORDS}, opt.dtype(at::kInt));
+  at::Tensor err = at::zeros({1}, opt.dtype(at::kInt));
+  IpcPeers peers{};
+  for (int r = 0; r < W; ++r) {
+    peers.stage[r] = stage[r].data_ptr<float>();
+    peers.flags[r] = reinterpret_cast<uint32_t*>(flags[r].data_ptr<int>());
+  }
+  hipStream_t s = c10::hip::getCurrentHIPStreamMasqueradingAsCUDA().stream();
+  uint32_t epoch = 0;
+  for (int64_t st = 0; st < steps; ++st)
+    for (auto& b : buckets) {
+      IpcData data{};
+      for (int r = 0; r < W; ++r) data.p[r] = b[r].data_ptr<float>();
+      const int64_t n = b[0].numel();
+      TORCH_CHECK(launch_ipc_allreduce(peers, data, W, 0, W, n, cap, epoch + 1, n * 4 > (256 << 10),
+                                       err.data_ptr<int>(), s),
+                  "ipc_allreduce_sim_buckets: bad arguments");
+      ++epoch;
+    }
+  return err.item<int>();
+}
+
 // 128 opaque bytes for ncclCommInitRank, created by one rank and shared by all.
 static pybind11::bytes rccl_unique_id() {
   ncclUniqueId id;
@@ -469,6 +513,8 @@ void register_comm(pybind11::module& m) {
   m.def("rccl_unique_id", &rccl_unique_id, "new RCCL unique id (bytes) for the reducer's communicator");
   m.def("ipc_allreduce_sim", &ipc_allreduce_sim,
         "single-device test of the IPC all-reduce: the W tensors play W ranks -> error word");
+  m.def("ipc_allreduce_sim_buckets", &ipc_allreduce_sim_buckets,
+        "single-device test of the reducer's IPC issue pattern: buckets[b][rank], steps -> error word");
   pybind11::class_<BucketReducer>(m, "BucketReducer")
       .def(pybind11::init<c10::intrusive_ptr<c10d::ProcessGroup>, at::Tensor, std::vector<int64_t>,
                           std::vector<int64_t>, bool, c10::optional<at::Tensor>, std::vector<int64_t>,

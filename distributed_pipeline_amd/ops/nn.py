@@ -15,6 +15,7 @@ buffer).  For bf16 compute an op reads the parameter's bf16 *shadow*
 every forward, and returns fp32 weight gradients so they accumulate straight
 into the flat fp32 gradient buffer.
 """
+import contextlib
 import math
 import os
 
@@ -261,6 +262,21 @@ class _WgradDeferral:
         self.ln_sites = {}    # id(gamma) -> [buf, R, D, dg, db, dyb, filled]
         self.bias_sites = {}  # id(bias) -> [buf, rows, K, gb, used]
         self.colsum = os.environ.get("DPA_DEFER_COLSUM", "1") != "0"
+        # debug (DPA_DEFER_CHECK=1): checksum every held operand when it is held and again when
+        # its launch runs - a held tensor whose memory was rewritten meanwhile is reported
+        self.check = os.environ.get("DPA_DEFER_CHECK", "0") == "1"
+        self.check_log = []
+
+    @staticmethod
+    def _sig(t):
+        return (float(t.detach().float().sum()), float(t.detach().float().abs().sum()))
+
+    def _verify(self, p, segs):
+        for i, s in enumerate(segs):
+            if len(s) > 2:
+                now = (self._sig(s[0]), self._sig(s[1]))
+                if now != s[2]:
+                    self.check_log.append((tuple(p.shape), i, s[2], now))
 
     def _cur(self, t):
         """The current stream (``cur``: set by the trainer per micro-batch, saving the
@@ -282,6 +298,9 @@ class _WgradDeferral:
         if cur is not None and side and self.stream is not None:
             run_on = self.stream
             run_on.wait_stream(cur)
+        if self.check:
+            self._verify(p, segs)
+        segs = [s[:2] for s in segs]
         if run_on is not None:
             for dz, x2 in segs:  # produced on other streams: keep them alive for run_on
                 dz.record_stream(run_on)
@@ -309,7 +328,7 @@ class _WgradDeferral:
                 segs, nb = [], 0
         else:
             segs, nb = [], 0
-        segs.append((dz, x2))
+        segs.append((dz, x2, (self._sig(dz), self._sig(x2))) if self.check else (dz, x2))
         nb += dz.numel() * dz.element_size() + x2.numel() * x2.element_size()
         if self.active and len(segs) < self.depth and self.held_bytes + nb <= self.budget_bytes:
             self.pending[key] = (p, bias, segs, nb)
@@ -435,12 +454,12 @@ def _accumulate_wgrad(p, dz, x2, bias):
     """
     ext = get_ext()
     dw_out = db_out = None
-    gw = p.grad
+    gw = p.grad if _INPLACE[0] else None
     if gw is None or gw.dtype != torch.float32 or not gw.is_contiguous():
         gw = dw_out = torch.zeros(p.shape, dtype=torch.float32, device=dz.device)
     gb = None
     if bias is not None and bias.requires_grad:
-        gb = bias.grad
+        gb = bias.grad if _INPLACE[0] else None
         if gb is None or gb.dtype != torch.float32:
             gb = db_out = torch.zeros(bias.shape, dtype=torch.float32, device=dz.device)
     if WGRAD_DEFER.offer(p, dz, x2, bias, gw, gb):
@@ -515,12 +534,30 @@ _ACCUMULATED = object()
 
 
 _GRAD_ACC = os.environ.get("DPA_LN_GRAD_ACC", "1") != "0"
+# In-place parameter gradients are an engine-internal contract: only inside the trainer's own
+# backward (``inplace_param_grads``) do the ops add into ``.grad`` and hand None to autograd.
+# Anywhere else (a user's ``loss.backward()``, ``torch.autograd.grad`` for a gradient penalty or
+# a norm probe) every parameter gradient is returned to autograd as usual.
+_INPLACE = [False]
+
+
+@contextlib.contextmanager
+def inplace_param_grads(on=True):
+    """Let the ops accumulate parameter gradients straight into the flat fp32 ``.grad`` buffers
+    for the duration (utils/trainer.py wraps its backward passes in this)."""
+    prev = _INPLACE[0]
+    _INPLACE[0] = bool(on)
+    try:
+        yield
+    finally:
+        _INPLACE[0] = prev
 
 
 def _grad_acc(p):
     """``p.grad`` when a kernel can accumulate onto it in place (the flat fp32 gradient
-    buffer views of the DDP engine), else None (the gradient is returned to autograd)."""
-    if p is None or not _GRAD_ACC:
+    buffer views of the DDP engine, inside ``inplace_param_grads``), else None (the gradient
+    is returned to autograd)."""
+    if p is None or not _GRAD_ACC or not _INPLACE[0]:
         return None
     g = p.grad
     if g is None or g.dtype != torch.float32 or not g.is_contiguous() or g.shape != p.shape:
@@ -1173,6 +1210,11 @@ def attention(qkv, n_heads, p=0.0, causal=False, training=True):
 # Fused linear + cross-entropy (tied lm_head), per-token loss
 # --------------------------------------------------------------------------- #
 
+# the fused CE weight gradient accumulates straight into the tied weight's flat fp32 .grad
+# (DPA_XENT_GRAD_ACC=0: into a zeroed scratch, then added by autograd)
+_XENT_GRAD_ACC = os.environ.get("DPA_XENT_GRAD_ACC", "1") != "0"
+
+
 class _LinearXentFn(torch.autograd.Function):
     """Per-token CE of x @ W^T + b, logits never materialised (csrc/xent.hip).  When x
     needs a gradient the forward also produces the unscaled input gradient
@@ -1199,12 +1241,18 @@ class _LinearXentFn(torch.autograd.Function):
         dxu, ctx.dxu = ctx.dxu, None
         g = dloss.contiguous().float()
         need_dx = ctx.needs_input_grad[0] and dxu is None
-        dx, dw, db = get_ext().lxent_bwd(g, x, w16, b16, target, lse, need_dx, ctx.needs_input_grad[1],
-                                         ctx.has_b and ctx.needs_input_grad[2], _XENT_ONEHOT_SCATTER)
+        w, b = ctx.wb
+        need_dw, need_db = ctx.needs_input_grad[1], ctx.has_b and ctx.needs_input_grad[2]
+        # straight into the flat fp32 .grad buffers when they exist (the kernel's partials are
+        # atomics: no zero-filled [V, E] scratch and no add per call)
+        acc = _XENT_GRAD_ACC
+        gw, gb = (_grad_acc(w) if need_dw and acc else None), (_grad_acc(b) if need_db and acc else None)
+        dx, dw, db = get_ext().lxent_bwd(g, x, w16, b16, target, lse, need_dx, need_dw, need_db,
+                                         _XENT_ONEHOT_SCATTER, dw_acc=gw, db_acc=gb)
         if dxu is not None:
             dx = dxu.mul_(g.unsqueeze(1)).to(x.dtype)
-        w, b = ctx.wb
-        return dx, _into_grad(w, dw), _into_grad(b, db), None, None, None
+        return (dx, None if (need_dw and gw is not None) else _into_grad(w, dw),
+                None if (need_db and gb is not None) else _into_grad(b, db), None, None, None)
 
 
 def _pad_vocab(w16, b16, mult=256):

@@ -184,7 +184,11 @@ class DDPEngine(nn.Module):
                 numel, process_group=process_group, device=torch.device(dev))
             if first_bucket_mb is None or first_bucket_mb <= 0:
                 first_bucket_mb = tuned_first
-            first_bucket_mb = min(first_bucket_mb, bucket_cap_mb)
+        elif first_bucket_mb is None or first_bucket_mb <= 0:
+            # an explicit cap with the first bucket left at "auto": the fixed 4 MiB default (a
+            # 0 MiB first bucket would close after one parameter)
+            first_bucket_mb = 4.0
+        first_bucket_mb = min(first_bucket_mb, bucket_cap_mb)
         self.world_size = dist.get_world_size(self.pg) if self.distributed else 1
         self.rank = dist.get_rank(self.pg) if self.distributed else 0
         # (world 1 keeps the sharded machinery - one shard - so it can be exercised alone)
@@ -204,6 +208,16 @@ class DDPEngine(nn.Module):
         self._arm_stream = None      # the armed backward's stream (see _arm)
         self._next_launch = 0
         self.bucket_cap_mb, self.first_bucket_mb = bucket_cap_mb, first_bucket_mb
+        if self.bucket_tune is not None and (not self.distributed or dist.get_rank() == 0):
+            # measured sizes can differ run to run (and change the summation order): say which
+            # were taken; pass them back as --ddp_bucket_cap_mb / --ddp_first_bucket_mb to repeat
+            # a run bit for bit
+            try:
+                from basic_utils import logger
+                logger.log(f"DDP buckets: cap {bucket_cap_mb} MiB, first {first_bucket_mb} MiB (measured; "
+                           f"set them explicitly for a bitwise-reproducible rerun)")
+            except ImportError:  # pragma: no cover
+                pass
         self.buckets = [_Bucket(i, s, e, ps) for i, (s, e, ps) in
                         enumerate(plan_buckets(self.space, bucket_cap_mb, first_bucket_mb))]
         self._bucket_of = {}

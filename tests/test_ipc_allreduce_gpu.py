@@ -55,3 +55,28 @@ def test_ipc_allreduce_rejects_bad_shapes():
     xs = [torch.ones(6, device="cuda") for _ in range(2)]
     with pytest.raises(RuntimeError):
         ext.ipc_allreduce_sim(xs, 0, 1)
+
+
+@pytest.mark.parametrize("W", [2, 4, 8])
+def test_ipc_allreduce_reducer_issue_pattern(W):
+    """The BucketReducer's direct-mode sequence (csrc/comm/reducer.cpp launch_direct): buckets of
+    different sizes back to back through one staging buffer sized for the largest, the epoch
+    advancing per bucket (alternating parity halves bucket to bucket, across steps), one-shot
+    below 256 KiB and two-shot above - over 3 steps = 15 consecutive epochs.  All-ones inputs
+    make the expected value of every element W ** steps."""
+    ext = _ext()
+    sizes = [4096, 100_000, 64, 70_000, 24]  # 16 KiB / 400 KB / ... : both modes, odd sizes
+    steps = 3
+    buckets = [[torch.ones(n, device="cuda") for _ in range(W)] for n in sizes]
+    assert ext.ipc_allreduce_sim_buckets(buckets, steps) == 0
+    for b in buckets:
+        for x in b:
+            assert torch.all(x == float(W) ** steps), (x.numel(), x.unique())
+    # random data, one step: every bucket equals the fp64 sum of its rank slices
+    g = torch.Generator(device="cuda").manual_seed(W)
+    buckets = [[torch.randn(n, device="cuda", generator=g) for _ in range(W)] for n in sizes]
+    refs = [torch.stack(b).double().sum(0) for b in buckets]
+    assert ext.ipc_allreduce_sim_buckets(buckets, 1) == 0
+    for b, ref in zip(buckets, refs):
+        for x in b:
+            torch.testing.assert_close(x.double(), ref, rtol=1e-5, atol=1e-5)

@@ -1,6 +1,7 @@
 """Which HSA queue does each kind of HIP stream land on?  (the stream plan's evidence)
 
-Run under a kernel trace, then summarise the trace (no GPU needed for the second step):
+Run under a kernel trace, then summarise the trace (no GPU needed for the second step); the probe
+starts a world-1 RCCL process group the way a training job does:
 
     rocprofv3 --kernel-trace --output-format csv -d gpurun_out/sq -o sq -- python3 tools/probes/stream_queues.py
     python3 tools/probes/stream_queues.py --trace gpurun_out/sq
@@ -17,9 +18,16 @@ import sys
 
 
 def probe(out):
+    """The real start-up order of a W = 1 RCCL job: dist_util.setup_dist (which claims the
+    stream plan before RCCL), a DDPEngine whose C++ reducer owns the direct communicator and
+    its comm stream, then other kinds of streams for comparison."""
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=os.environ.get("SQ_PORT", "29517"), RANK="0",
+                      WORLD_SIZE="1", LOCAL_RANK="0")
     import torch
 
+    from basic_utils import dist_util
     from distributed_pipeline_amd.ops._ext import get_ext
+    from distributed_pipeline_amd.parallel.ddp import DDPEngine
     from distributed_pipeline_amd.runtime.streams import StreamPlan
     ext = get_ext(required=True)
     x = torch.zeros(1 << 16, device="cuda")
@@ -32,23 +40,27 @@ def probe(out):
         order.append({"name": name, "handle": hex(s.cuda_stream)})
 
     mark("default", torch.cuda.current_stream())
-    plan = StreamPlan(torch.device("cuda", 0))   # the trainer's plan: created before any pool stream
+    assert dist_util.setup_dist(silent=True)
+    plan = StreamPlan.for_device(torch.device("cuda", 0))
     for role in plan.roles():
         mark("plan:" + role, plan.get(role))
-    for i in range(6):
+    model = torch.nn.Linear(256, 256).cuda()
+    eng = DDPEngine(model, bucket_cap_mb=1.0, first_bucket_mb=0.25)
+    comm = eng._native.comm_stream() if eng._native is not None else 0
+    if comm:
+        mark("reducer_comm", torch.cuda.ExternalStream(comm))
+    for i in range(4):
         mark(f"pool{i}", torch.cuda.Stream())
-    for i in range(2):
-        mark(f"pool_high{i}", torch.cuda.Stream(priority=-1))
-    for i in range(2):
-        mark(f"plain{i}", torch.cuda.ExternalStream(ext.stream_create(0, 0)))
-    for i in range(2):
-        mark(f"cumask{i}", torch.cuda.ExternalStream(ext.stream_create(1, 0)))
+    mark("plain", torch.cuda.ExternalStream(ext.stream_create(0, 0)))
     least, greatest = torch.cuda.Stream.priority_range()
-    mark("prio_greatest", torch.cuda.ExternalStream(ext.stream_create(2, greatest)))  # the reducer's kind
+    mark("prio_greatest", torch.cuda.ExternalStream(ext.stream_create(2, greatest)))
     mark("default_again", torch.cuda.current_stream())
     with open(out, "w") as f:
-        json.dump({"order": order, "plan": plan.describe()}, f, indent=1)
+        json.dump({"order": order, "plan": plan.describe(), "direct_reducer": bool(comm)}, f, indent=1)
     print(json.dumps(order))
+    del eng
+    import torch.distributed as dist
+    dist.destroy_process_group()
 
 
 def summarise(d):
@@ -80,5 +92,3 @@ if __name__ == "__main__":
         out = os.environ.get("SQ_OUT", "gpurun_out/sq/order.json")
         os.makedirs(os.path.dirname(out), exist_ok=True)
         probe(out)
-        sys.stdout.flush()
-        os._exit(0)  # skip static teardown: under rocprofv3 the process segfaulted in exit handlers

@@ -537,6 +537,15 @@ class TrainLoop:
             return False
         if self._exec_auto or not isinstance(batch, dict) or not getattr(self, "graph_logging", False):
             return False
+        st = getattr(self, "_graph_state", None)
+        if st is not None:
+            # the captured graph reads static copies of the first batch's tensors: a batch of
+            # another shape / dtype (a short last batch, a new sequence length) runs eagerly
+            ins = st["inputs"]
+            if set(ins) != set(batch) or any(
+                    not torch.is_tensor(v) or v.shape != ins[k].shape or v.dtype != ins[k].dtype
+                    for k, v in batch.items()):
+                return False
         sampler = getattr(self, "schedule_sampler", None)
         return sampler is None or getattr(sampler, "graph_safe", False)
 
@@ -743,7 +752,7 @@ class TrainLoop:
                     defer.active = k < len(starts) - 1
                     if not defer.active:
                         defer.flush()
-                with self._range("backward"):
+                with self._range("backward"), self._inplace_grads():
                     self.backward_from_losses(losses)
                 if join is not None:
                     # a side-stream term (the logged nll) overlaps the backward: log after it
@@ -761,6 +770,16 @@ class TrainLoop:
                 defer.release_retired(torch.cuda.current_stream())
         if self._graph_capturing:
             self._graph_log_buf, self._loss_log_buf = self._loss_log_buf, None
+
+    def _inplace_grads(self):
+        """The native engine's ops add parameter gradients straight into its flat fp32 .grad
+        buffers during the trainer's own backward passes (ops/nn.py ``inplace_param_grads``):
+        no leaf gradient then crosses streams through AccumulateGrad in the overlapped
+        schedule.  Outside them every op returns its gradients to autograd."""
+        if self.engine_kind != "native":
+            return contextlib.nullcontext()
+        from distributed_pipeline_amd.ops.nn import inplace_param_grads
+        return inplace_param_grads()
 
     # ---- overlapped micro-batch schedule (several executed chunks per step) ----------
     def _tile_starved(self):
@@ -886,7 +905,7 @@ class TrainLoop:
                         self.ddp_model.arm_for_backward()
                     self.loss_scale = self._chunk_loss_scale(starts[k], min(n, starts[k] + self.exec_microbatch), n)
                     t0 = time.perf_counter()
-                    with self._range("backward"):
+                    with self._range("backward"), self._inplace_grads():
                         self.backward_from_losses(losses)
                     self.host_time["bwd"] += time.perf_counter() - t0
                     done = torch.cuda.Event()
