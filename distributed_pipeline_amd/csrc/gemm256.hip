@@ -239,7 +239,7 @@ __device__ __forceinline__ int opaque(int x) {
 // XS / extra (persistent kernel): `extra` = XS stores of the previous tile were
 // issued between this tile's prologue DMA and its first iteration, so the waits
 // of phases 0-3 of that iteration leave them in flight.
-template <int P, bool A_TR, bool B_TR, bool CS, bool SWAP = false, int XS = 0, int DRAIN = 0>
+template <int P, bool A_TR, bool B_TR, bool CS, bool SWAP = false, int XS = 0, int DRAIN = 0, bool HM = false>
 __device__ __forceinline__ void phase(f32x4 (&acc)[2][2][4][2], bf16x8 (&fa)[4][2],
                                       bf16x8 (&fb0)[2][2], bf16x8 (&fb1)[2][2], float& cs,
                                       const Operand<A_TR>& opA, const Operand<B_TR>& opB,
@@ -255,7 +255,7 @@ __device__ __forceinline__ void phase(f32x4 (&acc)[2][2][4][2], bf16x8 (&fa)[4][
     read4<img_off(bf, 0)>(fa, opA);
   } else if constexpr (q == 1) {
     read2<img_off(bf, 1)>(fb1, opB);
-  } else if constexpr (q == 2) {
+  } else if constexpr (q == 2 && !HM) {
     read4<img_off(bf, 1)>(fa, opA);
   }
   // group 0 sums the A0 image, group 1 the A1 image (wave-uniform branch)
@@ -288,8 +288,10 @@ __device__ __forceinline__ void phase(f32x4 (&acc)[2][2][4][2], bf16x8 (&fa)[4][
   __builtin_amdgcn_sched_barrier(0);
   if constexpr (q == 0) mfma_quadrant<0, 0, SWAP>(acc, fa, fb0);
   if constexpr (q == 1) mfma_quadrant<0, 1, SWAP>(acc, fa, fb1);
-  if constexpr (q == 2) mfma_quadrant<1, 1, SWAP>(acc, fa, fb1);
-  if constexpr (q == 3) mfma_quadrant<1, 0, SWAP>(acc, fa, fb0);
+  // HM (128-row tiles): the A1 image is a copy of A0 (DMA kept: the counted waits stay
+  // exact) and its two quadrants are skipped
+  if constexpr (q == 2 && !HM) mfma_quadrant<1, 1, SWAP>(acc, fa, fb1);
+  if constexpr (q == 3 && !HM) mfma_quadrant<1, 0, SWAP>(acc, fa, fb0);
   __builtin_amdgcn_sched_barrier(0);
   barrier();
 }
@@ -565,6 +567,8 @@ struct PEpi {
   // EPI 2 a second 16 (z and y), EPI 3/4 the 12 aux loads of rounds 2..7, EPI 4 two partial stores
   static constexpr int XS = (EPI == 2 || EPI == 6 || EPI == 8) ? 32 : (EPI == 3 || EPI == 5 || EPI == 7) ? 28
                             : EPI == 4 ? 30 : 16;
+  // 128-row tiles: 4 rounds (8 stores, EPI 2/6/8 16; aux loads of rounds 2..3)
+  static constexpr int XS_H = (EPI == 2 || EPI == 6 || EPI == 8) ? 16 : (EPI == 3 || EPI == 5 || EPI == 7) ? 12 : 8;
 };
 
 template <int ACT>
@@ -740,7 +744,7 @@ __device__ __forceinline__ void tile_mn(int t, int NT, int& mt, int& nt) {
   }
 }
 
-template <bool B_TR, int EPI, int ACT, int POL = 0, int GM = 1, int STG = 0, int DU = 0>
+template <bool B_TR, int EPI, int ACT, int POL = 0, int GM = 1, int STG = 0, int DU = 0, bool HMT = false>
 __global__ void __launch_bounds__(512) gemmp_kernel(const bf16_t* __restrict__ A, int64_t lda,
                                                     const bf16_t* __restrict__ B, int64_t ldb, int M, int N,
                                                     int nk, bf16_t* __restrict__ C, int64_t ldc,
@@ -748,7 +752,11 @@ __global__ void __launch_bounds__(512) gemmp_kernel(const bf16_t* __restrict__ A
                                                     bf16_t* __restrict__ Zout, float* __restrict__ colpart,
                                                     int* __restrict__ tile_ctr, int hm, EpiArgs ea) {
   __shared__ __attribute__((aligned(1024))) char smem[P_LDS];
-  constexpr int XS = PEpi<EPI>::XS;
+  // HMT: 128 x 256 tiles (twice the tiles of a small-T launch: the reference schedule's
+  // 8192-token micro-batches give a 768-wide layer 96 256-row tiles for 256 CUs)
+  static_assert(!(HMT && EPI == 4), "column-sum partials are laid out per 256-row tile");
+  constexpr int TM = HMT ? 128 : 256, NRO = HMT ? 4 : 8;
+  constexpr int XS = HMT ? PEpi<EPI>::XS_H : PEpi<EPI>::XS;
   constexpr bool DACT = EPI == 3 || EPI == 4 || EPI == 5;  // data-gradient epilogues reading aux
   constexpr bool AUXR = DACT || EPI == 7;                  // epilogues that read aux
   constexpr bool Q8 = DACT && ACT == 5;                    // aux = act' as tile-native u8 codes
@@ -758,7 +766,7 @@ __global__ void __launch_bounds__(512) gemmp_kernel(const bf16_t* __restrict__ A
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int wm = (w >> 2) & 1, wn = w & 3;
   const int grp = w >> 2;
-  const int NT = N / 256, ntiles = (M / 256) * NT;
+  const int NT = N / 256, ntiles = (M / TM) * NT;
   const int G = gridDim.x;
   const uint32_t sbase = lds_u32(smem);
   char* const smB = smem + B_REGION;
@@ -776,7 +784,8 @@ __global__ void __launch_bounds__(512) gemmp_kernel(const bf16_t* __restrict__ A
     int mt, nt;
     tile_mn<GM>(t, NT, mt, nt);
     const int lane = lane_id();
-    opA.init(A, lda, mt * 256, w, lane, wm, 64, sbase);
+    opA.init(A, lda, mt * TM, w, lane, wm, 64, sbase);
+    if constexpr (HMT) opA.hstep = 0;  // the A1 half image re-reads rows 0..127 (L2 hits)
     opB.init(B, ldb, nt * 256, w, lane, wn, 32, sbase + B_REGION, /*remap=*/true);
     // bias slot: the tile's 256 bf16 = 2 x (64 lanes x 4 B); every wave issues one such
     // DMA (waves of equal parity write identical bytes) so the vmcnt counts stay uniform
@@ -800,7 +809,7 @@ __global__ void __launch_bounds__(512) gemmp_kernel(const bf16_t* __restrict__ A
     int mt, nt;
     tile_mn<GM>(t, NT, mt, nt);
     const int qa = ro >> 2, i = ro & 3;
-    const int64_t row = (int64_t)mt * 256 + qa * 128 + wm * 64 + i * 16 + k * 8 + (ln >> 3);
+    const int64_t row = (int64_t)mt * TM + qa * 128 + wm * 64 + i * 16 + k * 8 + (ln >> 3);
     const int col = nt * 256 + wn * 64 + (ln & 7) * 8;
     if (hm) {
       // head-major store [R >> hm][ldc / 64][1 << hm][64]: row = (b, l), col = (head j, d); a
@@ -817,6 +826,10 @@ __global__ void __launch_bounds__(512) gemmp_kernel(const bf16_t* __restrict__ A
   auto q8_off = [&](int t, int ro, int k, int ln) -> int64_t {
     int mt, nt;
     tile_mn<GM>(t, NT, mt, nt);
+    if constexpr (HMT) {  // the 256-row tile's layout: 128-row tile mt is its rounds (mt & 1) * 4 + ro
+      ro += (mt & 1) * 4;
+      mt >>= 1;
+    }
     return (((((int64_t)mt * NT + nt) * 8 + w) * 8 + ro) * 2 + k) * 512 + ln * 8;
   };
   auto load_aux = [&](int t, int ro, int k, int ln) -> uint4 {
@@ -857,7 +870,7 @@ __global__ void __launch_bounds__(512) gemmp_kernel(const bf16_t* __restrict__ A
         }
       }
 #pragma unroll
-    for (int ro = 0; ro < 8; ++ro) {
+    for (int ro = 0; ro < NRO; ++ro) {
       const int qa = ro >> 2, i = ro & 3;
       // stage: pack (+bias), permlane16 swap, one 16-B row segment per qb
 #pragma unroll
@@ -891,16 +904,16 @@ __global__ void __launch_bounds__(512) gemmp_kernel(const bf16_t* __restrict__ A
           if (has_next) wait_vm<15>(); else wait_vm<2>();
         } else if (ro == 1) {
           if (has_next) wait_vm<17>(); else wait_vm<4>();
-        } else if (ro < 7) {
+        } else if (ro < NRO - 1) {
           wait_vm<6>();
         } else {
-          wait_vm<4>();
+          wait_vm<4>();  // the last round: no aux(ro + 1) was issued after it
         }
         uint32_t drow = 0, dcol = 0;
         if constexpr (EPI == 7) {
           int mt, nt;
           tile_mn<GM>(t, NT, mt, nt);
-          drow = (uint32_t)(mt * 256 + qa * 128 + wm * 64 + i * 16 + (ln >> 3));
+          drow = (uint32_t)(mt * TM + qa * 128 + wm * 64 + i * 16 + (ln >> 3));
           dcol = (uint32_t)(nt * 256 + wn * 64 + (ln & 7) * 8);
         }
 #pragma unroll
@@ -935,7 +948,7 @@ __global__ void __launch_bounds__(512) gemmp_kernel(const bf16_t* __restrict__ A
           val[k] = make_uint4(o[0], o[1], o[2], o[3]);
         }
         // this round's aux slot is consumed: prefetch round ro + 2 into it
-        if (ro + 2 < 8) {
+        if (ro + 2 < NRO) {
 #pragma unroll
           for (int k = 0; k < 2; ++k) aux[ro & 1][k] = load_aux(t, ro + 2, k, ln);
         }
@@ -1037,14 +1050,14 @@ __global__ void __launch_bounds__(512) gemmp_kernel(const bf16_t* __restrict__ A
     // first iteration: the previous tile's XS epilogue ops may still be in flight
     {
       const bool more = 1 < niter;
-      phase<0, false, B_TR, false, true, XS>(acc, fa, fb0, fb1, cs, opA, opB, smem, csa, 0, more, false, grp, extra);
-      phase<1, false, B_TR, false, true, XS>(acc, fa, fb0, fb1, cs, opA, opB, smem, csa, 0, more, false, grp, extra);
-      phase<2, false, B_TR, false, true, XS>(acc, fa, fb0, fb1, cs, opA, opB, smem, csa, 0, more, false, grp, extra);
-      phase<3, false, B_TR, false, true, XS>(acc, fa, fb0, fb1, cs, opA, opB, smem, csa, 0, more, false, grp, extra);
-      phase<4, false, B_TR, false, true>(acc, fa, fb0, fb1, cs, opA, opB, smem, csa, 0, more, false, grp);
-      phase<5, false, B_TR, false, true>(acc, fa, fb0, fb1, cs, opA, opB, smem, csa, 0, more, false, grp);
-      phase<6, false, B_TR, false, true>(acc, fa, fb0, fb1, cs, opA, opB, smem, csa, 0, more, false, grp);
-      phase<7, false, B_TR, false, true>(acc, fa, fb0, fb1, cs, opA, opB, smem, csa, 0, more, false, grp);
+      phase<0, false, B_TR, false, true, XS, 0, HMT>(acc, fa, fb0, fb1, cs, opA, opB, smem, csa, 0, more, false, grp, extra);
+      phase<1, false, B_TR, false, true, XS, 0, HMT>(acc, fa, fb0, fb1, cs, opA, opB, smem, csa, 0, more, false, grp, extra);
+      phase<2, false, B_TR, false, true, XS, 0, HMT>(acc, fa, fb0, fb1, cs, opA, opB, smem, csa, 0, more, false, grp, extra);
+      phase<3, false, B_TR, false, true, XS, 0, HMT>(acc, fa, fb0, fb1, cs, opA, opB, smem, csa, 0, more, false, grp, extra);
+      phase<4, false, B_TR, false, true, 0, 0, HMT>(acc, fa, fb0, fb1, cs, opA, opB, smem, csa, 0, more, false, grp);
+      phase<5, false, B_TR, false, true, 0, 0, HMT>(acc, fa, fb0, fb1, cs, opA, opB, smem, csa, 0, more, false, grp);
+      phase<6, false, B_TR, false, true, 0, 0, HMT>(acc, fa, fb0, fb1, cs, opA, opB, smem, csa, 0, more, false, grp);
+      phase<7, false, B_TR, false, true, 0, 0, HMT>(acc, fa, fb0, fb1, cs, opA, opB, smem, csa, 0, more, false, grp);
     }
     // the epilogue's activation-backward operand (EPI 3/4/5) of rounds 0 and 1: issued in the
     // last K-iteration once its DMA is out (phases 2-7 then leave these 4 loads in flight),
@@ -1055,21 +1068,21 @@ __global__ void __launch_bounds__(512) gemmp_kernel(const bf16_t* __restrict__ A
     for (int it = 1; it < niter - (EARLY_AUX ? 1 : 0); ++it) {
       const int te = 2 * it;
       const bool more = it + 1 < niter;
-      phase<0, false, B_TR, false, true>(acc, fa, fb0, fb1, cs, opA, opB, smem, csa, te, more, false, grp);
-      phase<1, false, B_TR, false, true>(acc, fa, fb0, fb1, cs, opA, opB, smem, csa, te, more, false, grp);
-      phase<2, false, B_TR, false, true>(acc, fa, fb0, fb1, cs, opA, opB, smem, csa, te, more, false, grp);
-      phase<3, false, B_TR, false, true>(acc, fa, fb0, fb1, cs, opA, opB, smem, csa, te, more, false, grp);
-      phase<4, false, B_TR, false, true>(acc, fa, fb0, fb1, cs, opA, opB, smem, csa, te, more, false, grp);
-      phase<5, false, B_TR, false, true>(acc, fa, fb0, fb1, cs, opA, opB, smem, csa, te, more, false, grp);
-      phase<6, false, B_TR, false, true>(acc, fa, fb0, fb1, cs, opA, opB, smem, csa, te, more, false, grp);
-      phase<7, false, B_TR, false, true>(acc, fa, fb0, fb1, cs, opA, opB, smem, csa, te, more, false, grp);
+      phase<0, false, B_TR, false, true, 0, 0, HMT>(acc, fa, fb0, fb1, cs, opA, opB, smem, csa, te, more, false, grp);
+      phase<1, false, B_TR, false, true, 0, 0, HMT>(acc, fa, fb0, fb1, cs, opA, opB, smem, csa, te, more, false, grp);
+      phase<2, false, B_TR, false, true, 0, 0, HMT>(acc, fa, fb0, fb1, cs, opA, opB, smem, csa, te, more, false, grp);
+      phase<3, false, B_TR, false, true, 0, 0, HMT>(acc, fa, fb0, fb1, cs, opA, opB, smem, csa, te, more, false, grp);
+      phase<4, false, B_TR, false, true, 0, 0, HMT>(acc, fa, fb0, fb1, cs, opA, opB, smem, csa, te, more, false, grp);
+      phase<5, false, B_TR, false, true, 0, 0, HMT>(acc, fa, fb0, fb1, cs, opA, opB, smem, csa, te, more, false, grp);
+      phase<6, false, B_TR, false, true, 0, 0, HMT>(acc, fa, fb0, fb1, cs, opA, opB, smem, csa, te, more, false, grp);
+      phase<7, false, B_TR, false, true, 0, 0, HMT>(acc, fa, fb0, fb1, cs, opA, opB, smem, csa, te, more, false, grp);
     }
     bool aux_issued = false;
     if constexpr (EARLY_AUX) {
       if (niter > 1) {  // the peeled last iteration
         const int te = 2 * (niter - 1);
-        phase<0, false, B_TR, false, true>(acc, fa, fb0, fb1, cs, opA, opB, smem, csa, te, false, false, grp);
-        phase<1, false, B_TR, false, true>(acc, fa, fb0, fb1, cs, opA, opB, smem, csa, te, false, false, grp);
+        phase<0, false, B_TR, false, true, 0, 0, HMT>(acc, fa, fb0, fb1, cs, opA, opB, smem, csa, te, false, false, grp);
+        phase<1, false, B_TR, false, true, 0, 0, HMT>(acc, fa, fb0, fb1, cs, opA, opB, smem, csa, te, false, false, grp);
         {
           const int ln = opaque(lane_id());
 #pragma unroll
@@ -1078,12 +1091,12 @@ __global__ void __launch_bounds__(512) gemmp_kernel(const bf16_t* __restrict__ A
             for (int k = 0; k < 2; ++k) aux[ro][k] = load_aux(tile, ro, k, ln);
         }
         aux_issued = true;
-        phase<2, false, B_TR, false, true, 0, 4>(acc, fa, fb0, fb1, cs, opA, opB, smem, csa, te, false, false, grp);
-        phase<3, false, B_TR, false, true, 0, 4>(acc, fa, fb0, fb1, cs, opA, opB, smem, csa, te, false, false, grp);
-        phase<4, false, B_TR, false, true, 0, 4>(acc, fa, fb0, fb1, cs, opA, opB, smem, csa, te, false, false, grp);
-        phase<5, false, B_TR, false, true, 0, 4>(acc, fa, fb0, fb1, cs, opA, opB, smem, csa, te, false, false, grp);
-        phase<6, false, B_TR, false, true, 0, 4>(acc, fa, fb0, fb1, cs, opA, opB, smem, csa, te, false, false, grp);
-        phase<7, false, B_TR, false, true, 0, 4>(acc, fa, fb0, fb1, cs, opA, opB, smem, csa, te, false, false, grp);
+        phase<2, false, B_TR, false, true, 0, 4, HMT>(acc, fa, fb0, fb1, cs, opA, opB, smem, csa, te, false, false, grp);
+        phase<3, false, B_TR, false, true, 0, 4, HMT>(acc, fa, fb0, fb1, cs, opA, opB, smem, csa, te, false, false, grp);
+        phase<4, false, B_TR, false, true, 0, 4, HMT>(acc, fa, fb0, fb1, cs, opA, opB, smem, csa, te, false, false, grp);
+        phase<5, false, B_TR, false, true, 0, 4, HMT>(acc, fa, fb0, fb1, cs, opA, opB, smem, csa, te, false, false, grp);
+        phase<6, false, B_TR, false, true, 0, 4, HMT>(acc, fa, fb0, fb1, cs, opA, opB, smem, csa, te, false, false, grp);
+        phase<7, false, B_TR, false, true, 0, 4, HMT>(acc, fa, fb0, fb1, cs, opA, opB, smem, csa, te, false, false, grp);
       }
     }
     if (dyn && w == 0) {
@@ -1224,14 +1237,14 @@ static int* gemmp_queue(hipStream_t s) {
   return slot;
 }
 
-template <bool B_TR, int EPI, int ACT, int POL = 0, int GM = 1>
+template <bool B_TR, int EPI, int ACT, int POL = 0, int GM = 1, bool HMT = false>
 static void gemmp_launch(const uint16_t* a, int64_t lda, const uint16_t* b, int64_t ldb, int M, int N, int K,
                          uint16_t* c, const uint16_t* bias, uint16_t* z, int ncu, hipStream_t s,
                          float* colpart, int hm, const g256::EpiArgs& ea) {
-  const int tiles = (M / 256) * (N / 256);
+  const int tiles = (M / (HMT ? 128 : 256)) * (N / 256);
   const int grid = persistent_grid(tiles, ncu);
   int* q = (tiles > grid && grid >= 8) ? gemmp_queue(s) : nullptr;
-  hipLaunchKernelGGL((g256::gemmp_kernel<B_TR, EPI, ACT, POL, GM>), dim3(grid), dim3(512), 0, s,
+  hipLaunchKernelGGL((g256::gemmp_kernel<B_TR, EPI, ACT, POL, GM, 0, 0, HMT>), dim3(grid), dim3(512), 0, s,
                      (const bf16_t*)a, lda, (const bf16_t*)b, ldb, M, N, K / 64, (bf16_t*)c, (int64_t)N,
                      (const bf16_t*)bias, (bf16_t*)z, colpart, q, hm, ea);
 }
@@ -1240,6 +1253,31 @@ static void gemmp_launch(const uint16_t* a, int64_t lda, const uint16_t* b, int6
 // wide layers (>= 8 column tiles) walk tiles in groups of 8 tile rows with non-temporal
 // epilogue stores: 2.1% / 2.6% faster on the 3072-wide MLP GEMMs at T = 262144 (gemm_lab
 // "policy" study, profiles/gemm_lab_r3_policy.txt); neither helps the narrow GEMMs.
+// 128 x 256 tiles when the launch finishes sooner with them: R rounds of 256-row tiles over the
+// grid against ceil(2 tiles / grid) rounds of half tiles, each costing ~HALF_COST of a full one
+// (tools/probes/small_gemm.py).  At 8192 tokens every BERT-base GEMM gains (768 wide: 96 tiles
+// for 256 CUs -> 192; 2304 / 3072 wide: 2 rounds -> 3 half rounds); at 262144 tokens none does.
+// DPA_GEMMP_HALF: 0 off, 1 (default) by that rule, 2 wherever allowed (M % 256 == 0).
+static int g_gemmp_half = -1;
+void set_gemmp_half(int mode) { g_gemmp_half = mode < 0 ? -1 : mode; }  // -1: DPA_GEMMP_HALF / auto
+static bool use_half_tiles(int M, int N, int ncu) {
+  if (g_gemmp_half < 0) {
+    const char* e = std::getenv("DPA_GEMMP_HALF");
+    g_gemmp_half = e ? std::atoi(e) : 1;
+  }
+  const int mode = g_gemmp_half;
+  static const double HALF_COST = [] {
+    const char* e = std::getenv("DPA_GEMMP_HALF_COST");
+    return e ? std::atof(e) : 0.66;
+  }();
+  if (mode == 0 || M % 256) return false;
+  if (mode >= 2) return true;
+  const int g = persistent_grid(1 << 30, ncu);
+  const int t = (M / 256) * (N / 256);
+  const int rf = (t + g - 1) / g, rh = (2 * t + g - 1) / g;
+  return rh * HALF_COST < rf * 0.97;
+}
+
 template <bool B_TR, int EPI, int ACT>
 static void gemmp_go(const uint16_t* a, int64_t lda, const uint16_t* b, int64_t ldb, int M, int N, int K,
                      uint16_t* c, const uint16_t* bias, uint16_t* z, int ncu, hipStream_t s,
@@ -1248,6 +1286,12 @@ static void gemmp_go(const uint16_t* a, int64_t lda, const uint16_t* b, int64_t 
     const char* e = std::getenv("DPA_GEMMP_GROUPED");  // "0": default policy (A/B runs)
     return !(e && e[0] == '0');
   }();
+  if constexpr (EPI != 4) {
+    if (use_half_tiles(M, N, ncu)) {
+      gemmp_launch<B_TR, EPI, ACT, 0, 1, true>(a, lda, b, ldb, M, N, K, c, bias, z, ncu, s, colpart, hm, ea);
+      return;
+    }
+  }
   if constexpr (EPI == 4 || EPI == 6 || EPI == 8) {
     if (grouped && (M / 256) % 8 == 0 && N / 256 >= 8) {
       gemmp_launch<B_TR, EPI, ACT, 1, 8>(a, lda, b, ldb, M, N, K, c, bias, z, ncu, s, colpart, hm, ea);

@@ -175,6 +175,7 @@ bool launch_gemm256_nn(const uint16_t* dy, const uint16_t* W, uint16_t* dx, int 
 void set_gemm256(bool on);
 void set_gemmp_dynamic(bool on);  // dynamic tile schedule of the persistent GEMMs (world > 1)
 void set_gemmp_grid_cap(int cap);  // persistent-GEMM grid cap (0 = #CUs)
+void set_gemmp_half(int mode);     // 128-row tiles: 0 off, 1 auto (occupancy rule), 2 always
 bool launch_gemm256_nn_dact(const uint16_t* dy, const uint16_t* W, const uint16_t* aux,
                             uint16_t* dz, int T, int N, int K, int act, hipStream_t s);
 bool launch_gemm256_wgrad(const uint16_t* dy, const uint16_t* x, float* dW, float* db, int T,

@@ -10,7 +10,7 @@ import torch
 pytestmark = pytest.mark.gpu
 
 
-def _loop(overlap, defer=0):
+def _loop(overlap, defer=0, steps=2):
     from basic_utils import logger
     from distributed_pipeline_amd.ops.nn import RNG
     from utils.initialization import create_diffusion_from_config, create_model_from_config, seed_all
@@ -37,7 +37,7 @@ def _loop(overlap, defer=0):
                               device_prefetch=False, defer_wgrad=defer)
     torch.manual_seed(7)
     losses = []
-    for _ in range(2):
+    for _ in range(steps):
         loop.run_step(batch)
         losses.append(logger.dumpkvs()["loss"])
     torch.cuda.synchronize()
@@ -71,9 +71,10 @@ def test_deferred_wgrad_matches_sequential(depth, overlap):
     and in the one-stream sequential one.  Same fp32 sum in another order: gradients within
     fp32 rounding of the sequential loop's, and the multi-segment launch must actually have run."""
     from distributed_pipeline_amd.ops.nn import WGRAD_DEFER
-    g0, p0, l0 = _loop(False)
+    # gradients of the first step (identical parameters): the same fp32 sum in another order
+    g0, _, _ = _loop(False, steps=1)
     before = dict(WGRAD_DEFER.stats)
-    g1, p1, l1 = _loop(overlap, defer=depth)
+    g1, _, _ = _loop(overlap, defer=depth, steps=1)
     assert WGRAD_DEFER.stats["multi_launches"] > before["multi_launches"]
     assert not WGRAD_DEFER.pending
     # the LayerNorm / dact-bias column sums of the un-armed micro-batches were deferred too
@@ -85,8 +86,13 @@ def test_deferred_wgrad_matches_sequential(depth, overlap):
     scale = g0.abs().max().item()
     err = (g0 - g1).abs().max().item()
     assert err <= 2e-5 * scale, (err, scale)
-    # Adam turns rounding-level gradient differences of near-zero elements into at most
-    # ~lr-sized parameter differences (lr = 1e-4, two steps)
+    # After an optimizer step the gradients are no longer comparable element-wise: Adam turns a
+    # rounding-level difference of a near-zero gradient element into an lr-sized parameter
+    # difference (measured: step-2 gradients of the input-side parameters then differ by up to
+    # 3e-4 relative at depth 4, while step 1 agrees to 3e-7, tools/probes/overlap_diag.py).
+    # Two steps: parameters within ~lr (1e-4) per step, losses within rounding.
+    _, p0, l0 = _loop(False)
+    _, p1, l1 = _loop(overlap, defer=depth)
     assert (p0 - p1).abs().max().item() <= 2.5e-4
     for a, b in zip(l0, l1):
         assert abs(a - b) <= 1e-4 * abs(a)

@@ -27,11 +27,12 @@ def child():
             super().__init__(*a, **k)
             keep["loop"] = self
     tr.DiffusionTrainLoop = Spy
-    g0, p0, _ = T._loop(False)
+    steps = int(os.environ.get("DIAG_STEPS", "2"))
+    g0, p0, _ = T._loop(False, steps=steps)
     spans = _names(keep["loop"])
     res = {}
-    for overlap, defer in ((False, 4),):
-        g1, p1, _ = T._loop(overlap, defer=defer)
+    for overlap, defer in ((False, 4), (True, 4), (False, 2)):
+        g1, p1, _ = T._loop(overlap, defer=defer, steps=steps)
         scale = g0.abs().max().item()
         err = (g0 - g1).abs()
         worst = []
@@ -42,7 +43,7 @@ def child():
                 worst.append((n, round(e / max(m, 1e-30), 7), round(m, 6)))
         worst.sort(key=lambda x: -x[1])
         from distributed_pipeline_amd.ops.nn import WGRAD_DEFER
-        res[f"overlap={overlap},defer={defer}"] = {"err": err.max().item(), "scale": scale, "worst": worst[:60],
+        res[f"overlap={overlap},defer={defer}"] = {"err": err.max().item(), "scale": scale, "worst": worst[:8],
                                                    "held_changed": [str(x) for x in WGRAD_DEFER.check_log[:4]],
                                                    "n_changed": len(WGRAD_DEFER.check_log)}
         WGRAD_DEFER.check_log.clear()

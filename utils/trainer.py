@@ -881,6 +881,16 @@ class TrainLoop:
             defer.stream = None
         done = None
         self._loss_log_buf = []
+        # the two streams already fill the CUs a small chunk's GEMMs leave idle: 128-row GEMM
+        # tiles (gemm256.hip use_half_tiles) only add operand traffic here (32 x 64 schedule:
+        # 222.7 ms/step without, 233.8 with, profiles/half_tiles_r5.txt; DPA_OVERLAP_HALF_TILES=1
+        # keeps them)
+        hx = None
+        if os.environ.get("DPA_OVERLAP_HALF_TILES", "0") != "1":
+            from distributed_pipeline_amd.ops._ext import get_ext
+            hx = get_ext()
+            if hx is not None:
+                hx.set_gemmp_half(0)
         try:
             nxt = fwd(0)
             for k in range(nch):
@@ -915,6 +925,8 @@ class TrainLoop:
             self._loss_log_buf = None  # ... and its logged losses (as the sequential retry)
             raise
         finally:
+            if hx is not None:
+                hx.set_gemmp_half(-1)
             defer.active = False
             defer.cur = None
             if defer.stream is not None:
