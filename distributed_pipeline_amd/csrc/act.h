@@ -42,11 +42,13 @@ __device__ __forceinline__ float dgelu_f(float z) {
 // Two-lane forms for the GEMM epilogues: the polynomial part runs on packed fp32
 // (v_pk_fma_f32 / v_pk_mul_f32, two elements per instruction); the exp and rcp
 // stay per element.  Same math as phi_cdf.
+// (x = |z| / sqrt 2 folded into the constants: -x^2 log2 e = z * (-log2(e) / 2) * z, and
+// 1 + 0.3275911 x = 1 + (0.3275911 / sqrt 2) |z|)
 __device__ __forceinline__ f32x2 phi_cdf2(f32x2 z, f32x2& e) {
-  const f32x2 x = f32x2{fabsf(z.x), fabsf(z.y)} * 0.70710678118654752f;
-  const f32x2 nx2 = -(x * x) * 1.4426950408889634f;
+  const f32x2 az = {fabsf(z.x), fabsf(z.y)};
+  const f32x2 nx2 = (z * -0.72134752044448170f) * z;
   e = f32x2{__builtin_amdgcn_exp2f(nx2.x), __builtin_amdgcn_exp2f(nx2.y)};
-  const f32x2 d = x * 0.3275911f + 1.f;
+  const f32x2 d = az * (0.3275911f * 0.70710678118654752f) + 1.f;
   const f32x2 t = {__builtin_amdgcn_rcpf(d.x), __builtin_amdgcn_rcpf(d.y)};
   f32x2 p = t * 1.061405429f - 1.453152027f;
   p = p * t + 1.421413741f;

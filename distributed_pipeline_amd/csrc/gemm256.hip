@@ -628,12 +628,19 @@ __device__ __forceinline__ uint4 act8(const uint4& u) {
 // The segments are convex / concave at the joint, so the code is the max of the two lines'
 // codes and the value the min of the two lines' values (no compare / select).
 constexpr float Q8_LO_STEP = 0.5f / 74.f;
-__device__ __forceinline__ float q8_code(float d) {
-  const float c = fmaxf(fmaf(d, 148.f, 19.f), fmaf(d, 256.f, -35.f));
-  return __builtin_rintf(__builtin_amdgcn_fmed3f(c, 0.f, 255.f));
-}
-__device__ __forceinline__ float q8_value(float c) {
-  return fminf((c - 19.f) * Q8_LO_STEP, fmaf(c, 1.f / 256.f, 35.f / 256.f));
+// The codes of an act' pair: both lines of both elements on packed fp32 (two v_pk_fma_f32) and
+// one max per element; v_cvt_pk_u8_f32 then rounds to nearest (no explicit rint).  No clamp is
+// needed: every act' this encodes (gelu', silu', tanh') lies in [-0.1285, 1.13], i.e. codes in
+// [-0.02, 254.6].  DPA_Q8_CVT: 1 (default) = the conversion rounds to nearest; 0 = explicit rint.
+#ifndef DPA_Q8_CVT
+#define DPA_Q8_CVT 1
+#endif
+__device__ __forceinline__ f32x2 q8_codes2(f32x2 d) {
+  const f32x2 l1 = d * 148.f + 19.f;
+  const f32x2 l2 = d * 256.f - 35.f;
+  f32x2 c = {fmaxf(l1.x, l2.x), fmaxf(l1.y, l2.y)};
+  if constexpr (DPA_Q8_CVT == 0) c = f32x2{__builtin_rintf(c.x), __builtin_rintf(c.y)};
+  return c;
 }
 
 // 8 bf16 -> act(z) (returned, bf16) and act'(z) as 8 u8 codes (c)
@@ -646,18 +653,23 @@ __device__ __forceinline__ uint4 act_dact8q(const uint4& u, uint2& c) {
     f32x2 d;
     const f32x2 y = act_dact2<ACT>(f32x2{__uint_as_float(w[q] << 16), __uint_as_float(w[q] & 0xffff0000u)}, d);
     o[q] = pack_bf2(y.x, y.y);
-    cw[q >> 1] = __builtin_amdgcn_cvt_pk_u8_f32(q8_code(d.x), (q & 1) * 2, cw[q >> 1]);
-    cw[q >> 1] = __builtin_amdgcn_cvt_pk_u8_f32(q8_code(d.y), (q & 1) * 2 + 1, cw[q >> 1]);
+    const f32x2 cc = q8_codes2(d);
+    cw[q >> 1] = __builtin_amdgcn_cvt_pk_u8_f32(cc.x, (q & 1) * 2, cw[q >> 1]);
+    cw[q >> 1] = __builtin_amdgcn_cvt_pk_u8_f32(cc.y, (q & 1) * 2 + 1, cw[q >> 1]);
   }
   c = make_uint2(cw[0], cw[1]);
   return make_uint4(o[0], o[1], o[2], o[3]);
 }
 
-// decoded act' of elements 2q, 2q + 1 of an 8-code group
+// decoded act' of elements 2q, 2q + 1 of an 8-code group: min((c - 19) * 0.5 / 74, (c + 35) / 256)
+// on packed fp32 (the same roundings as the element-wise form, so 0 and 1 stay exact)
 __device__ __forceinline__ f32x2 q8_pair(const uint4& a, int q) {
   const uint32_t c = (q >> 1) ? a.y : a.x;
   const int sh = (q & 1) * 16;
-  return f32x2{q8_value((float)((c >> sh) & 0xffu)), q8_value((float)((c >> (sh + 8)) & 0xffu))};
+  const f32x2 cv = {(float)((c >> sh) & 0xffu), (float)((c >> (sh + 8)) & 0xffu)};
+  const f32x2 lo = (cv - 19.f) * Q8_LO_STEP;
+  const f32x2 hi = cv * (1.f / 256.f) + 35.f / 256.f;
+  return f32x2{fminf(lo.x, hi.x), fminf(lo.y, hi.y)};
 }
 
 __device__ __forceinline__ void lds_write_b32(uint32_t addr, int v) {

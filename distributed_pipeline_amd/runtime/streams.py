@@ -80,9 +80,17 @@ class StreamPlan:
             raise KeyError(role)
         return self.streams.get(role)
 
+    # HSA queue of each role as measured for the "ordered" plan (rocprofv3 kernel trace of the real
+    # start-up order, tools/probes/stream_queues.py, GPU_MAX_HW_QUEUES=4); HIP exposes no queue id
+    MEASURED_QUEUES = {"compute": 1, "side": 2, "wgrad": 3, "nll": 4, "copy": 4,
+                       "reducer_comm": "5 (high-priority pool)", "source": "profiles/stream_queues_r5.txt"}
+
     def describe(self):
-        return {"mode": self.mode, "roles": list(ROLES),
-                "handles": {r: hex(s.cuda_stream) for r, s in self.streams.items()}}
+        d = {"mode": self.mode, "roles": list(ROLES),
+             "handles": {r: hex(s.cuda_stream) for r, s in self.streams.items()}}
+        if self.mode == "ordered":
+            d["hw_queues_measured"] = dict(self.MEASURED_QUEUES)
+        return d
 
 
 def plan_stream(device, role):

@@ -53,24 +53,36 @@ def _train(precision, engine, tmp, B=128):
     return torch.tensor(losses), loop.exec_microbatch
 
 
-def test_base_bf16_native_tracks_fp32_reference_200_steps(tmp_path):
+def test_base_bf16_native_tracks_fp32_reference_200_steps(tmp_path, monkeypatch):
+    """Also the byte-cutting epilogues against the plain bf16 path: the default native run stores
+    act' as u8 codes and folds residual + dropout into the N = 768 GEMMs (ops/nn.py _ACT_Q8,
+    _RES_FUSE); a third run with both off must track the same curve (its dropout masks come from
+    the Philox stream instead of the pair hash, so the trajectories differ by dropout noise only)."""
+    from distributed_pipeline_amd.ops import nn as nn_ops
     ref, ex_r = _train("fp32", "torch", str(tmp_path))
     nat, ex_n = _train("bf16", "native", str(tmp_path))
+    monkeypatch.setattr(nn_ops, "_ACT_Q8", False)
+    monkeypatch.setattr(nn_ops, "_RES_FUSE", False)
+    plain, _ = _train("bf16", "native", str(tmp_path))
     assert ex_r == 64 and ex_n == 128  # reference schedule vs the fused default
-    assert torch.isfinite(nat).all() and torch.isfinite(ref).all()
+    assert torch.isfinite(nat).all() and torch.isfinite(ref).all() and torch.isfinite(plain).all()
     head_r, tail_r = ref[:20].mean().item(), ref[-50:].mean().item()
     head_n, tail_n = nat[:20].mean().item(), nat[-50:].mean().item()
+    tail_p = plain[-50:].mean().item()
     path = os.environ.get("DPA_CONVERGENCE_LOG")
     if path:
         with open(path, "w") as f:
             f.write("# DiffuSeq-base 768x12 seq128, batch 128 (2 x 64), lr 1e-4, 200 steps, synthetic\n")
-            f.write("# step fp32_torch_engine bf16_native_engine\n")
-            for i, (a, b) in enumerate(zip(ref.tolist(), nat.tolist())):
-                f.write(f"{i} {a:.5f} {b:.5f}\n")
+            f.write("# step fp32_torch_engine bf16_native_engine(u8 act', fused residual-dropout) "
+                    "bf16_native_engine(bf16 act', unfused)\n")
+            for i, (a, b, c) in enumerate(zip(ref.tolist(), nat.tolist(), plain.tolist())):
+                f.write(f"{i} {a:.5f} {b:.5f} {c:.5f}\n")
             f.write(f"# head(20) fp32 {head_r:.5f} bf16 {head_n:.5f} | tail(50) fp32 {tail_r:.5f} "
-                    f"bf16 {tail_n:.5f} | rel diff {abs(tail_n - tail_r) / tail_r:.4f}\n")
+                    f"bf16 {tail_n:.5f} bf16-plain {tail_p:.5f} | rel diff {abs(tail_n - tail_r) / tail_r:.4f} "
+                    f"(plain {abs(tail_p - tail_r) / tail_r:.4f})\n")
     assert tail_r < head_r and tail_n < head_n, (head_r, tail_r, head_n, tail_n)
     assert abs(tail_n - tail_r) / tail_r < 0.02, (tail_n, tail_r)
+    assert abs(tail_p - tail_r) / tail_r < 0.02, (tail_p, tail_r)
 
 
 def test_fused_exec_microbatch_equals_accumulation_full_shapes(monkeypatch):

@@ -28,6 +28,7 @@ def main(argv):
     if not files:  # the whole native tree of REV
         csrc = os.path.join(work, "csrc")
         os.makedirs(os.path.join(csrc, "comm"), exist_ok=True)
+        os.makedirs(os.path.join(csrc, "runtime"), exist_ok=True)
         names = subprocess.check_output(["git", "-C", HERE, "ls-tree", "-r", "--name-only", rev,
                                          "distributed_pipeline_amd/csrc"], text=True).split()
         for n in names:
@@ -58,7 +59,8 @@ def main(argv):
         obj = os.path.join(work, os.path.basename(src) + ".cur.o")
         B._run([B._hipcc()] + common + ["-c", src, "-o", obj])
         objs.append(obj)
-    for src in [os.path.join(csrc, "bindings.cpp")] + sorted(glob.glob(os.path.join(csrc, "comm", "*.cpp"))):
+    for src in [os.path.join(csrc, "bindings.cpp")] + sorted(glob.glob(os.path.join(csrc, "comm", "*.cpp"))
+                                                          + glob.glob(os.path.join(csrc, "runtime", "*.cpp"))):
         obj = os.path.join(work, os.path.basename(src) + ".ab.o")
         B._run([B._hipcc()] + bind + ["-c", src, "-o", obj])
         objs.append(obj)

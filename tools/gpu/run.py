@@ -44,8 +44,11 @@ def _run(cmd, log, limit, env=None, ok_codes=(0,)):
 
 
 def _bench_ms(path):
+    """headline ms/step, plus the reference schedule's when it ran"""
     with open(path) as f:
-        return json.load(f)["ms_per_step"]
+        d = json.load(f)
+    r = (d.get("reference_schedule") or {}).get("ms_per_step")
+    return f"{d['ms_per_step']}" + (f" (reference schedule {r})" if r else "")
 
 
 def main(steps):
