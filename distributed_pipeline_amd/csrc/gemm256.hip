@@ -193,7 +193,9 @@ __device__ __forceinline__ void colsum_read(float& cs, const uint32_t (&csa)[2])
 // SWAP: B.A^T instead of A.B^T - the accumulator then holds C transposed (lane =
 // row of C, registers = 4 consecutive columns), the layout of the persistent
 // kernel's register-direct epilogue.
-template <int QA, int QB, bool SWAP = false>
+// Z: the quadrant's first MFMAs of a tile take the inline constant 0 as their C operand (no
+// accumulator zeroing pass: 128 v_mov per wave per tile between the epilogue and the next main loop)
+template <int QA, int QB, bool SWAP = false, bool Z = false>
 __device__ __forceinline__ void mfma_quadrant(f32x4 (&acc)[2][2][4][2], const bf16x8 (&fa)[4][2],
                                               const bf16x8 (&fb)[2][2]) {
   __builtin_amdgcn_s_setprio(1);
@@ -203,8 +205,9 @@ __device__ __forceinline__ void mfma_quadrant(f32x4 (&acc)[2][2][4][2], const bf
     for (int i = 0; i < 4; ++i)
 #pragma unroll
       for (int j = 0; j < 2; ++j) {
-        if constexpr (SWAP) acc[QA][QB][i][j] = mfma16(fb[j][kk], fa[i][kk], acc[QA][QB][i][j]);
-        else acc[QA][QB][i][j] = mfma16(fa[i][kk], fb[j][kk], acc[QA][QB][i][j]);
+        const f32x4 c = (Z && kk == 0) ? f32x4{0.f, 0.f, 0.f, 0.f} : acc[QA][QB][i][j];
+        if constexpr (SWAP) acc[QA][QB][i][j] = mfma16(fb[j][kk], fa[i][kk], c);
+        else acc[QA][QB][i][j] = mfma16(fa[i][kk], fb[j][kk], c);
       }
   __builtin_amdgcn_s_setprio(0);
 }
@@ -239,7 +242,8 @@ __device__ __forceinline__ int opaque(int x) {
 // XS / extra (persistent kernel): `extra` = XS stores of the previous tile were
 // issued between this tile's prologue DMA and its first iteration, so the waits
 // of phases 0-3 of that iteration leave them in flight.
-template <int P, bool A_TR, bool B_TR, bool CS, bool SWAP = false, int XS = 0, int DRAIN = 0, bool HM = false>
+template <int P, bool A_TR, bool B_TR, bool CS, bool SWAP = false, int XS = 0, int DRAIN = 0, bool HM = false,
+          bool Z = false>
 __device__ __forceinline__ void phase(f32x4 (&acc)[2][2][4][2], bf16x8 (&fa)[4][2],
                                       bf16x8 (&fb0)[2][2], bf16x8 (&fb1)[2][2], float& cs,
                                       const Operand<A_TR>& opA, const Operand<B_TR>& opB,
@@ -286,12 +290,12 @@ __device__ __forceinline__ void phase(f32x4 (&acc)[2][2][4][2], bf16x8 (&fa)[4][
   barrier();
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
   __builtin_amdgcn_sched_barrier(0);
-  if constexpr (q == 0) mfma_quadrant<0, 0, SWAP>(acc, fa, fb0);
-  if constexpr (q == 1) mfma_quadrant<0, 1, SWAP>(acc, fa, fb1);
+  if constexpr (q == 0) mfma_quadrant<0, 0, SWAP, Z>(acc, fa, fb0);
+  if constexpr (q == 1) mfma_quadrant<0, 1, SWAP, Z>(acc, fa, fb1);
   // HM (128-row tiles): the A1 image is a copy of A0 (DMA kept: the counted waits stay
   // exact) and its two quadrants are skipped
-  if constexpr (q == 2 && !HM) mfma_quadrant<1, 1, SWAP>(acc, fa, fb1);
-  if constexpr (q == 3 && !HM) mfma_quadrant<1, 0, SWAP>(acc, fa, fb0);
+  if constexpr (q == 2 && !HM) mfma_quadrant<1, 1, SWAP, Z>(acc, fa, fb1);
+  if constexpr (q == 3 && !HM) mfma_quadrant<1, 0, SWAP, Z>(acc, fa, fb0);
   __builtin_amdgcn_sched_barrier(0);
   barrier();
 }
@@ -821,15 +825,18 @@ __global__ void __launch_bounds__(512) gemmp_kernel(const bf16_t* __restrict__ A
     int mt, nt;
     tile_mn<GM>(t, NT, mt, nt);
     const int qa = ro >> 2, i = ro & 3;
-    const int64_t row = (int64_t)mt * TM + qa * 128 + wm * 64 + i * 16 + k * 8 + (ln >> 3);
+    const int lrow = qa * 128 + wm * 64 + i * 16 + k * 8 + (ln >> 3);  // row within the tile, < 256
     const int col = nt * 256 + wn * 64 + (ln & 7) * 8;
-    if (hm) {
+    if (EPI == 0 && hm) {
       // head-major store [R >> hm][ldc / 64][1 << hm][64]: row = (b, l), col = (head j, d); a
       // wave's 64 columns are one head, so a store instruction's 8 rows are 1 KiB contiguous
+      const int64_t row = (int64_t)mt * TM + lrow;
       const int64_t b = row >> hm, l = row & ((1 << hm) - 1);
       return ((b * (ldc >> 6) + (col >> 6)) << hm) * 64 + l * 64 + (col & 63);
     }
-    return row * ldc + col;
+    // the tile origin's 64-bit offset is wave-uniform (scalar); the in-tile row takes one
+    // full-rate 24-bit multiply (lrow < 256, ldc < 2^24) instead of a 64-bit one per address
+    return (int64_t)(mt * TM) * ldc + (int64_t)__umul24((unsigned)lrow, (unsigned)ldc) + col;
   };
   // Tile-native byte offset of a u8 act' code group (EPI 8 writes, ACT 5 reads): the 8 codes
   // of (tile, wave, round, k, lane) are consecutive, so one wave instruction moves 512
@@ -921,12 +928,15 @@ __global__ void __launch_bounds__(512) gemmp_kernel(const bf16_t* __restrict__ A
         } else {
           wait_vm<4>();  // the last round: no aux(ro + 1) was issued after it
         }
-        uint32_t drow = 0, dcol = 0;
+        // pair_hash(dsm, row, col) = mix32(dsm ^ row A ^ (col / 2) B) with row = drow + 8 k and
+        // col / 2 = dcol / 2 + q: the two products strength-reduced to one per round (rA) and one
+        // per tile (cB) plus constant offsets (v_mul_lo_u32 is quarter rate)
+        uint32_t rA = 0, cB = 0;
         if constexpr (EPI == 7) {
           int mt, nt;
           tile_mn<GM>(t, NT, mt, nt);
-          drow = (uint32_t)(mt * TM + qa * 128 + wm * 64 + i * 16 + (ln >> 3));
-          dcol = (uint32_t)(nt * 256 + wn * 64 + (ln & 7) * 8);
+          rA = (uint32_t)(mt * TM + qa * 128 + wm * 64 + i * 16 + (ln >> 3)) * 0x9E3779B1u;
+          cB = (uint32_t)((nt * 256 + wn * 64 + (ln & 7) * 8) >> 1) * 0x85EBCA77u;
         }
 #pragma unroll
         for (int k = 0; k < 2; ++k) {
@@ -944,7 +954,8 @@ __global__ void __launch_bounds__(512) gemmp_kernel(const bf16_t* __restrict__ A
               // h = residual + dropout(y): y = the bf16 GEMM output (+bias), as a separate
               // dropout-add pass would see it; the bits are norm.hip's pair-hash mode's
               const f32x2 r = f32x2{bf_lo(aw[q]), bf_hi(aw[q])};
-              const uint32_t hsh = pair_hash(dsm, drow + k * 8, dcol + 2 * q);
+              const uint32_t hsh = mix32(dsm ^ (rA + (uint32_t)k * (8u * 0x9E3779B1u)) ^
+                                         (cB + (uint32_t)q * 0x85EBCA77u));
               const f32x2 m = {(hsh & 0xffffu) >= ea.thr16 ? ea.scale : 0.f, (hsh >> 16) >= ea.thr16 ? ea.scale : 0.f};
               d = x * m + r;
             } else {
@@ -1006,17 +1017,6 @@ __global__ void __launch_bounds__(512) gemmp_kernel(const bf16_t* __restrict__ A
     }
   };
 
-  auto zero_acc = [&]() {
-#pragma unroll
-    for (int a = 0; a < 2; ++a)
-#pragma unroll
-      for (int b = 0; b < 2; ++b)
-#pragma unroll
-        for (int i = 0; i < 4; ++i)
-#pragma unroll
-          for (int j = 0; j < 2; ++j) acc[a][b][i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-  };
-
   int tile = xcd_remap(blockIdx.x, G);
   if (tile >= ntiles) return;
   // Dynamic schedule (tile_ctr != nullptr, G >= 8): the first tile is static; later ones
@@ -1042,7 +1042,6 @@ __global__ void __launch_bounds__(512) gemmp_kernel(const bf16_t* __restrict__ A
   }
   int slot = 0;
   bool extra = false;
-  zero_acc();
   if constexpr (STG > 1) {
     // start-phase stagger: workgroup j of an XCD starts (j % STG) * DU x ~1 us late, so the
     // epilogue store bursts of the workgroups no longer coincide
@@ -1062,10 +1061,10 @@ __global__ void __launch_bounds__(512) gemmp_kernel(const bf16_t* __restrict__ A
     // first iteration: the previous tile's XS epilogue ops may still be in flight
     {
       const bool more = 1 < niter;
-      phase<0, false, B_TR, false, true, XS, 0, HMT>(acc, fa, fb0, fb1, cs, opA, opB, smem, csa, 0, more, false, grp, extra);
-      phase<1, false, B_TR, false, true, XS, 0, HMT>(acc, fa, fb0, fb1, cs, opA, opB, smem, csa, 0, more, false, grp, extra);
-      phase<2, false, B_TR, false, true, XS, 0, HMT>(acc, fa, fb0, fb1, cs, opA, opB, smem, csa, 0, more, false, grp, extra);
-      phase<3, false, B_TR, false, true, XS, 0, HMT>(acc, fa, fb0, fb1, cs, opA, opB, smem, csa, 0, more, false, grp, extra);
+      phase<0, false, B_TR, false, true, XS, 0, HMT, true>(acc, fa, fb0, fb1, cs, opA, opB, smem, csa, 0, more, false, grp, extra);
+      phase<1, false, B_TR, false, true, XS, 0, HMT, true>(acc, fa, fb0, fb1, cs, opA, opB, smem, csa, 0, more, false, grp, extra);
+      phase<2, false, B_TR, false, true, XS, 0, HMT, true>(acc, fa, fb0, fb1, cs, opA, opB, smem, csa, 0, more, false, grp, extra);
+      phase<3, false, B_TR, false, true, XS, 0, HMT, true>(acc, fa, fb0, fb1, cs, opA, opB, smem, csa, 0, more, false, grp, extra);
       phase<4, false, B_TR, false, true, 0, 0, HMT>(acc, fa, fb0, fb1, cs, opA, opB, smem, csa, 0, more, false, grp);
       phase<5, false, B_TR, false, true, 0, 0, HMT>(acc, fa, fb0, fb1, cs, opA, opB, smem, csa, 0, more, false, grp);
       phase<6, false, B_TR, false, true, 0, 0, HMT>(acc, fa, fb0, fb1, cs, opA, opB, smem, csa, 0, more, false, grp);
@@ -1140,7 +1139,6 @@ __global__ void __launch_bounds__(512) gemmp_kernel(const bf16_t* __restrict__ A
       }
       break;
     }
-    zero_acc();
     wait_vm<8 + XS>();  // next tile's K-tile 0 halves landed; this tile's epilogue ops may fly
     barrier();
     if (grp == 1) barrier();
@@ -1318,7 +1316,8 @@ static void gemmp_go(const uint16_t* a, int64_t lda, const uint16_t* b, int64_t 
 bool launch_gemmp_nt(const uint16_t* x, const uint16_t* W, const uint16_t* bias, uint16_t* y,
                      uint16_t* z, int T, int N, int K, int act, int ncu, hipStream_t s, bool zderiv, int hm,
                      bool z8) {
-  if (!g256_enabled() || T % 256 || N % 256 || K % 128 || K < 128 || act < 0 || act > 3) return false;
+  if (!g256_enabled() || T % 256 || N % 256 || K % 128 || K < 128 || act < 0 || act > 3 || N >= (1 << 24))
+    return false;  // (output width < 2^24: the epilogue's 24-bit row multiply)
   if (hm && (act != 0 || hm < 7 || hm > 30 || (T & ((1 << hm) - 1)) || N % 64)) return false;
   if (z8 && (act == 0 || z == nullptr || !zderiv)) return false;
   if (act == 0) gemmp_go<false, 0, 0>(x, K, W, K, T, N, K, y, bias, nullptr, ncu, s, nullptr, hm);
@@ -1351,7 +1350,8 @@ bool launch_gemmp_nt(const uint16_t* x, const uint16_t* W, const uint16_t* bias,
 bool launch_gemmp_nt_res(const uint16_t* x, const uint16_t* W, const uint16_t* bias, const uint16_t* res,
                          uint16_t* h, int T, int N, int K, int ncu, hipStream_t s, float p, uint32_t seed,
                          uint32_t offset) {
-  if (!g256_enabled() || T % 256 || N % 256 || K % 128 || K < 128 || !(p >= 0.f && p < 1.f)) return false;
+  if (!g256_enabled() || T % 256 || N % 256 || K % 128 || K < 128 || !(p >= 0.f && p < 1.f) || N >= (1 << 24))
+    return false;
   g256::EpiArgs ea;
   ea.seed = seed;
   ea.offset = offset;
@@ -1363,14 +1363,15 @@ bool launch_gemmp_nt_res(const uint16_t* x, const uint16_t* W, const uint16_t* b
 
 bool launch_gemmp_nn_acc(const uint16_t* dy, const uint16_t* W, uint16_t* dx, int T, int N, int K, int ncu,
                          hipStream_t s) {
-  if (!g256_enabled() || T % 256 || K % 256 || N % 128 || N < 128) return false;
+  if (!g256_enabled() || T % 256 || K % 256 || N % 128 || N < 128 || K >= (1 << 24)) return false;
   gemmp_go<true, 5, 0>(dy, N, W, K, T, K, N, dx, nullptr, dx, ncu, s);
   return true;
 }
 
 bool launch_gemmp_nn(const uint16_t* dy, const uint16_t* W, uint16_t* dx, const uint16_t* aux, int act,
                      int T, int N, int K, int ncu, hipStream_t s, float* colpart) {
-  if (!g256_enabled() || T % 256 || K % 256 || N % 128 || N < 128 || act < 0 || act > 5) return false;
+  if (!g256_enabled() || T % 256 || K % 256 || N % 128 || N < 128 || act < 0 || act > 5 || K >= (1 << 24))
+    return false;
   uint16_t* ax = const_cast<uint16_t*>(aux);
   if (act == 0 || aux == nullptr) {
     if (colpart) return false;
