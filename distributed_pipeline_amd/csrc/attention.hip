@@ -983,11 +983,11 @@ static void attn_bwd_general(const uint16_t* qkv, const uint16_t* out, const uin
 bool launch_attn_bwd(const uint16_t* qkv, const uint16_t* out, const uint16_t* dout, const float* lse,
                      float* delta, uint16_t* dqkv, float* dq_acc, float* colpart, float* dbias, int B,
                      int L, int H, int D, float p, bool causal, uint32_t seed, uint32_t offset,
-                     hipStream_t s, bool head_major, bool db_accumulate) {
+                     hipStream_t s, bool head_major, bool db_accumulate, bool defer_reduce) {
   (void)dq_acc;
   if (head_major)  // caller checked attn128_supports
     return launch_attn128_bwd(qkv, out, dout, lse, dqkv, colpart, dbias, B, L, H, p, causal, seed, offset, s,
-                              true, db_accumulate) && dbias != nullptr;
+                              true, db_accumulate, defer_reduce) && dbias != nullptr;
   // dbias != nullptr: the kernels also write per-block column-sum partials of dq / dk / dv
   // into colpart ([attn_colpart_rows][3 D], attn_colpart_floats) and one reduce pass adds
   // them into dbias (zeroed first unless db_accumulate)
@@ -997,11 +997,12 @@ bool launch_attn_bwd(const uint16_t* qkv, const uint16_t* out, const uint16_t* d
       attn_bwd_general<128>(qkv, out, dout, lse, delta, dqkv, B, L, H, p, causal, seed, offset, s, cp);
   } else {
     if (launch_attn128_bwd(qkv, out, dout, lse, dqkv, colpart, dbias, B, L, H, p, causal, seed, offset,
-                           s, false, db_accumulate))
+                           s, false, db_accumulate, defer_reduce))
       return dbias != nullptr;
     attn_bwd_general<64>(qkv, out, dout, lse, delta, dqkv, B, L, H, p, causal, seed, offset, s, cp);
   }
   if (!dbias) return false;
+  if (defer_reduce) return true;  // partials left in colpart for the caller's launch_colpart_reduce
   if (!db_accumulate) (void)hipMemsetAsync(dbias, 0, sizeof(float) * 3 * H * D, s);
   launch_colpart_reduce(colpart, dbias, (int)(attn_colpart_rows(B, L, H, D, causal) / H), H, D, s);
   return true;

@@ -1332,7 +1332,7 @@ bool launch_attn128_fwd_d128(const uint16_t* qkv, uint16_t* out, float* lse, int
 bool launch_attn128_bwd(const uint16_t* qkv, const uint16_t* out, const uint16_t* dout,
                         const float* lse, uint16_t* dqkv, float* colpart, float* dbias, int B,
                         int Lq, int H, float p, bool causal, uint32_t seed, uint32_t offset,
-                        hipStream_t s, bool head_major, bool db_accumulate) {
+                        hipStream_t s, bool head_major, bool db_accumulate, bool defer_reduce) {
   if (Lq != a128::L || causal || (!a128::enabled() && !head_major)) return false;
   const int items = B * H, slots = 2 * a128::num_cus();
   const int grid = items < slots ? items : slots;
@@ -1344,7 +1344,7 @@ bool launch_attn128_bwd(const uint16_t* qkv, const uint16_t* out, const uint16_t
     hipLaunchKernelGGL(a128::attn128_bwd_kernel<false>, dim3(grid), dim3(256), 0, s, (const bf16_t*)qkv,
                        (const bf16_t*)out, (const bf16_t*)dout, lse, (bf16_t*)dqkv,
                        dbias ? colpart : nullptr, B, H, p, seed, offset, head_major ? 1 : 0);
-  if (dbias) {
+  if (dbias && !defer_reduce) {  // deferred: the caller reduces several calls' partials at once
     const int bchunk = 64, nch = (B + bchunk - 1) / bchunk;
     if (!db_accumulate) (void)hipMemsetAsync(dbias, 0, sizeof(float) * 3 * H * a128::HD, s);
     hipLaunchKernelGGL(a128::colpart_reduce_kernel, dim3(3 * H, nch), dim3(256), 0, s, colpart,

@@ -437,10 +437,21 @@ static std::vector<at::Tensor> attn_fwd(const at::Tensor& qkv, int64_t heads, do
   return {out, lse};
 }
 
+static void attn_colpart_reduce(const at::Tensor& part, int64_t R, int64_t H, int64_t D, at::Tensor db) {
+  CHECK_DEV(part);
+  TORCH_CHECK(part.scalar_type() == at::kFloat && db.scalar_type() == at::kFloat && part.is_contiguous() &&
+                  db.is_contiguous() && part.numel() >= R * H * 3 * D && db.numel() == 3 * H * D &&
+                  D % 64 == 0 && R > 0,
+              "attn_colpart_reduce: fp32 part [R*H][3D], db [3HD]");
+  const c10::DeviceGuard guard(part.device());
+  dpa::launch_colpart_reduce(part.data_ptr<float>(), db.data_ptr<float>(), (int)R, (int)H, (int)D, cur_stream());
+}
+
 static std::vector<at::Tensor> attn_bwd(const at::Tensor& dout, const at::Tensor& qkv,
                                         const at::Tensor& out, const at::Tensor& lse, int64_t heads,
                                         double p, bool causal, int64_t seed, int64_t offset,
-                                        bool want_db, bool head_major, c10::optional<at::Tensor> db_acc) {
+                                        bool want_db, bool head_major, c10::optional<at::Tensor> db_acc,
+                                        c10::optional<at::Tensor> part_out) {
   CHECK_DEV(dout); CHECK_BF16(dout); CHECK_CONTIG(dout); CHECK_CONTIG(out); CHECK_CONTIG(qkv);
   const int B = (int)qkv.size(0), L = (int)qkv.size(1), H = (int)heads;
   TORCH_CHECK(dout.sizes() == out.sizes(), "dout shape");
@@ -460,15 +471,25 @@ static std::vector<at::Tensor> attn_bwd(const at::Tensor& dout, const at::Tensor
   // db_acc: the qkv bias gradient accumulated straight onto this fp32 .grad (returned undefined)
   const bool acc = want_db && db_acc.has_value() && db_acc->defined() && db_acc->scalar_type() == at::kFloat &&
                    db_acc->is_contiguous() && db_acc->numel() == 3LL * H * D && db_acc->device() == qkv.device();
+  // part_out: a caller-owned fp32 slot of attn_colpart_rows * 3 D floats; the bias-gradient
+  // partials are left there for a later colpart_reduce (deferral window), db is not produced
+  const int64_t cp_n = dpa::attn_colpart_rows(B, L, H, D, causal) * 3 * D;
+  const bool defer = want_db && acc && part_out.has_value() && part_out->defined() &&
+                     part_out->scalar_type() == at::kFloat && part_out->is_contiguous() &&
+                     part_out->numel() >= cp_n && part_out->device() == qkv.device();
   if (want_db) {
-    colpart = at::empty({dpa::attn_colpart_rows(B, L, H, D, causal) * 3 * D}, f32);
+    colpart = defer ? *part_out : at::empty({cp_n}, f32);
     db = acc ? *db_acc : at::empty({3 * H * D}, f32);
   }
   bool got = dpa::launch_attn_bwd(
       bf_ptr(qkv), bf_ptr(out), bf_ptr(dout), lse.data_ptr<float>(), delta.data_ptr<float>(),
       reinterpret_cast<uint16_t*>(dqkv.data_ptr()), dq.defined() ? dq.data_ptr<float>() : nullptr,
       want_db ? colpart.data_ptr<float>() : nullptr, want_db ? db.data_ptr<float>() : nullptr, B, L,
-      H, D, (float)p, causal, (uint32_t)seed, (uint32_t)offset, cur_stream(), head_major, acc);
+      H, D, (float)p, causal, (uint32_t)seed, (uint32_t)offset, cur_stream(), head_major, acc, defer);
+  if (defer) {
+    TORCH_CHECK(got, "attn_bwd: deferred column sums on a path without partials");
+    return {dqkv, at::Tensor()};
+  }
   if (want_db && !got) {
     // no fused column sums on this path (L != 128): one column-sum pass over the bf16 dqkv,
     // accumulated onto db (zeroed unless it is the parameter's .grad)
@@ -1064,7 +1085,11 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("attn_bwd", &attn_bwd, "fused attention backward -> (dqkv, colsum(dqkv) or None)",
         py::arg("dout"), py::arg("qkv"), py::arg("out"), py::arg("lse"), py::arg("heads"), py::arg("p"),
         py::arg("causal"), py::arg("seed"), py::arg("offset"), py::arg("want_db") = false,
-        py::arg("head_major") = false, py::arg("db_acc") = py::none());
+        py::arg("head_major") = false, py::arg("db_acc") = py::none(), py::arg("part_out") = py::none());
+  m.def("attn_colpart_rows", &dpa::attn_colpart_rows,
+        "rows of attn_bwd's bias-gradient partials ([rows][3 D] fp32) for (B, L, H, D, causal)");
+  m.def("attn_colpart_reduce", &attn_colpart_reduce,
+        "db[3 H D] += column sums of R x H rows of attn_bwd partials (deferred bias gradient)");
   m.def("gemm_nt", &gemm_nt,
         "y = act(x W^T + b) (bf16 MFMA) -> (y, z, z_is_derivative): z is the pre-activation, or "
         "act'(pre-activation) when want_deriv and the persistent kernel ran (backward act code 4)",

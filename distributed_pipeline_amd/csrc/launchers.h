@@ -110,12 +110,16 @@ bool launch_attn128_fwd(const uint16_t* qkv, uint16_t* out, float* lse, int B, i
 bool launch_attn128_bwd(const uint16_t* qkv, const uint16_t* out, const uint16_t* dout,
                         const float* lse, uint16_t* dqkv, float* colpart, float* dbias, int B,
                         int L, int H, float p, bool causal, uint32_t seed, uint32_t offset,
-                        hipStream_t s, bool head_major = false, bool db_accumulate = false);
-// Returns true when the column sums of dqkv were written to dbias (L == 128 path).
+                        hipStream_t s, bool head_major = false, bool db_accumulate = false,
+                        bool defer_reduce = false);
+// Returns true when the column sums of dqkv were written to dbias (L == 128 path).  defer_reduce:
+// the column-sum partials stay in colpart (dbias untouched) for one launch_colpart_reduce over
+// several calls' partials (the reference schedule's deferral window).
 bool launch_attn_bwd(const uint16_t* qkv, const uint16_t* out, const uint16_t* dout, const float* lse,
                      float* delta, uint16_t* dqkv, float* dq_acc, float* colpart, float* dbias, int B,
                      int L, int H, int D, float p, bool causal, uint32_t seed, uint32_t offset,
-                     hipStream_t s, bool head_major = false, bool db_accumulate = false);
+                     hipStream_t s, bool head_major = false, bool db_accumulate = false,
+                     bool defer_reduce = false);
 
 // ---- xent_rows.hip: row softmax-CE over materialised logits (wide-E chunked path) ----
 // forward that leaves softmax - onehot (unscaled) in place of the logits (false: row too long)

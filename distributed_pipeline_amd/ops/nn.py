@@ -249,7 +249,7 @@ class _WgradDeferral:
         # gains nothing from deferral and must not double its memory)
         self.budget_bytes = int(float(os.environ.get("DPA_DEFER_WGRAD_GB", "32")) * (1 << 30))
         self.stats = {"deferred": 0, "multi_launches": 0, "segments": 0, "ln_deferred": 0, "ln_reduces": 0,
-                      "bias_deferred": 0, "bias_reduces": 0}
+                      "bias_deferred": 0, "bias_reduces": 0, "attn_deferred": 0, "attn_reduces": 0}
         self.stream = None  # side stream for the un-armed micro-batches' launches (trainer-set)
         self.cur = None     # the stream the current backward runs on (trainer-set, optional)
         self._retired = []  # replaced column-sum buffers (other streams may still use them)
@@ -261,6 +261,9 @@ class _WgradDeferral:
         # reduction per site runs at flush().
         self.ln_sites = {}    # id(gamma) -> [buf, R, D, dg, db, dyb, filled]
         self.bias_sites = {}  # id(bias) -> [buf, rows, K, gb, used]
+        # the attention backward's qkv-bias partials likewise ([rows][3 D] per call, ext.attn_bwd
+        # part_out): one colpart reduction per site and flush instead of one per micro-batch
+        self.attn_sites = {}  # id(bias) -> [buf, rows, H, D, gb, used]
         self.colsum = os.environ.get("DPA_DEFER_COLSUM", "1") != "0"
         # debug (DPA_DEFER_CHECK=1): checksum every held operand when it is held and again when
         # its launch runs - a held tensor whose memory was rewritten meanwhile is reported
@@ -349,6 +352,8 @@ class _WgradDeferral:
             self._ln_reduce(e)
         for e in self.bias_sites.values():
             self._bias_reduce(e)
+        for e in self.attn_sites.values():
+            self._attn_reduce(e)
 
     def release_retired(self, stream):
         """Free the replaced column-sum buffers once ``stream`` has joined every stream that
@@ -369,6 +374,8 @@ class _WgradDeferral:
             e[6] = False
         for e in self.bias_sites.values():
             e[4] = 0
+        for e in self.attn_sites.values():
+            e[5] = 0
 
     # ---- column sums -----------------------------------------------------------------
     def _colsum_on(self):
@@ -441,6 +448,36 @@ class _WgradDeferral:
         slot = e[0][e[4] * rows:(e[4] + 1) * rows]
         e[4] += 1
         self.stats["bias_deferred"] += 1
+        return slot
+
+
+    ATTN_SLOTS = 8
+
+    def _attn_reduce(self, e):
+        if e[5]:
+            get_ext().attn_colpart_reduce(e[0], e[5] * e[1] // e[2], e[2], e[3], e[4])
+            e[5] = 0
+            self.stats["attn_reduces"] += 1
+
+    def attn_part(self, bias, gb, rows, H, D):
+        """A [rows * 3 D] fp32 slot for an attention backward's qkv-bias partials (rows =
+        ext.attn_colpart_rows), reduced onto gb at flush or when the site's slots are full; or None."""
+        if not self._colsum_on() or gb is None or rows % H or not hasattr(get_ext(), "attn_colpart_reduce"):
+            return None  # (an extension built before deferred attention partials: A/B variants)
+        n = rows * 3 * D
+        e = self.attn_sites.get(id(bias))
+        if e is not None and (e[1] != rows or e[2] != H or e[3] != D or not self._same(e[4], gb)):
+            self._attn_reduce(e)
+            self._retired.append(e[0])
+            e = None
+        if e is None:
+            e = [torch.empty(self.ATTN_SLOTS * n, dtype=torch.float32, device=gb.device), rows, H, D, gb, 0]
+            self.attn_sites[id(bias)] = e
+        if e[5] == self.ATTN_SLOTS:
+            self._attn_reduce(e)
+        slot = e[0][e[5] * n:(e[5] + 1) * n]
+        e[5] += 1
+        self.stats["attn_deferred"] += 1
         return slot
 
 
@@ -888,8 +925,14 @@ class _AttnLNFn(torch.autograd.Function):
         dwo, dbo = _lin_param_grads(wo, bo, dy, o2, ro[2], dyb if bo is not None else None)
         # attention
         gbq = _grad_acc(bq)
+        apart = None
+        if gbq is not None and WGRAD_DEFER.active and hasattr(ext, "attn_colpart_rows"):
+            B_, L_ = qkv3.shape[0], qkv3.shape[1]
+            D_ = qkv3.shape[-1] // (3 * heads)
+            apart = WGRAD_DEFER.attn_part(bq, gbq, ext.attn_colpart_rows(B_, L_, heads, D_, False), heads, D_)
+        kw = {"part_out": apart} if apart is not None else {}
         dqkv, dbq = ext.attn_bwd(do.view(o.shape), qkv3, o, lse, heads, float(p_attn), False, seed_a,
-                                 off_a, bq is not None, hm, db_acc=gbq)  # dqkv comes back token-major
+                                 off_a, bq is not None, hm, db_acc=gbq, **kw)  # dqkv comes back token-major
         if gbq is not None:
             dbq = _ACCUMULATED  # the column sums went straight onto bq.grad
         dz = dqkv.view(-1, dqkv.shape[-1])

@@ -163,3 +163,38 @@ def test_head_major_qkv_matches_token_major():
     d1, db1 = ext.attn_bwd(dout, tm.view(B, L, -1), o1, lse1, H, p, False, 3, 9, True)
     d2, db2 = ext.attn_bwd(dout, hm.view(B, L, -1), o2, lse2, H, p, False, 3, 9, True, True)
     assert torch.equal(d1, d2) and torch.equal(db1, db2)
+
+
+@pytest.mark.parametrize("head_major,L,D", [(True, 128, 64), (False, 128, 64), (False, 256, 64), (False, 128, 128)])
+def test_deferred_bias_partials_match_direct(head_major, L, D):
+    """attn_bwd with part_out leaves the qkv-bias partials in caller slots (the deferral window of
+    the reference schedule); one attn_colpart_reduce over several calls' slots adds the same
+    column sums onto the gradient as the per-call reductions."""
+    torch.manual_seed(6)
+    ext = _ext()
+    B, H = 4, 6 if D == 64 else 3
+    E = H * D
+    if head_major and not (L == 128 and D == 64):
+        pytest.skip("head-major needs L = 128, D = 64")
+    rows = ext.attn_colpart_rows(B, L, H, D, False)
+    n = rows * 3 * D
+    slots = torch.full((3 * n,), float("nan"), device="cuda")
+    direct = torch.randn(3 * H * D, device="cuda")
+    deferred = direct.clone()
+    dq_all = []
+    for k in range(3):
+        qkv = (torch.randn(B, L, 3 * E, device="cuda") * 0.5).bfloat16()
+        o, lse = ext.attn_fwd(qkv, H, 0.1, False, 3 + k, 9, head_major)
+        dout = torch.randn_like(o)
+        d1, db1 = ext.attn_bwd(dout, qkv, o, lse, H, 0.1, False, 3 + k, 9, True, head_major, db_acc=direct)
+        assert db1 is None  # accumulated onto direct
+        d2, db2 = ext.attn_bwd(dout, qkv, o, lse, H, 0.1, False, 3 + k, 9, True, head_major, db_acc=deferred,
+                               part_out=slots[k * n:(k + 1) * n])
+        assert db2 is None and torch.equal(d1, d2)
+        dq_all.append(d1)
+    before = deferred.clone()
+    ext.attn_colpart_reduce(slots, 3 * rows // H, H, D, deferred)
+    assert not torch.equal(before, deferred)
+    torch.testing.assert_close(deferred, direct, rtol=1e-5, atol=1e-4)
+    ref = before + sum(d.float().reshape(-1, 3 * E).sum(0) for d in dq_all)
+    torch.testing.assert_close(deferred, ref, rtol=2e-2, atol=2e-2)

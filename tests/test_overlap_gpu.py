@@ -79,10 +79,11 @@ def test_deferred_wgrad_matches_sequential(depth, overlap):
     assert not WGRAD_DEFER.pending
     # the LayerNorm / dact-bias column sums of the un-armed micro-batches were deferred too
     # (partials summed across micro-batches, one reduction per site at flush)
-    for k in ("ln_deferred", "ln_reduces", "bias_deferred", "bias_reduces"):
+    for k in ("ln_deferred", "ln_reduces", "bias_deferred", "bias_reduces", "attn_deferred", "attn_reduces"):
         assert WGRAD_DEFER.stats[k] > before[k], k
     assert not any(e[6] for e in WGRAD_DEFER.ln_sites.values())
     assert not any(e[4] for e in WGRAD_DEFER.bias_sites.values())
+    assert not any(e[5] for e in WGRAD_DEFER.attn_sites.values())
     scale = g0.abs().max().item()
     err = (g0 - g1).abs().max().item()
     assert err <= 2e-5 * scale, (err, scale)

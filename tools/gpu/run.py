@@ -100,6 +100,10 @@ def main(steps):
                  os.path.join(d, "summary.txt"), 120, env)
             with open(os.path.join(d, "summary.txt")) as fh:
                 print(fh.read()[:4000], flush=True)
+            # the trace database runs to tens of MB: only the summary comes back (gpurun's 64 MiB cap)
+            for f_ in os.listdir(d):
+                if f_.endswith(".db"):
+                    os.remove(os.path.join(d, f_))
         elif kind == "ab":
             var, a, b = f[1], f[2], f[3]
             reps = int(f[4]) if len(f) > 4 and f[4] else 2

@@ -34,7 +34,16 @@ for T in (8192, 262144):
             d2 = torch.zeros(N, K, device="cuda")
             ext.gemm_wgrad(dy[:4096].contiguous(), x[:4096].contiguous(), d2, None)
             err = float((d2 - ref).abs().max() / ref.abs().max())
+        # hipBLASLt yardstick: the same product, bf16 out (no fp32 accumulation into a gradient)
+        dyt = dy.t()
+        s.record()
+        for _ in range(reps):
+            torch.mm(dyt, x)
+        e.record()
+        torch.cuda.synchronize()
+        us_bl = s.elapsed_time(e) / reps * 1e3
         print(json.dumps({"T": T, "shape": name, "N": N, "K": K, "us": round(us, 2),
-                          "TF": round(2 * T * N * K / us / 1e6, 1), "relerr": err,
+                          "TF": round(2 * T * N * K / us / 1e6, 1), "blaslt_us": round(us_bl, 2),
+                          "blaslt_TF": round(2 * T * N * K / us_bl / 1e6, 1), "relerr": err,
                           "ws": os.environ.get("DPA_WGRAD_WS", "model")}), flush=True)
         del dy, x, dW
