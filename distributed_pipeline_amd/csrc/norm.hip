@@ -232,8 +232,10 @@ __global__ void __launch_bounds__(256) add_ln_fwd_kernel(
 // 6 x VEC live accumulator/row floats: 4 waves per SIMD up to D = 768, 2-3 up to D = 1024.
 // D >= 1536 takes add_ln_bwd_rowblk_kernel (one row per block) instead.
 // HK: the dy dropout bits come from the pair hash (pre-dropout placement only)
-template <int VEC, bool POST, bool XO, bool HK = false>
-__global__ void __launch_bounds__(256, VEC <= 12 ? 4 : VEC <= 16 ? 2 : 1) add_ln_bwd_kernel(
+// NW waves per block (4, or 8 for the small-R two-stage shapes: the same waves per CU with half the
+// blocks, so half the column-sum partials to store and re-read)
+template <int VEC, bool POST, bool XO, bool HK = false, int NW = 4>
+__global__ void __launch_bounds__(NW * 64, (VEC <= 12 ? 4 : VEC <= 16 ? 2 : 1) * 4 / NW) add_ln_bwd_kernel(
     const bf16_t* __restrict__ dout, const bf16_t* __restrict__ hsave,
     const float* __restrict__ mean_in, const float* __restrict__ rstd_in,
     const bf16_t* __restrict__ gamma, bf16_t* __restrict__ dres, bf16_t* __restrict__ dy,
@@ -241,7 +243,7 @@ __global__ void __launch_bounds__(256, VEC <= 12 ? 4 : VEC <= 16 ? 2 : 1) add_ln
     float p, uint32_t seed, uint32_t offset, const bf16_t* __restrict__ dh_in, float* __restrict__ part,
     bool part_acc, const bf16_t* __restrict__ beta, const bf16_t* __restrict__ hcopy) {
   constexpr int D = VEC * 64;
-  __shared__ float red[4][D];  // reused for dgamma, dbeta, dyb in turn
+  __shared__ float red[NW][D];  // reused for dgamma, dbeta, dyb in turn
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   float g[VEC], adg[VEC], adb[VEC], ady[VEC];
   RowIO<VEC>::load(gamma, lane, g);
@@ -268,7 +270,7 @@ __global__ void __launch_bounds__(256, VEC <= 12 ? 4 : VEC <= 16 ? 2 : 1) add_ln
   for (int i = 0; i < VEC; ++i) { adg[i] = 0.f; adb[i] = 0.f; ady[i] = 0.f; }
   const float sc = p > 0.f ? 1.f / (1.f - p) : 1.f;
   const uint32_t hsm = HK ? pair_seedmix(seed, offset + rng_base()) : 0u, hthr = pair_thr16(p);
-  for (int64_t row = (int64_t)blockIdx.x * 4 + w; row < R; row += (int64_t)gridDim.x * 4) {
+  for (int64_t row = (int64_t)blockIdx.x * NW + w; row < R; row += (int64_t)gridDim.x * NW) {
     float h[VEC], d[VEC];
     RowIO<VEC>::load(hsrc + row * D, lane, h);
     RowIO<VEC>::load(dout + row * D, lane, d);
@@ -361,12 +363,18 @@ __global__ void __launch_bounds__(256, VEC <= 12 ? 4 : VEC <= 16 ? 2 : 1) add_ln
     if (part) {
       float* pr = part + ((int64_t)blockIdx.x * 3 + a) * D;
       for (int c = threadIdx.x; c < D; c += blockDim.x) {
-        const float v = red[0][c] + red[1][c] + red[2][c] + red[3][c];
+        float v = 0.f;
+#pragma unroll
+        for (int k = 0; k < NW; ++k) v += red[k][c];
         pr[c] = part_acc ? pr[c] + v : v;  // part_acc: partials summed over micro-batches
       }
     } else {
-      for (int c = threadIdx.x; c < D; c += blockDim.x)
-        atomicAdd(dst[a] + c, red[0][c] + red[1][c] + red[2][c] + red[3][c]);
+      for (int c = threadIdx.x; c < D; c += blockDim.x) {
+        float v = 0.f;
+#pragma unroll
+        for (int k = 0; k < NW; ++k) v += red[k][c];
+        atomicAdd(dst[a] + c, v);
+      }
     }
   }
 }
@@ -621,12 +629,19 @@ int ln_bwd_blocks(int64_t R) {
 // stored as partials (9.4 MB at 8192 x 768, plain 16-byte stores) and reduced by a second
 // kernel - more blocks would otherwise cost one fp32 atomic per column per block.
 constexpr int64_t LN_SMALL_R = 65536;
+// rows per block of the small-R kernel: 8 waves x 2 rows (was 4 x 2: the 8192 x 768 partials were
+// 9.4 MB written and, deferred, re-read per call against ~38 MB of row traffic)
+#ifndef DPA_LN_SMALL_NW
+#define DPA_LN_SMALL_NW 8
+#endif
+constexpr int LN_SMALL_NW = DPA_LN_SMALL_NW;
+constexpr int LN_SMALL_ROWS = 2 * LN_SMALL_NW;
 // wide rows (D >= 1536, add_ln_bwd_rowblk_kernel): always two-stage, up to 1024 blocks (the
 // partials are 3 x D floats per block; the second stage reads them once)
 constexpr int LN_WIDE_D = 1536;
 static int64_t ln_bwd_two_stage_blocks(int64_t R, int D) {
   if (D >= LN_WIDE_D) return R < 1024 ? R : 1024;  // add_ln_bwd_rowblk_kernel: one row per block at a time
-  if (R <= LN_SMALL_R) return (R + 7) / 8;
+  if (R <= LN_SMALL_R) return (R + LN_SMALL_ROWS - 1) / LN_SMALL_ROWS;
   return 0;
 }
 int64_t ln_bwd_ws_floats(int64_t R, int D) { return ln_bwd_two_stage_blocks(R, D) * 3 * D; }
@@ -687,15 +702,27 @@ static void ln_bwd_impl(const uint16_t* dout, const uint16_t* hsave, const float
       return;
     }
   }
-#define DPA_LN_BWD(P, X, H)                                                                                  \
-  hipLaunchKernelGGL((add_ln_bwd_kernel<VEC, P, X, H>), dim3(nb), dim3(256), 0, s, (const bf16_t*)dout,      \
-                     (const bf16_t*)hsave, mean, rstd, (const bf16_t*)g, (bf16_t*)dres, (bf16_t*)dy, dyb_k, dg, \
-                     db, R, p, seed, off, (const bf16_t*)dh_in, part, pacc, bt, (const bf16_t*)hcopy)
+#define DPA_LN_BWD_NW(P, X, H, NWV)                                                                          \
+  hipLaunchKernelGGL((add_ln_bwd_kernel<VEC, P, X, H, NWV>), dim3(nb), dim3(NWV * 64), 0, s,                  \
+                     (const bf16_t*)dout, (const bf16_t*)hsave, mean, rstd, (const bf16_t*)g, (bf16_t*)dres,  \
+                     (bf16_t*)dy, dyb_k, dg, db, R, p, seed, off, (const bf16_t*)dh_in, part, pacc, bt,       \
+                     (const bf16_t*)hcopy)
+#define DPA_LN_BWD(P, X, H)                             \
+  do {                                                  \
+    if constexpr (D < LN_WIDE_D) {                      \
+      if (two_stage) {                                  \
+        DPA_LN_BWD_NW(P, X, H, LN_SMALL_NW);            \
+        break;                                          \
+      }                                                 \
+    }                                                   \
+    DPA_LN_BWD_NW(P, X, H, 4);                          \
+  } while (0)
   if (post) DPA_LN_BWD(true, false, false);
   else if (hk) DPA_LN_BWD(false, false, true);
   else if (xo) DPA_LN_BWD(false, true, false);
   else DPA_LN_BWD(false, false, false);
 #undef DPA_LN_BWD
+#undef DPA_LN_BWD_NW
   if (two_stage && reduce) ln_colreduce_launch(part, nb, D, dg, db, dyb_k, s);
 }
 
