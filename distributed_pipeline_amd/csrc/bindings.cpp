@@ -645,28 +645,38 @@ static void emb_grad(const at::Tensor& ids, const at::Tensor& dy, at::Tensor& dW
               "emb_grad: unsupported embedding width ", E);
 }
 
-static at::Tensor gemm_nn(const at::Tensor& dy, const at::Tensor& W) {
+// optional transposed weight W^T [K][N] (bf16, contiguous) of a data-gradient GEMM: nullptr when
+// absent; a tensor of any other shape / dtype is a caller bug
+static const uint16_t* wt_ptr(const c10::optional<at::Tensor>& wt, const at::Tensor& W) {
+  if (!wt.has_value() || !wt->defined()) return nullptr;
+  TORCH_CHECK(wt->scalar_type() == at::kBFloat16 && wt->is_contiguous() && wt->dim() == 2 &&
+                  wt->size(0) == W.size(1) && wt->size(1) == W.size(0) && wt->device() == W.device(),
+              "wt must be W^T: bf16 contiguous [K, N]");
+  return reinterpret_cast<const uint16_t*>(wt->data_ptr());
+}
+
+static at::Tensor gemm_nn(const at::Tensor& dy, const at::Tensor& W, c10::optional<at::Tensor> wt) {
   CHECK_DEV(dy); CHECK_BF16(dy); CHECK_BF16(W); CHECK_CONTIG(dy); CHECK_CONTIG(W);
   const int T = (int)dy.size(0), N = (int)dy.size(1), K = (int)W.size(1);
   TORCH_CHECK(W.size(0) == N, "gemm_nn: W [N, K]");
   const c10::DeviceGuard guard(dy.device());
   at::Tensor dx = at::empty({T, K}, dy.options());
   bool ok = dpa::launch_gemm_nn(bf_ptr(dy), bf_ptr(W), reinterpret_cast<uint16_t*>(dx.data_ptr()), T,
-                                N, K, cur_stream());
+                                N, K, cur_stream(), wt_ptr(wt, W));
   TORCH_CHECK(ok, "gemm_nn: unsupported shape");
   return dx;
 }
 
 // dx += dy . W in place (the residual-branch gradient accumulated by the dgrad GEMM);
 // false when the shape does not tile (caller adds separately).
-static bool gemm_nn_acc_(const at::Tensor& dy, const at::Tensor& W, at::Tensor& dx) {
+static bool gemm_nn_acc_(const at::Tensor& dy, const at::Tensor& W, at::Tensor& dx, c10::optional<at::Tensor> wt) {
   CHECK_DEV(dy); CHECK_BF16(dy); CHECK_BF16(W); CHECK_BF16(dx);
   CHECK_CONTIG(dy); CHECK_CONTIG(W); CHECK_CONTIG(dx);
   const int T = (int)dy.size(0), N = (int)dy.size(1), K = (int)W.size(1);
   TORCH_CHECK(W.size(0) == N && dx.size(0) == T && dx.size(1) == K, "gemm_nn_acc_ shapes");
   const c10::DeviceGuard guard(dy.device());
   return dpa::launch_gemmp_nn_acc(bf_ptr(dy), bf_ptr(W), reinterpret_cast<uint16_t*>(dx.data_ptr()), T, N, K,
-                                  dpa::device_cu_count(), cur_stream());
+                                  dpa::device_cu_count(), cur_stream(), wt_ptr(wt, W));
 }
 
 // dz = (dy . W) * act'(aux) [, db = colsum(dz) fp32 when want_db]; returns undefined
@@ -676,7 +686,7 @@ static bool gemm_nn_acc_(const at::Tensor& dy, const at::Tensor& W, at::Tensor& 
 static std::vector<at::Tensor> gemm_nn_dact(const at::Tensor& dy, const at::Tensor& W,
                                             const at::Tensor& aux, int64_t act, bool want_db,
                                             c10::optional<at::Tensor> db_acc,
-                                            c10::optional<at::Tensor> part_out) {
+                                            c10::optional<at::Tensor> part_out, c10::optional<at::Tensor> wt) {
   CHECK_DEV(dy); CHECK_BF16(dy); CHECK_BF16(W);
   CHECK_CONTIG(dy); CHECK_CONTIG(W); CHECK_CONTIG(aux);
   const int T = (int)dy.size(0), N = (int)dy.size(1), K = (int)W.size(1);
@@ -710,7 +720,7 @@ static std::vector<at::Tensor> gemm_nn_dact(const at::Tensor& dy, const at::Tens
   }
   if (dpa::launch_gemmp_nn(bf_ptr(dy), bf_ptr(W), dzp, reinterpret_cast<const uint16_t*>(aux.data_ptr()),
                            (int)act, T, N, K, dpa::device_cu_count(), cur_stream(),
-                           part.defined() ? part.data_ptr<float>() : nullptr)) {
+                           part.defined() ? part.data_ptr<float>() : nullptr, wt_ptr(wt, W))) {
     if (keep) return {dz, at::Tensor()};
     if (acc) {
       if (!part.defined() || !dpa::launch_colsum_acc(part.data_ptr<float>(), (int)part.size(0), K,
@@ -1097,12 +1107,14 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("head_major_L") = 0);
   m.def("gemm_nt_res", &gemm_nt_res, "h = res + dropout_p(x W^T + b) in the GEMM epilogue (None: shape not tiled)",
         py::arg("x"), py::arg("W"), py::arg("b"), py::arg("res"), py::arg("p"), py::arg("seed"), py::arg("offset"));
-  m.def("gemm_nn", &gemm_nn, "dx = dy W (bf16 MFMA)");
+  m.def("gemm_nn", &gemm_nn, "dx = dy W (bf16 MFMA; wt = W^T takes the row-form operand path)", py::arg("dy"),
+        py::arg("W"), py::arg("wt") = py::none());
   m.def("gemm_nn_dact", &gemm_nn_dact,
         "dz = (dy W) * act'(aux) (bf16 MFMA, fused act backward) -> (dz, colsum(dz) fp32 or None)",
         py::arg("dy"), py::arg("W"), py::arg("aux"), py::arg("act"), py::arg("want_db") = false,
-        py::arg("db_acc") = py::none(), py::arg("part_out") = py::none());
-  m.def("gemm_nn_acc_", &gemm_nn_acc_, "dx += dy W in place (bf16 MFMA); False if the shape does not tile");
+        py::arg("db_acc") = py::none(), py::arg("part_out") = py::none(), py::arg("wt") = py::none());
+  m.def("gemm_nn_acc_", &gemm_nn_acc_, "dx += dy W in place (bf16 MFMA); False if the shape does not tile",
+        py::arg("dy"), py::arg("W"), py::arg("dx"), py::arg("wt") = py::none());
   m.def("gemm_wgrad", &gemm_wgrad, "dW += dy^T x, db += colsum(dy) (fp32 atomics, split-K)");
   m.def("gemm_wgrad_multi", &gemm_wgrad_multi, "dW += sum_s dy_s^T x_s over equal token segments, one launch",
         py::arg("dys"), py::arg("xs"), py::arg("dW"), py::arg("db") = py::none());

@@ -297,9 +297,9 @@ bool launch_gemm_nt(const uint16_t* x, const uint16_t* W, const uint16_t* bias, 
 }
 
 bool launch_gemm_nn(const uint16_t* dy, const uint16_t* W, uint16_t* dx, int T, int N, int K,
-                    hipStream_t s) {
+                    hipStream_t s, const uint16_t* WT) {
   // dx[T][K] = dy[T][N] . W[N][K]: M = T, N' = K, reduction = N
-  if (launch_gemmp_nn(dy, W, dx, nullptr, 0, T, N, K, device_cu_count(), s, nullptr)) return true;
+  if (launch_gemmp_nn(dy, W, dx, nullptr, 0, T, N, K, device_cu_count(), s, nullptr, WT)) return true;
   if (launch_gemm256_nn(dy, W, dx, T, N, K, s)) return true;
   if (!gemm_shape_ok(T, K, N)) return false;
   const int blocks = (T / 128) * (K / 128);

@@ -167,7 +167,7 @@ bool launch_gemm_nt(const uint16_t* x, const uint16_t* W, const uint16_t* bias, 
                     uint16_t* z, int T, int N, int K, int act, hipStream_t s,
                     bool* zderiv = nullptr, int hm = 0);
 bool launch_gemm_nn(const uint16_t* dy, const uint16_t* W, uint16_t* dx, int T, int N, int K,
-                    hipStream_t s);
+                    hipStream_t s, const uint16_t* WT = nullptr);
 bool launch_gemm_wgrad(const uint16_t* dy, const uint16_t* x, float* dW, float* db, int T, int N,
                        int K, hipStream_t s, float* ws = nullptr);
 // gemm256.hip: 256x256 8-phase variants (return false when the shape does not tile
@@ -204,10 +204,11 @@ bool launch_gemmp_nt(const uint16_t* x, const uint16_t* W, const uint16_t* bias,
 bool launch_gemmp_nt_res(const uint16_t* x, const uint16_t* W, const uint16_t* bias, const uint16_t* res,
                          uint16_t* h, int T, int N, int K, int ncu, hipStream_t s, float p, uint32_t seed,
                          uint32_t offset);
+// WT (optional): W^T [K][N] bf16 - the data gradient then takes the row-form operand path
 bool launch_gemmp_nn(const uint16_t* dy, const uint16_t* W, uint16_t* dx, const uint16_t* aux, int act,
-                     int T, int N, int K, int ncu, hipStream_t s, float* colpart);
+                     int T, int N, int K, int ncu, hipStream_t s, float* colpart, const uint16_t* WT = nullptr);
 bool launch_gemmp_nn_acc(const uint16_t* dy, const uint16_t* W, uint16_t* dx, int T, int N, int K, int ncu,
-                         hipStream_t s);
+                         hipStream_t s, const uint16_t* WT = nullptr);
 int device_cu_count();
 // bump the device-side Philox offset base of each translation unit that draws numbers
 // (common.h g_rng_base: graph replays)

@@ -52,6 +52,37 @@ def shadow(p, dtype):
     return p.detach().to(dtype)
 
 
+# Transposed bf16 weight shadows for the data-gradient GEMMs (DPA_WT_SHADOW=0: off): dx = dy W reads
+# W^T [K][N] through the forward kernel's row-form operand path instead of W through transposed
+# LDS reads, 3-5% faster per call (tools/probes/dgrad_layout.py) for one transpose copy per weight
+# and optimizer step.
+_WT_SHADOW = os.environ.get("DPA_WT_SHADOW", "1") != "0"
+
+
+def shadow_t(w16):
+    """W^T of a bf16 weight shadow (``param._dpa_shadow``, parallel/flat.py), rebuilt on the current
+    stream the first time it is needed after each rewrite of the shadow; None for anything else."""
+    if not _WT_SHADOW or w16 is None or w16.dim() != 2:
+        return None
+    sp = getattr(w16, "_dpa_space", None)
+    if sp is None or not w16.is_cuda:
+        return None
+    st = getattr(w16, "_dpa_t", None)
+    if st is None:
+        st = torch.empty((w16.shape[1], w16.shape[0]), dtype=w16.dtype, device=w16.device)
+        w16._dpa_t = st
+        w16._dpa_tver = -1
+    if w16._dpa_tver != sp.shadow_version:
+        st.copy_(w16.t())
+        w16._dpa_tver = sp.shadow_version
+        WT_STATS["copies"] += 1
+    WT_STATS["used"] += 1
+    return st
+
+
+WT_STATS = {"used": 0, "copies": 0}
+
+
 def _mm_fp32(a, b):
     """a @ b with fp32 output (bf16 inputs on GPU keep fp32 accumulation)."""
     if a.is_cuda and a.dtype == torch.bfloat16:
@@ -642,7 +673,7 @@ def _lin_param_grads(w, b, dz, x2, native, db=None):
 
 
 def _dgrad(dz, w16, native):
-    return get_ext().gemm_nn(dz, w16) if native else dz @ w16
+    return get_ext().gemm_nn(dz, w16, wt=shadow_t(w16)) if native else dz @ w16
 
 
 class _LinearFn(torch.autograd.Function):
@@ -700,7 +731,7 @@ def _dgrad_acc(dz, w16, native, dx_acc):
         return _dgrad(dz, w16, native)
     if not native and dz.is_cuda:
         return dx_acc.addmm_(dz, w16)
-    if native and get_ext().gemm_nn_acc_(dz, w16, dx_acc):
+    if native and get_ext().gemm_nn_acc_(dz, w16, dx_acc, wt=shadow_t(w16)):
         return dx_acc
     return dx_acc.add_(_dgrad(dz, w16, native))
 
@@ -744,7 +775,7 @@ def _mlp_bwd(dy2, x2, w1_16, w2_16, h, z1, params, cfg, need_dx, db2=None, dx_ac
         gb1 = _grad_acc(b1)
         slot = WGRAD_DEFER.bias_part(b1, gb1, dy2.shape[0], w2_16.shape[1]) if b1 is not None else None
         dz1, db1 = get_ext().gemm_nn_dact(dy2, w2_16, aux, _ACTS.index(act), b1 is not None, db_acc=gb1,
-                                          part_out=slot)
+                                          part_out=slot, wt=shadow_t(w2_16))
         if dz1 is None:
             db1 = None
         elif gb1 is not None:

@@ -638,6 +638,7 @@ class DDPEngine(nn.Module):
                                                                       async_op=True))
             else:
                 dist.all_gather_into_tensor(whole, mine.clone(), group=self.pg)
+        self.space.shadow_written()
         self._master_stale = True
 
     def wait_shadow(self):

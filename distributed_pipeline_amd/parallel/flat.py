@@ -68,6 +68,9 @@ class FlatParamSpace:
         self.grad_flat = torch.zeros(self.numel, dtype=torch.float32, device=device)
         self.shadow_flat = (torch.zeros(self.numel, dtype=shadow_dtype, device=device)
                             if shadow_dtype is not None and shadow_dtype != torch.float32 else None)
+        # bumped whenever the shadow is rewritten (optimizer step, refresh, ZeRO gather): derived
+        # copies of it (the transposed weight shadows of ops/nn.py shadow_t) rebuild once per version
+        self.shadow_version = 0
         with torch.no_grad():
             for p in self.layout:
                 o, n = self.offsets[id(p)], p.numel()
@@ -78,6 +81,7 @@ class FlatParamSpace:
                 p.grad = self.grad_flat[o:o + n].view(p.shape)
                 if self.shadow_flat is not None:
                     p._dpa_shadow = self.shadow_flat[o:o + n].view(p.shape)
+                    p._dpa_shadow._dpa_space = self
         self.refresh_shadow()
 
     # -- views ---------------------------------------------------------------
@@ -98,6 +102,11 @@ class FlatParamSpace:
         if self.shadow_flat is not None:
             from ..ops.optim import cast_bf16_
             cast_bf16_(self.param_flat, self.shadow_flat)
+            self.shadow_version += 1
+
+    def shadow_written(self):
+        """The shadow was rewritten in place (fused optimizer, all-gather)."""
+        self.shadow_version += 1
 
     def zero_grad(self):
         self.grad_flat.zero_()

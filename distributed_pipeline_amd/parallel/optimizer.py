@@ -65,6 +65,8 @@ class FusedAdamW:
                          shadow_bf16=self.space.shadow_flat,
                          emas=self.ema_flats if update_ema else (),
                          ema_rates=self.ema_rates if update_ema else (), skip=skip)
+        if self.space.shadow_flat is not None:
+            self.space.shadow_written()
 
     def zero_grad(self, set_to_none=False):  # noqa: ARG002
         self.space.zero_grad()

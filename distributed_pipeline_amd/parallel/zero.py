@@ -91,6 +91,8 @@ class ZeroFusedAdamW(FusedAdamW):
                              shadow_bf16=None if self.space.shadow_flat is None else self.space.shadow_flat[s:s + c],
                              emas=[e[sl] for e in self.ema_flats] if update_ema else (),
                              ema_rates=self.ema_rates if update_ema else (), skip=skip)
+        if self.space.shadow_flat is not None:
+            self.space.shadow_written()
         self.engine.gather_params()
 
     def zero_grad(self, set_to_none=False):  # noqa: ARG002

@@ -278,3 +278,35 @@ def test_gemm_persistent_dynamic_schedule(T, K, N, act, dynamic_schedule):
         _close(y, yr)
     dy = torch.randn(T, N, device="cuda").bfloat16()
     _close(_ext().gemm_nn(dy, W), dy.float() @ W.float())
+
+
+@pytest.mark.parametrize("T,N,K", [(8192, 768, 3072), (32768, 3072, 768), (16384, 2304, 768), (8192, 768, 768)])
+def test_dgrad_with_transposed_weight_matches(T, N, K):
+    """wt = W^T (the transposed bf16 shadow, ops/nn.py shadow_t): the data-gradient GEMMs take the
+    row-form operand path and give the same products (plain, residual-accumulating, act' times
+    dgrad with bias column sums from u8 codes and from a bf16 act')."""
+    torch.manual_seed(8)
+    ext = _ext()
+    dy = torch.randn(T, N, device="cuda").bfloat16()
+    W = (torch.randn(N, K, device="cuda") * 0.05).bfloat16()
+    WT = W.t().contiguous()
+    ref = dy.float() @ W.float()
+    a, b = ext.gemm_nn(dy, W), ext.gemm_nn(dy, W, wt=WT)
+    _close(b, ref)
+    assert (a.float() - b.float()).abs().max().item() <= 1e-2 * ref.abs().max().item()
+    dx0 = torch.randn(T, K, device="cuda").bfloat16()
+    d1, d2 = dx0.clone(), dx0.clone()
+    assert ext.gemm_nn_acc_(dy, W, d1) and ext.gemm_nn_acc_(dy, W, d2, wt=WT)
+    _close(d2, dx0.float() + ref)
+    # act' from the ffn-in forward (u8 codes and bf16), through the dact dgrad with column sums
+    x = torch.randn(T, 256, device="cuda").bfloat16()
+    W1 = (torch.randn(K, 256, device="cuda") * 0.05).bfloat16()
+    _, z8, m8 = ext.gemm_nt(x, W1, None, 1, 2)
+    _, zb, mb = ext.gemm_nt(x, W1, None, 1, 1)
+    assert m8 == 2 and mb == 1
+    for aux, act in ((z8, 5), (zb, 4)):
+        r1, db1 = ext.gemm_nn_dact(dy, W, aux, act, True)
+        r2, db2 = ext.gemm_nn_dact(dy, W, aux, act, True, wt=WT)
+        d = (r1.float() - r2.float()).abs().max().item()
+        assert d <= 1e-2 * r1.float().abs().max().item(), d
+        torch.testing.assert_close(db2, r2.float().sum(0), rtol=1e-2, atol=1e-2 * db2.abs().max().item())
