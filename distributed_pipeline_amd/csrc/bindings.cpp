@@ -437,6 +437,35 @@ static std::vector<at::Tensor> attn_fwd(const at::Tensor& qkv, int64_t heads, do
   return {out, lse};
 }
 
+// dsts[i] = srcs[i]^T (bf16 2-D, rows / cols multiples of 64), batched into launches of <= MAXN
+static bool transpose_bf16_batch(const std::vector<at::Tensor>& srcs, const std::vector<at::Tensor>& dsts) {
+  TORCH_CHECK(srcs.size() == dsts.size(), "transpose_bf16_batch: src / dst lists differ");
+  if (srcs.empty()) return true;
+  const c10::DeviceGuard guard(srcs[0].device());
+  size_t i = 0;
+  while (i < srcs.size()) {
+    dpa::TransposeBatch d{};
+    int n = 0, tiles = 0;
+    for (; i < srcs.size() && n < dpa::TransposeBatch::MAXN; ++i, ++n) {
+      const at::Tensor &a = srcs[i], &b = dsts[i];
+      TORCH_CHECK(a.scalar_type() == at::kBFloat16 && b.scalar_type() == at::kBFloat16 && a.dim() == 2 &&
+                      b.dim() == 2 && a.is_contiguous() && b.is_contiguous() && b.size(0) == a.size(1) &&
+                      b.size(1) == a.size(0) && a.device() == b.device(),
+                  "transpose_bf16_batch: bf16 contiguous [R, C] -> [C, R]");
+      d.src[n] = reinterpret_cast<const uint16_t*>(a.data_ptr());
+      d.dst[n] = reinterpret_cast<uint16_t*>(b.data_ptr());
+      d.rows[n] = (int)a.size(0);
+      d.cols[n] = (int)a.size(1);
+      d.tile_start[n] = tiles;
+      tiles += (int)(a.size(0) / 64) * (int)(a.size(1) / 64);
+    }
+    d.n = n;
+    d.tile_start[n] = tiles;
+    if (!dpa::launch_transpose_bf16_batch(d, cur_stream())) return false;
+  }
+  return true;
+}
+
 static void attn_colpart_reduce(const at::Tensor& part, int64_t R, int64_t H, int64_t D, at::Tensor db) {
   CHECK_DEV(part);
   TORCH_CHECK(part.scalar_type() == at::kFloat && db.scalar_type() == at::kFloat && part.is_contiguous() &&
@@ -1065,6 +1094,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("adamw_ema", &adamw_ema, "fused AdamW + EMA + bf16 shadow refresh");
   m.def("ema_update", &ema_update, "flat EMA update");
   m.def("cast_bf16", &cast_bf16, "flat fp32->bf16");
+  m.def("transpose_bf16_batch", &transpose_bf16_batch,
+        "dsts[i] = srcs[i]^T for bf16 matrices with 64-multiple sides, one launch per 96 (False: a shape does not tile)");
   m.def("add_ln_fwd", &add_ln_fwd,
         "LN(dropout(y [+pos] [+temb]) + res) (post: dropout(LN(...))) -> (out, hsave, mean, rstd)",
         py::arg("y"), py::arg("res"), py::arg("gamma"), py::arg("beta"), py::arg("p"), py::arg("eps"),

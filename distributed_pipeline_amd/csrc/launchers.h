@@ -32,6 +32,16 @@ void launch_adamw_ema(float* p, const void* g, bool g_bf16, float* m, float* v, 
                       const int* skip = nullptr);
 void launch_ema(float* e, const float* p, int64_t n, float rate, hipStream_t s);
 void launch_cast_bf16(const float* src, uint16_t* dst, int64_t n, hipStream_t s);
+// dst_i = src_i^T for up to MAXN bf16 matrices [rows_i][cols_i] (multiples of 64), one launch;
+// tile_start = prefix sums of (rows / 64) * (cols / 64), tile_start[n] = total
+struct TransposeBatch {
+  static constexpr int MAXN = 96;
+  const uint16_t* src[MAXN];
+  uint16_t* dst[MAXN];
+  int rows[MAXN], cols[MAXN], tile_start[MAXN + 1];
+  int n;
+};
+bool launch_transpose_bf16_batch(const TransposeBatch& d, hipStream_t s);
 void launch_cast_f32(const uint16_t* src, float* dst, int64_t n, hipStream_t s);  // n % 4 == 0
 
 // ---- xent.hip (fused linear + cross-entropy) ----------------------------------

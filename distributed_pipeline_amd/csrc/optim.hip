@@ -242,4 +242,42 @@ void launch_cast_bf16(const float* src, uint16_t* dst, int64_t n, hipStream_t s)
                      (bf16_t*)dst, n);
 }
 
+// ---- batched bf16 transpose (the transposed weight shadows of ops/nn.py shadow_t) -------------
+// One launch for every weight: block b takes the 64 x 64 tile that the prefix sums of the per-weight
+// tile counts assign it, reads it with 4-byte row loads into LDS (a 66-element row pitch: the
+// column reads hit distinct banks) and writes it transposed with 4-byte row stores.
+__global__ void __launch_bounds__(256) transpose_bf16_batch_kernel(TransposeBatch d) {
+  __shared__ uint16_t tile[64][66];
+  int w = 0;
+  while (w + 1 < d.n && (int)blockIdx.x >= d.tile_start[w + 1]) ++w;
+  const int rows = d.rows[w], cols = d.cols[w];
+  const int lt = (int)blockIdx.x - d.tile_start[w], tc = cols / 64;
+  const int r0 = (lt / tc) * 64, c0 = (lt % tc) * 64;
+  const int tx = threadIdx.x & 31, ty = threadIdx.x >> 5;
+  const uint16_t* src = d.src[w];
+  uint16_t* dst = d.dst[w];
+#pragma unroll
+  for (int r = ty; r < 64; r += 8) {
+    const uint32_t v = *reinterpret_cast<const uint32_t*>(src + (int64_t)(r0 + r) * cols + c0 + 2 * tx);
+    tile[r][2 * tx] = (uint16_t)(v & 0xffffu);
+    tile[r][2 * tx + 1] = (uint16_t)(v >> 16);
+  }
+  __syncthreads();
+#pragma unroll
+  for (int c = ty; c < 64; c += 8) {
+    const uint32_t v = (uint32_t)tile[2 * tx][c] | ((uint32_t)tile[2 * tx + 1][c] << 16);
+    *reinterpret_cast<uint32_t*>(dst + (int64_t)(c0 + c) * rows + r0 + 2 * tx) = v;
+  }
+}
+
+bool launch_transpose_bf16_batch(const TransposeBatch& d, hipStream_t s) {
+  if (d.n <= 0 || d.n > TransposeBatch::MAXN) return false;
+  for (int i = 0; i < d.n; ++i)
+    if (d.rows[i] % 64 || d.cols[i] % 64 || d.rows[i] <= 0 || d.cols[i] <= 0) return false;
+  const int tiles = d.tile_start[d.n];
+  if (tiles <= 0) return false;
+  hipLaunchKernelGGL(transpose_bf16_batch_kernel, dim3(tiles), dim3(256), 0, s, d);
+  return true;
+}
+
 }  // namespace dpa

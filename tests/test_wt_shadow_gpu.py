@@ -54,3 +54,17 @@ def test_wt_shadow_training_matches(monkeypatch):
     # noise of the fp32 atomic column sums (3.6e-7 measured); a W^T one step stale would move the
     # weights by Adam's lr-sized (1e-3) steps
     assert err <= 1e-5, err
+
+
+def test_transpose_bf16_batch_matches_torch():
+    from distributed_pipeline_amd.ops._ext import get_ext
+    ext = get_ext(required=True)
+    torch.manual_seed(3)
+    shapes = [(768, 2304), (2304, 768), (768, 768), (3072, 768), (768, 3072), (128, 768), (768, 128), (64, 64)]
+    srcs = [torch.randn(r, c, device="cuda").bfloat16() for r, c in shapes * 13]  # 104: two launches
+    dsts = [torch.empty(c, r, device="cuda", dtype=torch.bfloat16) for r, c in shapes * 13]
+    assert ext.transpose_bf16_batch(srcs, dsts)
+    for a, b in zip(srcs, dsts):
+        assert torch.equal(b, a.t())
+    assert not ext.transpose_bf16_batch([torch.zeros(96, 64, device="cuda", dtype=torch.bfloat16)],
+                                        [torch.zeros(64, 96, device="cuda", dtype=torch.bfloat16)])
