@@ -19,6 +19,8 @@
 //
 // dgamma/dbeta: each block accumulates its rows' contributions in registers,
 // reduces its 4 waves through LDS and adds one fp32 atomic per column.
+#include <cstdlib>
+
 #include "common.h"
 #include "launchers.h"
 
@@ -158,8 +160,22 @@ __global__ void __launch_bounds__(256) add_ln_fwd_kernel(
     int L, int post, int hguard) {
   constexpr int D = VEC * 64;
   const int lane = threadIdx.x & 63;
-  const int64_t row = (int64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
-  if (row >= R) return;
+  // grid-stride over rows (4 per block per pass): gamma / beta are loaded once per wave instead
+  // of once per row, and a capped grid replaces R / 4 short-lived blocks
+  float g[VEC], b[VEC];
+  RowIO<VEC>::load(gamma, lane, g);
+  RowIO<VEC>::load(beta, lane, b);
+  bool write_h0 = hsave != nullptr;
+  if (write_h0 && hguard) {
+    // output-based backward unless some |gamma| is small (the row holds all of gamma)
+    bool small = false;
+#pragma unroll
+    for (int i = 0; i < VEC; ++i) small |= xo_unsafe(g[i], b[i]);
+    write_h0 = __builtin_amdgcn_ballot_w64(small) != 0;
+  }
+  const bool write_h = write_h0;
+  for (int64_t row = (int64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6); row < R;
+       row += (int64_t)gridDim.x * (blockDim.x >> 6)) {
   float h[VEC];
   RowIO<VEC>::load(y + row * D, lane, h);
   if (pos) {
@@ -190,17 +206,7 @@ __global__ void __launch_bounds__(256) add_ln_fwd_kernel(
   // round h to bf16 first so the backward (which reloads the bf16 copy) is consistent
 #pragma unroll
   for (int i = 0; i < VEC; ++i) h[i] = bf2f(f2bf(h[i]));
-  float g[VEC], b[VEC], o[VEC];
-  RowIO<VEC>::load(gamma, lane, g);
-  RowIO<VEC>::load(beta, lane, b);
-  bool write_h = hsave != nullptr;
-  if (write_h && hguard) {
-    // output-based backward unless some |gamma| is small (the row holds all of gamma)
-    bool small = false;
-#pragma unroll
-    for (int i = 0; i < VEC; ++i) small |= xo_unsafe(g[i], b[i]);
-    write_h = __builtin_amdgcn_ballot_w64(small) != 0;
-  }
+  float o[VEC];
   if (write_h) RowIO<VEC>::store(hsave + row * D, lane, h);
   float s = 0.f;
 #pragma unroll
@@ -223,6 +229,7 @@ __global__ void __launch_bounds__(256) add_ln_fwd_kernel(
   if (lane == 0) {
     mean_out[row] = mean;
     rstd_out[row] = rstd;
+  }
   }
 }
 
@@ -598,7 +605,14 @@ static void ln_fwd_impl(const uint16_t* y, const uint16_t* res, const uint16_t* 
                         uint16_t* out, uint16_t* hsave, float* mean, float* rstd, int64_t R, float p,
                         float eps, uint32_t seed, uint32_t off, const uint16_t* pos, const uint16_t* temb,
                         int L, bool post, bool hguard, hipStream_t s) {
-  const unsigned grid = (unsigned)((R + 3) / 4);
+  // a few resident waves per SIMD, each walking rows (DPA_LN_FWD_BLOCKS overrides the cap)
+  static const int64_t cap = [] {
+    const char* e = std::getenv("DPA_LN_FWD_BLOCKS");
+    return e ? (int64_t)std::atoll(e) : (int64_t)device_cu_count() * 32;
+  }();
+  int64_t nb = (R + 3) / 4;
+  if (cap > 0 && nb > cap) nb = cap;
+  const unsigned grid = (unsigned)nb;
   hipLaunchKernelGGL(add_ln_fwd_kernel<VEC>, dim3(grid), dim3(256), 0, s, (const bf16_t*)y,
                      (const bf16_t*)res, (const bf16_t*)g, (const bf16_t*)b, (bf16_t*)out,
                      (bf16_t*)hsave, mean, rstd, R, p, eps, seed, off, (const bf16_t*)pos,
