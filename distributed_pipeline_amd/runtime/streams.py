@@ -8,10 +8,16 @@ got therefore depended on how many pool streams had been taken before it, and tw
 queue serialise: one extra pool stream taken by the logged-nll overlap moved the reference
 schedule's side streams and slowed it from 222 to 240 ms/step (profiles/nll_side_stream_ab_r4.txt).
 
-Here each role gets a stream created with a full CU mask (``stream_create(mode=1)``,
-csrc/runtime/streams.cpp): the CU mask is a queue property, so the runtime gives such a stream an
-HSA queue of its own, never shared with the compute stream, the other roles or torch's pool.
-Roles (reference call sites whose work they carry):
+Here the plan ("ordered", the default) creates its plain streams (``stream_create(mode=0)``,
+csrc/runtime/streams.cpp) once per device, before RCCL and torch's pool take any queue
+(basic_utils/dist_util.py ``claim_stream_plan`` runs right after ``set_device``): HIP hands a new
+stream the least-used queue, so side, wgrad and nll/copy land on queues 2, 3 and 4, and the
+compute stream keeps queue 1 (measured from a rocprofv3 trace of the real start-up order,
+profiles/stream_queues_r5.txt; bench.py reports it as ``streams.hw_queues_measured``).  A CU-masked
+stream (mode 1, plan "cumask") gets a dedicated HSA queue, but the overlapped reference schedule
+ran 523-529 ms/step on such streams against ~222 (profiles/stream_plan_ab_r5.txt), so it stays an
+A/B option.  Roles (reference call sites whose work they carry; the reference runs everything on
+the default stream of its DDP setup, /root/reference/utils/trainer.py:115-128):
 
 =========  ==========================================================================
 compute    the current stream (not created here): forward, backward, optimizer
@@ -25,7 +31,7 @@ copy       H2D prefetch of the next batch (data/prefetch.py; reference trainer.p
 The data plane's comm stream is the C++ reducer's own (csrc/comm/reducer.cpp), created on the
 highest-priority queue pool, which the compute stream (normal priority) never uses.
 
-``DPA_STREAM_PLAN=pool`` restores torch pool streams (A/B runs)."""
+``DPA_STREAM_PLAN=pool`` restores torch pool streams, ``cumask`` the CU-masked ones (A/B runs)."""
 import os
 
 import torch
