@@ -734,7 +734,7 @@ class TrainLoop:
         if len(starts) > 1 and self.defer_wgrad > 1 and self._tile_starved():
             from distributed_pipeline_amd.ops import nn as nn_ops
             defer = nn_ops.WGRAD_DEFER
-            defer.depth, defer.stream, defer.cur = self.defer_wgrad, None, torch.cuda.current_stream()
+            defer.depth, defer.stream, defer.cur = self._defer_depth(), None, torch.cuda.current_stream()
         diff = getattr(self, "diffusion", None)
         if diff is not None:
             # the logged nll may overlap the backward of a whole-batch step; with many small
@@ -790,6 +790,17 @@ class TrainLoop:
         max_toks = int(os.environ.get("DPA_OVERLAP_MAX_TOKENS", "65536"))
         return (not self._probing and self.engine_kind == "native" and self.device.type == "cuda"
                 and toks <= max_toks)
+
+    def _defer_depth(self):
+        """Weight-gradient deferral depth for this chunk size: ``defer_wgrad`` micro-batches at the
+        reference's 8192-token chunks, fewer for larger chunks so the held segments stay near 64K
+        tokens (a 32768-token chunk - seq 512 x 64 - ran 212.6 ms/step at depth 8 and 210.4 at
+        depth 2, profiles/exec_microbatch_ab_r5.txt); DPA_DEFER_WGRAD pins it."""
+        if os.environ.get("DPA_DEFER_WGRAD") is not None or os.environ.get("DPA_DEFER_AUTO", "1") == "0":
+            return self.defer_wgrad
+        toks = self.exec_microbatch * (self._tokens_per_sample or 1)
+        fit = max(2, 65536 // max(1, toks))
+        return min(self.defer_wgrad, fit)
 
     def _overlap_ok(self, nchunks):
         # only tile-starved chunks gain from a second stream; under HIP-graph capture the
@@ -870,7 +881,7 @@ class TrainLoop:
         # the armed backward's grad-ready events follow every contribution to the buffer
         from distributed_pipeline_amd.ops import nn as nn_ops
         defer = nn_ops.WGRAD_DEFER
-        defer.depth = self.defer_wgrad
+        defer.depth = self._defer_depth()
         # the un-armed micro-batches' weight-gradient launches run on a third stream, off the
         # backward chain (DPA_WGRAD_SIDE_STREAM=0: on the backward's own stream)
         if os.environ.get("DPA_WGRAD_SIDE_STREAM", "1") != "0":
