@@ -13,7 +13,8 @@ def _ext():
 
 
 @pytest.mark.parametrize("R,D,res", [(1000, 768, True), (37, 128, False), (4096, 2048, True), (64, 64, True),
-                                     (70000, 2048, True), (3000, 1536, False), (70000, 768, True)])
+                                     (70000, 2048, True), (3000, 1536, False), (70000, 768, True),
+                                     (40000, 768, True)])  # 40000: the capped small-R grid
 def test_add_ln_no_dropout(R, D, res):
     torch.manual_seed(0)
     y = torch.randn(R, D, device="cuda").bfloat16()
@@ -153,7 +154,7 @@ def test_add_ln_dropout_statistics_and_consistency(R, D):
     torch.testing.assert_close(dyb, dy.float().sum(0), rtol=1e-3, atol=1e-2)
 
 
-@pytest.mark.parametrize("R,D", [(2048, 768), (8192, 768), (1024, 2048)])
+@pytest.mark.parametrize("R,D", [(2048, 768), (8192, 768), (1024, 2048), (32768, 768)])
 def test_add_ln_bwd_deferred_partials(R, D):
     """add_ln_bwd(part_buf=...) over three micro-batches (store, add, add) and one
     ln_colreduce give the dgamma / dbeta / colsum(dy) that three immediate calls accumulate."""

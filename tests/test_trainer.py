@@ -302,3 +302,22 @@ def test_device_prefetcher_stages_next_batch_on_side_stream():
         del junk
     with pytest.raises(StopIteration):
         next(pf)
+
+
+def test_defer_depth_scales_with_chunk_tokens(monkeypatch):
+    """Weight-gradient deferral depth: the configured depth at the reference's 8192-token
+    chunks, max(2, 65536 // chunk tokens) for larger ones; DPA_DEFER_WGRAD / DPA_DEFER_AUTO=0 pin it."""
+    from types import SimpleNamespace
+    monkeypatch.delenv("DPA_DEFER_WGRAD", raising=False)
+    monkeypatch.delenv("DPA_DEFER_AUTO", raising=False)
+
+    def depth(mb, toks, d=8):
+        return TrainLoop._defer_depth(SimpleNamespace(defer_wgrad=d, exec_microbatch=mb, _tokens_per_sample=toks))
+
+    assert depth(64, 128) == 8  # seq 128 x 64: 8192 tokens
+    assert depth(64, 512) == 2  # seq 512 x 64: 32768 tokens
+    assert depth(16, 1024) == 4  # GPT-2 seq 1024 x 16: 16384 tokens
+    assert depth(64, 128, d=3) == 3
+    assert depth(1024, 128) == 2
+    monkeypatch.setenv("DPA_DEFER_AUTO", "0")
+    assert depth(64, 512) == 8
