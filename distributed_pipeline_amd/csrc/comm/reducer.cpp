@@ -227,7 +227,7 @@ class BucketReducer {
   // the compute stream (the retry's zero_grad and backward) is ordered after them.
   void disarm() {
     std::lock_guard<std::mutex> g(mu_);
-    if (armed_ && rcomm_ && next_ > 0) {
+    if (armed_ && cs_ && next_ > 0) {
       DPA_HIP_CHECK(hipEventRecord(done_, cs_));
       DPA_HIP_CHECK(hipStreamWaitEvent(compute_stream(), done_, 0));
     }
@@ -264,7 +264,7 @@ class BucketReducer {
       launch(b);
     }
     next_ = nb;
-    if (rcomm_) {
+    if (cs_) {
       if (bf16_) {
         for (int b = 0; b < nb; ++b) {
           if (rs_) {
@@ -318,7 +318,7 @@ class BucketReducer {
   // Phase 1: allocate this rank's staging buffer (two parity halves of the largest
   // bucket) and flag words with hipMalloc and export their IPC handles.
   pybind11::bytes ipc_export() {
-    TORCH_CHECK(rcomm_ != nullptr, "the IPC data plane rides on the direct mode's comm stream");
+    TORCH_CHECK(cs_ != nullptr, "the IPC data plane rides on the direct mode's comm stream (or init_ipc_only)");
     TORCH_CHECK(!rs_ && !bf16_, "IPC all-reduce: fp32 all-reduce buckets only");
     const c10::DeviceGuard guard(grad_.device());
     ipc_cap_ = 0;
@@ -385,6 +385,29 @@ class BucketReducer {
   static hipStream_t compute_stream() { return c10::hip::getCurrentHIPStreamMasqueradingAsCUDA().stream(); }
   static uint16_t* bf_ptr(const at::Tensor& t) { return reinterpret_cast<uint16_t*>(t.data_ptr()); }
 
+  // The IPC data plane without an RCCL communicator: the comm stream and events of the direct
+  // mode, every bucket through csrc/ipc_allreduce.hip (tests: two processes on one device over
+  // gloo, where RCCL refuses two ranks per GPU - tests/test_ipc_reducer_gpu.py).
+ public:
+  void init_ipc_only(int64_t rank) {
+    TORCH_CHECK(cs_ == nullptr, "the reducer already has a comm stream");
+    TORCH_CHECK(grad_.is_cuda() && !rs_ && !bf16_, "IPC-only: fp32 all-reduce buckets of device gradients");
+    TORCH_CHECK(world_ > 1 && world_ <= IPC_MAXW && rank >= 0 && rank < world_, "IPC-only: 2..8 ranks");
+    const c10::DeviceGuard guard(grad_.device());
+    rank_ = (int)rank;
+    make_comm_stream();
+  }
+
+ private:
+  void make_comm_stream() {
+    int least = 0, greatest = 0;
+    DPA_HIP_CHECK(hipDeviceGetStreamPriorityRange(&least, &greatest));
+    DPA_HIP_CHECK(hipStreamCreateWithPriority(&cs_, hipStreamNonBlocking, greatest));
+    ready_.assign(launched_.size(), nullptr);
+    for (auto& e : ready_) DPA_HIP_CHECK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+    DPA_HIP_CHECK(hipEventCreateWithFlags(&done_, hipEventDisableTiming));
+  }
+
   void init_direct(const std::string& uid, int rank, int world) {
     TORCH_CHECK(grad_.is_cuda(), "the direct RCCL data plane needs device gradients");
     TORCH_CHECK(uid.size() == NCCL_UNIQUE_ID_BYTES, "RCCL unique id must be ", NCCL_UNIQUE_ID_BYTES, " bytes");
@@ -394,12 +417,7 @@ class BucketReducer {
     std::memcpy(id.internal, uid.data(), NCCL_UNIQUE_ID_BYTES);
     rank_ = rank;
     DPA_RCCL_CHECK(ncclCommInitRank(&rcomm_, world, id, rank));
-    int least = 0, greatest = 0;
-    DPA_HIP_CHECK(hipDeviceGetStreamPriorityRange(&least, &greatest));
-    DPA_HIP_CHECK(hipStreamCreateWithPriority(&cs_, hipStreamNonBlocking, greatest));
-    ready_.assign(launched_.size(), nullptr);
-    for (auto& e : ready_) DPA_HIP_CHECK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
-    DPA_HIP_CHECK(hipEventCreateWithFlags(&done_, hipEventDisableTiming));
+    make_comm_stream();
   }
 
   at::Tensor slice(const at::Tensor& t, int b) const { return t.slice(0, bounds_[b], bounds_[b + 1]); }
@@ -415,7 +433,7 @@ class BucketReducer {
 
   void launch(int b) {
     if (launched_[b]) return;
-    if (rcomm_) launch_direct(b);
+    if (cs_) launch_direct(b);
     else launch_pg(b);
     launched_[b] = true;
   }
@@ -446,6 +464,8 @@ class BucketReducer {
         return;
       }
     }
+    TORCH_CHECK(rcomm_ != nullptr, "IPC-only data plane: bucket ", b, " (", n,
+                " floats) cannot take the IPC kernel and there is no RCCL communicator");
     if (rs_) {
       void* out = bf16_ ? (void*)(bf_ptr(comm_out_) + shard_off_[b]) : (void*)(shard_.data_ptr<float>() + shard_off_[b]);
       DPA_RCCL_CHECK(ncclReduceScatter(buf, out, (size_t)(n / world_), dt, ncclSum, rcomm_, cs_));
@@ -530,6 +550,7 @@ void register_comm(pybind11::module& m) {
       .def("direct", &BucketReducer::direct)
       .def("stream_priority", &BucketReducer::stream_priority)
       .def("comm_stream", &BucketReducer::comm_stream)
+      .def("init_ipc_only", &BucketReducer::init_ipc_only, pybind11::arg("rank"))
       .def("ipc_export", &BucketReducer::ipc_export)
       .def("ipc_open", &BucketReducer::ipc_open)
       .def("ipc_ready", &BucketReducer::ipc_ready)

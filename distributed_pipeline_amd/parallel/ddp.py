@@ -256,7 +256,15 @@ class DDPEngine(nn.Module):
         # the Python implementation below stays as the reference / test transport.
         # The sharded (reduce-scatter) mode needs a backend with reduce_scatter: RCCL.
         self._native = None
-        if (self.distributed and not self._host_sync_before_comm
+        # opt-in direct xGMI all-reduce over IPC-mapped peer buffers (fp32 all-reduce buckets;
+        # csrc/ipc_allreduce.hip) instead of RCCL rings.  Over gloo (several ranks on one device,
+        # where RCCL refuses to run) the reducer takes it without a communicator: gloo only
+        # exchanges the IPC handles and carries the control plane (tests/test_ipc_reducer_gpu.py)
+        ipc_req = (self.distributed and os.environ.get("DPA_IPC_ALLREDUCE", "0") == "1" and not self.sharded
+                   and self.reduce_dtype == torch.float32 and 1 < self.world_size <= 8
+                   and self.space.device.type == "cuda")
+        ipc_only = ipc_req and self._backend == "gloo"
+        if (self.distributed and (not self._host_sync_before_comm or ipc_only)
                 and (not self.sharded or self._backend == "nccl")
                 and os.environ.get("DPA_NATIVE_REDUCER", "1") != "0"):
             ext = get_ext(required=False)
@@ -278,10 +286,9 @@ class DDPEngine(nn.Module):
                                                  self.grad_shard if self.sharded else None,
                                                  [c[2] for c in self.shard_chunks], uid, self.rank,
                                                  self.world_size)
-                # opt-in: the direct xGMI all-reduce over IPC-mapped peer buffers (fp32
-                # all-reduce buckets; csrc/ipc_allreduce.hip) instead of RCCL rings
-                if (uid and os.environ.get("DPA_IPC_ALLREDUCE", "0") == "1" and not self.sharded
-                        and self.reduce_dtype == torch.float32 and 1 < self.world_size <= 8):
+                if ipc_req and (uid or ipc_only):
+                    if not uid:
+                        self._native.init_ipc_only(self.rank)
                     blobs = [None] * self.world_size
                     dist.all_gather_object(blobs, self._native.ipc_export(), group=self.pg)
                     self._native.ipc_open(blobs)
