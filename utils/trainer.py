@@ -848,14 +848,31 @@ class TrainLoop:
             from distributed_pipeline_amd.ops._ext import get_ext
             ext = get_ext()
 
+        # the two streams already fill the CUs a small chunk's GEMMs leave idle: 128-row GEMM
+        # tiles (gemm256.hip use_half_tiles) only add operand traffic here (32 x 64 schedule:
+        # 222.7 ms/step without, 233.8 with, profiles/half_tiles_r5.txt).  DPA_OVERLAP_HALF_TILES:
+        # 0 off (default), 1 the launcher's own rule everywhere, bwd only on the backward chain
+        half_mode = os.environ.get("DPA_OVERLAP_HALF_TILES", "0")
+        hx = None
+        if half_mode != "1":
+            from distributed_pipeline_amd.ops._ext import get_ext
+            hx = get_ext()
+            if hx is not None:
+                hx.set_gemmp_half(-1 if half_mode == "bwd" else 0)
+        fwd_half = hx is not None and half_mode == "bwd"
+
         def fwd(k):
             if ext is not None:
                 ext.set_gemmp_grid_cap(fwd_cap)
+            if fwd_half:
+                hx.set_gemmp_half(0)
             try:
                 return fwd_(k)
             finally:
                 if ext is not None:
                     ext.set_gemmp_grid_cap(0)
+                if fwd_half:
+                    hx.set_gemmp_half(-1)
 
         def fwd_(k):
             t0 = time.perf_counter()
@@ -892,16 +909,6 @@ class TrainLoop:
             defer.stream = None
         done = None
         self._loss_log_buf = []
-        # the two streams already fill the CUs a small chunk's GEMMs leave idle: 128-row GEMM
-        # tiles (gemm256.hip use_half_tiles) only add operand traffic here (32 x 64 schedule:
-        # 222.7 ms/step without, 233.8 with, profiles/half_tiles_r5.txt; DPA_OVERLAP_HALF_TILES=1
-        # keeps them)
-        hx = None
-        if os.environ.get("DPA_OVERLAP_HALF_TILES", "0") != "1":
-            from distributed_pipeline_amd.ops._ext import get_ext
-            hx = get_ext()
-            if hx is not None:
-                hx.set_gemmp_half(0)
         try:
             nxt = fwd(0)
             for k in range(nch):
