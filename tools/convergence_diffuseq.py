@@ -34,7 +34,7 @@ def _fresh(B, L):
         yield {"input_ids": torch.randint(1000, 30000, (B, L), generator=g), "input_mask": mask}
 
 
-def _train(precision, engine, tmp, steps, B, L, seed=7, fresh=False, stream_seed=None):
+def _train(precision, engine, tmp, steps, B, L, seed=7, fresh=False, stream_seed=None, native_exec=0):
     from basic_utils import logger
     from utils.initialization import create_diffusion_from_config, create_model_from_config, seed_all
     from utils.trainer import DiffusionTrainLoop
@@ -51,7 +51,7 @@ def _train(precision, engine, tmp, steps, B, L, seed=7, fresh=False, stream_seed
                               ema_rate="0.5,0.9,0.99", log_interval=10 ** 9, save_interval=10 ** 9,
                               resume_checkpoint="", learning_steps=0, checkpoint_path=tmp,
                               ddp_engine=engine, precision=precision,
-                              exec_microbatch=-1 if engine == "torch" else 0)
+                              exec_microbatch=-1 if engine == "torch" else native_exec)
     losses = []
     torch.manual_seed(seed if stream_seed is None else stream_seed)
     for i in range(steps):
@@ -74,10 +74,13 @@ def main():
     ap.add_argument("--fresh", action="store_true", help="a new synthetic batch every step")
     ap.add_argument("--control", action="store_true", help="fp32 control run with another noise stream")
     ap.add_argument("--window", type=int, default=0, help="tail window (default min(50, steps/4))")
+    ap.add_argument("--native-exec", type=int, default=0,
+                    help="bf16 engine's executed micro-batch: 0 fused (default), -1 the 64-sample "
+                         "micro-batch schedule under no_sync (BASELINE config #3's own schedule)")
     a = ap.parse_args()
     tmp = tempfile.mkdtemp()
     ref = _train("fp32", "torch", tmp, a.steps, a.batch, a.seq_len, a.seed, a.fresh)
-    nat = _train("bf16", "native", tmp, a.steps, a.batch, a.seq_len, a.seed, a.fresh)
+    nat = _train("bf16", "native", tmp, a.steps, a.batch, a.seq_len, a.seed, a.fresh, native_exec=a.native_exec)
     ctl = (_train("fp32", "torch", tmp, a.steps, a.batch, a.seq_len, a.seed, a.fresh, stream_seed=a.seed + 1000)
            if a.control else None)
     w = a.window or min(50, a.steps // 4)
@@ -86,7 +89,7 @@ def main():
     rel = abs(tail_n - tail_r) / abs(tail_r)
     lines = [f"# DiffuSeq-base 768x12 seq{a.seq_len}, batch {a.batch} ({a.batch // 64} x 64), lr 1e-4, "
              f"{a.steps} steps, synthetic ({'fresh batch every step' if a.fresh else '4 cycled batches'}), "
-             f"seed {a.seed}",
+             f"seed {a.seed}, bf16 schedule {'fused' if a.native_exec == 0 else 'micro-batch ' + str(a.native_exec)}",
              "# step fp32_torch_engine bf16_native_engine" + (" fp32_control(other noise stream)" if a.control else "")]
     for i in range(a.steps):
         row = f"{i} {ref[i].item():.5f} {nat[i].item():.5f}"
