@@ -97,3 +97,19 @@ def test_deferred_wgrad_matches_sequential(depth, overlap):
     assert (p0 - p1).abs().max().item() <= 2.5e-4
     for a, b in zip(l0, l1):
         assert abs(a - b) <= 1e-4 * abs(a)
+
+
+@pytest.mark.parametrize("mode", ["1", "bwd"])
+def test_overlapped_schedule_half_tile_modes(mode, monkeypatch):
+    """DPA_OVERLAP_HALF_TILES=1 (the launcher's 128-row tile rule on both streams) and =bwd (on the
+    backward chain only; utils/trainer.py toggles it around every forward): the tiny model's
+    launches are single partial rounds, so 128-row tiles run; every epilogue is bitwise equal
+    between tile heights, so the first step's gradient matches the sequential loop's."""
+    g0, _, _ = _loop(False, steps=1)
+    ga, _, _ = _loop(False, steps=1)
+    monkeypatch.setenv("DPA_OVERLAP_HALF_TILES", mode)
+    g1, _, _ = _loop(True, steps=1)
+    noise = (g0 - ga).abs().max().item()
+    scale = g0.abs().max().item()
+    err = (g0 - g1).abs().max().item()
+    assert err <= max(4 * noise, 1e-6 * scale), (err, noise, scale)
