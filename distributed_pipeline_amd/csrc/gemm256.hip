@@ -1423,7 +1423,10 @@ static WgradPlan wgrad_plan(int T, int N, int K, int nseg = 1) {
   const int ncu = device_cu_count();
   const double mb = (double)N * K * 4.0 / 1e6;  // gradient bytes, MB
   static int force_ws = -2, force_s = -2;
+  static double merge_cost = 1.0;  // DPA_WGRAD_MERGE_COST: scale of the workspace-merge term (A/B)
   if (force_ws == -2) {
+    const char* m = std::getenv("DPA_WGRAD_MERGE_COST");
+    if (m) merge_cost = std::atof(m);
     // default: merge through the workspace whenever K is split (measured faster at every
     // encoder shape: 8192 tokens -17%, 262144 tokens -2..5%, tools/wgrad_bench.py)
     const char* e = std::getenv("DPA_WGRAD_WS");
@@ -1446,7 +1449,7 @@ static WgradPlan wgrad_plan(int T, int N, int K, int nseg = 1) {
     for (int w = 0; w < 2; ++w) {
       if (w == 1 && slabs < 2) continue;
       if (force_ws >= 0 && w != force_ws && !(w == 0 && slabs < 2)) continue;
-      const double t = w ? main + (2.0 * slabs + 2.0) * mb / 4.0 : fmax(main, wgs * 0.35);
+      const double t = w ? main + merge_cost * (2.0 * slabs + 2.0) * mb / 4.0 : fmax(main, wgs * 0.35);
       if (t < best * 0.98) {
         best = t;
         best_p = WgradPlan{s_eff, kps, w == 1};
