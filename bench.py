@@ -83,6 +83,15 @@ def parse():
     ap.add_argument("--data-workers", type=int, default=2)
     ap.add_argument("--log-interval", type=int, default=20)
     ap.add_argument("--json-out", default=None)
+    ap.add_argument("--project", default="",
+                    help="N = 1 only, after the measurements: a one-GPU PROJECTION of the W > 1 data plane. "
+                         "';'-separated specs W,busbw_GBps[,cus[,lat_us[,bucket_cap_mb,first_bucket_mb]]]: each "
+                         "bucket's all-reduce is replaced by a calibrated kernel on the reducer's comm stream "
+                         "(parallel/ddp.py enable_sim_comm); reported under 'projection'")
+    ap.add_argument("--project-schedules", default="fused,reference",
+                    help="schedules the projection times: fused and/or reference (the 32 x 64 one)")
+    ap.add_argument("--project-wire", default="",
+                    help="'fp32,bf16': time each spec with both wire formats (default: --grad-wire)")
     ap.add_argument("--comm-probe", type=int, default=1,
                     help="N > 1: after the timed runs, time the full gradient reduction and the "
                          "process group's all-reduce at 1-128 MB (reported under comm_probe)")
@@ -155,6 +164,61 @@ def comm_probe(loop, engine, dev, sync):
     # the RCCL knobs this run saw (none set = RCCL's own topology-derived defaults)
     res["rccl_env"] = {k: v for k, v in os.environ.items() if k.startswith(("NCCL_", "RCCL_"))}
     return res
+
+
+def project(a, loop, one_step, timed, exec_used, base):
+    """One-GPU projection of W > 1: the same process's trainer with its
+    DDP engine on the SIMULATED data plane (csrc/comm_sim.hip) - every bucket's all-reduce is a
+    kernel on the reducer's high-priority comm stream that holds `cus` CUs for the link model's
+    time and moves the ring's local HBM bytes.  The step math stays world 1.  Reported per spec,
+    wire and schedule: projected ms/step, exposed comm (ms/step over this process's own
+    no-sim time), the exposed tail after the backward's last kernel, the grad-ready -> start
+    delay (CU contention with the persistent GEMMs) and the link model's total comm time."""
+    import torch
+    eng = loop.ddp_model
+    out = []
+    wires = [w for w in a.project_wire.split(",") if w] or [a.grad_wire]
+    scheds = [x for x in a.project_schedules.split(",") if x]
+    for spec in [x for x in a.project.split(";") if x.strip()]:
+        f = [float(v) for v in spec.split(",")]
+        world, bw = int(f[0]), f[1]
+        cus = int(f[2]) if len(f) > 2 else 64
+        lat = f[3] if len(f) > 3 else 10.0
+        cap = f[4] if len(f) > 4 else None
+        first = f[5] if len(f) > 5 else None
+        for wire in wires:
+            eng.reduce_dtype = torch.bfloat16 if wire == "bf16" else torch.float32
+            eng._comm_buf = None
+            info = eng.enable_sim_comm(world, bw, cus=cus, lat_us=lat, bucket_cap_mb=cap, first_bucket_mb=first)
+            loop.use_ddp = True
+            row = {"spec": dict(info), "schedules": {}}
+            for sch in scheds:
+                if sch == "fused":
+                    loop.exec_microbatch, n = exec_used, a.steps
+                else:
+                    loop.exec_microbatch, n = a.microbatch, a.ref_steps or 8
+                for _ in range(2):  # untimed: the sim reducer's first steps
+                    one_step()
+                eng.sim_stats(reset=True)
+                e = timed(n)
+                st = eng.sim_stats(reset=True)
+                st["last_step_timeline_ms"] = eng.sim_timeline()
+                ms = e / n * 1e3
+                b = base.get(sch)
+                row["schedules"][sch] = dict(st, projected_ms_per_step=round(ms, 3),
+                                             base_ms_per_step=b,
+                                             exposed_comm_ms=round(ms - b, 3) if b else None,
+                                             projected_value=round(world / (ms / 1e3), 4))
+                print(f"[bench] projection W={world} {bw} GB/s {wire} {sch}: {ms:.2f} ms/step "
+                      f"(base {b}), tail {st['exposed_tail_ms']} ms", file=sys.stderr, flush=True)
+            out.append(row)
+            eng.disable_sim_comm()
+            loop.use_ddp = False
+    eng.reduce_dtype = torch.bfloat16 if a.grad_wire == "bf16" else torch.float32
+    loop.exec_microbatch = exec_used
+    return {"kind": "PROJECTION (one GPU, simulated data plane; not a scaling measurement)",
+            "link_model": "busbw per spec; ring time = lat + 2 (W-1)/W x bucket bytes / busbw",
+            "runs": out}
 
 
 def main():
@@ -308,6 +372,13 @@ def main():
             ref_sched["windows_ms"] = [round(w / a.ref_steps * 1e3, 2) for w in wins]
             ref_sched["windows_diag"] = diag
 
+    projection = None
+    if a.project and world == 1 and engine == "native" and dev.type == "cuda":
+        base = {"fused": round(elapsed / a.steps * 1e3, 3),
+                "reference": ref_sched["ms_per_step"] if ref_sched else None}
+        projection = project(a, loop, one_step, timed, exec_used, base)
+        loop._exec_auto = False
+
     ms = elapsed / a.steps * 1e3
     steps_per_s = a.steps / elapsed
     value = steps_per_s * world
@@ -356,16 +427,27 @@ def main():
                     else "reference: one fwd/bwd per micro-batch",
         "reference_schedule": ref_sched,
     }
+    if projection is not None:
+        out["projection"] = projection
     if engine == "native":
         out["config"]["bucket_mb"] = loop.ddp_model.bucket_sizes_mb()
         if loop.ddp_model.bucket_tune is not None:
-            out["config"]["bucket_tune"] = {"cap_mb": loop.ddp_model.bucket_cap_mb,
-                                            "first_mb": loop.ddp_model.first_bucket_mb,
-                                            "sweep": loop.ddp_model.bucket_tune}
+            out["config"]["bucket_tune"] = dict({"cap_mb": loop.ddp_model.bucket_cap_mb,
+                                                 "first_mb": loop.ddp_model.first_bucket_mb},
+                                                **loop.ddp_model.bucket_tune)
         nat = getattr(loop.ddp_model, "_native", None)
+        direct = nat is not None and nat.direct()
         out["config"]["comm"] = ("reducer-owned RCCL communicator, priority %d stream" % nat.stream_priority()
-                                 if nat is not None and nat.direct() else
-                                 ("c10d process group" if world > 1 else "none (world 1)"))
+                                 if direct else ("c10d process group" if world > 1 else "none (world 1)"))
+        # where each collective of a W > 1 step runs (the W > 1 resource plan)
+        eng_ = loop.ddp_model
+        out["config"]["data_plane"] = {
+            "bucket_reduce": out["config"]["comm"],
+            "bucket_tuning": ((eng_.bucket_tune or {}).get("timed_on") or
+                              ("fixed sizes (--bucket-cap-mb)" if a.bucket_cap_mb > 0 else "none (world 1)")),
+            "zero1_param_gather": ("n/a" if not eng_.sharded else
+                                   "reducer-owned RCCL communicator, comm stream" if direct else "process group"),
+            "control_plane": "process group (loss / grad-norm logging means, checksums)" if world > 1 else "none"}
     # evidence of what the job ran on: the backend's world size, the ranks of the communicator
     # the gradient buckets are reduced over (the reducer-owned RCCL communicator's
     # ncclCommCount in direct mode), and the spread of per-rank step times

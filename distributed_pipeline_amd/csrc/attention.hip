@@ -902,19 +902,6 @@ template <int D>
 static void attn_fwd_general(const uint16_t* qkv, uint16_t* out, float* lse, int B, int L, int H,
                              float p, bool causal, uint32_t seed, uint32_t offset, hipStream_t s) {
   dim3 grid(attn_grid(B, L, H, causal));  // attn_item() layout
-  static const bool two_pass = [] {
-    const char* e = getenv("DPA_ATTN_TWOPASS");
-    return e != nullptr && e[0] == '1';
-  }();
-  if (two_pass) {
-    if (causal)
-      hipLaunchKernelGGL((attn_fwd_kernel<D, true>), grid, dim3(256), 0, s, (const bf16_t*)qkv,
-                         (bf16_t*)out, lse, L, H, p, seed, offset);
-    else
-      hipLaunchKernelGGL((attn_fwd_kernel<D, false>), grid, dim3(256), 0, s, (const bf16_t*)qkv,
-                         (bf16_t*)out, lse, L, H, p, seed, offset);
-    return;
-  }
 #define DPA_FWD_ONLINE(C, DR)                                                                      \
   hipLaunchKernelGGL((attn_fwd_online_kernel<D, C, DR>), grid, dim3(256), 0, s, (const bf16_t*)qkv, \
                      (bf16_t*)out, lse, L, H, p, seed, offset)

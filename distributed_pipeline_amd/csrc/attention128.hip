@@ -1262,14 +1262,7 @@ __global__ void __launch_bounds__(256) colpart_reduce_kernel(const float* __rest
   if (r == 0) atomicAdd(db + q * H * HD + h * HD + d, red[0][d] + red[1][d] + red[2][d] + red[3][d]);
 }
 
-static bool enabled() {
-  static int on = -1;
-  if (on < 0) {
-    const char* e = std::getenv("DPA_ATTN128");
-    on = (e && e[0] == '0') ? 0 : 1;
-  }
-  return on != 0;
-}
+static bool enabled() { return true; }
 
 static int num_cus() {
   static int n = 0;

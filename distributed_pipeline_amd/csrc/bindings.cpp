@@ -441,6 +441,9 @@ static std::vector<at::Tensor> attn_fwd(const at::Tensor& qkv, int64_t heads, do
 static bool transpose_bf16_batch(const std::vector<at::Tensor>& srcs, const std::vector<at::Tensor>& dsts) {
   TORCH_CHECK(srcs.size() == dsts.size(), "transpose_bf16_batch: src / dst lists differ");
   if (srcs.empty()) return true;
+  // every shape is validated before the first chunk launches: a False return means nothing ran
+  for (const at::Tensor& a : srcs)
+    if (a.dim() != 2 || a.size(0) % 64 || a.size(1) % 64) return false;
   const c10::DeviceGuard guard(srcs[0].device());
   size_t i = 0;
   while (i < srcs.size()) {
@@ -759,11 +762,14 @@ static std::vector<at::Tensor> gemm_nn_dact(const at::Tensor& dy, const at::Tens
     }
     return {dz, part.defined() ? part.sum(0) : at::Tensor()};
   }
-  TORCH_CHECK(act != 5, "gemm_nn_dact: u8 act' codes need the persistent kernel (shape T=", T, " K=", K, ")");
   // no persistent kernel for this shape: the column sums from dz itself (a kept partial slot
   // gets them in row 0, zeros elsewhere; all zeros when no fused kernel ran either - the
   // caller then computes db itself)
   if (keep) part_out->zero_();
+  // u8 act' codes (act 5) are read only by the persistent kernel: decline, and the caller decodes
+  // the codes and runs the plain dgrad + bias_act_bwd (a launcher gate flipped between the q8
+  // forward and this backward, e.g. set_gemm256(False) in an A/B, must not crash the step)
+  if (act == 5) return {at::Tensor(), at::Tensor()};
   if (dpa::launch_gemm256_nn_dact(bf_ptr(dy), bf_ptr(W), bf_ptr(aux), dzp, T, N, K, (int)act, cur_stream())) {
     if (!want_db) return {dz, at::Tensor()};
     at::Tensor cs = dz.sum(0, false, at::kFloat);
@@ -793,12 +799,8 @@ static void gemm_wgrad(const at::Tensor& dy, const at::Tensor& x, at::Tensor& dW
   // shape: the 128-tile kernel then merges its ~170 token splits with device-scope fp32
   // atomics, which run at the memory side (0.39 ms for a 0.05 TFLOP gradient).  Zero-padding
   // that side to 256 (a [T, 256] copy) runs it on the 256 x 256 split-K kernel with its
-  // workspace merge instead; the padded half of the result is discarded
-  // (DPA_WGRAD_PAD=0: the 128-tile kernel).
-  static const bool pad_ok = [] {
-    const char* e = std::getenv("DPA_WGRAD_PAD");
-    return !e || std::atoi(e) != 0;
-  }();
+  // workspace merge instead; the padded half of the result is discarded.
+  constexpr bool pad_ok = true;
   const int Np = (N + 255) / 256 * 256, Kp = (K + 255) / 256 * 256;
   if (pad_ok && (Np != N || Kp != K) && N % 64 == 0 && K % 64 == 0 && T % 256 == 0 && T >= 256 &&
       (int64_t)Np * Kp <= 2 * (int64_t)N * K) {

@@ -201,6 +201,7 @@ class BucketReducer {
     if (ipc_flags_) (void)hipFree(ipc_flags_);
     for (hipEvent_t e : ready_) if (e) (void)hipEventDestroy(e);
     if (done_) (void)hipEventDestroy(done_);
+    if (gather_ev_) (void)hipEventDestroy(gather_ev_);
     if (cs_) (void)hipStreamDestroy(cs_);
   }
 
@@ -220,6 +221,9 @@ class BucketReducer {
     for (auto& w : work_) w.reset();
     next_ = 0;
     armed_ = true;
+    if (sim_)  // fresh timeline: every word all-ones (the kernels keep minima)
+      DPA_HIP_CHECK(hipMemsetAsync(sim_tl_.data_ptr(), 0xff, sim_tl_.nbytes(),
+                                   arm_stream_ ? arm_stream_ : compute_stream()));
   }
 
   // Abandon a partially run backward (out-of-memory retry).  Buckets its hooks already
@@ -276,8 +280,12 @@ class BucketReducer {
           }
         }
       }
+      if (sim_) launch_time_marker(sim_end_slot(), compute_stream());  // the backward's end
       DPA_HIP_CHECK(hipEventRecord(done_, cs_));
       DPA_HIP_CHECK(hipStreamWaitEvent(compute_stream(), done_, 0));
+      if (sim_)
+        launch_comm_sim_stats(sim_slot(0, 0), (int)launched_.size(), sim_end_slot(),
+                              reinterpret_cast<unsigned long long*>(sim_acc_.data_ptr()), compute_stream());
     } else {
       for (int b = 0; b < nb; ++b) {
         if (work_[b]) {
@@ -298,6 +306,93 @@ class BucketReducer {
     arm(0);
     finalize();
   }
+
+  // ---- the data plane's own collectives beyond the bucket reductions (direct mode) ----
+  // Start-up bucket tuning on THIS communicator and comm stream (not the process group's, whose
+  // pool stream lands on a compute-shared queue): mean ms of `iters` all-reduces of n floats.
+  double time_allreduce(int64_t n, int64_t iters) {
+    TORCH_CHECK(rcomm_ != nullptr && n > 0 && iters > 0, "time_allreduce: direct mode only");
+    const c10::DeviceGuard guard(grad_.device());
+    at::Tensor x = at::zeros({n}, grad_.options());
+    hipEvent_t e0, e1;
+    DPA_HIP_CHECK(hipEventCreate(&e0));
+    DPA_HIP_CHECK(hipEventCreate(&e1));
+    DPA_RCCL_CHECK(ncclAllReduce(x.data_ptr(), x.data_ptr(), (size_t)n, ncclFloat32, ncclSum, rcomm_, cs_));  // warm
+    DPA_HIP_CHECK(hipEventRecord(e0, cs_));
+    for (int64_t i = 0; i < iters; ++i)
+      DPA_RCCL_CHECK(ncclAllReduce(x.data_ptr(), x.data_ptr(), (size_t)n, ncclFloat32, ncclSum, rcomm_, cs_));
+    DPA_HIP_CHECK(hipEventRecord(e1, cs_));
+    DPA_HIP_CHECK(hipEventSynchronize(e1));
+    float ms = 0.f;
+    DPA_HIP_CHECK(hipEventElapsedTime(&ms, e0, e1));
+    (void)hipEventDestroy(e0);
+    (void)hipEventDestroy(e1);
+    last_coll_stream_ = cs_;
+    return (double)ms / (double)iters;
+  }
+
+  // Re-plan the buckets (not while armed): the engine's measured plan replaces the provisional one
+  // the communicator was created with.  All-reduce mode only (ZeRO-1's layout pads bucket ends).
+  void set_buckets(std::vector<int64_t> bounds, std::vector<int64_t> param_bucket) {
+    std::lock_guard<std::mutex> g(mu_);
+    TORCH_CHECK(!armed_ && !rs_, "set_buckets: all-reduce mode, not armed");
+    TORCH_CHECK(bounds.size() >= 2 && bounds.front() == 0 && bounds.back() <= grad_.numel() &&
+                    param_bucket.size() == bucket_of_.size(), "set_buckets: bad plan");
+    const int nb = (int)bounds.size() - 1;
+    std::vector<int> size(nb, 0);
+    for (int64_t b : param_bucket) {
+      TORCH_CHECK(b >= 0 && b < nb, "param bucket index out of range");
+      size[b] += 1;
+    }
+    for (int b = 0; b < nb; ++b) TORCH_CHECK(size[b] > 0, "empty bucket ", b);
+    bounds_ = std::move(bounds);
+    bucket_of_ = std::move(param_bucket);
+    size_ = size;
+    pending_ = size_;
+    work_.assign(nb, {});
+    launched_.assign(nb, false);
+    for (hipEvent_t e : ready_) if (e) (void)hipEventDestroy(e);
+    ready_.assign(nb, nullptr);
+    if (cs_)
+      for (auto& e : ready_) DPA_HIP_CHECK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+  }
+
+  // ZeRO-1 parameter all-gather on the data plane's communicator and comm stream: for each bucket
+  // in `order`, flat[bounds[b], bounds[b + 1]) is gathered in place from every rank's chunk
+  // (chunk r of the bucket is rank r's).  flat: fp32 master or bf16 shadow, laid out like the
+  // gradients.  Ordered after the current stream's work (an event); wait_gather() orders the
+  // current stream after it.  Nothing blocks the host.
+  void all_gather_buckets(at::Tensor flat, std::vector<int64_t> order) {
+    TORCH_CHECK(rcomm_ != nullptr, "all_gather_buckets: direct mode only");
+    TORCH_CHECK(flat.is_contiguous() && flat.dim() == 1 && flat.numel() >= bounds_.back() &&
+                    (flat.scalar_type() == at::kFloat || flat.scalar_type() == at::kBFloat16),
+                "all_gather_buckets: 1-D fp32 / bf16 flat buffer laid out like the gradients");
+    const c10::DeviceGuard guard(grad_.device());
+    const ncclDataType_t dt = flat.scalar_type() == at::kFloat ? ncclFloat32 : ncclBfloat16;
+    const int64_t es = flat.element_size();
+    char* base = static_cast<char*>(flat.data_ptr());
+    if (!gather_ev_) DPA_HIP_CHECK(hipEventCreateWithFlags(&gather_ev_, hipEventDisableTiming));
+    DPA_HIP_CHECK(hipEventRecord(gather_ev_, compute_stream()));
+    DPA_HIP_CHECK(hipStreamWaitEvent(cs_, gather_ev_, 0));
+    for (int64_t b : order) {
+      TORCH_CHECK(b >= 0 && b + 1 < (int64_t)bounds_.size(), "bucket out of range");
+      const int64_t n = bounds_[b + 1] - bounds_[b];
+      TORCH_CHECK(n % world_ == 0, "bucket ", b, " is not divisible by the world size");
+      const int64_t c = n / world_;
+      char* whole = base + bounds_[b] * es;
+      DPA_RCCL_CHECK(ncclAllGather(whole + (int64_t)rank_ * c * es, whole, (size_t)c, dt, rcomm_, cs_));
+    }
+    DPA_HIP_CHECK(hipEventRecord(gather_ev_, cs_));
+    gather_pending_ = true;
+    last_coll_stream_ = cs_;
+  }
+  void wait_gather() {
+    if (!gather_pending_) return;
+    DPA_HIP_CHECK(hipStreamWaitEvent(compute_stream(), gather_ev_, 0));
+    gather_pending_ = false;
+  }
+  // stream of the last tuning / gather collective (tests: it is the comm stream)
+  int64_t last_collective_stream() const { return (int64_t)reinterpret_cast<uintptr_t>(last_coll_stream_); }
 
   // ranks of the reducer-owned RCCL communicator (ncclCommCount), -1 without one
   int64_t comm_size() const {
@@ -398,7 +493,88 @@ class BucketReducer {
     make_comm_stream();
   }
 
+  // Simulated data plane (csrc/comm_sim.hip): a one-GPU PROJECTION of a world-`world` all-reduce.
+  // Every bucket launches comm_sim_kernel on the comm stream instead of a collective: `cus`
+  // workgroups that hold their CU slots for lat_us + 2 (W - 1) / W x bytes / busbw and move the
+  // ring's local HBM bytes; the gradients stay this rank's (world-1 math).  Per-step timeline
+  // sums accumulate on the device (sim_stats).
+  void init_sim(int64_t world, double busbw_gbps, int64_t cus, double lat_us) {
+    TORCH_CHECK(cs_ == nullptr, "the reducer already has a comm stream");
+    TORCH_CHECK(grad_.is_cuda() && !rs_, "sim data plane: all-reduce buckets of device gradients");
+    const c10::DeviceGuard guard(grad_.device());
+    sim_ = true;
+    set_sim(world, busbw_gbps, cus, lat_us);
+    const int nb = (int)launched_.size();
+    sim_tl_ = at::empty({(int64_t)nb * 4 + 8}, grad_.options().dtype(at::kLong));
+    DPA_HIP_CHECK(hipMemset(sim_tl_.data_ptr(), 0xff, sim_tl_.nbytes()));
+    sim_acc_ = at::zeros({8}, grad_.options().dtype(at::kLong));
+    make_comm_stream();
+  }
+  void set_sim(int64_t world, double busbw_gbps, int64_t cus, double lat_us) {
+    TORCH_CHECK(world >= 2 && busbw_gbps > 0 && cus >= 1 && cus <= 1024 && lat_us >= 0, "sim: bad parameters");
+    sim_world_ = (int)world;
+    sim_bw_ = busbw_gbps;
+    sim_cus_ = (int)cus;
+    sim_lat_ = lat_us;
+  }
+  bool sim() const { return sim_; }
+  // {steps, exposed tail, ready->start delay, bucket busy time, comm span, last tail} in ms
+  // (sums over the steps since the last reset; the device accumulates in 10 ns ticks)
+  std::vector<double> sim_stats() {
+    TORCH_CHECK(sim_, "not in sim mode");
+    at::Tensor a = sim_acc_.cpu();
+    const int64_t* v = a.data_ptr<int64_t>();
+    std::vector<double> out{(double)v[0]};
+    for (int i = 1; i < 6; ++i) out.push_back((double)v[i] * 1e-5);
+    return out;
+  }
+  // the last step's per-bucket timeline [nb][3] = {grad ready, first start, last end} in ms after
+  // the first grad-ready stamp, plus the backward's end as a last row (-1: not stamped)
+  at::Tensor sim_timeline() {
+    TORCH_CHECK(sim_, "not in sim mode");
+    DPA_HIP_CHECK(hipStreamSynchronize(cs_));
+    at::Tensor t = sim_tl_.cpu();
+    const uint64_t* v = reinterpret_cast<const uint64_t*>(t.data_ptr<int64_t>());
+    const int nb = (int)launched_.size();
+    uint64_t t0 = ~0ull;
+    for (int b = 0; b < nb; ++b) t0 = std::min(t0, v[b * 4 + 2]);
+    at::Tensor out = at::full({nb + 1, 3}, -1.0, at::kDouble);
+    double* o = out.data_ptr<double>();
+    auto ms = [&](uint64_t x) { return (x == ~0ull || t0 == ~0ull) ? -1.0 : (double)(x - t0) * 1e-5; };
+    for (int b = 0; b < nb; ++b) {
+      o[b * 3] = ms(v[b * 4 + 2]);
+      o[b * 3 + 1] = ms(v[b * 4]);
+      o[b * 3 + 2] = v[b * 4 + 1] == ~0ull ? -1.0 : ms(~v[b * 4 + 1]);
+    }
+    o[nb * 3] = ms(v[(int64_t)nb * 4]);  // backward end
+    return out;
+  }
+  void sim_reset() {
+    TORCH_CHECK(sim_, "not in sim mode");
+    sim_acc_.zero_();
+  }
+  // simulated duration of a bucket of `bytes` on the wire (ms)
+  double sim_bucket_ms(int64_t bytes) const {
+    return sim_lat_ * 1e-3 + 2.0 * (sim_world_ - 1) / sim_world_ * (double)bytes / (sim_bw_ * 1e9) * 1e3;
+  }
+
  private:
+  // words of bucket b: {0: first start, 1: ~last end, 2: grad ready, 3: unused}; after the
+  // nb buckets: the backward's end
+  unsigned long long* sim_slot(int b, int k) {
+    return reinterpret_cast<unsigned long long*>(sim_tl_.data_ptr()) + (int64_t)b * 4 + k;
+  }
+  unsigned long long* sim_end_slot() { return sim_slot((int)launched_.size(), 0); }
+
+  void launch_sim(int b, void* buf, int64_t bytes) {
+    // grad-ready stamp on the producing stream (index 2 of the bucket's words), then the
+    // collective's stand-in on the comm stream (words 0 / 1)
+    const double ms = sim_bucket_ms(bytes);
+    const uint64_t ticks = (uint64_t)(ms * 1e5);  // 100 MHz constant clock
+    const int64_t touch = (int64_t)(2.0 * (sim_world_ - 1) / sim_world_ * (double)bytes);
+    launch_comm_sim(buf, bytes, touch, ticks, sim_cus_, sim_slot(b, 0), cs_);
+  }
+
   void make_comm_stream() {
     int least = 0, greatest = 0;
     DPA_HIP_CHECK(hipDeviceGetStreamPriorityRange(&least, &greatest));
@@ -441,6 +617,7 @@ class BucketReducer {
   void launch_direct(int b) {
     const int64_t n = bounds_[b + 1] - bounds_[b];
     // the grad-ready point: everything the backward's stream queued so far
+    if (sim_) launch_time_marker(sim_slot(b, 2), arm_stream_ ? arm_stream_ : compute_stream());
     DPA_HIP_CHECK(hipEventRecord(ready_[b], arm_stream_ ? arm_stream_ : compute_stream()));
     DPA_HIP_CHECK(hipStreamWaitEvent(cs_, ready_[b], 0));
     float* g = grad_.data_ptr<float>() + bounds_[b];
@@ -451,6 +628,10 @@ class BucketReducer {
       launch_cast_bf16(g, w, n, cs_);
       buf = w;
       dt = ncclBfloat16;
+    }
+    if (sim_) {
+      launch_sim(b, buf, n * (bf16_ ? 2 : 4));
+      return;
     }
     if (ipc_ready_) {
       // one-shot below 256 KiB (latency), two-shot above (bandwidth: (W-1)/W n reads twice)
@@ -522,6 +703,14 @@ class BucketReducer {
   int64_t ipc_cap_ = 0;
   uint32_t ipc_epoch_ = 0;
   IpcPeers peers_{};
+  hipEvent_t gather_ev_ = nullptr;
+  bool gather_pending_ = false;
+  hipStream_t last_coll_stream_ = nullptr;
+  // simulated data plane
+  bool sim_ = false;
+  int sim_world_ = 2, sim_cus_ = 1;
+  double sim_bw_ = 1.0, sim_lat_ = 0.0;
+  at::Tensor sim_tl_, sim_acc_;
   hipStream_t cs_ = nullptr;
   hipStream_t arm_stream_ = nullptr;  // the armed backward's stream (arm()), null: current
   std::vector<hipEvent_t> ready_;
@@ -551,6 +740,29 @@ void register_comm(pybind11::module& m) {
       .def("stream_priority", &BucketReducer::stream_priority)
       .def("comm_stream", &BucketReducer::comm_stream)
       .def("init_ipc_only", &BucketReducer::init_ipc_only, pybind11::arg("rank"))
+      .def_static("simulated",
+                  [](at::Tensor grad_flat, std::vector<int64_t> bounds, std::vector<int64_t> param_bucket,
+                     bool bf16_wire) {
+                    return std::make_unique<BucketReducer>(c10::intrusive_ptr<c10d::ProcessGroup>(), grad_flat,
+                                                           bounds, param_bucket, bf16_wire, c10::nullopt,
+                                                           std::vector<int64_t>(), std::string(), 0, 1);
+                  },
+                  "a reducer without a process group, for the simulated data plane (then init_sim)")
+      .def("init_sim", &BucketReducer::init_sim, pybind11::arg("world"), pybind11::arg("busbw_gbps"),
+           pybind11::arg("cus"), pybind11::arg("lat_us"))
+      .def("set_sim", &BucketReducer::set_sim, pybind11::arg("world"), pybind11::arg("busbw_gbps"),
+           pybind11::arg("cus"), pybind11::arg("lat_us"))
+      .def("sim", &BucketReducer::sim)
+      .def("sim_stats", &BucketReducer::sim_stats)
+      .def("sim_reset", &BucketReducer::sim_reset)
+      .def("sim_timeline", &BucketReducer::sim_timeline)
+      .def("time_allreduce", &BucketReducer::time_allreduce, pybind11::arg("n"), pybind11::arg("iters"),
+           pybind11::call_guard<pybind11::gil_scoped_release>())
+      .def("set_buckets", &BucketReducer::set_buckets)
+      .def("all_gather_buckets", &BucketReducer::all_gather_buckets)
+      .def("wait_gather", &BucketReducer::wait_gather)
+      .def("last_collective_stream", &BucketReducer::last_collective_stream)
+      .def("sim_bucket_ms", &BucketReducer::sim_bucket_ms)
       .def("ipc_export", &BucketReducer::ipc_export)
       .def("ipc_open", &BucketReducer::ipc_open)
       .def("ipc_ready", &BucketReducer::ipc_ready)

@@ -1276,10 +1276,7 @@ static bool use_half_tiles(int M, int N, int ncu) {
     g_gemmp_half = e ? std::atoi(e) : 1;
   }
   const int mode = g_gemmp_half;
-  static const double HALF_COST = [] {
-    const char* e = std::getenv("DPA_GEMMP_HALF_COST");
-    return e ? std::atof(e) : 0.66;
-  }();
+  constexpr double HALF_COST = 0.66;
   if (mode == 0 || M % 256) return false;
   if (mode >= 2) return true;
   const int g = persistent_grid(1 << 30, ncu);
@@ -1292,10 +1289,6 @@ template <bool B_TR, int EPI, int ACT>
 static void gemmp_go(const uint16_t* a, int64_t lda, const uint16_t* b, int64_t ldb, int M, int N, int K,
                      uint16_t* c, const uint16_t* bias, uint16_t* z, int ncu, hipStream_t s,
                      float* colpart = nullptr, int hm = 0, const g256::EpiArgs& ea = g256::EpiArgs{}) {
-  static const bool grouped = [] {
-    const char* e = std::getenv("DPA_GEMMP_GROUPED");  // "0": default policy (A/B runs)
-    return !(e && e[0] == '0');
-  }();
   if constexpr (EPI != 4) {
     if (use_half_tiles(M, N, ncu)) {
       gemmp_launch<B_TR, EPI, ACT, 0, 1, true>(a, lda, b, ldb, M, N, K, c, bias, z, ncu, s, colpart, hm, ea);
@@ -1303,7 +1296,7 @@ static void gemmp_go(const uint16_t* a, int64_t lda, const uint16_t* b, int64_t 
     }
   }
   if constexpr (EPI == 4 || EPI == 6 || EPI == 8) {
-    if (grouped && (M / 256) % 8 == 0 && N / 256 >= 8) {
+    if ((M / 256) % 8 == 0 && N / 256 >= 8) {
       gemmp_launch<B_TR, EPI, ACT, 1, 8>(a, lda, b, ldb, M, N, K, c, bias, z, ncu, s, colpart, hm, ea);
       return;
     }
@@ -1422,18 +1415,10 @@ static WgradPlan wgrad_plan(int T, int N, int K, int nseg = 1) {
   const int ktot = T / 64;
   const int ncu = device_cu_count();
   const double mb = (double)N * K * 4.0 / 1e6;  // gradient bytes, MB
-  static int force_ws = -2, force_s = -2;
-  static double merge_cost = 1.0;  // DPA_WGRAD_MERGE_COST: scale of the workspace-merge term (A/B)
-  if (force_ws == -2) {
-    const char* m = std::getenv("DPA_WGRAD_MERGE_COST");
-    if (m) merge_cost = std::atof(m);
-    // default: merge through the workspace whenever K is split (measured faster at every
-    // encoder shape: 8192 tokens -17%, 262144 tokens -2..5%, tools/wgrad_bench.py)
-    const char* e = std::getenv("DPA_WGRAD_WS");
-    force_ws = e ? std::atoi(e) : 1;
-    const char* f = std::getenv("DPA_WGRAD_SPLITS");
-    force_s = f ? std::atoi(f) : -1;
-  }
+  // merge through the workspace whenever K is split (measured faster at every encoder shape:
+  // 8192 tokens -17%, 262144 tokens -2..5%, tools/wgrad_bench.py)
+  constexpr int force_ws = 1, force_s = -1;
+  constexpr double merge_cost = 1.0;
   WgradPlan best_p{1, ktot + (ktot & 1), false};
   double best = 1e30;
   const int smax = ktot / 2 < 1 ? 1 : ktot / 2;

@@ -22,6 +22,14 @@ int ipc_allreduce_blocks(int64_t n, int W, bool two_shot);
 bool launch_ipc_allreduce(const IpcPeers& peers, const IpcData& data, int W, int rank, int sim_ranks,
                           int64_t n, int64_t cap, uint32_t epoch, bool two_shot, int* err, hipStream_t s);
 
+// ---- comm_sim.hip: one-GPU projection of the W > 1 data plane (reducer sim mode) ----
+// tl: this bucket's timeline words {first start, ~last end} (both reset to all-ones)
+void launch_comm_sim(void* buf, int64_t bytes, int64_t touch_bytes, uint64_t ticks, int cus,
+                     unsigned long long* tl, hipStream_t s);
+void launch_time_marker(unsigned long long* slot, hipStream_t s);
+void launch_comm_sim_stats(const unsigned long long* tl, int nb, const unsigned long long* bwd_end,
+                           unsigned long long* acc, hipStream_t s);
+
 // ---- optim.hip -------------------------------------------------------------
 void launch_sqnorm(const void* g, bool g_bf16, int64_t n, float* partial, int nparts, float scale,
                    float max_norm, float* out, hipStream_t s);

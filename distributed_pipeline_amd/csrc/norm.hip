@@ -607,21 +607,14 @@ static void ln_fwd_impl(const uint16_t* y, const uint16_t* res, const uint16_t* 
                         float eps, uint32_t seed, uint32_t off, const uint16_t* pos, const uint16_t* temb,
                         int L, bool post, bool hguard, hipStream_t s) {
   // a few resident waves per SIMD, each walking rows: R / 32 blocks (8 rows per wave) clamped to
-  // [4, 32] blocks per CU (DPA_LN_FWD_BLOCKS overrides: a fixed cap, 0 = uncapped).  Interleaved
+  // [4, 32] blocks per CU.  Interleaved
   // A/Bs: 262144 rows best at 8192 blocks (profiles/wt_shadow_r5.txt); 32768 rows (seq 512 x 64)
   // and 8192 rows (the 32 x 64 schedule) -0.25% each at 1024 blocks vs 8192 / 2048
   // (profiles/ln_bwd_blocks_r5.txt)
-  static const int64_t force = [] {
-    const char* e = std::getenv("DPA_LN_FWD_BLOCKS");
-    return e ? (int64_t)std::atoll(e) : (int64_t)-1;
-  }();
   int64_t nb = (R + 3) / 4;
-  int64_t cap = force;
-  if (cap < 0) {
-    const int64_t cu = device_cu_count();
-    cap = std::min(std::max((R + 31) / 32, cu * 4), cu * 32);
-  }
-  if (cap > 0 && nb > cap) nb = cap;
+  const int64_t cu = device_cu_count();
+  const int64_t cap = std::min(std::max((R + 31) / 32, cu * 4), cu * 32);
+  if (nb > cap) nb = cap;
   const unsigned grid = (unsigned)nb;
   hipLaunchKernelGGL(add_ln_fwd_kernel<VEC>, dim3(grid), dim3(256), 0, s, (const bf16_t*)y,
                      (const bf16_t*)res, (const bf16_t*)g, (const bf16_t*)b, (bf16_t*)out,
@@ -664,16 +657,13 @@ constexpr int LN_SMALL_ROWS = 2 * LN_SMALL_NW;
 // partials are 3 x D floats per block; the second stage reads them once)
 constexpr int LN_WIDE_D = 1536;
 // The small-R kernel grid-strides, so its block count is capped at one 8-wave block per CU
-// (DPA_LN_BWD_MAXBLK overrides, 0 = none): a 32768-row micro-batch (seq 512 x 64) walks 16 rows
+// a 32768-row micro-batch (seq 512 x 64) walks 16 rows
 // per wave and stores 2.4 MB of partials instead of 18.9 MB, 8192 rows 4 per wave.  Interleaved
 // A/Bs (profiles/ln_bwd_blocks_r5.txt): seq512 8 x 64 -1.1% at 1024 blocks and -0.2% more at
 // 256; the 32 x 64 schedule -0.75% at 256 vs 1024 (= the old 512 at 8192 rows), +0.3% at 128.
 static int64_t ln_bwd_two_stage_blocks(int64_t R, int D) {
   if (D >= LN_WIDE_D) return R < 1024 ? R : 1024;  // add_ln_bwd_rowblk_kernel: one row per block at a time
-  static const int64_t cap = [] {
-    const char* e = std::getenv("DPA_LN_BWD_MAXBLK");
-    return e ? (int64_t)std::atoll(e) : (int64_t)device_cu_count();
-  }();
+  const int64_t cap = device_cu_count();
   if (R <= LN_SMALL_R) {
     const int64_t nb = (R + LN_SMALL_ROWS - 1) / LN_SMALL_ROWS;
     return cap > 0 && nb > cap ? cap : nb;

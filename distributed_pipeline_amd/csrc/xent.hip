@@ -639,11 +639,7 @@ static int fwd_splits(int N, int V) {
   const int tb = (N + 127) / 128;
   const int vchunks = (V + 63) / 64;
   int S = pick_splits(tb, vchunks, 1024);
-  static int xs = -1;
-  if (xs < 0) {
-    const char* e = std::getenv("DPA_XENT_XSPLIT");
-    xs = e ? std::atoi(e) : 8;
-  }
+  constexpr int xs = 8;
   if (xs > 1 && vchunks >= xs) S = (S + xs - 1) / xs * xs;
   return S;
 }

@@ -299,13 +299,7 @@ __global__ void __launch_bounds__(512) xent_rows_reg_kernel(bf16_t* __restrict__
   }
 }
 
-static int xent_rows_reg_mode() {
-  static const int mode = [] {
-    const char* e = std::getenv("DPA_XROWS_REG");
-    return e ? std::atoi(e) : 1;
-  }();
-  return mode;
-}
+static int xent_rows_reg_mode() { return 1; }
 
 bool launch_xent_rows_fwd_grad(uint16_t* lg, int64_t ld, int V, const int64_t* tgt, int64_t R, float* loss,
                                float* lse, hipStream_t s) {

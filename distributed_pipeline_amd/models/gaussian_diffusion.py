@@ -284,16 +284,18 @@ def _mask_first_order(fm):
 
 
 _NLL_SIDE = {}
+# the logged nll on its own stream (an A/B hook; off: with the round-5 stream plan it measured
+# 0.15-0.37 ms/step slower than inline, profiles/stream_plan_ab_r5.txt)
+NLL_SIDE_STREAM = False
 
 
 def _nll_side_stream(dev):
-    """The side stream of the logged nll, or None (DPA_NLL_SIDE=0, CPU, graph capture).
+    """The side stream of the logged nll, or None (NLL_SIDE_STREAM off, CPU, graph capture).
     Overlapping the backward, the forward-only CE sweep over the vocabulary takes CUs while the
     memory-bound kernels run: 164.9 vs 165.6 ms/step (profiles/nll_side_stream_ab_r4.txt).  Only
     a whole-batch step uses it (the trainer sets ``nll_side_ok``): per 64-sample chunk of the
     reference schedule it cost 8-10% (222 -> 241-246 ms/step)."""
-    import os
-    if (os.environ.get("DPA_NLL_SIDE", "0") != "1" or dev.type != "cuda"
+    if (not NLL_SIDE_STREAM or dev.type != "cuda"
             or torch.cuda.is_current_stream_capturing()):  # a captured step logs after replay
         return None
     if dev not in _NLL_SIDE:

@@ -64,6 +64,10 @@ def shadow_t(w16):
     stream the first time it is needed after each rewrite of the shadow; None for anything else."""
     if not _WT_SHADOW or w16 is None or w16.dim() != 2:
         return None
+    # only shapes the persistent row-form dgrad can tile (dx[T][K] = dy[T][N] . W[N][K]: K % 256,
+    # N % 128; launch_gemmp_nn) get a shadow, so no other weight is copied or pinned
+    if w16.shape[1] % 256 or w16.shape[0] % 128:
+        return None
     sp = getattr(w16, "_dpa_space", None)
     if sp is None or not w16.is_cuda:
         return None
@@ -94,6 +98,13 @@ def _refresh_wt(sp):
     for w in stale:
         w._dpa_tver = ver
     WT_STATS["copies"] += len(stale)
+    if _WT_CHECK:  # DPA_DEFER_CHECK=1: every refreshed W^T against the shadow it was built from
+        for w in stale:
+            if not torch.equal(w._dpa_t, w.t()):
+                raise RuntimeError(f"stale or corrupt W^T shadow of a {tuple(w.shape)} weight")
+
+
+_WT_CHECK = os.environ.get("DPA_DEFER_CHECK", "0") == "1"
 
 
 WT_STATS = {"used": 0, "copies": 0}
@@ -183,7 +194,7 @@ def _bias_act_bwd(dy2d, z, y, act, want_db):
     return dz, db
 
 
-# Linear GEMM routing (DPA_GEMM):
+# Linear GEMM routing (GEMM_MODE):
 #   "auto" / "native" (default) - every Linear GEMM on the hand-written gfx950
 #            kernels: forward and data-gradient GEMMs on the persistent 256 x 256
 #            kernel of csrc/gemm256.hip (bias, activation and pre-activation copy
@@ -194,10 +205,9 @@ def _bias_act_bwd(dy2d, z, y, act, want_db):
 #            at 262144 tokens: profiles/gemm_lab_r2.txt;
 #   "blas"   - every Linear GEMM on hipBLASLt (plus separate epilogue kernels), the
 #            A/B reference.
-GEMM_MODE = os.environ.get("DPA_GEMM", "auto")
+GEMM_MODE = "auto"  # "blas": stock torch.mm for every Linear (tests / A/B; set the attribute)
 # post-LN attention sublayer at L = 128: QKV stored head-major for the attention kernels
-# (DPA_QKV_HEAD_MAJOR=0: token-major, the Linear layout)
-_QKV_HEAD_MAJOR = os.environ.get("DPA_QKV_HEAD_MAJOR", "1") != "0"
+_QKV_HEAD_MAJOR = True
 # forward GEMM epilogues store act'(z) instead of z for the backward (DPA_SAVE_ACT_DERIV=0: z)
 _SAVE_ACT_DERIV = os.environ.get("DPA_SAVE_ACT_DERIV", "1") != "0"
 # ... and, for the fused MLP (whose backward is the persistent dact GEMM), as 8-bit codes:
@@ -207,17 +217,10 @@ _ACT_Q8 = os.environ.get("DPA_ACT_Q8", "1") != "0"
 # (h = x + dropout(y) written once; the LayerNorm reads h alone and writes no h copy)
 # (DPA_RES_FUSE=0: the GEMM writes y and the LayerNorm kernel adds the residual)
 _RES_FUSE = os.environ.get("DPA_RES_FUSE", "1") != "0"
-# post-LN sublayers: the LayerNorm backward reconstructs xhat = (out - beta) / gamma from the
-# sublayer's output - which the next sublayer keeps alive anyway as its input - instead of
-# the forward writing a bf16 copy of h (one [T, D] store less per sublayer).  Guarded: a
-# LayerNorm with any column where |gamma| < 0.125 or |beta| > |gamma| (where the
-# reconstruction would amplify out's bf16 rounding) keeps the exact h-copy path - both kernels
-# test the same gamma / beta on the device, no host sync (norm.hip xo_unsafe).
-# Opt-in (DPA_LN_SAVE_OUT=1): measured 1.9-2.0 ms/step SLOWER than the h copy on the headline
-# (6 interleaved runs, 167.1-167.2 vs 165.2-165.4 ms: profiles/ln_save_out_ab_r4.txt) - the
-# guarded forward still writes the h copy and the backward's extra gamma/beta reads and
-# reconstruction cost more than the saved store - so the default is the h copy.
-_LN_SAVE_OUT = os.environ.get("DPA_LN_SAVE_OUT", "0") == "1"
+# post-LN sublayers keep the exact h copy for the LayerNorm backward.  (An output-based backward
+# reconstructing xhat from the sublayer's output measured 1.9-2.0 ms/step slower in round 4,
+# profiles/ln_save_out_ab_r4.txt, and was retired in round 6; the kernel's h_guard mode stays
+# for the norm tests.)
 
 
 def _gemm_shape_ok(x2, n_out):
@@ -311,7 +314,7 @@ class _WgradDeferral:
         # the attention backward's qkv-bias partials likewise ([rows][3 D] per call, ext.attn_bwd
         # part_out): one colpart reduction per site and flush instead of one per micro-batch
         self.attn_sites = {}  # id(bias) -> [buf, rows, H, D, gb, used]
-        self.colsum = os.environ.get("DPA_DEFER_COLSUM", "1") != "0"
+        self.colsum = True
         # debug (DPA_DEFER_CHECK=1): checksum every held operand when it is held and again when
         # its launch runs - a held tensor whose memory was rewritten meanwhile is reported
         self.check = os.environ.get("DPA_DEFER_CHECK", "0") == "1"
@@ -617,7 +620,7 @@ def _take_db(g):
 _ACCUMULATED = object()
 
 
-_GRAD_ACC = os.environ.get("DPA_LN_GRAD_ACC", "1") != "0"
+_GRAD_ACC = True
 # In-place parameter gradients are an engine-internal contract: only inside the trainer's own
 # backward (``inplace_param_grads``) do the ops add into ``.grad`` and hand None to autograd.
 # Anywhere else (a user's ``loss.backward()``, ``torch.autograd.grad`` for a gradient penalty or
@@ -845,15 +848,13 @@ def _ln_after_branch(y, x2, lw16, lb16, p, eps, seed, off, fused):
 
     fused: y already is h = x + dropout(branch) (the GEMM epilogue, pair-hash bits): the kernel
     reads h alone, and h itself is what the backward keeps.  Otherwise the kernel adds the
-    dropped-out branch and the residual and writes the h copy (or, with DPA_LN_SAVE_OUT, only
-    where the output-based backward is unsafe: xo)."""
+    dropped-out branch and the residual and writes the h copy."""
     ext = get_ext()
     if fused:
         out, _, mean, rstd = ext.add_ln_fwd(y, None, lw16, lb16, 0.0, float(eps), 0, 0, save_h=False)
         return out, y, mean, rstd, False
-    out, hsave, mean, rstd = ext.add_ln_fwd(y, x2, lw16, lb16, float(p), float(eps), seed, off,
-                                            h_guard=_LN_SAVE_OUT)
-    return out, hsave, mean, rstd, _LN_SAVE_OUT
+    out, hsave, mean, rstd = ext.add_ln_fwd(y, x2, lw16, lb16, float(p), float(eps), seed, off)
+    return out, hsave, mean, rstd, False
 
 
 class _MLPLNFn(torch.autograd.Function):
@@ -1301,8 +1302,7 @@ def attention(qkv, n_heads, p=0.0, causal=False, training=True):
 # --------------------------------------------------------------------------- #
 
 # the fused CE weight gradient accumulates straight into the tied weight's flat fp32 .grad
-# (DPA_XENT_GRAD_ACC=0: into a zeroed scratch, then added by autograd)
-_XENT_GRAD_ACC = os.environ.get("DPA_XENT_GRAD_ACC", "1") != "0"
+_XENT_GRAD_ACC = True
 
 
 class _LinearXentFn(torch.autograd.Function):
@@ -1408,7 +1408,7 @@ class _ChunkedLinearXentFn(torch.autograd.Function):
         kept_is_grad = keep and _XENT_ROWS_FUSED
         allg = torch.empty(N, wp.shape[0], dtype=x.dtype, device=x.device) if keep else None
         if kept_is_grad:
-            # kept chunks (DPA_XENT_FWD_CHUNK_MB): the backward's GEMMs run over all N tokens at
+            # kept chunks (_XENT_FWD_CHUNK_BYTES): the backward's GEMMs run over all N tokens at
             # once, so the forward chunk size is free
             chunk = min(chunk, max(256, (_XENT_FWD_CHUNK_BYTES // (wp.shape[0] * 2)) // 256 * 256))
         for s in range(0, N, chunk):
@@ -1484,29 +1484,28 @@ class _ChunkedLinearXentFn(torch.autograd.Function):
 
 
 # wide-E CE: kept logit chunks become softmax - onehot in the forward's row pass
-# (DPA_XENT_ROWS_FUSED=0: forward statistics only, separate backward row pass)
-_XENT_ROWS_FUSED = os.environ.get("DPA_XENT_ROWS_FUSED", "1") != "0"
+_XENT_ROWS_FUSED = True
 
-# fused CE backward, DPA_XENT_ONEHOT_SCATTER=1: the weight-gradient kernel computes softmax only
+# fused CE backward, _XENT_ONEHOT_SCATTER: the weight-gradient kernel computes softmax only
 # and the target one-hot goes in as a sorted scatter. Off by default: the kernel saves 0.35
 # ms/step but the scatter and the bias index_add cost 1.7 (profiles/xent_onehot_scatter_ab_r4.txt)
-_XENT_ONEHOT_SCATTER = os.environ.get("DPA_XENT_ONEHOT_SCATTER", "0") == "1"
+_XENT_ONEHOT_SCATTER = False
 
-# fused CE: forward also emits the unscaled input gradient (DPA_XENT_FUSED_DX=0: separate dx pass)
-_XENT_FUSED_DX = os.environ.get("DPA_XENT_FUSED_DX", "1") != "0"
+# fused CE: forward also emits the unscaled input gradient (False: separate dx pass)
+_XENT_FUSED_DX = True
 
 # tokens per logits chunk of the wide-E path: about 2 GiB of bf16 logits (fewer, larger
 # GEMMs: GPT-2 bs128 171 -> 162 ms/step against 0.5 GiB chunks)
-_XENT_CHUNK_BYTES = int(os.environ.get("DPA_XENT_CHUNK_MB", "2048")) << 20
+_XENT_CHUNK_BYTES = 2048 << 20
 # logits kept from the forward for the backward (bytes; GPT-2 small at 128 x 1024 tokens
 # needs 13 GB): above this the backward recomputes each chunk
-_XENT_KEEP_BYTES = int(os.environ.get("DPA_XENT_KEEP_GB", "24")) << 30
-# kept logits: the backward's dx as one GEMM over all tokens (DPA_XENT_DX_ALL=0: per chunk)
-_XENT_DX_ALL = os.environ.get("DPA_XENT_DX_ALL", "1") != "0"
+_XENT_KEEP_BYTES = 24 << 30
+# kept logits: the backward's dx as one GEMM over all tokens (False: per chunk)
+_XENT_DX_ALL = True
 # forward chunk when the logits are kept (softmax - onehot in place).  128 MB chunks (resident
 # in the 256 MB Infinity Cache) did not speed the row pass up (profiles/gpt2_head_ab_r4.txt) and
 # cost ~200 small loss/lse copies per GPT-2 step, so the default keeps the 2 GB chunks
-_XENT_FWD_CHUNK_BYTES = int(os.environ.get("DPA_XENT_FWD_CHUNK_MB", "2048")) << 20
+_XENT_FWD_CHUNK_BYTES = 2048 << 20
 
 
 def linear_cross_entropy(x, weight, bias, target):

@@ -113,7 +113,7 @@ def plan_buckets(space, cap_mb, first_mb):
 
 
 def tune_bucket_sizes(numel, *, process_group=None, device=None, sizes_mb=(2, 4, 8, 16, 32, 64, 128),
-                      min_buckets=4, frac=0.9, iters=5):
+                      min_buckets=4, frac=0.9, iters=5, timer=None):
     """Bucket sizes MEASURED on this job's links (``bucket_cap_mb <= 0``): the
     all-reduce bus bandwidth of the process group at each size in ``sizes_mb``, timed on every
     rank and MAX-reduced so all ranks take the same decision.  The cap is the smallest size
@@ -122,6 +122,9 @@ def tune_bucket_sizes(numel, *, process_group=None, device=None, sizes_mb=(2, 4,
     backward); the first bucket is the smallest size within half the best bandwidth, at most
     the cap.  On point-to-point xGMI the knee sits where one ring step's payload stops being
     latency-bound, which depends on the ring count RCCL picks - hence measured, not assumed.
+    ``timer(nfloats, iters) -> seconds`` times the all-reduce on the data plane that will carry
+    the buckets (the C++ reducer's own RCCL communicator and high-priority comm stream,
+    ``BucketReducer.time_allreduce``); without it the process group's ``dist.all_reduce`` is timed.
     Returns ``(cap_mb, first_mb, table)``; ``(32, 4, None)`` without a multi-rank group."""
     import time
     if not (dist.is_available() and dist.is_initialized()) or dist.get_world_size(process_group) < 2:
@@ -133,6 +136,9 @@ def tune_bucket_sizes(numel, *, process_group=None, device=None, sizes_mb=(2, 4,
     sizes = [mb for mb in sizes_mb if mb <= max(sizes_mb[0], grad_mb)]
     times = []
     for mb in sizes:
+        if timer is not None:
+            times.append(timer(int(mb * _MiB) // 4, iters))
+            continue
         x = torch.ones(int(mb * _MiB) // 4, dtype=torch.float32, device=dev)
         dist.all_reduce(x, group=process_group)  # warm: channel / buffer setup outside the timing
         if dev.type == "cuda":
@@ -176,14 +182,30 @@ class DDPEngine(nn.Module):
         self.module = module
         self.pg = process_group
         self.distributed = dist.is_available() and dist.is_initialized()
+        self.sim_comm = None  # enable_sim_comm(): the simulated data plane's parameters
         self.bucket_tune = None
-        if bucket_cap_mb is None or bucket_cap_mb <= 0:  # "auto": measured on this job's links
-            dev = device if device is not None else next(module.parameters()).device
+        # "auto" bucket sizes are measured on this job's links.  ZeRO-1 pads the flat space at
+        # bucket ends, so its plan is measured up front on the process group; otherwise the plan
+        # starts provisional (32 / 4 MiB) and is re-measured on the data plane itself once the
+        # reducer's communicator exists (_tune_on_data_plane)
+        self._tune_later = None
+        if bucket_cap_mb is None or bucket_cap_mb <= 0:
             numel = sum(p.numel() for p in module.parameters() if p.requires_grad)
-            bucket_cap_mb, tuned_first, self.bucket_tune = tune_bucket_sizes(
-                numel, process_group=process_group, device=torch.device(dev))
-            if first_bucket_mb is None or first_bucket_mb <= 0:
-                first_bucket_mb = tuned_first
+            auto_first = first_bucket_mb is None or first_bucket_mb <= 0
+            if shard_optimizer and dist.is_available() and dist.is_initialized():
+                dev = device if device is not None else next(module.parameters()).device
+                bucket_cap_mb, tuned_first, self.bucket_tune = tune_bucket_sizes(
+                    numel, process_group=process_group, device=torch.device(dev))
+                if self.bucket_tune is not None:
+                    self.bucket_tune = {"timed_on": "process group (ZeRO-1 layout is fixed before the reducer)",
+                                        "sweep": self.bucket_tune}
+                if auto_first:
+                    first_bucket_mb = tuned_first
+            else:
+                self._tune_later = (numel, auto_first, device)
+                bucket_cap_mb = 32.0
+                if auto_first:
+                    first_bucket_mb = 4.0
         elif first_bucket_mb is None or first_bucket_mb <= 0:
             # an explicit cap with the first bucket left at "auto": the fixed 4 MiB default (a
             # 0 MiB first bucket would close after one parameter)
@@ -208,16 +230,7 @@ class DDPEngine(nn.Module):
         self._arm_stream = None      # the armed backward's stream (see _arm)
         self._next_launch = 0
         self.bucket_cap_mb, self.first_bucket_mb = bucket_cap_mb, first_bucket_mb
-        if self.bucket_tune is not None and (not self.distributed or dist.get_rank() == 0):
-            # measured sizes can differ run to run (and change the summation order): say which
-            # were taken; pass them back as --ddp_bucket_cap_mb / --ddp_first_bucket_mb to repeat
-            # a run bit for bit
-            try:
-                from basic_utils import logger
-                logger.log(f"DDP buckets: cap {bucket_cap_mb} MiB, first {first_bucket_mb} MiB (measured; "
-                           f"set them explicitly for a bitwise-reproducible rerun)")
-            except ImportError:  # pragma: no cover
-                pass
+        self._log_bucket_plan()
         self.buckets = [_Bucket(i, s, e, ps) for i, (s, e, ps) in
                         enumerate(plan_buckets(self.space, bucket_cap_mb, first_bucket_mb))]
         self._bucket_of = {}
@@ -295,6 +308,8 @@ class DDPEngine(nn.Module):
                     self._ipc_flag = self._native.ipc_error_flag()
                     self._ipc_host = torch.zeros(1, dtype=torch.int32, pin_memory=True)
                     self._ipc_event = torch.cuda.Event()
+        if self._tune_later is not None:
+            self._tune_on_data_plane()
         if self.distributed and self.world_size > 1 and self.space.device.type == "cuda":
             # collectives share the CUs with the persistent GEMMs: let late-starting GEMM
             # workgroups take fewer tiles instead of finishing last (csrc/gemm256.hip)
@@ -313,6 +328,43 @@ class DDPEngine(nn.Module):
                 self._hooks.append(p.register_post_accumulate_grad_hook(hook))
 
     # -- setup ---------------------------------------------------------------
+    def _log_bucket_plan(self):
+        if self.bucket_tune is None or (self.distributed and dist.get_rank() != 0):
+            return
+        # measured sizes can differ run to run (and so can the bucket boundaries, hence the
+        # order of the summation): say which were taken; pass them back as --ddp_bucket_cap_mb /
+        # --ddp_first_bucket_mb to repeat the same bucket plan
+        try:
+            from basic_utils import logger
+            logger.log(f"DDP buckets: cap {self.bucket_cap_mb} MiB, first {self.first_bucket_mb} MiB (measured on "
+                       f"{self.bucket_tune.get('timed_on')}; set them explicitly to repeat this bucket plan)")
+        except ImportError:  # pragma: no cover
+            pass
+
+    def _tune_on_data_plane(self):
+        """Measure the bucket sizes on the data plane that carries them: the reducer's own RCCL
+        communicator and comm stream when it has one (direct mode), else the process group;
+        then re-plan the buckets (C++ reducer: ``set_buckets``)."""
+        numel, auto_first, device = self._tune_later
+        self._tune_later = None
+        direct = self._native is not None and self._native.direct()
+        timer = (lambda n, it: self._native.time_allreduce(n, it) / 1e3) if direct else None
+        dev = device if device is not None else self.space.device
+        cap, first, table = tune_bucket_sizes(numel, process_group=self.pg, device=torch.device(dev), timer=timer)
+        if table is None:
+            return
+        self.bucket_tune = {"timed_on": ("reducer-owned RCCL communicator, comm stream" if direct
+                                         else "process group"), "sweep": table}
+        self.bucket_cap_mb = cap
+        self.first_bucket_mb = min(first if auto_first else self.first_bucket_mb, cap)
+        self.buckets = [_Bucket(i, s, e, ps) for i, (s, e, ps) in
+                        enumerate(plan_buckets(self.space, self.bucket_cap_mb, self.first_bucket_mb))]
+        self._bucket_of = {id(p): b for b in self.buckets for p in b.params}
+        if self._native is not None:
+            self._native.set_buckets([b.start for b in self.buckets] + [self.buckets[-1].end],
+                                     [self._bucket_of[id(p)].index for p in self.space.layout])
+        self._log_bucket_plan()
+
     def _coll_device(self):
         return self.space.device
 
@@ -335,10 +387,95 @@ class DDPEngine(nn.Module):
         if self.distributed:
             dist.broadcast(flat, src, group=self.pg)
 
+    @property
+    def _reducing(self):
+        """Gradients go through a data plane: a real process group, or the simulated one."""
+        return self.distributed or self.sim_comm is not None
+
+    # -- one-GPU projection of W > 1 (SURVEY 5.8, §4 item 6) ------------------------------
+    def enable_sim_comm(self, world, busbw_gbps, cus=64, lat_us=10.0, bucket_cap_mb=None, first_bucket_mb=None):
+        """Run this world-1 engine's backward against a SIMULATED world-``world`` data plane
+        (csrc/comm_sim.hip via the C++ reducer's sim mode): every bucket, when its gradients are
+        ready, launches on the reducer's high-priority comm stream a kernel of ``cus`` workgroups
+        that holds its CUs for ``lat_us + 2 (W - 1) / W x bytes / busbw`` and moves the ring's
+        local HBM bytes; ``finalize()`` orders the optimizer after it, as after a real
+        all-reduce.  The gradients stay this rank's (the step's math is world 1), the GEMMs take
+        the dynamic tile schedule a W > 1 run uses, and the reducer accumulates per-step timeline
+        sums on the device (:meth:`sim_stats`).  A projection, not a scaling measurement: the
+        link model is the caller's (``busbw_gbps``), the overlap with this rank's compute is
+        measured.  ``bucket_cap_mb`` / ``first_bucket_mb`` re-plan the buckets first (e.g. the
+        reference's 128 / 1 MiB)."""
+        if self.distributed:
+            raise RuntimeError("enable_sim_comm: a world-1 engine only (the real data plane is active)")
+        if self.space.device.type != "cuda":
+            raise RuntimeError("enable_sim_comm: device gradients only")
+        ext = get_ext(required=True)
+        self.disable_sim_comm()
+        if bucket_cap_mb is not None:
+            first = first_bucket_mb if first_bucket_mb is not None else min(4.0, bucket_cap_mb)
+            self.bucket_cap_mb, self.first_bucket_mb = bucket_cap_mb, min(first, bucket_cap_mb)
+            self.buckets = [_Bucket(i, s, e, ps) for i, (s, e, ps) in
+                            enumerate(plan_buckets(self.space, self.bucket_cap_mb, self.first_bucket_mb))]
+            self._bucket_of = {id(p): b for b in self.buckets for p in b.params}
+        bounds = [b.start for b in self.buckets] + [self.buckets[-1].end]
+        param_bucket = [self._bucket_of[id(p)].index for p in self.space.layout]
+        red = ext.BucketReducer.simulated(self.space.grad_flat, bounds, param_bucket,
+                                          self.reduce_dtype == torch.bfloat16)
+        red.init_sim(int(world), float(busbw_gbps), int(cus), float(lat_us))
+        self._native = red
+        self.sim_comm = {"world": int(world), "busbw_GBps": float(busbw_gbps), "cus": int(cus),
+                         "lat_us": float(lat_us), "bucket_mb": self.bucket_sizes_mb(),
+                         "wire": "bf16" if self.reduce_dtype == torch.bfloat16 else "fp32"}
+        for i, p in enumerate(self.space.layout):
+            self._hooks.append(p.register_post_accumulate_grad_hook(
+                lambda _p, i=i: self._native.mark_ready(i) if self._native is not None else None))
+        if hasattr(ext, "set_gemmp_dynamic"):
+            ext.set_gemmp_dynamic(True)  # as a W > 1 run (collectives share the CUs)
+        return self.sim_comm
+
+    def disable_sim_comm(self):
+        if self.sim_comm is None:
+            return
+        for h in self._hooks:
+            h.remove()
+        self._hooks = []
+        self._native = None
+        self.sim_comm = None
+        self._armed = False
+        ext = get_ext(required=False)
+        if ext is not None and hasattr(ext, "set_gemmp_dynamic"):
+            ext.set_gemmp_dynamic(False)
+
+    def sim_timeline(self):
+        """The last step's per-bucket [grad ready, first start, last end] (ms after the first
+        grad-ready stamp) and, as the last row, the backward's end (host sync; diagnostics)."""
+        if self.sim_comm is None:
+            return None
+        return [[round(x, 3) for x in row] for row in self._native.sim_timeline().tolist()]
+
+    def sim_stats(self, reset=False):
+        """Simulated data plane, sums since the last reset (ms): steps, exposed tail (comm
+        still running after the backward's last kernel), grad-ready -> first-workgroup delay
+        summed over buckets, bucket busy time summed, comm-stream span; plus per-step means."""
+        if self.sim_comm is None:
+            return None
+        v = self._native.sim_stats()
+        n = max(1.0, v[0])
+        out = {"steps": int(v[0]), "exposed_tail_ms": round(v[1] / n, 3), "ready_to_start_ms": round(v[2] / n, 3),
+               "bucket_busy_ms": round(v[3] / n, 3), "comm_span_ms": round(v[4] / n, 3),
+               "last_step_tail_ms": round(v[5], 3),
+               "model_ms_per_step": round(sum(self._native.sim_bucket_ms(int((b.end - b.start) * (
+                   2 if self.reduce_dtype == torch.bfloat16 else 4))) for b in self.buckets), 3),
+               "last_bucket_model_ms": round(self._native.sim_bucket_ms(int((self.buckets[-1].end - self.buckets[-1].start) * (
+                   2 if self.reduce_dtype == torch.bfloat16 else 4))), 3)}
+        if reset:
+            self._native.sim_reset()
+        return out
+
     # -- forward ---------------------------------------------------------------
     def forward(self, *args, **kwargs):
         self.wait_shadow()
-        if self.distributed and torch.is_grad_enabled() and self.training:
+        if self._reducing and torch.is_grad_enabled() and self.training:
             self._armed = self._sync_enabled
             if self._armed:
                 self._arm()
@@ -368,7 +505,7 @@ class DDPEngine(nn.Module):
         overlapped micro-batch schedule (utils/trainer.py) runs every forward under
         ``no_sync`` - the last micro-batch's forward is issued while an earlier backward
         is still being issued - and arms right before the last backward."""
-        if not self.distributed:
+        if not self._reducing:
             return
         self._armed = True
         self._arm()
@@ -479,7 +616,7 @@ class DDPEngine(nn.Module):
 
     def finalize(self):
         """Wait for (and launch any not-yet-launched) bucket reductions."""
-        if not self.distributed or not self._armed:
+        if not self._reducing or not self._armed:
             return
         if self._native is not None:
             self._check_ipc_error()
@@ -574,7 +711,7 @@ class DDPEngine(nn.Module):
 
     def reduce_all_now(self):
         """Graph mode: backward ran without hooks; reduce every bucket now."""
-        if not self.distributed:
+        if not self._reducing:
             return
         if self._native is not None:
             self._native.reduce_all()
@@ -590,9 +727,18 @@ class DDPEngine(nn.Module):
             (self.grad_shard if self.sharded else self.space.grad_flat).mul_(1.0 / self.world_size)
 
     # -- ZeRO-1 helpers -----------------------------------------------------------------
+    def _gather_direct(self):
+        """ZeRO-1 gathers go through the reducer's own communicator and comm stream (direct mode):
+        never on the process group's pool stream, which shares a hardware queue with compute."""
+        return self._native is not None and self._native.direct()
+
     def all_gather_chunks(self, full):
         """``full`` is a flat buffer laid out like the parameters whose per-bucket chunk
         ``shard_chunks[b]`` is valid on each owning rank: gather every bucket in place."""
+        if self._gather_direct():
+            self._native.all_gather_buckets(full, list(range(len(self.buckets))))
+            self._native.wait_gather()
+            return
         for b, (s, c, _off) in zip(self.buckets, self.shard_chunks):
             whole = full[b.start:b.end]
             mine = full[s:s + c]
@@ -627,6 +773,15 @@ class DDPEngine(nn.Module):
             for s_, c, _ in self.shard_chunks:
                 keep[s_:s_ + c] = True
             self.space.param_flat.masked_fill_(~keep, float("nan"))
+        if self._gather_direct():
+            # the layout runs from the last layers to the first: the buckets the next forward
+            # needs first (the highest) go first, on the comm stream; wait_shadow() orders the
+            # next forward after them
+            self._native.all_gather_buckets(sh, list(reversed(range(len(self.buckets)))))
+            self._shadow_works.append("native")
+            self.space.shadow_written()
+            self._master_stale = True
+            return
         # bit copy as int32 pairs (gloo has no 16-bit all-gather; every bucket and chunk
         # boundary is a multiple of 16 elements)
         wire = sh.view(torch.int32)
@@ -653,7 +808,10 @@ class DDPEngine(nn.Module):
         (a stream-side wait on RCCL, no host block)."""
         works, self._shadow_works = self._shadow_works, []
         for w in works:
-            w.wait()
+            if w == "native":
+                self._native.wait_gather()
+            else:
+                w.wait()
 
     def materialize_master(self):
         """Collective (every rank): make the full fp32 master current after shadow-only

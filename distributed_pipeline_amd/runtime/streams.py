@@ -13,7 +13,7 @@ csrc/runtime/streams.cpp) once per device, before RCCL and torch's pool take any
 (basic_utils/dist_util.py ``claim_stream_plan`` runs right after ``set_device``): HIP hands a new
 stream the least-used queue, so side, wgrad and nll/copy land on queues 2, 3 and 4, and the
 compute stream keeps queue 1 (measured from a rocprofv3 trace of the real start-up order,
-profiles/stream_queues_r5.txt; bench.py reports it as ``streams.hw_queues_measured``).  A CU-masked
+profiles/stream_queues_r5.txt; bench.py reports it as ``streams.hw_queues_expected``).  A CU-masked
 stream (mode 1, plan "cumask") gets a dedicated HSA queue, but the overlapped reference schedule
 ran 523-529 ms/step on such streams against ~222 (profiles/stream_plan_ab_r5.txt), so it stays an
 A/B option.  Roles (reference call sites whose work they carry; the reference runs everything on
@@ -31,7 +31,8 @@ copy       H2D prefetch of the next batch (data/prefetch.py; reference trainer.p
 The data plane's comm stream is the C++ reducer's own (csrc/comm/reducer.cpp), created on the
 highest-priority queue pool, which the compute stream (normal priority) never uses.
 
-``DPA_STREAM_PLAN=pool`` restores torch pool streams, ``cumask`` the CU-masked ones (A/B runs)."""
+``StreamPlan(device, mode="pool")`` gives torch pool streams, ``"cumask"`` the CU-masked ones (A/B
+runs); without the native extension the plan falls back to ``"pool"``."""
 import os
 
 import torch
@@ -44,14 +45,16 @@ class StreamPlan:
 
     def __init__(self, device, mode=None):
         self.device = torch.device(device)
-        self.mode = mode or os.environ.get("DPA_STREAM_PLAN", "ordered")
+        self.mode = mode or "ordered"
         self.streams = {}
         if self.device.type != "cuda":
             return
         ext = None
         if self.mode in ("ordered", "cumask"):
             from ..ops._ext import get_ext
-            ext = get_ext()
+            # required=False: a stock run (use_hip_kernels=False, --stock) needs no native code,
+            # and without the extension the plan falls back to torch pool streams
+            ext = get_ext(required=False)
             if ext is None or not hasattr(ext, "stream_create"):
                 self.mode = "pool"
         with torch.cuda.device(self.device):
@@ -86,16 +89,19 @@ class StreamPlan:
             raise KeyError(role)
         return self.streams.get(role)
 
-    # HSA queue of each role as measured for the "ordered" plan (rocprofv3 kernel trace of the real
-    # start-up order, tools/probes/stream_queues.py, GPU_MAX_HW_QUEUES=4); HIP exposes no queue id
-    MEASURED_QUEUES = {"compute": 1, "side": 2, "wgrad": 3, "nll": 4, "copy": 4,
-                       "reducer_comm": "5 (high-priority pool)", "source": "profiles/stream_queues_r5.txt"}
+    # HSA queue of each role EXPECTED for the "ordered" plan: measured once from a rocprofv3 kernel
+    # trace of the real start-up order (tools/probes/stream_queues.py, GPU_MAX_HW_QUEUES=4), not
+    # re-measured per run (HIP exposes no queue id)
+    EXPECTED_QUEUES = {"compute": 1, "side": 2, "wgrad": 3, "nll": 4, "copy": 4,
+                       "reducer_comm": "5 (high-priority pool)", "zero_gather": "reducer_comm",
+                       "source": "profiles/stream_queues_r5.txt (one trace, not this run)"}
 
     def describe(self):
         d = {"mode": self.mode, "roles": list(ROLES),
-             "handles": {r: hex(s.cuda_stream) for r, s in self.streams.items()}}
+             "handles": {r: hex(s.cuda_stream) for r, s in self.streams.items()},
+             "gpu_max_hw_queues": os.environ.get("GPU_MAX_HW_QUEUES", "4 (HIP default)")}
         if self.mode == "ordered":
-            d["hw_queues_measured"] = dict(self.MEASURED_QUEUES)
+            d["hw_queues_expected"] = dict(self.EXPECTED_QUEUES)
         return d
 
 

@@ -167,7 +167,14 @@ def _zero_rccl_worker(port, wire, q):
                 if sharded:
                     eng.gather_params()
             out.append(eng.space.param_flat.detach().cpu().numpy().copy())
-        q.put(out)
+            if sharded:
+                # the parameter all-gathers ran on the reducer's own communicator and comm stream
+                # (not the process group's pool stream), and so does the bucket-size timing
+                nat = eng._native
+                gather_on_comm = nat.direct() and nat.last_collective_stream() == nat.comm_stream() != 0
+                ms = nat.time_allreduce(1 << 20, 3)
+                tune_on_comm = nat.last_collective_stream() == nat.comm_stream() and ms > 0
+        q.put((out, gather_on_comm, tune_on_comm))
     finally:
         dist.destroy_process_group()
 
@@ -181,9 +188,10 @@ def test_zero1_reduce_scatter_over_rccl_single_rank(wire):
     q = ctx.Queue()
     p = ctx.Process(target=_zero_rccl_worker, args=(find_free_port(), wire, q))
     p.start()
-    plain, sharded = q.get(timeout=300)
+    (plain, sharded), gather_on_comm, tune_on_comm = q.get(timeout=300)
     p.join(timeout=60)
     assert p.exitcode == 0
+    assert gather_on_comm and tune_on_comm
     torch.testing.assert_close(torch.from_numpy(sharded), torch.from_numpy(plain), rtol=1e-6, atol=1e-7)
 
 

@@ -101,13 +101,14 @@ def test_deferred_wgrad_matches_sequential(depth, overlap):
 
 @pytest.mark.parametrize("mode", ["1", "bwd"])
 def test_overlapped_schedule_half_tile_modes(mode, monkeypatch):
-    """DPA_OVERLAP_HALF_TILES=1 (the launcher's 128-row tile rule on both streams) and =bwd (on the
+    """overlap_half_tiles "1" (the launcher's 128-row tile rule on both streams) and "bwd" (on the
     backward chain only; utils/trainer.py toggles it around every forward): the tiny model's
     launches are single partial rounds, so 128-row tiles run; every epilogue is bitwise equal
     between tile heights, so the first step's gradient matches the sequential loop's."""
     g0, _, _ = _loop(False, steps=1)
     ga, _, _ = _loop(False, steps=1)
-    monkeypatch.setenv("DPA_OVERLAP_HALF_TILES", mode)
+    from utils.trainer import TrainLoop
+    monkeypatch.setattr(TrainLoop, "overlap_half_tiles", mode)
     g1, _, _ = _loop(True, steps=1)
     noise = (g0 - ga).abs().max().item()
     scale = g0.abs().max().item()

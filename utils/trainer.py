@@ -105,6 +105,11 @@ class TrainLoop:
         raise TypeError("Unsupported batch type: {}".format(type(batch).__name__))
 
     # -------------------------------------------------------------- construct
+    # overlapped micro-batch schedule A/B hooks (class attributes, not settings): the forward
+    # stream's persistent-GEMM grid cap (None: half the CUs) and the 128-row tile mode
+    overlap_fwd_cap = None
+    overlap_half_tiles = "0"
+
     def __init__(
             self,
             *,
@@ -213,8 +218,8 @@ class TrainLoop:
         self._profile_window = _parse_window(profile_steps)
         # HIP-graph mode (native engine, fixed executed micro-batch): after two eager steps the
         # whole forward/backward of a step - every micro-batch, all streams - is captured once
-        # and replayed; DPA_CUDA_GRAPH=1 turns it on as well
-        self.cuda_graph = (bool(cuda_graph) or os.environ.get("DPA_CUDA_GRAPH", "0") == "1")
+        # and replayed (the cuda_graph setting)
+        self.cuda_graph = bool(cuda_graph)
         self._graph = None
         self._graph_eager_steps = 0
         self._graph_capturing = False
@@ -804,9 +809,7 @@ class TrainLoop:
 
     def _overlap_ok(self, nchunks):
         # only tile-starved chunks gain from a second stream; under HIP-graph capture the
-        # overlap is optional (DPA_GRAPH_OVERLAP=0: the captured step runs on one stream)
-        if self._graph_capturing and os.environ.get("DPA_GRAPH_OVERLAP", "1") == "0":
-            return False
+        # overlap is kept (one replay issues both streams' work)
         return nchunks > 1 and self.overlap_microbatches and self._tile_starved()
 
     def _chunk_state(self):
@@ -835,13 +838,12 @@ class TrainLoop:
         def stream_of(k):  # the last chunk on the current stream
             return streams[(nch - 1 - k) % 2]
 
-        # grid cap of the forward stream's persistent GEMMs (DPA_OVERLAP_FWD_CAP, 0 = none;
+        # grid cap of the forward stream's persistent GEMMs (``overlap_fwd_cap``, 0 = none;
         # default half the CUs): the concurrent backward's kernels - the critical chain - then
         # always find free CUs.  Uncapped, a forward GEMM of 1.5 waves of workgroups can hold
         # every CU while the backward waits; same-box runs of the 32 x 64 schedule spread
         # 227-306 ms/step uncapped vs 223.4-226.3 capped at 128 (profiles/ref_schedule_fwd_cap_r3.txt)
-        cap_env = os.environ.get("DPA_OVERLAP_FWD_CAP", "")
-        fwd_cap = (int(cap_env) if cap_env.strip() else
+        fwd_cap = (self.overlap_fwd_cap if self.overlap_fwd_cap is not None else
                    torch.cuda.get_device_properties(self.device).multi_processor_count // 2)
         ext = None
         if fwd_cap > 0:
@@ -850,9 +852,9 @@ class TrainLoop:
 
         # the two streams already fill the CUs a small chunk's GEMMs leave idle: 128-row GEMM
         # tiles (gemm256.hip use_half_tiles) only add operand traffic here (32 x 64 schedule:
-        # 222.7 ms/step without, 233.8 with, profiles/half_tiles_r5.txt).  DPA_OVERLAP_HALF_TILES:
-        # 0 off (default), 1 the launcher's own rule everywhere, bwd only on the backward chain
-        half_mode = os.environ.get("DPA_OVERLAP_HALF_TILES", "0")
+        # 222.7 ms/step without, 233.8 with, profiles/half_tiles_r5.txt).  ``overlap_half_tiles``:
+        # "0" off (default), "1" the launcher's own rule everywhere, "bwd" only on the backward chain
+        half_mode = self.overlap_half_tiles
         hx = None
         if half_mode != "1":
             from distributed_pipeline_amd.ops._ext import get_ext
@@ -900,13 +902,10 @@ class TrainLoop:
         defer = nn_ops.WGRAD_DEFER
         defer.depth = self._defer_depth()
         # the un-armed micro-batches' weight-gradient launches run on a third stream, off the
-        # backward chain (DPA_WGRAD_SIDE_STREAM=0: on the backward's own stream)
-        if os.environ.get("DPA_WGRAD_SIDE_STREAM", "1") != "0":
-            if getattr(self, "_wgrad_stream", None) is None:
-                self._wgrad_stream = plan_stream(self.device, "wgrad")
-            defer.stream = self._wgrad_stream
-        else:
-            defer.stream = None
+        # backward chain (profiles/overlap_side_stream_ab_r3.txt: 251.7 -> 235.5 ms/step)
+        if getattr(self, "_wgrad_stream", None) is None:
+            self._wgrad_stream = plan_stream(self.device, "wgrad")
+        defer.stream = self._wgrad_stream
         done = None
         self._loss_log_buf = []
         try:
@@ -1326,7 +1325,7 @@ class DiffusionTrainLoop(TrainLoop):
             return
         join = getattr(getattr(self, "diffusion", None), "join_side", None)
         if join is not None:
-            join()  # buffered terms may come from a side stream (DPA_NLL_SIDE)
+            join()  # buffered terms may come from a side stream (NLL_SIDE_STREAM)
         groups = {}
         for keys, t, w, vals in buf:  # equal chunk sizes batch together (the usual case)
             groups.setdefault((keys, t.shape[0]), []).append((t, w, vals))
