@@ -85,7 +85,8 @@ def parse():
     ap.add_argument("--json-out", default=None)
     ap.add_argument("--project", default="",
                     help="N = 1 only, after the measurements: a one-GPU PROJECTION of the W > 1 data plane. "
-                         "';'-separated specs W,busbw_GBps[,cus[,lat_us[,bucket_cap_mb,first_bucket_mb]]]: each "
+                         "';'-separated specs W,busbw_GBps[,cus[,lat_us[,bucket_cap_mb,first_bucket_mb]]] ('/' "
+                         "may replace ','): each "
                          "bucket's all-reduce is replaced by a calibrated kernel on the reducer's comm stream "
                          "(parallel/ddp.py enable_sim_comm); reported under 'projection'")
     ap.add_argument("--project-schedules", default="fused,reference",
@@ -180,7 +181,7 @@ def project(a, loop, one_step, timed, exec_used, base):
     wires = [w for w in a.project_wire.split(",") if w] or [a.grad_wire]
     scheds = [x for x in a.project_schedules.split(",") if x]
     for spec in [x for x in a.project.split(";") if x.strip()]:
-        f = [float(v) for v in spec.split(",")]
+        f = [float(v) for v in spec.replace("/", ",").split(",")]
         world, bw = int(f[0]), f[1]
         cus = int(f[2]) if len(f) > 2 else 64
         lat = f[3] if len(f) > 3 else 10.0

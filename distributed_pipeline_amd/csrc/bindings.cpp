@@ -615,20 +615,21 @@ static void gemm_nn_into(const at::Tensor& dy, const at::Tensor& W, at::Tensor& 
   TORCH_CHECK(ok, "gemm_nn_into: unsupported shape T=", T, " N=", N, " K=", K);
 }
 
-// (sorted ids, permutation) with equal ids adjacent: the counting sort of csrc/sort.hip
-// (histogram, scan, wave-aggregated scatter) for vocabularies < 2^17, else at::sort.
+// (sorted ids, permutation) with equal ids adjacent in index order: the stable counting sort of
+// csrc/sort.hip (block histograms, scans, ordered scatter) for vocabularies up to 81919, else a
+// stable at::sort.
 static std::tuple<at::Tensor, at::Tensor> bucket_sort_ids(const at::Tensor& ids, int64_t V) {
   const at::Tensor flat = ids.reshape({-1}).contiguous();
   const int64_t n = flat.numel();
   auto i64 = flat.options().dtype(at::kLong);
   at::Tensor sorted = at::empty({n}, i64), perm = at::empty({n}, i64);
-  at::Tensor ws = at::empty({dpa::id_sort_workspace_ints((int)std::min<int64_t>(V, 1 << 20))},
-                            flat.options().dtype(at::kInt));
+  const int Vc = (int)std::min<int64_t>(V, 1 << 20);
+  at::Tensor ws = at::empty({dpa::id_sort_workspace_ints(n, Vc)}, flat.options().dtype(at::kInt));
   if (V < (1 << 17) &&
       dpa::launch_id_bucket_sort(flat.data_ptr<int64_t>(), n, (int)V, ws.data_ptr<int>(),
                                  sorted.data_ptr<int64_t>(), perm.data_ptr<int64_t>(), cur_stream()))
     return {sorted, perm};
-  return at::sort(flat);
+  return at::sort(flat, /*stable=*/true, 0, false);
 }
 
 static std::vector<at::Tensor> id_sort(const at::Tensor& ids, int64_t V) {
@@ -671,9 +672,10 @@ static void emb_grad(const at::Tensor& ids, const at::Tensor& dy, at::Tensor& dW
   at::Tensor sorted, perm;
   std::tie(sorted, perm) = bucket_sort_ids(ids, dW.size(0));
   const bool b16 = dy.scalar_type() == at::kBFloat16;
+  at::Tensor part = at::empty({dpa::emb_grad_part_floats(NT, (int)E, false)}, dW.options());
   TORCH_CHECK(dpa::launch_emb_grad(sorted.data_ptr<int64_t>(), perm.data_ptr<int64_t>(),
                                    b16 ? nullptr : dy.data_ptr<float>(), b16 ? bf_ptr(dy) : nullptr, NT, (int)E,
-                                   (int)dW.size(0), dW.data_ptr<float>(), cur_stream()),
+                                   (int)dW.size(0), dW.data_ptr<float>(), part.data_ptr<float>(), cur_stream()),
               "emb_grad: unsupported embedding width ", E);
 }
 
@@ -987,15 +989,19 @@ static void emb_qsample_bwd(const at::Tensor& ids, const at::Tensor& mask, const
   }
   const c10::DeviceGuard guard(dW.device());
   if (n > 0) {
-    // counting sort of the token ids -> runs of equal ids summed in registers (one atomic
-    // per run and column instead of per token and column)
-    at::Tensor sorted, perm;
-    if (E == 128 || E == 256) std::tie(sorted, perm) = bucket_sort_ids(ids, dW.size(0));
+    // stable counting sort of the token ids -> runs of equal ids summed in registers, one
+    // writer per gradient row (deterministic; csrc/sort.hip, csrc/diffusion.hip)
+    at::Tensor sorted, perm, part;
+    if (E == 128 || E == 256) {
+      std::tie(sorted, perm) = bucket_sort_ids(ids, dW.size(0));
+      part = at::empty({dpa::emb_grad_part_floats(B * L, (int)E, true)}, dW.options());
+    }
     dpa::launch_emb_qsample_bwd(ids.data_ptr<int64_t>(), mask.data_ptr<int64_t>(), t.data_ptr<int64_t>(),
                                 sa.data_ptr<float>(), p_xs, p_xs16, p_xt16, p_xt32, B * L, (int)L, (int)E,
                                 (int)dW.size(0), dW.data_ptr<float>(), cur_stream(),
                                 sorted.defined() ? sorted.data_ptr<int64_t>() : nullptr,
-                                perm.defined() ? perm.data_ptr<int64_t>() : nullptr);
+                                perm.defined() ? perm.data_ptr<int64_t>() : nullptr,
+                                part.defined() ? part.data_ptr<float>() : nullptr);
   };
 }
 

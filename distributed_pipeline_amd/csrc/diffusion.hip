@@ -120,38 +120,56 @@ __global__ void __launch_bounds__(256) emb_qsample_bwd_kernel(
   }
 }
 
-// Sorted variant (ids sorted on the device beforehand, perm = the sort permutation):
-// one wave walks `chunk` consecutive sorted tokens with its lanes over the E columns,
-// sums the gradients of equal ids in registers and flushes one fp32 atomic per (run,
-// column) - ~8 tokens share an id at DiffuSeq-base shapes, so 8x fewer atomics than
-// one per (token, column), and the gradient rows are read as coalesced lines.
+// Sorted variant (ids STABLY sorted on the device beforehand, csrc/sort.hip; perm = the sort
+// permutation): one wave walks `chunk` consecutive sorted tokens with its lanes over the E
+// columns and sums the gradients of equal ids in registers - ~8 tokens share an id at
+// DiffuSeq-base shapes, and the gradient rows are read as coalesced lines.  Deterministic: every
+// row of dW has exactly one writer, in a fixed order.
+//  * a run of equal ids that lies inside the wave's chunk is added to dW by the wave (plain
+//    read-modify-write: no other wave touches that row in this kernel);
+//  * a run crossing a chunk boundary leaves per-chunk partials in part[chunk][2][E]: slot 0 = the
+//    piece that continues a run from the previous chunk, slot 1 = the piece of a run that starts
+//    in this chunk and continues past it; emb_grad_fixup_kernel adds them in chunk order.
 template <int CPL>
 __global__ void __launch_bounds__(256) emb_grad_sorted_kernel(
     const int64_t* __restrict__ sid, const int64_t* __restrict__ perm, const int64_t* __restrict__ mask,
     const int64_t* __restrict__ t, const float* __restrict__ sa, const float* __restrict__ d_xs,
     const bf16_t* __restrict__ d_xs16, const bf16_t* __restrict__ d_xt16, const float* __restrict__ d_xt32,
-    int64_t NT, int L, int V, float* __restrict__ dW, int chunk) {
+    int64_t NT, int L, int V, float* __restrict__ dW, int chunk, float* __restrict__ part) {
   constexpr int E = 64 * CPL;
   const int lane = threadIdx.x & 63;
-  const int64_t j0 = ((int64_t)blockIdx.x * 4 + (threadIdx.x >> 6)) * chunk;
+  const int64_t c = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int64_t j0 = c * chunk;
   if (j0 >= NT) return;
   const int64_t j1 = j0 + chunk < NT ? j0 + chunk : NT;
   float acc[CPL];
 #pragma unroll
   for (int k = 0; k < CPL; ++k) acc[k] = 0.f;
   int64_t cur = sid[j0];
-  auto flush = [&]() {
-    if (cur >= 0 && cur < V) {
+  bool first = true;
+  const bool head = j0 > 0 && sid[j0 - 1] == cur;  // the first run continues one from the left
+  auto flush = [&](bool at_end) {
+    const bool cont = at_end && j1 < NT && sid[j1] == cur;  // the run goes on past the chunk
+    float* dst = nullptr;
+    bool add = false;
+    if (first && head) dst = part + (c * 2) * E;               // continuation piece
+    else if (cont) dst = part + (c * 2 + 1) * E;               // head piece of a crossing run
+    else if (cur >= 0 && cur < V) { dst = dW + cur * E; add = true; }  // a whole run
+    if (dst) {
 #pragma unroll
-      for (int k = 0; k < CPL; ++k) atomicAdd(dW + cur * E + lane + 64 * k, acc[k]);
+      for (int k = 0; k < CPL; ++k) {
+        float* q = dst + lane + 64 * k;
+        *q = add ? *q + acc[k] : acc[k];
+      }
     }
 #pragma unroll
     for (int k = 0; k < CPL; ++k) acc[k] = 0.f;
+    first = false;
   };
   for (int64_t j = j0; j < j1; ++j) {
     const int64_t id = sid[j];
     if (id != cur) {  // wave-uniform: every lane reads the same sorted position
-      flush();
+      flush(false);
       cur = id;
     }
     const int64_t tok = perm[j];
@@ -168,7 +186,46 @@ __global__ void __launch_bounds__(256) emb_grad_sorted_kernel(
       acc[k] += g;
     }
   }
-  flush();
+  flush(true);
+}
+
+// The runs that cross chunk boundaries: the chunk where such a run starts (its slot-1 piece) adds
+// the slot-0 pieces of the chunks it continues into, in chunk order, and writes dW once.
+template <int CPL>
+__global__ void __launch_bounds__(256) emb_grad_fixup_kernel(const int64_t* __restrict__ sid, int64_t NT, int V,
+                                                             int chunk, const float* __restrict__ part,
+                                                             float* __restrict__ dW) {
+  constexpr int E = 64 * CPL;
+  const int lane = threadIdx.x & 63;
+  const int64_t nch = (NT + chunk - 1) / chunk;
+  const int64_t c = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (c >= nch) return;
+  const int64_t j0 = c * chunk, j1 = j0 + chunk < NT ? j0 + chunk : NT;
+  if (j1 >= NT) return;
+  const int64_t r = sid[j1 - 1];
+  if (sid[j1] != r) return;                                    // the last run ends in the chunk
+  if (sid[j0] == r && j0 > 0 && sid[j0 - 1] == r) return;      // ... or is a continuation piece
+  float acc[CPL];
+#pragma unroll
+  for (int k = 0; k < CPL; ++k) acc[k] = part[(c * 2 + 1) * E + lane + 64 * k];
+  for (int64_t c2 = c + 1; c2 < nch && sid[c2 * chunk] == r; ++c2)
+#pragma unroll
+    for (int k = 0; k < CPL; ++k) acc[k] += part[(c2 * 2) * E + lane + 64 * k];
+  if (r < 0 || r >= V) return;
+#pragma unroll
+  for (int k = 0; k < CPL; ++k) dW[r * E + lane + 64 * k] += acc[k];
+}
+
+// sorted tokens per wave: 16 for large NT (runs of equal ids summed in registers), down to 1 for
+// a few hundred rows (e.g. a position-embedding gradient of 128 distinct ids), so the launch
+// still spans the chip instead of a handful of latency-bound waves; the q_sample backward: 16
+static int emb_chunk(int64_t NT, bool qsample) {
+  if (qsample) return 16;
+  const int64_t chunk = NT / 8192;
+  return (int)(chunk < 1 ? 1 : chunk > 16 ? 16 : chunk);
+}
+int64_t emb_grad_part_floats(int64_t NT, int E, bool qsample) {
+  return ((NT + emb_chunk(NT, qsample) - 1) / emb_chunk(NT, qsample)) * 2 * (int64_t)E;
 }
 
 // One workgroup per sample: reductions over the sample's L*E elements.
@@ -309,18 +366,23 @@ bool launch_emb_qsample_bwd(const int64_t* ids, const int64_t* mask, const int64
                             const float* d_xs, const uint16_t* d_xs16, const uint16_t* d_xt16,
                             const float* d_xt32, int64_t NT, int L, int E, int V, float* dW,
                             hipStream_t s, const int64_t* sorted_ids,
-                            const int64_t* perm) {
+                            const int64_t* perm, float* part) {
   if (L <= 0 || E <= 0) return false;
-  if (sorted_ids && perm && (E == 128 || E == 256)) {
-    constexpr int CHUNK = 16;
+  if (sorted_ids && perm && part && (E == 128 || E == 256)) {
+    const int CHUNK = emb_chunk(NT, true);
     const int64_t waves = (NT + CHUNK - 1) / CHUNK;
     const unsigned grid = (unsigned)((waves + 3) / 4);
-    if (E == 128)
+    if (E == 128) {
       hipLaunchKernelGGL(emb_grad_sorted_kernel<2>, dim3(grid), dim3(256), 0, s, sorted_ids, perm, mask, t, sa,
-                         d_xs, (const bf16_t*)d_xs16, (const bf16_t*)d_xt16, d_xt32, NT, L, V, dW, CHUNK);
-    else
+                         d_xs, (const bf16_t*)d_xs16, (const bf16_t*)d_xt16, d_xt32, NT, L, V, dW, CHUNK, part);
+      hipLaunchKernelGGL(emb_grad_fixup_kernel<2>, dim3(grid), dim3(256), 0, s, sorted_ids, NT, V, CHUNK,
+                         (const float*)part, dW);
+    } else {
       hipLaunchKernelGGL(emb_grad_sorted_kernel<4>, dim3(grid), dim3(256), 0, s, sorted_ids, perm, mask, t, sa,
-                         d_xs, (const bf16_t*)d_xs16, (const bf16_t*)d_xt16, d_xt32, NT, L, V, dW, CHUNK);
+                         d_xs, (const bf16_t*)d_xs16, (const bf16_t*)d_xt16, d_xt32, NT, L, V, dW, CHUNK, part);
+      hipLaunchKernelGGL(emb_grad_fixup_kernel<4>, dim3(grid), dim3(256), 0, s, sorted_ids, NT, V, CHUNK,
+                         (const float*)part, dW);
+    }
     return true;
   }
   hipLaunchKernelGGL(emb_qsample_bwd_kernel, dim3(grid_cap(NT * E, 256 * 16)), dim3(256), 0, s, ids,
@@ -332,24 +394,21 @@ bool launch_emb_qsample_bwd(const int64_t* ids, const int64_t* mask, const int64
 // Plain token-embedding backward over sorted ids (GPT-2 wte / wpe): the same sorted
 // segment-sum kernel with only the upstream gradient as input.
 bool launch_emb_grad(const int64_t* sorted_ids, const int64_t* perm, const float* dy32, const uint16_t* dy16,
-                     int64_t NT, int E, int V, float* dW, hipStream_t s) {
-  // tokens per wave: 16 for large NT (runs of equal ids summed in registers), down to 1 for
-  // a few hundred rows (e.g. a position-embedding gradient of 128 distinct ids), so the
-  // launch still spans the chip instead of a handful of latency-bound waves
-  int64_t chunk = NT / 8192;
-  const int CHUNK = (int)(chunk < 1 ? 1 : chunk > 16 ? 16 : chunk);
+                     int64_t NT, int E, int V, float* dW, float* part, hipStream_t s) {
+  const int CHUNK = emb_chunk(NT, false);
   const unsigned grid = (unsigned)(((NT + CHUNK - 1) / CHUNK + 3) / 4);
-  auto go = [&](auto kern) {
+  auto go = [&](auto kern, auto fix) {
     hipLaunchKernelGGL(kern, dim3(grid), dim3(256), 0, s, sorted_ids, perm, (const int64_t*)nullptr,
                        (const int64_t*)nullptr, (const float*)nullptr, dy32, (const bf16_t*)dy16,
-                       (const bf16_t*)nullptr, (const float*)nullptr, NT, 1, V, dW, CHUNK);
+                       (const bf16_t*)nullptr, (const float*)nullptr, NT, 1, V, dW, CHUNK, part);
+    hipLaunchKernelGGL(fix, dim3(grid), dim3(256), 0, s, sorted_ids, NT, V, CHUNK, (const float*)part, dW);
   };
   switch (E) {
-    case 128: go(emb_grad_sorted_kernel<2>); return true;
-    case 256: go(emb_grad_sorted_kernel<4>); return true;
-    case 768: go(emb_grad_sorted_kernel<12>); return true;
-    case 1024: go(emb_grad_sorted_kernel<16>); return true;
-    case 2048: go(emb_grad_sorted_kernel<32>); return true;
+    case 128: go(emb_grad_sorted_kernel<2>, emb_grad_fixup_kernel<2>); return true;
+    case 256: go(emb_grad_sorted_kernel<4>, emb_grad_fixup_kernel<4>); return true;
+    case 768: go(emb_grad_sorted_kernel<12>, emb_grad_fixup_kernel<12>); return true;
+    case 1024: go(emb_grad_sorted_kernel<16>, emb_grad_fixup_kernel<16>); return true;
+    case 2048: go(emb_grad_sorted_kernel<32>, emb_grad_fixup_kernel<32>); return true;
     default: return false;
   }
 }

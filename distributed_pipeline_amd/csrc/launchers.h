@@ -153,13 +153,16 @@ bool launch_emb_qsample_fwd(const int64_t* ids, const int64_t* mask, const int64
                             const float* sa, const float* s1a, int64_t NT, int L, int E, int V,
                             float std0, uint32_t seed, uint32_t offset, float* x_start,
                             uint16_t* x_start16, uint16_t* x_t, hipStream_t s);
+// Deterministic segment sums over a STABLE sort: part = emb_grad_part_floats(NT, E, qsample) fp32
+// scratch (qsample: for launch_emb_qsample_bwd, else launch_emb_grad)
+int64_t emb_grad_part_floats(int64_t NT, int E, bool qsample);
 bool launch_emb_grad(const int64_t* sorted_ids, const int64_t* perm, const float* dy32, const uint16_t* dy16,
-                     int64_t NT, int E, int V, float* dW, hipStream_t s);
+                     int64_t NT, int E, int V, float* dW, float* part, hipStream_t s);
 bool launch_emb_qsample_bwd(const int64_t* ids, const int64_t* mask, const int64_t* t, const float* sa,
                             const float* d_xs, const uint16_t* d_xs16, const uint16_t* d_xt16,
                             const float* d_xt32, int64_t NT, int L, int E, int V, float* dW,
                             hipStream_t s, const int64_t* sorted_ids = nullptr,
-                            const int64_t* perm = nullptr);
+                            const int64_t* perm = nullptr, float* part = nullptr);
 bool launch_diff_loss_fwd(const float* x_start, const void* out, bool out_bf16, const int64_t* ids,
                           const int64_t* t, const float* W, int B, int L, int E, int V, float sa_last,
                           float* mse, float* tT, hipStream_t s);
@@ -171,9 +174,10 @@ void launch_timestep_emb(const float* ts, int B, int dim, float max_period, uint
                          hipStream_t s);
 
 // ---- sort.hip: counting sort of token ids, stable 0/1 partition ---------------------
-// ids into V + 1 buckets (out-of-range ids -> bucket V); ws: id_sort_workspace_ints(V) ints.
-// Equal ids end up adjacent (order inside a bucket unspecified).  false: V >= 2^17 or n == 0.
-int64_t id_sort_workspace_ints(int V);
+// STABLE counting sort of ids into V + 1 buckets (out-of-range ids -> bucket V); ws:
+// id_sort_workspace_ints(n, V) ints.  Equal ids end up adjacent in index order (the same
+// permutation on every run).  false: V + 1 > 81920 or n == 0.
+int64_t id_sort_workspace_ints(int64_t n, int V);
 bool launch_id_bucket_sort(const int64_t* ids, int64_t n, int V, int* ws, int64_t* sorted, int64_t* perm,
                            hipStream_t s);
 // order = indices of the nonzero mask entries, then of the zero ones, each in index order

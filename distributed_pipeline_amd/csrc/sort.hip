@@ -3,14 +3,20 @@
 // (at::sort of the 262144 ids: a rocprim merge sort, 2.85 ms/step, and a stable argsort of
 // the 0/1 target mask) with passes whose cost is a few reads of the ids:
 //
-//   id_bucket_sort : counting sort of ids < 2^17 into V + 1 buckets (bucket V collects the
-//                    out-of-range ids, which the segment-sum kernels skip):
-//                    histogram -> exclusive scan -> scatter.  Histogram and scatter aggregate
-//                    per wave: lanes holding the same bucket are found with 17 ballots (one
-//                    per key bit) and one lane issues the wave's atomic for the group, so a
-//                    frequent id (a padding token in real data) costs one atomic per wave, not
-//                    one per token.  The order inside a bucket is the atomics' order (not
-//                    stable); the embedding gradient only needs equal ids adjacent.
+//   id_bucket_sort : STABLE counting sort of ids < 2^17 into V + 1 buckets (bucket V collects
+//                    the out-of-range ids, which the segment-sum kernels skip), so that the
+//                    embedding gradient's fp32 segment sums are bitwise reproducible (SURVEY 7.4
+//                    hard part 2; reference utils/trainer.py:235):
+//                      1. per-block histograms of SORT_BLK = 2048 tokens (LDS counters as 16-bit
+//                         pairs, so a 50257-token vocabulary fits the 160 KiB LDS), dense
+//                         [nblk][V + 1];
+//                      2. per bucket, the exclusive prefix over blocks (one thread per bucket);
+//                      3. exclusive scan of the bucket totals (bucket_scan_kernel);
+//                      4. one wave per block places its tokens in index order: lanes holding the
+//                         same bucket are found with 17 ballots and the group's leader takes the
+//                         bucket's block-local cursor with one LDS atomic, so a token's position
+//                         is off[b] + (tokens of b in earlier blocks) + (earlier tokens of b in
+//                         this block) - the same on every run.
 //   partition01    : stable partition of a 0/1 mask (nonzero first) -> the permutation.  Block
 //                    counts, then each block scans the counts before it and places its
 //                    elements with wave ballots (one 64-lane prefix per instruction).
@@ -40,23 +46,6 @@ __device__ __forceinline__ uint64_t match_key(uint32_t key) {
 
 __device__ __forceinline__ uint32_t bucket_of(int64_t id, int V) {
   return (id >= 0 && id < V) ? (uint32_t)id : (uint32_t)V;
-}
-
-// grid-stride over ids: cnt[bucket] += 1 (one atomic per distinct bucket per wave)
-__global__ void __launch_bounds__(256) id_hist_kernel(const int64_t* __restrict__ ids, int64_t n, int V,
-                                                      int* __restrict__ cnt) {
-  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
-  // whole waves iterate together (every lane runs the same number of iterations; tail lanes
-  // are inactive inside the body) so the ballots see the full wave
-  const int64_t base0 = (int64_t)blockIdx.x * blockDim.x + (threadIdx.x & ~63);
-  for (int64_t base = base0; base < n; base += stride) {
-    const int64_t i = base + (threadIdx.x & 63);
-    if (i < n) {
-      const uint32_t b = bucket_of(ids[i], V);
-      const uint64_t m = match_key(b);
-      if ((m & lanemask_lt()) == 0) atomicAdd(cnt + b, (int)__popcll(m));
-    }
-  }
 }
 
 // exclusive scan of cnt[0..nb) into off[0..nb) by one 1024-thread block: thread t owns the
@@ -129,51 +118,127 @@ __global__ void __launch_bounds__(1024) bucket_scan_kernel(const int* __restrict
   }
 }
 
-// pos = cur[bucket]++ per token (one atomic per distinct bucket per wave): sorted[pos] = id,
-// perm[pos] = token index
-__global__ void __launch_bounds__(256) id_scatter_kernel(const int64_t* __restrict__ ids, int64_t n, int V,
-                                                         int* __restrict__ cur, int64_t* __restrict__ sorted,
-                                                         int64_t* __restrict__ perm) {
-  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
-  const int64_t base0 = (int64_t)blockIdx.x * blockDim.x + (threadIdx.x & ~63);
-  for (int64_t base = base0; base < n; base += stride) {
-    const int64_t i = base + (threadIdx.x & 63);
+// ---- stable counting sort -------------------------------------------------------------
+constexpr int SORT_BLK = 2048;         // tokens per block (< 2^16: counts fit 16-bit LDS halves)
+constexpr int SORT_LDS_WORDS = 40960;  // 160 KiB: two 16-bit counters per word -> V + 1 <= 81920
+
+__device__ __forceinline__ uint32_t half_of(uint32_t w, uint32_t b) { return (w >> ((b & 1u) * 16u)) & 0xffffu; }
+
+// 1. hist[blk][b] = tokens of bucket b in block blk
+__global__ void __launch_bounds__(256) id_blockhist_kernel(const int64_t* __restrict__ ids, int64_t n, int V,
+                                                           int* __restrict__ hist) {
+  __shared__ uint32_t c32[SORT_LDS_WORDS];
+  const int nb = V + 1, nw = (nb + 1) / 2;
+  for (int q = threadIdx.x; q < nw; q += blockDim.x) c32[q] = 0u;
+  __syncthreads();
+  const int64_t t0 = (int64_t)blockIdx.x * SORT_BLK;
+  for (int r = threadIdx.x; r < SORT_BLK; r += blockDim.x) {
+    const int64_t i = t0 + r;
     if (i < n) {
-      const int64_t id = ids[i];
-      const uint32_t b = bucket_of(id, V);
-      const uint64_t m = match_key(b);
-      const uint64_t lt = m & lanemask_lt();
-      const int leader = __ffsll((unsigned long long)m) - 1;
-      int p0 = 0;
-      if (lt == 0) p0 = atomicAdd(cur + b, (int)__popcll(m));
-      p0 = __shfl(p0, leader, 64);
-      const int64_t pos = (int64_t)p0 + __popcll(lt);
-      sorted[pos] = id;
-      perm[pos] = i;
+      const uint32_t b = bucket_of(ids[i], V);
+      atomicAdd(c32 + (b >> 1), 1u << ((b & 1u) * 16u));  // counts are order-free
+    }
+  }
+  __syncthreads();
+  int* row = hist + (int64_t)blockIdx.x * nb;
+  for (int b = threadIdx.x; b < nb; b += blockDim.x) row[b] = (int)half_of(c32[b >> 1], (uint32_t)b);
+}
+
+// 2. hist[k][b] <- sum over blocks k' < k of hist[k'][b]; tot[b] = sum over all blocks
+__global__ void __launch_bounds__(256) id_colscan_kernel(int* __restrict__ hist, int nblk, int nb,
+                                                         int* __restrict__ tot) {
+  const int b = blockIdx.x * blockDim.x + threadIdx.x;
+  if (b >= nb) return;
+  int run = 0;
+  int k = 0;
+  for (; k + 8 <= nblk; k += 8) {  // 8 loads in flight per thread
+    int v[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) v[u] = hist[(int64_t)(k + u) * nb + b];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      hist[(int64_t)(k + u) * nb + b] = run;
+      run += v[u];
+    }
+  }
+  for (; k < nblk; ++k) {
+    const int v = hist[(int64_t)k * nb + b];
+    hist[(int64_t)k * nb + b] = run;
+    run += v;
+  }
+  tot[b] = run;
+}
+
+// 4. one wave per block walks its tokens in index order (32 rounds of 64)
+__global__ void __launch_bounds__(64) id_stable_scatter_kernel(const int64_t* __restrict__ ids, int64_t n, int V,
+                                                               const int* __restrict__ pre,
+                                                               const int* __restrict__ off,
+                                                               int64_t* __restrict__ sorted,
+                                                               int64_t* __restrict__ perm) {
+  __shared__ uint32_t c32[SORT_LDS_WORDS];
+  const int nb = V + 1, nw = (nb + 1) / 2;
+  const int lane = threadIdx.x;
+  for (int q = lane; q < nw; q += 64) c32[q] = 0u;
+  __syncthreads();
+  const int64_t t0 = (int64_t)blockIdx.x * SORT_BLK;
+  const int* prow = pre + (int64_t)blockIdx.x * nb;
+  constexpr int ROUNDS = SORT_BLK / 64, GROUP = 8;
+  for (int r0 = 0; r0 < ROUNDS; r0 += GROUP) {
+    int64_t idv[GROUP];
+#pragma unroll
+    for (int u = 0; u < GROUP; ++u) {  // a group of rounds' ids in flight at once
+      const int64_t i = t0 + (int64_t)(r0 + u) * 64 + lane;
+      idv[u] = i < n ? ids[i] : -1;
+    }
+#pragma unroll
+    for (int u = 0; u < GROUP; ++u) {
+      const int64_t base = t0 + (int64_t)(r0 + u) * 64;
+      if (base < n) {  // wave-uniform
+        const int64_t i = base + lane;
+        const bool in = i < n;
+        // tail lanes carry key 2^17 - 1 (no bucket: V + 1 <= 2^17 - 1), matching only each other
+        const uint32_t b = in ? bucket_of(idv[u], V) : (1u << SORT_KEY_BITS) - 1u;
+        const uint64_t m = match_key(b);
+        const uint64_t lt = m & lanemask_lt();
+        const int leader = __ffsll((unsigned long long)m) - 1;
+        uint32_t old = 0u;
+        if (in && lt == 0) old = atomicAdd(c32 + (b >> 1), (uint32_t)__popcll(m) << ((b & 1u) * 16u));
+        old = __shfl(old, leader, 64);
+        if (in) {
+          const int64_t pos = (int64_t)off[b] + prow[b] + half_of(old, b) + __popcll(lt);
+          sorted[pos] = idv[u];
+          perm[pos] = i;
+        }
+      }
     }
   }
 }
 
-// cnt[0..nb) then off at the next multiple of 4 ints (16-byte aligned for the int4 scan)
-static int64_t id_sort_off(int V) { return ((int64_t)V + 1 + 3) / 4 * 4; }
-int64_t id_sort_workspace_ints(int V) { return id_sort_off(V) + V + 1; }
+// ws: hist [nblk][V + 1], then tot and off (each 16-byte aligned)
+static int64_t nblk_of(int64_t n) { return (n + SORT_BLK - 1) / SORT_BLK; }
+static int64_t pad4(int64_t x) { return (x + 3) / 4 * 4; }
+int64_t id_sort_workspace_ints(int64_t n, int V) { return pad4(nblk_of(n) * (V + 1)) + 2 * pad4(V + 1); }
 
 bool launch_id_bucket_sort(const int64_t* ids, int64_t n, int V, int* ws, int64_t* sorted, int64_t* perm,
                            hipStream_t s) {
-  if (V < 1 || V >= (1 << SORT_KEY_BITS) || n <= 0 || n > (int64_t)INT32_MAX) return false;
+  if (V < 1 || V + 1 > 2 * SORT_LDS_WORDS || V + 1 >= (1 << SORT_KEY_BITS) - 1 || n <= 0 ||
+      n > (int64_t)INT32_MAX)
+    return false;
   const int nb = V + 1;
-  int* cnt = ws;
-  int* off = ws + id_sort_off(V);
-  if (hipMemsetAsync(cnt, 0, sizeof(int) * nb, s) != hipSuccess) return false;
-  int64_t g = (n + 255) / 256;
-  const unsigned grid = (unsigned)(g > 2048 ? 2048 : g);
-  hipLaunchKernelGGL(id_hist_kernel, dim3(grid), dim3(256), 0, s, ids, n, V, cnt);
-  // (the int4 path needs 16-byte aligned cnt / off: ws from the caching allocator is)
-  if (nb <= 32 * 1024 && (reinterpret_cast<uintptr_t>(ws) & 15) == 0)
-    hipLaunchKernelGGL(bucket_scan_kernel<32>, dim3(1), dim3(1024), 0, s, (const int*)cnt, nb, off);
+  const int64_t nblk = nblk_of(n);
+  int* hist = ws;
+  int* tot = ws + pad4(nblk * nb);
+  int* off = tot + pad4(nb);
+  hipLaunchKernelGGL(id_blockhist_kernel, dim3((unsigned)nblk), dim3(256), 0, s, ids, n, V, hist);
+  hipLaunchKernelGGL(id_colscan_kernel, dim3((unsigned)((nb + 255) / 256)), dim3(256), 0, s, hist, (int)nblk, nb,
+                     tot);
+  // (the int4 path needs 16-byte aligned tot / off: ws from the caching allocator is)
+  if (nb <= 32 * 1024 && (reinterpret_cast<uintptr_t>(tot) & 15) == 0)
+    hipLaunchKernelGGL(bucket_scan_kernel<32>, dim3(1), dim3(1024), 0, s, (const int*)tot, nb, off);
   else
-    hipLaunchKernelGGL(bucket_scan_kernel<0>, dim3(1), dim3(1024), 0, s, (const int*)cnt, nb, off);
-  hipLaunchKernelGGL(id_scatter_kernel, dim3(grid), dim3(256), 0, s, ids, n, V, off, sorted, perm);
+    hipLaunchKernelGGL(bucket_scan_kernel<0>, dim3(1), dim3(1024), 0, s, (const int*)tot, nb, off);
+  hipLaunchKernelGGL(id_stable_scatter_kernel, dim3((unsigned)nblk), dim3(64), 0, s, ids, n, V, (const int*)hist,
+                     (const int*)off, sorted, perm);
   return true;
 }
 

@@ -1,7 +1,8 @@
-"""Sort-free id orderings (csrc/sort.hip): the counting sort behind the embedding gradients
+"""Sort-free id orderings (csrc/sort.hip): the STABLE counting sort behind the embedding gradients
 and the stable 0/1 partition behind the logged nll, against torch references.  The embedding
-gradient over the counting sort is compared with an fp32 ``index_add_`` on duplicate-heavy ids
-(a few hot ids holding most tokens, as padding does in real data)."""
+gradient over the counting sort is compared with an fp64 ``index_add_`` on duplicate-heavy ids
+(a few hot ids holding most tokens, as padding does in real data), and two runs of it must give
+bitwise-equal gradients (one writer per row, a fixed summation order)."""
 import pytest
 import torch
 
@@ -20,9 +21,12 @@ def _check_bucket_sort(ids, V):
     # p is a permutation and s = ids[p]
     assert torch.equal(torch.sort(p).values, torch.arange(n, device=DEV))
     assert torch.equal(s, flat[p])
-    # buckets ascending, out-of-range ids (bucket V) last
+    # buckets ascending, out-of-range ids (bucket V) last, and STABLE: inside a bucket the
+    # tokens keep their index order (the permutation torch's stable argsort gives)
     b = torch.where((s >= 0) & (s < V), s, torch.full_like(s, V))
     assert bool((b[1:] >= b[:-1]).all())
+    key = torch.where((flat >= 0) & (flat < V), flat, torch.full_like(flat, V))
+    assert torch.equal(p, torch.argsort(key, stable=True))
     return s, p
 
 
@@ -89,3 +93,45 @@ def test_emb_qsample_bwd_uses_counting_sort_same_result():
     ref = torch.zeros(V, E, dtype=torch.float64, device=DEV).index_add_(0, ids.reshape(-1), rows.reshape(-1, E))
     err = (dW.double() - ref).abs().max().item()
     assert err <= 3e-5 * max(1.0, ref.abs().max().item()), err
+
+
+@pytest.mark.parametrize("E,n", [(128, 262144), (768, 65536)])
+def test_emb_grad_bitwise_reproducible(E, n):
+    """Two runs of the embedding gradient over the same inputs give the same bits (SURVEY 7.4:
+    the tied-embedding reduction deterministic), onto a non-zero gradient buffer, including a
+    padding-like id whose run crosses thousands of chunk boundaries."""
+    g = torch.Generator(device="cpu").manual_seed(11)
+    V = 30522
+    ids = torch.randint(0, V, (n,), generator=g)
+    ids[torch.rand(n, generator=g) < 0.45] = 0
+    ids = ids.to(DEV)
+    dy = torch.randn(n, E, generator=g).to(DEV).to(torch.bfloat16)
+    base = torch.randn(V, E, generator=g).to(DEV)
+    outs = []
+    for _ in range(2):
+        dW = base.clone()
+        get_ext().emb_grad(ids, dy, dW)
+        outs.append(dW)
+    assert torch.equal(outs[0], outs[1])
+    ref = base.double().index_add_(0, ids, dy.double())
+    err = (outs[0].double() - ref).abs().max().item()
+    assert err <= 3e-5 * max(1.0, ref.abs().max().item()), err
+
+
+def test_emb_qsample_bwd_bitwise_reproducible():
+    g = torch.Generator(device="cpu").manual_seed(6)
+    B, L, E, V = 2048, 128, 128, 30522
+    ids = torch.randint(0, V, (B, L), generator=g)
+    ids[:, 90:] = 0
+    ids = ids.to(DEV)
+    mask = (torch.rand(B, L, generator=g) > 0.3).long().to(DEV)
+    t = torch.randint(0, 2000, (B,), generator=g).to(DEV)
+    sa = torch.rand(2000, generator=g).to(DEV)
+    d_xs = torch.randn(B, L, E, generator=g).to(DEV)
+    d_xt = torch.randn(B, L, E, generator=g).to(DEV).to(torch.bfloat16)
+    outs = []
+    for _ in range(2):
+        dW = torch.zeros(V, E, device=DEV)
+        get_ext().emb_qsample_bwd(ids, mask, t, sa, d_xs, None, d_xt, dW)
+        outs.append(dW)
+    assert torch.equal(outs[0], outs[1])
