@@ -208,22 +208,27 @@ class BucketReducer {
   // Called at forward time when gradient synchronisation is enabled (torch-DDP
   // semantics: the no_sync decision is taken when the graph is built).
   //
-  // ``stream``: the stream the armed backward produces its gradients on (0: the current
-  // stream at launch time).  The grad-ready hooks do NOT run on it reliably: autograd
-  // runs a leaf's AccumulateGrad - and its hook - on the stream of the forward that
-  // first used the leaf, which in the overlapped micro-batch schedule is often the
-  // other stream; an event recorded there would not follow the gradient kernels.
+  // ``stream``: the stream the armed backward produces its gradients on (0: the calling
+  // thread's current stream NOW - which may be the null stream, handle 0 too).  The grad-ready
+  // hooks do NOT run on it reliably: autograd runs a leaf's AccumulateGrad - and its hook - on
+  // the stream of the forward that first used the leaf, which in the overlapped micro-batch
+  // schedule is often the other stream; an event recorded there would not follow the gradient
+  // kernels.  (Deferring the choice to launch time, as before round 6, took the HOOK thread's
+  // stream whenever the trainer ran on the null stream, whose handle is 0.)
   void arm(int64_t stream = 0) {
     std::lock_guard<std::mutex> g(mu_);
-    arm_stream_ = reinterpret_cast<hipStream_t>(stream);
+    if (grad_.is_cuda())
+      arm_c10_ = stream ? c10::hip::getStreamFromExternalMasqueradingAsCUDA(reinterpret_cast<hipStream_t>(stream),
+                                                                             grad_.device().index())
+                        : c10::hip::getCurrentHIPStreamMasqueradingAsCUDA(grad_.device().index());
+    arm_stream_ = arm_c10_ ? arm_c10_->stream() : nullptr;
     pending_ = size_;
     std::fill(launched_.begin(), launched_.end(), false);
     for (auto& w : work_) w.reset();
     next_ = 0;
     armed_ = true;
     if (sim_)  // fresh timeline: every word all-ones (the kernels keep minima)
-      DPA_HIP_CHECK(hipMemsetAsync(sim_tl_.data_ptr(), 0xff, sim_tl_.nbytes(),
-                                   arm_stream_ ? arm_stream_ : compute_stream()));
+      DPA_HIP_CHECK(hipMemsetAsync(sim_tl_.data_ptr(), 0xff, sim_tl_.nbytes(), producer()));
   }
 
   // Abandon a partially run backward (out-of-memory retry).  Buckets its hooks already
@@ -478,6 +483,8 @@ class BucketReducer {
 
  private:
   static hipStream_t compute_stream() { return c10::hip::getCurrentHIPStreamMasqueradingAsCUDA().stream(); }
+  // the armed backward's stream (captured by arm(); the null stream included), else the current
+  hipStream_t producer() const { return arm_c10_ ? arm_stream_ : compute_stream(); }
   static uint16_t* bf_ptr(const at::Tensor& t) { return reinterpret_cast<uint16_t*>(t.data_ptr()); }
 
   // The IPC data plane without an RCCL communicator: the comm stream and events of the direct
@@ -617,8 +624,8 @@ class BucketReducer {
   void launch_direct(int b) {
     const int64_t n = bounds_[b + 1] - bounds_[b];
     // the grad-ready point: everything the backward's stream queued so far
-    if (sim_) launch_time_marker(sim_slot(b, 2), arm_stream_ ? arm_stream_ : compute_stream());
-    DPA_HIP_CHECK(hipEventRecord(ready_[b], arm_stream_ ? arm_stream_ : compute_stream()));
+    if (sim_) launch_time_marker(sim_slot(b, 2), producer());
+    DPA_HIP_CHECK(hipEventRecord(ready_[b], producer()));
     DPA_HIP_CHECK(hipStreamWaitEvent(cs_, ready_[b], 0));
     float* g = grad_.data_ptr<float>() + bounds_[b];
     void* buf = g;
@@ -660,8 +667,7 @@ class BucketReducer {
     // CURRENT stream: make that the armed backward's stream, not whichever stream autograd
     // runs this parameter's hook on (in the overlapped schedule often the other one)
     c10::optional<c10::hip::HIPStreamGuardMasqueradingAsCUDA> guard;
-    if (arm_stream_ && grad_.is_cuda())
-      guard.emplace(c10::hip::getStreamFromExternalMasqueradingAsCUDA(arm_stream_, grad_.device().index()));
+    if (arm_c10_ && grad_.is_cuda()) guard.emplace(*arm_c10_);
     at::Tensor view = slice(grad_, b);
     if (bf16_) {
       at::Tensor wire = slice(comm_, b);
@@ -712,7 +718,8 @@ class BucketReducer {
   double sim_bw_ = 1.0, sim_lat_ = 0.0;
   at::Tensor sim_tl_, sim_acc_;
   hipStream_t cs_ = nullptr;
-  hipStream_t arm_stream_ = nullptr;  // the armed backward's stream (arm()), null: current
+  hipStream_t arm_stream_ = nullptr;  // the armed backward's stream (arm()); may be the null stream
+  c10::optional<c10::hip::HIPStreamMasqueradingAsCUDA> arm_c10_;
   std::vector<hipEvent_t> ready_;
   hipEvent_t done_ = nullptr;
   std::mutex mu_;

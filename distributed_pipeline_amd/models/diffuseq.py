@@ -59,6 +59,17 @@ class TransformerNetModel(nn.Module):
         self.LayerNorm = LayerNorm(H, eps=cfg["layer_norm_eps"])
         self.output_down_proj = MLP(H, H, input_dims, act="tanh")
 
+    def grad_ready_order(self):
+        """Parameters in the order their gradients complete in the backward (the DDP engine's flat
+        layout, parallel/ddp.py: buckets are all-reduced front to back as they complete).  The
+        reverse of the registration order - DiffuSeq's, kept for checkpoint parity - would put
+        ``position_embeddings`` and ``LayerNorm`` (registered after the encoder, used at its input)
+        into the first bucket, which then completes only at the end of the backward and holds every
+        later bucket's all-reduce with it (measured: profiles/sim_comm_r6.txt)."""
+        rev = list(reversed(list(self.parameters())))
+        first = {id(p) for m in (self.output_down_proj, self.input_transformers) for p in m.parameters()}
+        return [p for p in rev if id(p) in first] + [p for p in rev if id(p) not in first]
+
     # -- DiffuSeq API -------------------------------------------------------
     def get_embeds(self, input_ids):
         """Word embeddings in fp32 (diffusion space stays fp32), times emb_scale_factor."""

@@ -215,13 +215,17 @@ class DDPEngine(nn.Module):
         self.rank = dist.get_rank(self.pg) if self.distributed else 0
         # (world 1 keeps the sharded machinery - one shard - so it can be exercised alone)
         self.sharded = bool(shard_optimizer) and self.distributed
+        # the flat layout follows the order gradients complete in the backward when the module
+        # says it (grad_ready_order): buckets are launched in layout order, so one parameter
+        # whose gradient completes late holds back every bucket after its own
+        ready_order = module.grad_ready_order() if callable(getattr(module, "grad_ready_order", None)) else None
         if space is None:
-            kw = {}
+            kw = {"order": ready_order}
             if self.sharded:
                 # pad every bucket end so each bucket splits into world equal 16-aligned chunks
-                layout = layout_order(module.parameters())
+                layout = layout_order(module.parameters(), order=ready_order)
                 groups = bucket_members([p.numel() for p in layout], bucket_cap_mb, first_bucket_mb)
-                kw = dict(break_after={g[-1] for g in groups}, break_align=self.world_size * ALIGN)
+                kw.update(break_after={g[-1] for g in groups}, break_align=self.world_size * ALIGN)
             space = FlatParamSpace(module.parameters(), device=device, shadow_dtype=shadow_dtype, **kw)
         self.space = space
         self.reduce_dtype = reduce_dtype
@@ -241,6 +245,8 @@ class DDPEngine(nn.Module):
         self._shadow_works = []      # ZeRO-1: outstanding async shadow all-gathers
         self._master_stale = False   # ZeRO-1: fp32 master valid only in this rank's chunks
         self._fired = set()          # layout indices whose hook fired (first armed step only)
+        self._fire_seq = []          # ... in firing order
+        self.bucket_order_report = None  # first armed step: do buckets complete in launch order?
         self._track_unused = True
         self._ipc_flag = None        # device int32 error word of the IPC all-reduce
         self._ipc_host = None
@@ -426,9 +432,9 @@ class DDPEngine(nn.Module):
         self.sim_comm = {"world": int(world), "busbw_GBps": float(busbw_gbps), "cus": int(cus),
                          "lat_us": float(lat_us), "bucket_mb": self.bucket_sizes_mb(),
                          "wire": "bf16" if self.reduce_dtype == torch.bfloat16 else "fp32"}
+        self._track_unused = True  # the first simulated step checks the bucket completion order
         for i, p in enumerate(self.space.layout):
-            self._hooks.append(p.register_post_accumulate_grad_hook(
-                lambda _p, i=i: self._native.mark_ready(i) if self._native is not None else None))
+            self._hooks.append(p.register_post_accumulate_grad_hook(self._make_hook(p, i)))
         if hasattr(ext, "set_gemmp_dynamic"):
             ext.set_gemmp_dynamic(True)  # as a W > 1 run (collectives share the CUs)
         return self.sim_comm
@@ -534,6 +540,7 @@ class DDPEngine(nn.Module):
             def native_hook(_param):
                 if self._track_unused and self._armed:
                     self._fired.add(index)
+                    self._fire_seq.append(index)
                 native.mark_ready(index)  # no-op unless armed
             return native_hook
 
@@ -542,6 +549,7 @@ class DDPEngine(nn.Module):
                 return
             if self._track_unused:
                 self._fired.add(index)
+                self._fire_seq.append(index)
             b = self._bucket_of[id(p)]
             b.pending -= 1
             if b.pending == 0:
@@ -648,6 +656,7 @@ class DDPEngine(nn.Module):
         if not self._track_unused:
             return
         self._track_unused = False
+        self._check_bucket_order()
         if not late_buckets:
             self._fired.clear()
             return
@@ -663,6 +672,29 @@ class DDPEngine(nn.Module):
         if os.environ.get("DPA_DDP_UNUSED", "warn") == "error":
             raise RuntimeError(msg)
         warnings.warn(msg, RuntimeWarning, stacklevel=3)
+
+    def _check_bucket_order(self):
+        """First armed step: buckets are launched in layout order, so a bucket whose last
+        gradient completes after a later bucket's holds that one back (no overlap for it).  Warn
+        and name the parameter; the fix is a ``grad_ready_order()`` on the module."""
+        seq, self._fire_seq = self._fire_seq, []
+        if not seq:
+            return
+        pos = {i: k for k, i in enumerate(seq)}
+        idx = {id(p): i for i, p in enumerate(self.space.layout)}
+        done = []
+        for b in self.buckets:
+            ks = [pos.get(idx[id(p)], -1) for p in b.params]
+            done.append(max(ks))
+        held = [b for b in range(len(done) - 1) if done[b] > min(done[b + 1:])]
+        self.bucket_order_report = {"bucket_completion_rank": done, "held_back_by": held}
+        if held:
+            names = {id(p): n for n, p in self.module.named_parameters()}
+            b = held[0]
+            late = max(self.buckets[b].params, key=lambda p: pos.get(idx[id(p)], -1))
+            warnings.warn(f"DDPEngine: bucket {b} completes after later buckets (its last gradient: "
+                          f"{names.get(id(late), '?')}), so their all-reduces wait for it; give the module a "
+                          f"grad_ready_order() (parallel/flat.py layout_order)", RuntimeWarning, stacklevel=3)
 
     def step_skip_flag(self):
         """Device int32 word that is non-zero when this step's gradient reduction failed

@@ -9,8 +9,9 @@ flat layout each of those is a single memory pass (one kernel), the DDP buckets
 are plain slices (no pack/unpack copies, SURVEY K-3), and broadcast at startup
 is one collective (SURVEY X-3/X-4).
 
-Layout: parameters are laid out in *reverse* registration order, so the
-gradients that backward produces first (last layers) sit at the front and the
+Layout: parameters are laid out in the order backward completes their gradients -
+the module's ``grad_ready_order()`` when it has one, else the *reverse* registration
+order - so the gradients produced first (last layers) sit at the front and the
 all-reduce buckets fill in order.  Every parameter starts on a 16-element
 (64-byte) boundary so views are aligned for 16-byte vector loads; the total is
 padded to a multiple of 64 elements.
@@ -36,9 +37,17 @@ def unique_trainable(params):
     return uniq
 
 
-def layout_order(params, reverse=True):
-    """The order :class:`FlatParamSpace` lays ``params`` out in."""
+def layout_order(params, reverse=True, order=None):
+    """The order :class:`FlatParamSpace` lays ``params`` out in: ``order`` (a module's
+    ``grad_ready_order()``: the parameters in the order their gradients complete in the backward)
+    when given, else the reverse of the registration order."""
     uniq = unique_trainable(params)
+    if order is not None:
+        ids = {id(p) for p in uniq}
+        lay = [p for p in unique_trainable(order) if id(p) in ids]
+        if len(lay) != len(uniq):
+            raise ValueError(f"grad_ready_order covers {len(lay)} of {len(uniq)} trainable parameters")
+        return lay
     return list(reversed(uniq)) if reverse else uniq
 
 
@@ -49,10 +58,10 @@ class FlatParamSpace:
     gradient bucket into world-size equal, aligned chunks."""
 
     def __init__(self, params, device=None, shadow_dtype=None, reverse=True, break_after=(),
-                 break_align=ALIGN):
+                 break_align=ALIGN, order=None):
         uniq = unique_trainable(params)
         self.params = uniq                       # model.parameters() order
-        self.layout = list(reversed(uniq)) if reverse else list(uniq)
+        self.layout = layout_order(uniq, reverse, order)
         device = torch.device(device) if device is not None else uniq[0].device
         self.device = device
         self.offsets = {}
