@@ -178,8 +178,8 @@ def project(a, loop, one_step, timed, exec_used, base):
     import torch
     eng = loop.ddp_model
     out = []
-    wires = [w for w in a.project_wire.split(",") if w] or [a.grad_wire]
-    scheds = [x for x in a.project_schedules.split(",") if x]
+    wires = [w for w in a.project_wire.replace("/", ",").split(",") if w] or [a.grad_wire]
+    scheds = [x for x in a.project_schedules.replace("/", ",").split(",") if x]
     for spec in [x for x in a.project.split(";") if x.strip()]:
         f = [float(v) for v in spec.replace("/", ",").split(",")]
         world, bw = int(f[0]), f[1]

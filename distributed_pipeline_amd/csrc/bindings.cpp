@@ -1160,6 +1160,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("gemm_supported", &gemm_supported, "shape check for the native GEMMs");
   m.def("set_gemm256", &dpa::set_gemm256, "enable/disable the 256x256 8-phase GEMM path");
   m.def("set_gemmp_grid_cap", &dpa::set_gemmp_grid_cap, "cap the persistent GEMM grid (0 = #CUs)");
+  m.def("set_wgrad4w", &dpa::set_wgrad4w,
+        "weight gradients without in-kernel bias sums on the one-wave-per-SIMD kernel (wgrad4w.hip; default on)");
   m.def("set_gemmp_half", &dpa::set_gemmp_half,
         "128-row tiles of the persistent GEMMs: 0 off, 1 auto (when they finish sooner), 2 always, -1 default");
   m.def("set_gemmp_dynamic", &dpa::set_gemmp_dynamic,

@@ -1464,6 +1464,25 @@ __global__ void __launch_bounds__(256) wgrad_reduce_kernel(const float* __restri
   reinterpret_cast<f32x4*>(dW)[i] = acc;
 }
 
+// The one-wave-per-SIMD TR x TR kernel (csrc/wgrad4w.hip) takes every weight gradient whose bias
+// gradient comes from elsewhere (db == nullptr: the encoder's biases are reduced by the LayerNorm,
+// dact-GEMM and attention backwards) with the same split plan; the 8-phase kernel keeps the
+// in-kernel bias column sums.  set_wgrad4w(false): the 8-phase kernel everywhere (A/B, tests).
+static bool g_wgrad4w = false;  // on once measured (see the header comment of wgrad4w.hip)
+void set_wgrad4w(bool on) { g_wgrad4w = on; }
+
+static bool wgrad4w_go(const uint16_t* const* dys, const uint16_t* const* xs, int nseg, float* dW, int T, int N,
+                       int K, const WgradPlan& p, float* wsp, hipStream_t s) {
+  if (!g_wgrad4w || (wsp == nullptr && p.splits * nseg != 1)) return false;
+  if (!launch_wgrad4w(dys, xs, nseg, T, N, K, p.splits, p.kps, dW, wsp, s)) return false;
+  if (wsp) {
+    const int64_t n4 = (int64_t)N * K / 4;
+    hipLaunchKernelGGL(wgrad_reduce_kernel, dim3((unsigned)((n4 + 255) / 256)), dim3(256), 0, s, wsp, dW, n4,
+                       p.splits * nseg);
+  }
+  return true;
+}
+
 bool launch_gemm256_wgrad(const uint16_t* dy, const uint16_t* x, float* dW, float* db, int T,
                           int N, int K, hipStream_t s, float* ws) {
   // dW[N][K] += dy[T][N]^T . x[T][K]: M = N, N' = K, reduction = T split over workgroups
@@ -1472,6 +1491,7 @@ bool launch_gemm256_wgrad(const uint16_t* dy, const uint16_t* x, float* dW, floa
   const int ktot = T / 64;
   const WgradPlan p = wgrad_plan(T, N, K);
   float* wsp = (p.ws && ws != nullptr) ? ws : nullptr;
+  if (db == nullptr && wgrad4w_go(&dy, &x, 1, dW, T, N, K, p, wsp, s)) return true;
   hipLaunchKernelGGL((g256::gemm256_kernel<true, true, g256::EPI_ATOMIC_F32>),
                      dim3(tiles * p.splits), dim3(512), 0, s, (const bf16_t*)dy, (int64_t)N,
                      (const bf16_t*)x, (int64_t)K, N, K, ktot, p.kps, p.splits, nullptr, (int64_t)K, dW,
@@ -1502,6 +1522,7 @@ bool launch_gemm256_wgrad_multi(const uint16_t* const* dys, const uint16_t* cons
   const int ktot = T / 64;
   const WgradPlan p = wgrad_plan(T, N, K, nseg);
   float* wsp = (p.ws && ws != nullptr) ? ws : nullptr;
+  if (db == nullptr && wgrad4w_go(dys, xs, nseg, dW, T, N, K, p, wsp, s)) return true;
   hipLaunchKernelGGL((g256::gemm256_kernel<true, true, g256::EPI_ATOMIC_F32>),
                      dim3(tiles * p.splits * nseg), dim3(512), 0, s, sg.a[0], (int64_t)N, sg.b[0], (int64_t)K,
                      N, K, ktot, p.kps, p.splits, nullptr, (int64_t)K, dW, nullptr, 0, nullptr, db, wsp, sg);

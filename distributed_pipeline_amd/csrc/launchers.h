@@ -30,6 +30,11 @@ void launch_time_marker(unsigned long long* slot, hipStream_t s);
 void launch_comm_sim_stats(const unsigned long long* tl, int nb, const unsigned long long* bwd_end,
                            unsigned long long* acc, hipStream_t s);
 
+// ---- wgrad4w.hip: one-wave-per-SIMD weight gradient (both operands token-major) ----
+bool launch_wgrad4w(const uint16_t* const* as, const uint16_t* const* bs, int nseg, int T, int M, int N, int splits,
+                    int kps, float* dW, float* ws, hipStream_t s);
+void set_wgrad4w(bool on);  // gemm256.hip: route db-free weight gradients to wgrad4w (default on)
+
 // ---- optim.hip -------------------------------------------------------------
 void launch_sqnorm(const void* g, bool g_bf16, int64_t n, float* partial, int nparts, float scale,
                    float max_norm, float* out, hipStream_t s);

@@ -310,3 +310,42 @@ def test_dgrad_with_transposed_weight_matches(T, N, K):
         d = (r1.float() - r2.float()).abs().max().item()
         assert d <= 1e-2 * r1.float().abs().max().item(), d
         torch.testing.assert_close(db2, r2.float().sum(0), rtol=1e-2, atol=1e-2 * db2.abs().max().item())
+
+
+@pytest.mark.parametrize("four_w", [True, False], ids=["wgrad4w", "8phase"])
+@pytest.mark.parametrize("T,N,K", [(256, 256, 256), (4096, 768, 768), (8192, 2304, 768), (16384, 768, 3072),
+                                   (65536, 3072, 768), (512, 512, 768)])
+def test_gemm_wgrad_no_bias(T, N, K, four_w):
+    """dW += dy^T x without an in-kernel bias sum: the one-wave-per-SIMD kernel (csrc/wgrad4w.hip,
+    split-K workspace merge, or an in-place add when unsplit) and the 8-phase kernel, against fp32."""
+    ext = _ext()
+    ext.set_wgrad4w(four_w)
+    try:
+        torch.manual_seed(1)
+        dy = torch.randn(T, N, device="cuda").bfloat16()
+        x = torch.randn(T, K, device="cuda").bfloat16()
+        dW = torch.randn(N, K, device="cuda")
+        ref = dW + dy.float().t() @ x.float()
+        ext.gemm_wgrad(dy, x, dW, None)
+        _close(dW, ref, 1e-3)
+    finally:
+        ext.set_wgrad4w(False)  # the library default is restored by the multi-segment test below
+
+
+@pytest.mark.parametrize("nseg", [2, 8])
+@pytest.mark.parametrize("T,N,K", [(8192, 768, 768), (8192, 2304, 768), (2048, 768, 3072)])
+def test_gemm_wgrad_multi_segment_no_bias(T, N, K, nseg):
+    """Multi-segment launches (the deferred weight gradients of the micro-batch schedule) on wgrad4w."""
+    _ext().set_wgrad4w(True)
+    torch.manual_seed(2)
+    dys = [torch.randn(T, N, device="cuda").bfloat16() for _ in range(nseg)]
+    xs = [torch.randn(T, K, device="cuda").bfloat16() for _ in range(nseg)]
+    dW = torch.randn(N, K, device="cuda")
+    ref = dW.clone()
+    for dy, x in zip(dys, xs):
+        ref += dy.float().t() @ x.float()
+    try:
+        assert _ext().gemm_wgrad_multi(dys, xs, dW, None)
+    finally:
+        _ext().set_wgrad4w(False)
+    _close(dW, ref, 1e-3)
