@@ -91,6 +91,8 @@ def parse():
                          "(parallel/ddp.py enable_sim_comm); reported under 'projection'")
     ap.add_argument("--project-schedules", default="fused,reference",
                     help="schedules the projection times: fused and/or reference (the 32 x 64 one)")
+    ap.add_argument("--project-reps", type=int, default=2,
+                    help="alternating plain / simulated segments per projection point (medians reported)")
     ap.add_argument("--project-wire", default="",
                     help="'fp32,bf16': time each spec with both wire formats (default: --grad-wire)")
     ap.add_argument("--comm-probe", type=int, default=1,
@@ -171,15 +173,35 @@ def project(a, loop, one_step, timed, exec_used, base):
     """One-GPU projection of W > 1: the same process's trainer with its
     DDP engine on the SIMULATED data plane (csrc/comm_sim.hip) - every bucket's all-reduce is a
     kernel on the reducer's high-priority comm stream that holds `cus` CUs for the link model's
-    time and moves the ring's local HBM bytes.  The step math stays world 1.  Reported per spec,
-    wire and schedule: projected ms/step, exposed comm (ms/step over this process's own
-    no-sim time), the exposed tail after the backward's last kernel, the grad-ready -> start
-    delay (CU contention with the persistent GEMMs) and the link model's total comm time."""
+    time and moves the ring's local HBM bytes.  The step math stays world 1.  Each (spec, wire,
+    schedule) alternates a plain segment (no data plane) and a simulated one, --project-reps
+    times, so clock drift over the run cancels: reported are the medians, the exposed comm
+    (median of the paired differences), the exposed tail after the backward's last kernel, the
+    grad-ready -> start delay (CU contention with the persistent GEMMs) and the link model's
+    total comm time."""
+    import statistics
+
     import torch
     eng = loop.ddp_model
     out = []
     wires = [w for w in a.project_wire.replace("/", ",").split(",") if w] or [a.grad_wire]
     scheds = [x for x in a.project_schedules.replace("/", ",").split(",") if x]
+
+    def seg(sch, sim):
+        if sch == "fused":
+            loop.exec_microbatch, n = exec_used, a.steps
+        else:
+            loop.exec_microbatch, n = a.microbatch, a.ref_steps or 8
+        for _ in range(2):  # untimed: a fresh reducer's / schedule's first steps
+            one_step()
+        if sim:
+            eng.sim_stats(reset=True)
+        h0 = dict(getattr(loop, "host_time", {}))
+        e = timed(n) / n * 1e3
+        host.append({k: round((v - h0.get(k, 0.0)) / n * 1e3, 2) for k, v in getattr(loop, "host_time", {}).items()})
+        return e
+
+    host = []  # per segment: the trainer's host ms per step (fwd / bwd enqueue), plain and sim alternating
     for spec in [x for x in a.project.split(";") if x.strip()]:
         f = [float(v) for v in spec.replace("/", ",").split(",")]
         world, bw = int(f[0]), f[1]
@@ -188,38 +210,44 @@ def project(a, loop, one_step, timed, exec_used, base):
         cap = f[4] if len(f) > 4 else None
         first = f[5] if len(f) > 5 else None
         for wire in wires:
-            eng.reduce_dtype = torch.bfloat16 if wire == "bf16" else torch.float32
-            eng._comm_buf = None
-            info = eng.enable_sim_comm(world, bw, cus=cus, lat_us=lat, bucket_cap_mb=cap, first_bucket_mb=first)
-            loop.use_ddp = True
-            row = {"spec": dict(info), "schedules": {}}
+            row = {"spec": None, "schedules": {}}
             for sch in scheds:
-                if sch == "fused":
-                    loop.exec_microbatch, n = exec_used, a.steps
-                else:
-                    loop.exec_microbatch, n = a.microbatch, a.ref_steps or 8
-                for _ in range(2):  # untimed: the sim reducer's first steps
-                    one_step()
-                eng.sim_stats(reset=True)
-                e = timed(n)
-                st = eng.sim_stats(reset=True)
+                plain, simt, stats = [], [], []
+                host.clear()
+                for _ in range(max(1, a.project_reps)):
+                    eng.disable_sim_comm()
+                    loop.use_ddp = False
+                    plain.append(seg(sch, False))
+                    eng.reduce_dtype = torch.bfloat16 if wire == "bf16" else torch.float32
+                    info = eng.enable_sim_comm(world, bw, cus=cus, lat_us=lat, bucket_cap_mb=cap,
+                                               first_bucket_mb=first)
+                    row["spec"] = dict(info)
+                    loop.use_ddp = True
+                    simt.append(seg(sch, True))
+                    stats.append(eng.sim_stats(reset=True))
+                st = dict(stats[-1])
+                for k in ("exposed_tail_ms", "ready_to_start_ms", "bucket_busy_ms", "comm_span_ms"):
+                    st[k] = round(statistics.median(x[k] for x in stats), 3)
                 st["last_step_timeline_ms"] = eng.sim_timeline()
-                ms = e / n * 1e3
-                b = base.get(sch)
-                row["schedules"][sch] = dict(st, projected_ms_per_step=round(ms, 3),
-                                             base_ms_per_step=b,
-                                             exposed_comm_ms=round(ms - b, 3) if b else None,
-                                             projected_value=round(world / (ms / 1e3), 4))
+                ms, pl = statistics.median(simt), statistics.median(plain)
+                row["schedules"][sch] = dict(st, projected_ms_per_step=round(ms, 3), plain_ms_per_step=round(pl, 3),
+                                             plain_runs=[round(x, 2) for x in plain],
+                                             sim_runs=[round(x, 2) for x in simt],
+                                             exposed_comm_ms=round(statistics.median(
+                                                 s_ - p_ for s_, p_ in zip(simt, plain)), 3),
+                                             projected_value=round(world / (ms / 1e3), 4),
+                                             host_ms_per_step={"plain": host[0::2], "sim": host[1::2]})
                 print(f"[bench] projection W={world} {bw} GB/s {wire} {sch}: {ms:.2f} ms/step "
-                      f"(base {b}), tail {st['exposed_tail_ms']} ms", file=sys.stderr, flush=True)
+                      f"(plain {pl:.2f}), tail {st['exposed_tail_ms']} ms", file=sys.stderr, flush=True)
+                eng.disable_sim_comm()
+                loop.use_ddp = False
             out.append(row)
-            eng.disable_sim_comm()
-            loop.use_ddp = False
     eng.reduce_dtype = torch.bfloat16 if a.grad_wire == "bf16" else torch.float32
     loop.exec_microbatch = exec_used
     return {"kind": "PROJECTION (one GPU, simulated data plane; not a scaling measurement)",
-            "link_model": "busbw per spec; ring time = lat + 2 (W-1)/W x bucket bytes / busbw",
-            "runs": out}
+            "link_model": "busbw per spec; ring time = lat + 2 (W-1)/W x bucket bytes / busbw; the stand-in "
+                          "kernel also reads and writes back 2 (W-1)/W x the bucket bytes",
+            "base_ms_per_step": base, "reps": a.project_reps, "runs": out}
 
 
 def main():

@@ -741,7 +741,11 @@ void register_comm(pybind11::module& m) {
            pybind11::arg("shard_offsets") = std::vector<int64_t>(),
            pybind11::arg("rccl_uid") = std::string(), pybind11::arg("rank") = 0, pybind11::arg("world") = 1)
       .def("arm", &BucketReducer::arm, pybind11::arg("stream") = 0)
-      .def("disarm", &BucketReducer::disarm, pybind11::call_guard<pybind11::gil_scoped_release>())
+      // disarm / mark_ready / finalize keep the GIL: they only enqueue work (microseconds), and a
+      // release hands the GIL to another Python thread (the device prefetch thread) for up to its
+      // 5 ms switch interval - 32 no_sync forwards per step of the reference 32 x 64 schedule each
+      // called disarm and ran 55 ms/step slower (profiles/sim_comm_r6.json)
+      .def("disarm", &BucketReducer::disarm)
       .def("armed", &BucketReducer::armed)
       .def("direct", &BucketReducer::direct)
       .def("stream_priority", &BucketReducer::stream_priority)
@@ -777,8 +781,8 @@ void register_comm(pybind11::module& m) {
       .def("ipc_error_flag", &BucketReducer::ipc_error_flag)
       .def("launched_count", &BucketReducer::launched_count)
       .def("late_buckets", &BucketReducer::late_buckets)
-      .def("mark_ready", &BucketReducer::mark_ready, pybind11::call_guard<pybind11::gil_scoped_release>())
-      .def("finalize", &BucketReducer::finalize, pybind11::call_guard<pybind11::gil_scoped_release>())
+      .def("mark_ready", &BucketReducer::mark_ready)
+      .def("finalize", &BucketReducer::finalize)
       .def("reduce_all", &BucketReducer::reduce_all, pybind11::call_guard<pybind11::gil_scoped_release>())
       .def("num_buckets", &BucketReducer::num_buckets)
       .def("comm_size", &BucketReducer::comm_size)

@@ -497,7 +497,7 @@ class DDPEngine(nn.Module):
             if self._armed:
                 self._arm()
             else:
-                if self._native is not None:
+                if self._native is not None and self._native.armed():
                     self._native.disarm()
                 self._remove_hooks()  # a no_sync backward reduces nothing: no hook calls
         return self.module(*args, **kwargs)

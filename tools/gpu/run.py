@@ -14,6 +14,7 @@ Steps (``:``-separated fields; ``,`` separates extra command-line arguments):
     ab:VAR:A:B[:REPS[:ARGS]]    interleaved headline benches with VAR=A / VAR=B -> gpurun_out/ab_VAR.txt
     py:NAME:SCRIPT[:ARGS]       python SCRIPT ARGS -> gpurun_out/NAME.log
     trace:NAME:SCRIPT[:ARGS]    rocprofv3 --kernel-trace (csv) of python SCRIPT ARGS -> gpurun_out/NAME/
+    profpy:NAME:SCRIPT[:ARGS[:N]]  rocprofv3 --kernel-trace --stats of python SCRIPT ARGS, summarised per N steps
 
 This process never touches the GPU itself (it only starts children), so the children
 may exec freely.
@@ -101,6 +102,20 @@ def main(steps):
             with open(os.path.join(d, "summary.txt")) as fh:
                 print(fh.read()[:4000], flush=True)
             # the trace database runs to tens of MB: only the summary comes back (gpurun's 64 MiB cap)
+            for f_ in os.listdir(d):
+                if f_.endswith(".db"):
+                    os.remove(os.path.join(d, f_))
+        elif kind == "profpy":  # profpy:NAME:SCRIPT[:ARGS[:STEPS]] - kernel stats of a python script
+            name, script = f[1], f[2]
+            args = f[3].split(",") if len(f) > 3 and f[3] else []
+            nsteps = f[4] if len(f) > 4 and f[4] else "1"
+            d = os.path.join(OUT, name)
+            os.makedirs(d, exist_ok=True)
+            _run(["rocprofv3", "--kernel-trace", "--stats", "-d", d, "-o", "run", "--", sys.executable, "-u", script]
+                 + args, os.path.join(d, "prof.log"), 600, dict(env, TMPDIR="/tmp"))
+            _run([sys.executable, "tools/prof_summary.py", d, "40", nsteps], os.path.join(d, "summary.txt"), 120, env)
+            with open(os.path.join(d, "summary.txt")) as fh:
+                print(fh.read()[:3000], flush=True)
             for f_ in os.listdir(d):
                 if f_.endswith(".db"):
                     os.remove(os.path.join(d, f_))
