@@ -466,7 +466,8 @@ def main():
                                                 **loop.ddp_model.bucket_tune)
         nat = getattr(loop.ddp_model, "_native", None)
         direct = nat is not None and nat.direct()
-        out["config"]["comm"] = ("reducer-owned RCCL communicator, priority %d stream" % nat.stream_priority()
+        out["config"]["comm"] = ("reducer-owned RCCL communicator on the stream plan's comm stream (pooled "
+                                 "queue, priority %d)" % nat.stream_priority()
                                  if direct else ("c10d process group" if world > 1 else "none (world 1)"))
         # where each collective of a W > 1 step runs (the W > 1 resource plan)
         eng_ = loop.ddp_model

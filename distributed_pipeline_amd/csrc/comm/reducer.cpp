@@ -153,8 +153,8 @@ class BucketReducer {
   BucketReducer(c10::intrusive_ptr<c10d::ProcessGroup> pg, at::Tensor grad_flat,
                 std::vector<int64_t> bounds, std::vector<int64_t> param_bucket, bool bf16_wire,
                 c10::optional<at::Tensor> shard_out, std::vector<int64_t> shard_offsets,
-                std::string rccl_uid, int64_t rank, int64_t world)
-      : pg_(std::move(pg)), grad_(std::move(grad_flat)), bounds_(std::move(bounds)),
+                std::string rccl_uid, int64_t rank, int64_t world, int64_t comm_stream = 0)
+      : given_cs_(reinterpret_cast<hipStream_t>(comm_stream)), pg_(std::move(pg)), grad_(std::move(grad_flat)), bounds_(std::move(bounds)),
         bucket_of_(std::move(param_bucket)), bf16_(bf16_wire) {
     TORCH_CHECK(grad_.is_contiguous() && grad_.dim() == 1, "grad_flat must be a 1-D contiguous tensor");
     TORCH_CHECK(bounds_.size() >= 2 && bounds_.front() == 0 && bounds_.back() <= grad_.numel(),
@@ -202,7 +202,7 @@ class BucketReducer {
     for (hipEvent_t e : ready_) if (e) (void)hipEventDestroy(e);
     if (done_) (void)hipEventDestroy(done_);
     if (gather_ev_) (void)hipEventDestroy(gather_ev_);
-    if (cs_) (void)hipStreamDestroy(cs_);
+    if (cs_ && own_cs_) (void)hipStreamDestroy(cs_);
   }
 
   // Called at forward time when gradient synchronisation is enabled (torch-DDP
@@ -497,7 +497,7 @@ class BucketReducer {
     TORCH_CHECK(world_ > 1 && world_ <= IPC_MAXW && rank >= 0 && rank < world_, "IPC-only: 2..8 ranks");
     const c10::DeviceGuard guard(grad_.device());
     rank_ = (int)rank;
-    make_comm_stream();
+    make_comm_stream(given_cs_);
   }
 
   // Simulated data plane (csrc/comm_sim.hip): a one-GPU PROJECTION of a world-`world` all-reduce.
@@ -505,7 +505,9 @@ class BucketReducer {
   // workgroups that hold their CU slots for lat_us + 2 (W - 1) / W x bytes / busbw and move the
   // ring's local HBM bytes; the gradients stay this rank's (world-1 math).  Per-step timeline
   // sums accumulate on the device (sim_stats).
-  void init_sim(int64_t world, double busbw_gbps, int64_t cus, double lat_us) {
+  // comm_stream: 0 = a new highest-priority stream (as the direct mode), else the handle of an
+  // existing stream to run the stand-in kernels on (A/B of the stream's hardware queue)
+  void init_sim(int64_t world, double busbw_gbps, int64_t cus, double lat_us, int64_t comm_stream) {
     TORCH_CHECK(cs_ == nullptr, "the reducer already has a comm stream");
     TORCH_CHECK(grad_.is_cuda() && !rs_, "sim data plane: all-reduce buckets of device gradients");
     const c10::DeviceGuard guard(grad_.device());
@@ -515,7 +517,7 @@ class BucketReducer {
     sim_tl_ = at::empty({(int64_t)nb * 4 + 8}, grad_.options().dtype(at::kLong));
     DPA_HIP_CHECK(hipMemset(sim_tl_.data_ptr(), 0xff, sim_tl_.nbytes()));
     sim_acc_ = at::zeros({8}, grad_.options().dtype(at::kLong));
-    make_comm_stream();
+    make_comm_stream(reinterpret_cast<hipStream_t>(comm_stream));
   }
   void set_sim(int64_t world, double busbw_gbps, int64_t cus, double lat_us) {
     TORCH_CHECK(world >= 2 && busbw_gbps > 0 && cus >= 1 && cus <= 1024 && lat_us >= 0, "sim: bad parameters");
@@ -582,10 +584,20 @@ class BucketReducer {
     launch_comm_sim(buf, bytes, touch, ticks, sim_cus_, sim_slot(b, 0), cs_);
   }
 
-  void make_comm_stream() {
-    int least = 0, greatest = 0;
-    DPA_HIP_CHECK(hipDeviceGetStreamPriorityRange(&least, &greatest));
-    DPA_HIP_CHECK(hipStreamCreateWithPriority(&cs_, hipStreamNonBlocking, greatest));
+  // The data plane's stream.  `given` (the stream plan's, runtime/streams.py): a stream on one of
+  // the process's GPU_MAX_HW_QUEUES pooled queues.  Otherwise a new highest-priority stream - which
+  // gets an HSA queue of its own, one more than the pooled four: with it present the overlapped
+  // reference schedule ran 228.9 ms/step against 209.2 on a pooled normal-priority stream and 208.9
+  // without any data plane (simulated comm, profiles/sim_comm_r6.json), so the engine passes the plan's.
+  void make_comm_stream(hipStream_t given = nullptr) {
+    if (given) {
+      cs_ = given;
+      own_cs_ = false;
+    } else {
+      int least = 0, greatest = 0;
+      DPA_HIP_CHECK(hipDeviceGetStreamPriorityRange(&least, &greatest));
+      DPA_HIP_CHECK(hipStreamCreateWithPriority(&cs_, hipStreamNonBlocking, greatest));
+    }
     ready_.assign(launched_.size(), nullptr);
     for (auto& e : ready_) DPA_HIP_CHECK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
     DPA_HIP_CHECK(hipEventCreateWithFlags(&done_, hipEventDisableTiming));
@@ -600,7 +612,7 @@ class BucketReducer {
     std::memcpy(id.internal, uid.data(), NCCL_UNIQUE_ID_BYTES);
     rank_ = rank;
     DPA_RCCL_CHECK(ncclCommInitRank(&rcomm_, world, id, rank));
-    make_comm_stream();
+    make_comm_stream(given_cs_);
   }
 
   at::Tensor slice(const at::Tensor& t, int b) const { return t.slice(0, bounds_[b], bounds_[b + 1]); }
@@ -717,7 +729,9 @@ class BucketReducer {
   int sim_world_ = 2, sim_cus_ = 1;
   double sim_bw_ = 1.0, sim_lat_ = 0.0;
   at::Tensor sim_tl_, sim_acc_;
+  hipStream_t given_cs_ = nullptr;  // the constructor's comm_stream (0: create one)
   hipStream_t cs_ = nullptr;
+  bool own_cs_ = true;
   hipStream_t arm_stream_ = nullptr;  // the armed backward's stream (arm()); may be the null stream
   c10::optional<c10::hip::HIPStreamMasqueradingAsCUDA> arm_c10_;
   std::vector<hipEvent_t> ready_;
@@ -734,12 +748,13 @@ void register_comm(pybind11::module& m) {
   pybind11::class_<BucketReducer>(m, "BucketReducer")
       .def(pybind11::init<c10::intrusive_ptr<c10d::ProcessGroup>, at::Tensor, std::vector<int64_t>,
                           std::vector<int64_t>, bool, c10::optional<at::Tensor>, std::vector<int64_t>,
-                          std::string, int64_t, int64_t>(),
+                          std::string, int64_t, int64_t, int64_t>(),
            pybind11::arg("process_group"), pybind11::arg("grad_flat"), pybind11::arg("bounds"),
            pybind11::arg("param_bucket"), pybind11::arg("bf16_wire") = false,
            pybind11::arg("shard_out") = pybind11::none(),
            pybind11::arg("shard_offsets") = std::vector<int64_t>(),
-           pybind11::arg("rccl_uid") = std::string(), pybind11::arg("rank") = 0, pybind11::arg("world") = 1)
+           pybind11::arg("rccl_uid") = std::string(), pybind11::arg("rank") = 0, pybind11::arg("world") = 1,
+           pybind11::arg("comm_stream") = 0)
       .def("arm", &BucketReducer::arm, pybind11::arg("stream") = 0)
       // disarm / mark_ready / finalize keep the GIL: they only enqueue work (microseconds), and a
       // release hands the GIL to another Python thread (the device prefetch thread) for up to its
@@ -760,7 +775,7 @@ void register_comm(pybind11::module& m) {
                   },
                   "a reducer without a process group, for the simulated data plane (then init_sim)")
       .def("init_sim", &BucketReducer::init_sim, pybind11::arg("world"), pybind11::arg("busbw_gbps"),
-           pybind11::arg("cus"), pybind11::arg("lat_us"))
+           pybind11::arg("cus"), pybind11::arg("lat_us"), pybind11::arg("comm_stream") = 0)
       .def("set_sim", &BucketReducer::set_sim, pybind11::arg("world"), pybind11::arg("busbw_gbps"),
            pybind11::arg("cus"), pybind11::arg("lat_us"))
       .def("sim", &BucketReducer::sim)

@@ -304,7 +304,7 @@ class DDPEngine(nn.Module):
                                                  self.reduce_dtype == torch.bfloat16,
                                                  self.grad_shard if self.sharded else None,
                                                  [c[2] for c in self.shard_chunks], uid, self.rank,
-                                                 self.world_size)
+                                                 self.world_size, self._plan_comm_stream())
                 if ipc_req and (uid or ipc_only):
                     if not uid:
                         self._native.init_ipc_only(self.rank)
@@ -329,6 +329,18 @@ class DDPEngine(nn.Module):
             self._install_hooks()
 
     # -- setup ---------------------------------------------------------------
+    def _plan_comm_stream(self):
+        """Handle of the stream plan's data-plane stream (runtime/streams.py role "comm": one of
+        the pooled hardware queues); 0 (the reducer creates its own) off the GPU or without a plan."""
+        if self.space.device.type != "cuda":
+            return 0
+        try:
+            from ..runtime.streams import plan_stream
+            s = plan_stream(self.space.device, "comm")
+        except Exception:  # noqa: BLE001 - a plan is an optimisation, never a requirement
+            return 0
+        return int(s.cuda_stream) if s is not None else 0
+
     def _install_hooks(self):
         """One post-accumulate-grad hook per parameter.  It fires once per backward per leaf,
         also when a fused op wrote the gradient in place and returned None for it
@@ -413,7 +425,8 @@ class DDPEngine(nn.Module):
         return self.distributed or self.sim_comm is not None
 
     # -- one-GPU projection of W > 1 ------------------------------
-    def enable_sim_comm(self, world, busbw_gbps, cus=64, lat_us=10.0, bucket_cap_mb=None, first_bucket_mb=None):
+    def enable_sim_comm(self, world, busbw_gbps, cus=64, lat_us=10.0, bucket_cap_mb=None, first_bucket_mb=None,
+                        comm_stream=None):
         """Run this world-1 engine's backward against a SIMULATED world-``world`` data plane
         (csrc/comm_sim.hip via the C++ reducer's sim mode): every bucket, when its gradients are
         ready, launches on the reducer's high-priority comm stream a kernel of ``cus`` workgroups
@@ -441,7 +454,10 @@ class DDPEngine(nn.Module):
         param_bucket = [self._bucket_of[id(p)].index for p in self.space.layout]
         red = ext.BucketReducer.simulated(self.space.grad_flat, bounds, param_bucket,
                                           self.reduce_dtype == torch.bfloat16)
-        red.init_sim(int(world), float(busbw_gbps), int(cus), float(lat_us))
+        # comm_stream: a torch stream for the stand-in kernels (A/B of the queue the data plane runs
+        # on); None: the stream plan's comm stream, as the real data plane
+        red.init_sim(int(world), float(busbw_gbps), int(cus), float(lat_us),
+                     int(comm_stream.cuda_stream) if comm_stream is not None else self._plan_comm_stream())
         self._native = red
         self.sim_comm = {"world": int(world), "busbw_GBps": float(busbw_gbps), "cus": int(cus),
                          "lat_us": float(lat_us), "bucket_mb": self.bucket_sizes_mb(),

@@ -26,10 +26,15 @@ side       second forward/backward stream of the overlapped micro-batch schedule
 wgrad      deferred weight gradients of the un-armed micro-batches (ops/nn.py deferral)
 nll        the logged nll's forward-only vocabulary sweep (models/gaussian_diffusion.py)
 copy       H2D prefetch of the next batch (data/prefetch.py; reference trainer.py:210-213)
+comm       the data plane: the C++ reducer's bucket all-reduces / reduce-scatters and ZeRO-1
+           gathers (csrc/comm/reducer.cpp; reference trainer.py:115-128), on the nll queue
 =========  ==========================================================================
 
-The data plane's comm stream is the C++ reducer's own (csrc/comm/reducer.cpp), created on the
-highest-priority queue pool, which the compute stream (normal priority) never uses.
+Every stream stays on the GPU_MAX_HW_QUEUES pooled queues.  Round 5 gave the reducer a new
+highest-priority stream, which HIP puts on a queue of its own; measured on the simulated data
+plane (round 6) that fifth queue slowed the overlapped reference schedule from 209 to 229
+ms/step while the stand-in comm kernels on a pooled queue cost nothing (CU-masked streams, also
+one queue each, had cost far more: 523 ms/step, profiles/stream_plan_ab_r5.txt).
 
 ``StreamPlan(device, mode="pool")`` gives torch pool streams, ``"cumask"`` the CU-masked ones (A/B
 runs); without the native extension the plan falls back to ``"pool"``."""
@@ -37,7 +42,7 @@ import os
 
 import torch
 
-ROLES = ("side", "wgrad", "nll", "copy")
+ROLES = ("side", "wgrad", "nll", "copy", "comm")
 
 
 class StreamPlan:
@@ -59,8 +64,11 @@ class StreamPlan:
                 self.mode = "pool"
         with torch.cuda.device(self.device):
             for role in ROLES:  # fixed creation order
-                if self.mode == "ordered" and role == "copy":
-                    s = self.streams["nll"]  # 4 queues: the brief H2D prefetch shares the nll queue
+                if self.mode == "ordered" and role in ("copy", "comm"):
+                    # 4 queues: the brief H2D prefetch and the data plane share the nll queue (an
+                    # extra high-priority queue for the data plane cost the overlapped reference
+                    # schedule 20 ms/step: profiles/sim_comm_r6.json)
+                    s = self.streams["nll"]
                 elif self.mode in ("ordered", "cumask"):
                     s = torch.cuda.ExternalStream(ext.stream_create(1 if self.mode == "cumask" else 0, 0),
                                                   device=self.device)
@@ -92,9 +100,9 @@ class StreamPlan:
     # HSA queue of each role EXPECTED for the "ordered" plan: measured once from a rocprofv3 kernel
     # trace of the real start-up order (tools/probes/stream_queues.py, GPU_MAX_HW_QUEUES=4), not
     # re-measured per run (HIP exposes no queue id)
-    EXPECTED_QUEUES = {"compute": 1, "side": 2, "wgrad": 3, "nll": 4, "copy": 4,
-                       "reducer_comm": "5 (high-priority pool)", "zero_gather": "reducer_comm",
-                       "source": "profiles/stream_queues_r5.txt (one trace, not this run)"}
+    EXPECTED_QUEUES = {"compute": 1, "side": 2, "wgrad": 3, "nll": 4, "copy": 4, "comm": 4,
+                       "zero_gather": "comm",
+                       "source": "profiles/stream_queues_r5.txt (one trace, not this run; comm: round 6)"}
 
     def describe(self):
         d = {"mode": self.mode, "roles": list(ROLES),

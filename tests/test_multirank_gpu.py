@@ -103,7 +103,9 @@ def _rccl_worker(port, wire, q):
         local, _ = run(sync=False)   # no collective
         reduced, launched = run(sync=True)  # RCCL all-reduce of every bucket (world 1: identity)
         direct = bool(native and eng._native.direct())
-        prio = eng._native.stream_priority() if native else 0
+        # the data plane runs on the stream plan's comm stream (a pooled hardware queue)
+        from distributed_pipeline_amd.runtime.streams import plan_stream
+        prio = int(native and eng._native.comm_stream() == plan_stream(torch.device("cuda", 0), "comm").cuda_stream)
         q.put((native, len(eng.buckets), local.cpu().numpy(), reduced.cpu().numpy(), launched, direct,
                prio))
     finally:
@@ -124,9 +126,10 @@ def test_native_reducer_over_rccl_single_rank(wire):
     assert p.exitcode == 0
     assert native, "native BucketReducer not used with the RCCL process group"
     assert nb > 3
-    # the reducer-owned RCCL communicator on a highest-priority comm stream (SURVEY N-2),
-    # every bucket launched from the grad-ready hooks while backward ran (overlap)
-    assert direct and prio < 0, (direct, prio)
+    # the reducer-owned RCCL communicator on the stream plan's comm stream (SURVEY N-2; a pooled
+    # queue, not a fifth high-priority one: profiles/sim_comm_r6.json), every bucket launched from
+    # the grad-ready hooks while backward ran (overlap)
+    assert direct and prio == 1, (direct, prio)
     assert launched == nb, f"{launched}/{nb} buckets launched before finalize()"
     local, reduced = torch.from_numpy(local), torch.from_numpy(reduced)
     assert local.abs().sum() > 0

@@ -20,6 +20,9 @@ def main():
     ap.add_argument("--sim", type=int, default=1)
     ap.add_argument("--steps", type=int, default=3)
     ap.add_argument("--spec", default="8,1000000,64,0")
+    ap.add_argument("--comm", default="high", choices=["high", "normal", "nll"],
+                    help="stream of the stand-in kernels: a new highest-priority one, a new normal one, "
+                         "or the stream plan's nll stream")
     a = ap.parse_args()
     import torch
 
@@ -51,16 +54,63 @@ def main():
         step()
     if a.sim:
         w, bw, cus, lat = (float(x) for x in a.spec.split(","))
-        loop.ddp_model.enable_sim_comm(int(w), bw, cus=int(cus), lat_us=lat)
+        cs = None
+        if a.comm == "normal":
+            cs = torch.cuda.Stream()
+        elif a.comm == "nll":
+            from distributed_pipeline_amd.runtime.streams import plan_stream
+            cs = plan_stream(torch.device("cuda", 0), "nll")
+        loop.ddp_model.enable_sim_comm(int(w), bw, cus=int(cus), lat_us=lat, comm_stream=cs)
         loop.use_ddp = True
         for _ in range(2):
             step()
+    # host time inside the engine's calls (wrapped; the engine's own work, not the model's)
+    eng = loop.ddp_model
+    acc = {}
+
+    def wrap(obj, name, label=None):
+        fn = getattr(obj, name)
+
+        def w(*args, **kw):
+            t0 = time.perf_counter()
+            try:
+                return fn(*args, **kw)
+            finally:
+                k = label or name
+                acc[k] = acc.get(k, 0.0) + time.perf_counter() - t0
+        setattr(obj, name, w)
+
+    for n in ("arm_for_backward", "finalize", "_install_hooks", "_remove_hooks", "_arm", "wait_shadow"):
+        wrap(eng, n)
+    if eng._native is not None:
+        nat = eng._native
+
+        class W:
+            def __getattr__(self, k):
+                return getattr(nat, k)
+        wn = W()
+        for n in ("disarm", "armed", "mark_ready", "finalize", "arm"):
+            f0 = getattr(nat, n)
+
+            def mk(f0=f0, n=n):
+                def g(*args):
+                    t0 = time.perf_counter()
+                    try:
+                        return f0(*args)
+                    finally:
+                        acc["native." + n] = acc.get("native." + n, 0.0) + time.perf_counter() - t0
+                return g
+            setattr(wn, n, mk())
+        eng._native = wn
     torch.cuda.synchronize()
     t = time.perf_counter()
     for _ in range(a.steps):
         step()
+    host = time.perf_counter() - t
     torch.cuda.synchronize()
-    print(f"sim={a.sim}: {(time.perf_counter() - t) / a.steps * 1e3:.2f} ms/step", flush=True)
+    print(f"sim={a.sim} comm={a.comm}: {(time.perf_counter() - t) / a.steps * 1e3:.2f} ms/step (host enqueue "
+          f"{host / a.steps * 1e3:.2f} ms/step); engine host ms/step: "
+          + ", ".join(f"{k} {v / a.steps * 1e3:.2f}" for k, v in sorted(acc.items())), flush=True)
 
 
 if __name__ == "__main__":
