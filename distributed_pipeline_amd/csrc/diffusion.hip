@@ -130,6 +130,20 @@ __global__ void __launch_bounds__(256) emb_qsample_bwd_kernel(
 //  * a run crossing a chunk boundary leaves per-chunk partials in part[chunk][2][E]: slot 0 = the
 //    piece that continues a run from the previous chunk, slot 1 = the piece of a run that starts
 //    in this chunk and continues past it; emb_grad_fixup_kernel adds them in chunk order.
+//
+// The chunk's per-token metadata (sorted id, token, q_sample coefficient) is loaded lane-parallel
+// once - lane l holds token l of the chunk - and broadcast with readlane, so the token loop has
+// no dependent global loads; the gradient rows of a batch of TB tokens are all in flight before
+// the in-order run accumulation consumes them.
+__device__ __forceinline__ int64_t readlane64(int64_t v, int l) {
+  const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)v, l);
+  const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)((uint64_t)v >> 32), l);
+  return (int64_t)(((uint64_t)hi << 32) | lo);
+}
+__device__ __forceinline__ float readlanef(float v, int l) {
+  return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), l));
+}
+
 template <int CPL>
 __global__ void __launch_bounds__(256) emb_grad_sorted_kernel(
     const int64_t* __restrict__ sid, const int64_t* __restrict__ perm, const int64_t* __restrict__ mask,
@@ -137,19 +151,29 @@ __global__ void __launch_bounds__(256) emb_grad_sorted_kernel(
     const bf16_t* __restrict__ d_xs16, const bf16_t* __restrict__ d_xt16, const float* __restrict__ d_xt32,
     int64_t NT, int L, int V, float* __restrict__ dW, int chunk, float* __restrict__ part) {
   constexpr int E = 64 * CPL;
+  constexpr int TB = 64 / CPL > 16 ? 16 : 64 / CPL;  // tokens whose rows are loaded together
   const int lane = threadIdx.x & 63;
   const int64_t c = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
   const int64_t j0 = c * chunk;
   if (j0 >= NT) return;
   const int64_t j1 = j0 + chunk < NT ? j0 + chunk : NT;
+  const int n = (int)(j1 - j0);  // <= 64 (emb_chunk)
+  int64_t my_id = 0, my_tok = 0;
+  float my_a = 0.f;
+  if (lane < n) {
+    my_id = sid[j0 + lane];
+    my_tok = perm[j0 + lane];
+    if (d_xt16 || d_xt32) my_a = mask[my_tok] != 0 ? sa[t[my_tok / L]] : 1.f;
+  }
   float acc[CPL];
 #pragma unroll
   for (int k = 0; k < CPL; ++k) acc[k] = 0.f;
-  int64_t cur = sid[j0];
+  int64_t cur = readlane64(my_id, 0);
   bool first = true;
   const bool head = j0 > 0 && sid[j0 - 1] == cur;  // the first run continues one from the left
+  const int64_t next = j1 < NT ? sid[j1] : -1;
   auto flush = [&](bool at_end) {
-    const bool cont = at_end && j1 < NT && sid[j1] == cur;  // the run goes on past the chunk
+    const bool cont = at_end && j1 < NT && next == cur;  // the run goes on past the chunk
     float* dst = nullptr;
     bool add = false;
     if (first && head) dst = part + (c * 2) * E;               // continuation piece
@@ -166,38 +190,101 @@ __global__ void __launch_bounds__(256) emb_grad_sorted_kernel(
     for (int k = 0; k < CPL; ++k) acc[k] = 0.f;
     first = false;
   };
-  for (int64_t j = j0; j < j1; ++j) {
-    const int64_t id = sid[j];
-    if (id != cur) {  // wave-uniform: every lane reads the same sorted position
-      flush(false);
-      cur = id;
-    }
-    const int64_t tok = perm[j];
-    const int64_t base = tok * E;
-    const float a = (d_xt16 || d_xt32) ? (mask[tok] != 0 ? sa[t[tok / L]] : 1.f) : 0.f;
+  for (int b = 0; b < n; b += TB) {
+    float g[TB][CPL];
 #pragma unroll
-    for (int k = 0; k < CPL; ++k) {
-      const int64_t o = base + lane + 64 * k;
-      float g = 0.f;
-      if (d_xs) g = d_xs[o];
-      if (d_xs16) g += bf2f(d_xs16[o]);
-      if (d_xt16) g += a * bf2f(d_xt16[o]);
-      else if (d_xt32) g += a * d_xt32[o];
-      acc[k] += g;
+    for (int u = 0; u < TB; ++u) {  // every row of the batch in flight (clamped index past n)
+      const int jj = b + u < n ? b + u : n - 1;
+      const int64_t base = readlane64(my_tok, jj) * E;
+      const float a = readlanef(my_a, jj);
+#pragma unroll
+      for (int k = 0; k < CPL; ++k) {
+        const int64_t o = base + lane + 64 * k;
+        float v = 0.f;
+        if (d_xs) v = d_xs[o];
+        if (d_xs16) v += bf2f(d_xs16[o]);
+        if (d_xt16) v += a * bf2f(d_xt16[o]);
+        else if (d_xt32) v += a * d_xt32[o];
+        g[u][k] = v;
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < TB; ++u) {
+      if (b + u < n) {
+        const int64_t id = readlane64(my_id, b + u);
+        if (id != cur) {  // wave-uniform
+          flush(false);
+          cur = id;
+        }
+#pragma unroll
+        for (int k = 0; k < CPL; ++k) acc[k] += g[u][k];
+      }
     }
   }
   flush(true);
 }
 
-// The runs that cross chunk boundaries: the chunk where such a run starts (its slot-1 piece) adds
-// the slot-0 pieces of the chunks it continues into, in chunk order, and writes dW once.
+// Runs crossing chunk boundaries are combined in two fixed-order levels so a run of tens of
+// thousands of tokens (the padding id) is not one wave's serial walk: chunks are grouped by
+// EMB_G; emb_grad_group_kernel sums, per group that starts inside a run, the continuation pieces
+// (slot 0) of the group's chunks that belong to that run; emb_grad_fixup_kernel then has the
+// run's starting chunk add its head piece, the continuation pieces up to its group's end, and
+// the group sums of the groups the run covers, in order, and write dW once.
+constexpr int EMB_G = 64;
+
+// sum_{k < n} src[k * stride + lane + 64 kk] in k order, U rows in flight
+template <int CPL>
+__device__ __forceinline__ void emb_sum_rows(float (&acc)[CPL], const float* __restrict__ src, int64_t stride,
+                                             int n, int lane) {
+  constexpr int U = CPL <= 4 ? 8 : CPL <= 16 ? 2 : 1;
+  for (int k0 = 0; k0 < n; k0 += U) {
+    float v[U][CPL];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int k = k0 + u < n ? k0 + u : n - 1;
+#pragma unroll
+      for (int kk = 0; kk < CPL; ++kk) v[u][kk] = src[k * stride + lane + 64 * kk];
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u)
+      if (k0 + u < n) {
+#pragma unroll
+        for (int kk = 0; kk < CPL; ++kk) acc[kk] += v[u][kk];
+      }
+  }
+}
+
+template <int CPL>
+__global__ void __launch_bounds__(256) emb_grad_group_kernel(const int64_t* __restrict__ sid, int64_t NT,
+                                                             int chunk, const float* __restrict__ part,
+                                                             float* __restrict__ gsum) {
+  constexpr int E = 64 * CPL;
+  const int lane = threadIdx.x & 63;
+  const int64_t nch = (NT + chunk - 1) / chunk, ng = (nch + EMB_G - 1) / EMB_G;
+  const int64_t g = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (g == 0 || g >= ng) return;
+  const int64_t c0 = g * EMB_G, r = sid[c0 * chunk];
+  if (sid[c0 * chunk - 1] != r) return;  // the group does not start inside a run
+  const int64_t cl = c0 + lane;
+  const bool in = cl < nch && sid[cl * chunk] == r;
+  const uint64_t out = __ballot(!in);
+  const int n = out ? __builtin_ctzll(out) : 64;  // chunks c0 .. c0+n-1 continue the run
+  float acc[CPL];
+#pragma unroll
+  for (int k = 0; k < CPL; ++k) acc[k] = 0.f;
+  emb_sum_rows<CPL>(acc, part + (c0 * 2) * E, 2 * E, n, lane);
+#pragma unroll
+  for (int k = 0; k < CPL; ++k) gsum[g * E + lane + 64 * k] = acc[k];
+}
+
 template <int CPL>
 __global__ void __launch_bounds__(256) emb_grad_fixup_kernel(const int64_t* __restrict__ sid, int64_t NT, int V,
                                                              int chunk, const float* __restrict__ part,
+                                                             const float* __restrict__ gsum,
                                                              float* __restrict__ dW) {
   constexpr int E = 64 * CPL;
   const int lane = threadIdx.x & 63;
-  const int64_t nch = (NT + chunk - 1) / chunk;
+  const int64_t nch = (NT + chunk - 1) / chunk, ng = (nch + EMB_G - 1) / EMB_G;
   const int64_t c = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
   if (c >= nch) return;
   const int64_t j0 = c * chunk, j1 = j0 + chunk < NT ? j0 + chunk : NT;
@@ -208,9 +295,24 @@ __global__ void __launch_bounds__(256) emb_grad_fixup_kernel(const int64_t* __re
   float acc[CPL];
 #pragma unroll
   for (int k = 0; k < CPL; ++k) acc[k] = part[(c * 2 + 1) * E + lane + 64 * k];
-  for (int64_t c2 = c + 1; c2 < nch && sid[c2 * chunk] == r; ++c2)
-#pragma unroll
-    for (int k = 0; k < CPL; ++k) acc[k] += part[(c2 * 2) * E + lane + 64 * k];
+  // continuation pieces up to the end of this chunk's group (< EMB_G <= 64 chunks)
+  const int64_t gend = (c / EMB_G + 1) * EMB_G < nch ? (c / EMB_G + 1) * EMB_G : nch;
+  const int64_t cl = c + 1 + lane;
+  const bool in = cl < gend && sid[cl * chunk] == r;
+  const uint64_t out = __ballot(!in);
+  const int n = out ? __builtin_ctzll(out) : 64;
+  emb_sum_rows<CPL>(acc, part + ((c + 1) * 2) * E, 2 * E, n, lane);
+  if (c + 1 + n == gend && gend < nch) {  // the run reached the group's end: group sums, 64 at a time
+    for (int64_t g2 = gend / EMB_G; g2 < ng;) {
+      const int64_t gl = g2 + lane;
+      const bool gin = gl < ng && sid[gl * EMB_G * chunk] == r;
+      const uint64_t gout = __ballot(!gin);
+      const int m = gout ? __builtin_ctzll(gout) : 64;
+      emb_sum_rows<CPL>(acc, gsum + g2 * E, E, m, lane);
+      if (m < 64) break;
+      g2 += 64;
+    }
+  }
   if (r < 0 || r >= V) return;
 #pragma unroll
   for (int k = 0; k < CPL; ++k) dW[r * E + lane + 64 * k] += acc[k];
@@ -224,8 +326,32 @@ static int emb_chunk(int64_t NT, bool qsample) {
   const int64_t chunk = NT / 8192;
   return (int)(chunk < 1 ? 1 : chunk > 16 ? 16 : chunk);
 }
+static int64_t emb_groups(int64_t NT, bool qsample) {
+  const int64_t nch = (NT + emb_chunk(NT, qsample) - 1) / emb_chunk(NT, qsample);
+  return (nch + EMB_G - 1) / EMB_G;
+}
+// part = [nch][2][E] chunk pieces, then [ngroups][E] group sums
 int64_t emb_grad_part_floats(int64_t NT, int E, bool qsample) {
-  return ((NT + emb_chunk(NT, qsample) - 1) / emb_chunk(NT, qsample)) * 2 * (int64_t)E;
+  const int64_t nch = (NT + emb_chunk(NT, qsample) - 1) / emb_chunk(NT, qsample);
+  return (nch * 2 + emb_groups(NT, qsample)) * (int64_t)E;
+}
+
+template <int CPL>
+static void launch_emb_sorted(const int64_t* sid, const int64_t* perm, const int64_t* mask, const int64_t* t,
+                              const float* sa, const float* d_xs, const bf16_t* d_xs16, const bf16_t* d_xt16,
+                              const float* d_xt32, int64_t NT, int L, int V, float* dW, int chunk, float* part,
+                              int64_t ng, hipStream_t s) {
+  constexpr int E = 64 * CPL;
+  const int64_t nch = (NT + chunk - 1) / chunk;
+  float* gsum = part + nch * 2 * E;
+  const unsigned grid = (unsigned)((nch + 3) / 4);
+  hipLaunchKernelGGL(emb_grad_sorted_kernel<CPL>, dim3(grid), dim3(256), 0, s, sid, perm, mask, t, sa, d_xs,
+                     d_xs16, d_xt16, d_xt32, NT, L, V, dW, chunk, part);
+  if (ng > 1)
+    hipLaunchKernelGGL(emb_grad_group_kernel<CPL>, dim3((unsigned)((ng + 3) / 4)), dim3(256), 0, s, sid, NT, chunk,
+                       (const float*)part, gsum);
+  hipLaunchKernelGGL(emb_grad_fixup_kernel<CPL>, dim3(grid), dim3(256), 0, s, sid, NT, V, chunk,
+                     (const float*)part, (const float*)gsum, dW);
 }
 
 // One workgroup per sample: reductions over the sample's L*E elements.
@@ -370,19 +496,13 @@ bool launch_emb_qsample_bwd(const int64_t* ids, const int64_t* mask, const int64
   if (L <= 0 || E <= 0) return false;
   if (sorted_ids && perm && part && (E == 128 || E == 256)) {
     const int CHUNK = emb_chunk(NT, true);
-    const int64_t waves = (NT + CHUNK - 1) / CHUNK;
-    const unsigned grid = (unsigned)((waves + 3) / 4);
-    if (E == 128) {
-      hipLaunchKernelGGL(emb_grad_sorted_kernel<2>, dim3(grid), dim3(256), 0, s, sorted_ids, perm, mask, t, sa,
-                         d_xs, (const bf16_t*)d_xs16, (const bf16_t*)d_xt16, d_xt32, NT, L, V, dW, CHUNK, part);
-      hipLaunchKernelGGL(emb_grad_fixup_kernel<2>, dim3(grid), dim3(256), 0, s, sorted_ids, NT, V, CHUNK,
-                         (const float*)part, dW);
-    } else {
-      hipLaunchKernelGGL(emb_grad_sorted_kernel<4>, dim3(grid), dim3(256), 0, s, sorted_ids, perm, mask, t, sa,
-                         d_xs, (const bf16_t*)d_xs16, (const bf16_t*)d_xt16, d_xt32, NT, L, V, dW, CHUNK, part);
-      hipLaunchKernelGGL(emb_grad_fixup_kernel<4>, dim3(grid), dim3(256), 0, s, sorted_ids, NT, V, CHUNK,
-                         (const float*)part, dW);
-    }
+    const int64_t ng = emb_groups(NT, true);
+    if (E == 128)
+      launch_emb_sorted<2>(sorted_ids, perm, mask, t, sa, d_xs, (const bf16_t*)d_xs16, (const bf16_t*)d_xt16, d_xt32,
+                           NT, L, V, dW, CHUNK, part, ng, s);
+    else
+      launch_emb_sorted<4>(sorted_ids, perm, mask, t, sa, d_xs, (const bf16_t*)d_xs16, (const bf16_t*)d_xt16, d_xt32,
+                           NT, L, V, dW, CHUNK, part, ng, s);
     return true;
   }
   hipLaunchKernelGGL(emb_qsample_bwd_kernel, dim3(grid_cap(NT * E, 256 * 16)), dim3(256), 0, s, ids,
@@ -396,21 +516,19 @@ bool launch_emb_qsample_bwd(const int64_t* ids, const int64_t* mask, const int64
 bool launch_emb_grad(const int64_t* sorted_ids, const int64_t* perm, const float* dy32, const uint16_t* dy16,
                      int64_t NT, int E, int V, float* dW, float* part, hipStream_t s) {
   const int CHUNK = emb_chunk(NT, false);
-  const unsigned grid = (unsigned)(((NT + CHUNK - 1) / CHUNK + 3) / 4);
-  auto go = [&](auto kern, auto fix) {
-    hipLaunchKernelGGL(kern, dim3(grid), dim3(256), 0, s, sorted_ids, perm, (const int64_t*)nullptr,
-                       (const int64_t*)nullptr, (const float*)nullptr, dy32, (const bf16_t*)dy16,
-                       (const bf16_t*)nullptr, (const float*)nullptr, NT, 1, V, dW, CHUNK, part);
-    hipLaunchKernelGGL(fix, dim3(grid), dim3(256), 0, s, sorted_ids, NT, V, CHUNK, (const float*)part, dW);
-  };
+  const int64_t ng = emb_groups(NT, false);
+#define DPA_EMB_GO(CPL)                                                                                      \
+  launch_emb_sorted<CPL>(sorted_ids, perm, nullptr, nullptr, nullptr, dy32, (const bf16_t*)dy16, nullptr, nullptr, \
+                         NT, 1, V, dW, CHUNK, part, ng, s)
   switch (E) {
-    case 128: go(emb_grad_sorted_kernel<2>, emb_grad_fixup_kernel<2>); return true;
-    case 256: go(emb_grad_sorted_kernel<4>, emb_grad_fixup_kernel<4>); return true;
-    case 768: go(emb_grad_sorted_kernel<12>, emb_grad_fixup_kernel<12>); return true;
-    case 1024: go(emb_grad_sorted_kernel<16>, emb_grad_fixup_kernel<16>); return true;
-    case 2048: go(emb_grad_sorted_kernel<32>, emb_grad_fixup_kernel<32>); return true;
+    case 128: DPA_EMB_GO(2); return true;
+    case 256: DPA_EMB_GO(4); return true;
+    case 768: DPA_EMB_GO(12); return true;
+    case 1024: DPA_EMB_GO(16); return true;
+    case 2048: DPA_EMB_GO(32); return true;
     default: return false;
   }
+#undef DPA_EMB_GO
 }
 
 bool launch_diff_loss_fwd(const float* x_start, const void* out, bool out_bf16, const int64_t* ids,
