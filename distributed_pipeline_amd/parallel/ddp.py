@@ -703,6 +703,8 @@ class DDPEngine(nn.Module):
             raise RuntimeError(msg)
         warnings.warn(msg, RuntimeWarning, stacklevel=3)
 
+    ORDER_SLACK = 8  # hook firings (see _check_bucket_order)
+
     def _check_bucket_order(self):
         """First armed step: buckets are launched in layout order, so a bucket whose last
         gradient completes after a later bucket's holds that one back (no overlap for it).  Warn
@@ -716,7 +718,10 @@ class DDPEngine(nn.Module):
         for b in self.buckets:
             ks = [pos.get(idx[id(p)], -1) for p in b.params]
             done.append(max(ks))
-        held = [b for b in range(len(done) - 1) if done[b] > min(done[b + 1:])]
+        # a later bucket completing a few hook firings earlier is one fused backward op returning
+        # several parameters' gradients at once (their hooks fire back to back in an order autograd
+        # picks): no real hold-back.  Only a completion more than ORDER_SLACK firings late is.
+        held = [b for b in range(len(done) - 1) if done[b] > min(done[b + 1:]) + self.ORDER_SLACK]
         self.bucket_order_report = {"bucket_completion_rank": done, "held_back_by": held}
         if held:
             names = {id(p): n for n, p in self.module.named_parameters()}

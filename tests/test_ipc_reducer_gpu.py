@@ -4,8 +4,9 @@ gradient bucket is all-reduced by csrc/ipc_allreduce.hip over the peer's IPC-map
 buffer and flag words, launched from the autograd hooks on the reducer's comm stream while the
 backward still runs (``BucketReducer::init_ipc_only``: the direct mode's stream and events
 without an RCCL communicator, which refuses two ranks per GPU).  Over three steps the epochs
-alternate the staging parity; the 0.25 MiB first bucket takes the one-shot kernel and the
-1 MiB buckets the two-shot one.  The reduced gradient must equal the sum of both ranks' local
+alternate the staging parity; the first bucket (output_down_proj's last Linear, first in the
+model's gradient-ready layout: 0.13 MiB) takes the one-shot kernel and the 1 MiB buckets the
+two-shot one.  The reduced gradient must equal the sum of both ranks' local
 (no_sync) gradients.
 
 Reference: /root/reference/utils/trainer.py:216-220 (DDP's bucketed all-reduce of the
@@ -36,7 +37,7 @@ def _worker(rank, world, port, q):
         from distributed_pipeline_amd.parallel.ddp import DDPEngine
         torch.manual_seed(1234)
         model = build_model(**CFG).cuda()
-        eng = DDPEngine(model, shadow_dtype=torch.bfloat16, bucket_cap_mb=1.0, first_bucket_mb=0.25)
+        eng = DDPEngine(model, shadow_dtype=torch.bfloat16, bucket_cap_mb=1.0, first_bucket_mb=0.1)
         assert eng._native is not None and eng._native.ipc_ready(), "IPC data plane not set up"
         assert not eng._native.direct()  # no RCCL communicator: IPC only
         diff = create_gaussian_diffusion(steps=100)

@@ -55,8 +55,7 @@ def main():
         gb_b = (qkv.numel() * 2 + out.numel() * 2) * 2 / 1e9
         fl = 4.0 * B * H * L * L * D * (0.5 if c else 1.0)   # QK^T + PV
         print(json.dumps({"B": B, "H": H, "L": L, "D": D, "causal": c, "p": p,
-                          "twopass": os.environ.get("DPA_ATTN_TWOPASS", "0"),
-                          "fwd_TF": round(fl / f / 1e9, 1), "bwd_TF": round(2.5 * fl / b / 1e9, 1), "attn128": os.environ.get("DPA_ATTN128", "1"),
+                          "fwd_TF": round(fl / f / 1e9, 1), "bwd_TF": round(2.5 * fl / b / 1e9, 1),
                           "fwd_ms": round(f, 3), "fwd_GBps": round(gb_f / f * 1e3, 1),
                           "bwd_ms": round(b, 3), "bwd_GBps": round(gb_b / b * 1e3, 1),
                           "bwd_with_bias_colsum_ms": round(bdb, 3),
