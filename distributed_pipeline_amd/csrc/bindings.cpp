@@ -2,6 +2,7 @@
 // Every op launches on the *current* HIP stream of the tensor's device, so it
 // composes with torch's stream semantics and with HIP-graph capture.
 #include <cstdlib>
+#include <cstring>
 #include <torch/extension.h>
 #include <ATen/hip/impl/HIPStreamMasqueradingAsCUDA.h>
 #include <c10/core/DeviceGuard.h>
@@ -860,6 +861,60 @@ static bool gemm_wgrad_multi(const std::vector<at::Tensor>& dys, const std::vect
                                          cur_stream(), wsn ? ws.data_ptr<float>() : nullptr);
 }
 
+// Grouped weight gradients (one launch per deferral flush): site i adds sum_s dys[i][s]^T xs[i][s]
+// into dWs[i] (+ column sums of the dy segments into dbs[i] when defined).  False (nothing
+// launched) when a site does not tile; the caller then runs the sites one by one.  The site table
+// goes to the device through a pinned staging copy on the current stream.
+static bool gemm_wgrad_grouped(const std::vector<std::vector<at::Tensor>>& dys,
+                               const std::vector<std::vector<at::Tensor>>& xs, const std::vector<at::Tensor>& dWs,
+                               const std::vector<c10::optional<at::Tensor>>& dbs) {
+  const size_t ns = dys.size();
+  TORCH_CHECK(ns > 0 && xs.size() == ns && dWs.size() == ns && dbs.size() == ns, "gemm_wgrad_grouped: site lists");
+  std::vector<dpa::WgGroupSite> sites(ns);
+  for (size_t i = 0; i < ns; ++i) {
+    const auto& d = dys[i];
+    const auto& x = xs[i];
+    const at::Tensor& dW = dWs[i];
+    TORCH_CHECK(!d.empty() && d.size() == x.size(), "gemm_wgrad_grouped: segment lists of site ", i);
+    if (d.size() > 8) return false;
+    CHECK_F32(dW); CHECK_CONTIG(dW);
+    const int64_t T = d[0].size(0), M = d[0].size(1), N = x[0].size(1);
+    TORCH_CHECK(dW.dim() == 2 && dW.size(0) == M && dW.size(1) == N, "gemm_wgrad_grouped: dW shape of site ", i);
+    dpa::WgGroupSite& s = sites[i];
+    s = dpa::WgGroupSite{};
+    for (size_t k = 0; k < d.size(); ++k) {
+      CHECK_DEV(d[k]); CHECK_BF16(d[k]); CHECK_BF16(x[k]); CHECK_CONTIG(d[k]); CHECK_CONTIG(x[k]);
+      TORCH_CHECK(d[k].dim() == 2 && x[k].dim() == 2 && d[k].size(0) == T && d[k].size(1) == M &&
+                  x[k].size(0) == T && x[k].size(1) == N, "gemm_wgrad_grouped: segment shapes of site ", i);
+      TORCH_CHECK(d[k].device() == dWs[0].device() && x[k].device() == dWs[0].device() &&
+                  dW.device() == dWs[0].device(), "gemm_wgrad_grouped: devices");
+      s.a[k] = bf_ptr(d[k]);
+      s.b[k] = bf_ptr(x[k]);
+    }
+    if (T % 128 || T > (int64_t)INT32_MAX) return false;
+    s.dW = dW.data_ptr<float>();
+    if (dbs[i].has_value() && dbs[i]->defined()) {
+      CHECK_F32((*dbs[i])); CHECK_CONTIG((*dbs[i]));
+      TORCH_CHECK(dbs[i]->numel() == M, "gemm_wgrad_grouped: db size of site ", i);
+      s.colsum = dbs[i]->data_ptr<float>();
+    }
+    s.nseg = (int)d.size();
+    s.M = (int)M;
+    s.N = (int)N;
+    s.ktiles = (int)(T / 64);
+  }
+  const int ntiles = dpa::wgrad_group_prepare(sites.data(), (int)ns);
+  if (ntiles <= 0) return false;
+  const c10::DeviceGuard guard(dWs[0].device());
+  const int64_t bytes = (int64_t)(ns * sizeof(dpa::WgGroupSite));
+  at::Tensor host = at::empty({bytes}, at::TensorOptions().dtype(at::kByte).pinned_memory(true));
+  std::memcpy(host.data_ptr(), sites.data(), (size_t)bytes);
+  at::Tensor dev = at::empty({bytes}, dWs[0].options().dtype(at::kByte));
+  dev.copy_(host, /*non_blocking=*/true);
+  return dpa::launch_wgrad_group(reinterpret_cast<const dpa::WgGroupSite*>(dev.data_ptr()), (int)ns, ntiles,
+                                 cur_stream());
+}
+
 // ---- row softmax cross-entropy (chunked wide-E linear-CE) ------------------------------
 static void check_i64(const at::Tensor& t, const char* name) {
   TORCH_CHECK(t.is_cuda() && t.scalar_type() == at::kLong && t.is_contiguous(), name,
@@ -1157,6 +1212,9 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("gemm_wgrad", &gemm_wgrad, "dW += dy^T x, db += colsum(dy) (fp32 atomics, split-K)");
   m.def("gemm_wgrad_multi", &gemm_wgrad_multi, "dW += sum_s dy_s^T x_s over equal token segments, one launch",
         py::arg("dys"), py::arg("xs"), py::arg("dW"), py::arg("db") = py::none());
+  m.def("gemm_wgrad_grouped", &gemm_wgrad_grouped,
+        "dW_i += sum_s dy_is^T x_is for several Linears in one launch (no token split); false if a site does not tile",
+        py::arg("dys"), py::arg("xs"), py::arg("dWs"), py::arg("dbs"));
   m.def("gemm_supported", &gemm_supported, "shape check for the native GEMMs");
   m.def("set_gemm256", &dpa::set_gemm256, "enable/disable the 256x256 8-phase GEMM path");
   m.def("set_gemmp_grid_cap", &dpa::set_gemmp_grid_cap, "cap the persistent GEMM grid (0 = #CUs)");

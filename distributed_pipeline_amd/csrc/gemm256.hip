@@ -533,6 +533,124 @@ __global__ void __launch_bounds__(512) gemm256_kernel(
   }
 }
 
+// ---- grouped weight gradient (one launch per deferral flush) -----------------
+// The reference schedule's deferred weight gradients (ops/nn.py _WgradDeferral) of EVERY Linear
+// of a flush in one launch: the sites together have ~1300 256 x 256 tiles, ~5 rounds of the 256
+// CUs, so no tile is split over the tokens.  Workgroup = one tile of one site; it walks all of
+// the site's token segments (a prologue + 8-phase main loop each) with its accumulators live and
+// adds the tile into dW with a plain read-add-write: one writer per element, no split-K slabs,
+// no reduce pass, deterministic.  The site table lives in device memory (uniform scalar loads).
+__global__ void __launch_bounds__(512) wgrad_group_kernel(const WgGroupSite* __restrict__ sites, int nsites,
+                                                          int ntiles) {
+  static_assert(WG_MAXSEG == 8, "WgGroupSite holds 8 segments");
+  __shared__ __attribute__((aligned(1024))) char smem[2 * B_REGION];
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int wm = (w >> 2) & 1, wn = w & 3;
+  const int grp = __builtin_amdgcn_readfirstlane(w >> 2);
+  const int tile = xcd_remap(blockIdx.x, ntiles);
+  int si = 0;
+  for (int i = 1; i < nsites; ++i)
+    if (sites[i].tile0 <= tile) si = i;
+  const WgGroupSite* st = sites + si;
+  const int M = st->M, N = st->N, nseg = st->nseg, ktiles = st->ktiles;
+  float* const dW = st->dW;
+  float* const colsum = st->colsum;
+  const int local = tile - st->tile0, NT = N / 256;
+  const int mt = local / NT, nt = local - mt * NT;
+  const int m0 = mt * 256, n0 = nt * 256;
+  const bool do_cs = colsum != nullptr && nt == 0;
+  float cs = 0.f;
+
+  f32x4 acc[2][2][4][2];
+#pragma unroll
+  for (int a = 0; a < 2; ++a)
+#pragma unroll
+    for (int b = 0; b < 2; ++b)
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j) acc[a][b][i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  bf16x8 fa[4][2], fb0[2][2], fb1[2][2];
+  const uint32_t sbase = lds_u32(smem);
+  uint32_t csa[2];
+  {
+    const int t = tid & 255, q = (lane & 15) >> 2, p = lane & 3;
+#pragma unroll
+    for (int b3 = 0; b3 < 2; ++b3) {
+      const int row = q + 8 * b3;
+      const int ch = (2 * ((t >> 4) & 7) + (p >> 1)) ^ tr_x(row);
+      csa[b3] = sbase + (uint32_t)((32 * (t >> 7) + q) * 256 + ch * 16 + (p & 1) * 8);
+    }
+  }
+  char* const smB = smem + B_REGION;
+  const int niter = ktiles >> 1;
+  for (int sg = 0; sg < nseg; ++sg) {
+    Operand<true> opA;
+    Operand<true> opB;
+    opA.init((const bf16_t*)st->a[sg], M, m0, w, lane, wm, 64, sbase);
+    opB.init((const bf16_t*)st->b[sg], N, n0, w, lane, wn, 32, sbase + B_REGION);
+    opA.stage(smem + img_off(0, 0), 0, 0);
+    opB.stage(smB + img_off(0, 0), 0, 0);
+    opB.stage(smB + img_off(0, 1), 1, 0);
+    opA.stage(smem + img_off(0, 1), 1, 0);
+    opA.stage(smem + img_off(1, 0), 0, 1);
+    opB.stage(smB + img_off(1, 0), 0, 1);
+    asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+    barrier();
+    if (grp == 1) barrier();
+    for (int it = 0; it < niter; ++it) {
+      const int te = 2 * it;
+      const bool more = it + 1 < niter;
+      phase<0, true, true, true>(acc, fa, fb0, fb1, cs, opA, opB, smem, csa, te, more, do_cs, grp);
+      phase<1, true, true, true>(acc, fa, fb0, fb1, cs, opA, opB, smem, csa, te, more, do_cs, grp);
+      phase<2, true, true, true>(acc, fa, fb0, fb1, cs, opA, opB, smem, csa, te, more, do_cs, grp);
+      phase<3, true, true, true>(acc, fa, fb0, fb1, cs, opA, opB, smem, csa, te, more, do_cs, grp);
+      phase<4, true, true, true>(acc, fa, fb0, fb1, cs, opA, opB, smem, csa, te, more, do_cs, grp);
+      phase<5, true, true, true>(acc, fa, fb0, fb1, cs, opA, opB, smem, csa, te, more, do_cs, grp);
+      phase<6, true, true, true>(acc, fa, fb0, fb1, cs, opA, opB, smem, csa, te, more, do_cs, grp);
+      phase<7, true, true, true>(acc, fa, fb0, fb1, cs, opA, opB, smem, csa, te, more, do_cs, grp);
+    }
+    if (grp == 0) barrier();  // re-align the groups; every LDS read of this segment is retired
+  }
+
+  // epilogue: bias column sums (one workgroup per tile row: a single adder per element), then each
+  // 128-row half of the fp32 tile staged in LDS and added into dW with 16-B read-add-writes
+  const int g4 = (lane >> 4) * 4, li = lane & 15;
+  if (do_cs) {
+    float* red = reinterpret_cast<float*>(smem);
+    const int t = tid & 255;
+    red[(t >> 7) * 256 + grp * 128 + (t & 127)] = cs;
+    __syncthreads();
+    if (tid < 256) colsum[m0 + tid] += red[tid] + red[256 + tid];
+  }
+  float* ct = reinterpret_cast<float*>(smem);
+#pragma unroll
+  for (int qa = 0; qa < 2; ++qa) {
+    __syncthreads();
+#pragma unroll
+    for (int qb = 0; qb < 2; ++qb)
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const int row = wm * 64 + i * 16 + g4 + r;
+            const int col = (qb * 128 + wn * 32 + j * 16 + li) ^ ((row & 3) << 4);
+            ct[row * 256 + col] = acc[qa][qb][i][j][r];
+          }
+    __syncthreads();
+    float* dst = dW + (int64_t)(m0 + qa * 128) * N + n0;
+#pragma unroll 4
+    for (int c = 0; c < 16; ++c) {
+      const int idx = tid + c * 512;
+      const int row = idx >> 6, col = (idx & 63) * 4;
+      const f32x4 v = *reinterpret_cast<const f32x4*>(ct + row * 256 + (col ^ ((row & 3) << 4)));
+      f32x4* d = reinterpret_cast<f32x4*>(dst + (int64_t)row * N + col);
+      *d = *d + v;
+    }
+  }
+}
 
 // ---- persistent variant (forward / data-gradient GEMMs) ----------------------
 //
@@ -1531,6 +1649,28 @@ bool launch_gemm256_wgrad_multi(const uint16_t* const* dys, const uint16_t* cons
     hipLaunchKernelGGL(wgrad_reduce_kernel, dim3((unsigned)((n4 + 255) / 256)), dim3(256), 0, s, wsp, dW, n4,
                        p.splits * nseg);
   }
+  return true;
+}
+
+// Tile offsets of a grouped weight-gradient launch; -1 when a site does not tile (256-multiple
+// sides, an even number of 64-token K-tiles per segment, 1..8 segments).
+int wgrad_group_prepare(WgGroupSite* sites, int nsites) {
+  if (!g256_enabled() || nsites < 1) return -1;
+  int total = 0;
+  for (int i = 0; i < nsites; ++i) {
+    WgGroupSite& s = sites[i];
+    if (s.M % 256 || s.N % 256 || s.M <= 0 || s.N <= 0 || s.nseg < 1 || s.nseg > g256::WG_MAXSEG ||
+        s.ktiles < 2 || (s.ktiles & 1) || s.dW == nullptr)
+      return -1;
+    s.tile0 = total;
+    total += (s.M / 256) * (s.N / 256);
+  }
+  return total;
+}
+
+bool launch_wgrad_group(const WgGroupSite* d_sites, int nsites, int ntiles, hipStream_t s) {
+  if (ntiles <= 0 || nsites < 1) return false;
+  hipLaunchKernelGGL(g256::wgrad_group_kernel, dim3((unsigned)ntiles), dim3(512), 0, s, d_sites, nsites, ntiles);
   return true;
 }
 

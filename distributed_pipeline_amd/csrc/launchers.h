@@ -213,9 +213,23 @@ bool launch_gemm256_wgrad(const uint16_t* dy, const uint16_t* x, float* dW, floa
                           int N, int K, hipStream_t s, float* ws = nullptr);
 // fp32 workspace the split-K weight gradient merges through (0: atomics / no split)
 int64_t gemm256_wgrad_workspace_floats(int T, int N, int K, int nseg = 1);
-// dW += sum_s dy_s^T x_s over nseg (<= 4) equal token segments in one split-K launch
+// dW += sum_s dy_s^T x_s over nseg (<= 8) equal token segments in one split-K launch
 bool launch_gemm256_wgrad_multi(const uint16_t* const* dys, const uint16_t* const* xs, int nseg, float* dW,
                                 float* db, int T, int N, int K, hipStream_t s, float* ws);
+// Grouped weight gradient of several Linears (the deferral flush): site i adds
+// sum_s a[s]^T b[s] (a: dy [T][M], b: x [T][N], bf16) into dW [M][N] fp32 (+ colsum[M] += column
+// sums of the dy segments when colsum != null); one workgroup per 256 x 256 tile, no token split.
+// The table is filled on the host (wgrad_group_prepare: tile0, returns the tile total or -1 when a
+// site does not tile) and passed in device memory.
+struct WgGroupSite {
+  const uint16_t* a[8];
+  const uint16_t* b[8];
+  float* dW;
+  float* colsum;
+  int nseg, M, N, ktiles, tile0, pad[3];
+};
+int wgrad_group_prepare(WgGroupSite* sites, int nsites);
+bool launch_wgrad_group(const WgGroupSite* d_sites, int nsites, int ntiles, hipStream_t s);
 // gemm256.hip persistent forward / data-gradient kernels with fused epilogues (false when
 // the shape does not tile).  ncu: compute units (grid = min(tiles, ncu)).
 //   nt: y[T][N] = act(x[T][K] W[N][K]^T + bias); z (nullable) = pre-activation, or act'(it)

@@ -287,7 +287,13 @@ class _WgradDeferral:
     the d segments run as ONE multi-segment split-K launch (each segment split fewer ways, one
     reduce pass): the same sum into the same fp32 gradient, at most d - 1 micro-batches of
     extra operand memory.  ``active`` is set by the trainer around every backward except the
-    last (DDP-armed) one, before which ``flush()`` runs whatever is still held."""
+    last (DDP-armed) one, before which ``flush()`` runs whatever is still held.
+
+    Grouped flushes (``grouped``): the sites that complete their d segments in a backward are not
+    launched one by one (a split-K launch each, whose fp32 partial slabs a reduce pass merges) but
+    together after it (``end_backward``), as ONE grouped kernel over all their 256 x 256 tiles
+    (~1300 for DiffuSeq-base: ~5 rounds of the CUs, so no token split, no slabs, no reduce; each
+    dW element has one writer)."""
 
     def __init__(self):
         self.depth = 0
@@ -299,7 +305,11 @@ class _WgradDeferral:
         # gains nothing from deferral and must not double its memory)
         self.budget_bytes = int(float(os.environ.get("DPA_DEFER_WGRAD_GB", "32")) * (1 << 30))
         self.stats = {"deferred": 0, "multi_launches": 0, "segments": 0, "ln_deferred": 0, "ln_reduces": 0,
-                      "bias_deferred": 0, "bias_reduces": 0, "attn_deferred": 0, "attn_reduces": 0}
+                      "bias_deferred": 0, "bias_reduces": 0, "attn_deferred": 0, "attn_reduces": 0,
+                      "group_launches": 0, "group_sites": 0}
+        # sites whose segments are complete in the current backward: launched together by
+        # end_backward() (or flush()) as ONE grouped weight-gradient kernel
+        self.ready = []
         self.stream = None  # side stream for the un-armed micro-batches' launches (trainer-set)
         self.cur = None     # the stream the current backward runs on (trainer-set, optional)
         self._retired = []  # replaced column-sum buffers (other streams may still use them)
@@ -338,19 +348,33 @@ class _WgradDeferral:
             return self.cur
         return torch.cuda.current_stream(t.device) if t.is_cuda else None
 
-    def _run(self, p, bias, segs, side=False):
-        """Launch the held segments.  ``side``: on ``self.stream`` (ordered after the current
-        stream's work so far) instead of the current stream - the weight gradients of the
-        un-armed micro-batches are off the backward chain's critical path; nothing reads
-        them before the trainer joins that stream ahead of the last backward."""
-        ext = get_ext()
-        gw = p.grad
-        gb = bias.grad if (bias is not None and bias.requires_grad) else None
+    # grouped flushes (one kernel over every complete site, csrc/gemm256.hip wgrad_group_kernel);
+    # False: one split-K launch per site.  A group runs when its sites have at least
+    # group_min_tiles 256 x 256 tiles (None: one per CU; fewer are split-K per site, which fills
+    # the chip by splitting the tokens)
+    grouped = True
+    group_min_tiles = None
+
+    @staticmethod
+    def _gb(bias):
+        return bias.grad if (bias is not None and bias.requires_grad) else None
+
+    def _stream_for(self, segs, side):
+        """(current stream, stream to launch on) - ``side``: ``self.stream``, ordered after the
+        current stream's work so far; the held operands are kept alive for it."""
         cur = self._cur(segs[0][0])
         run_on = cur
         if cur is not None and side and self.stream is not None:
             run_on = self.stream
             run_on.wait_stream(cur)
+        return cur, run_on
+
+    def _run(self, p, bias, segs, side=False):
+        """Launch the held segments.  ``side``: on ``self.stream`` (ordered after the current
+        stream's work so far) instead of the current stream - the weight gradients of the
+        un-armed micro-batches are off the backward chain's critical path; nothing reads
+        them before the trainer joins that stream ahead of the last backward."""
+        cur, run_on = self._stream_for(segs, side)
         if self.check:
             self._verify(p, segs)
         segs = [s[:2] for s in segs]
@@ -359,12 +383,71 @@ class _WgradDeferral:
                 dz.record_stream(run_on)
                 x2.record_stream(run_on)
         with torch.cuda.stream(run_on) if run_on is not None and run_on is not cur else _nullctx():
-            if len(segs) > 1 and ext.gemm_wgrad_multi([s[0] for s in segs], [s[1] for s in segs], gw, gb):
-                self.stats["multi_launches"] += 1
-                self.stats["segments"] += len(segs)
-                return
-            for dz, x2 in segs:
-                ext.gemm_wgrad(dz, x2, gw, gb)
+            self._launch_site(p, bias, segs)
+
+    def _launch_site(self, p, bias, segs):
+        ext = get_ext()
+        gw, gb = p.grad, self._gb(bias)
+        if len(segs) > 1 and ext.gemm_wgrad_multi([s[0] for s in segs], [s[1] for s in segs], gw, gb):
+            self.stats["multi_launches"] += 1
+            self.stats["segments"] += len(segs)
+            return
+        for dz, x2 in segs:
+            ext.gemm_wgrad(dz, x2, gw, gb)
+
+    @staticmethod
+    def _groupable(segs):
+        dz, x2 = segs[0][0], segs[0][1]
+        return (len(segs) <= 8 and dz.shape[1] % 256 == 0 and x2.shape[1] % 256 == 0 and dz.shape[0] % 128 == 0
+                and dz.shape[0] >= 128)
+
+    def _run_group(self, items, side=True):
+        """Every site of ``items`` ((weight, bias, segs, ...)): the ones that tile as ONE grouped
+        launch when together they fill the chip (no token split, no reduce pass), the rest one by
+        one."""
+        if not items:
+            return
+        ext = get_ext()
+        grp, seen = [], set()
+        for it in items:  # one entry per weight: two sites adding into one dW must not share a launch
+            if self.grouped and it[2][0][0].is_cuda and self._groupable(it[2]) and id(it[0]) not in seen:
+                grp.append(it)
+                seen.add(id(it[0]))
+        if grp and hasattr(ext, "gemm_wgrad_grouped"):
+            tiles = sum((it[2][0][0].shape[1] // 256) * (it[2][0][1].shape[1] // 256) for it in grp)
+            dev = grp[0][2][0][0].device
+            ncu = torch.cuda.get_device_properties(dev).multi_processor_count if dev.type == "cuda" else 1
+            if len(grp) > 1 and tiles >= (ncu if self.group_min_tiles is None else self.group_min_tiles):
+                cur, run_on = self._stream_for(grp[0][2], side)
+                for p, _b, segs, *_ in grp:
+                    if self.check:
+                        self._verify(p, segs)
+                    if run_on is not None:
+                        for s in segs:
+                            s[0].record_stream(run_on)
+                            s[1].record_stream(run_on)
+                with torch.cuda.stream(run_on) if run_on is not None and run_on is not cur else _nullctx():
+                    ok = ext.gemm_wgrad_grouped([[s[0] for s in it[2]] for it in grp],
+                                                [[s[1] for s in it[2]] for it in grp],
+                                                [it[0].grad for it in grp], [self._gb(it[1]) for it in grp])
+                    if ok:
+                        self.stats["group_launches"] += 1
+                        self.stats["group_sites"] += len(grp)
+                        self.stats["segments"] += sum(len(it[2]) for it in grp)
+                    else:
+                        for p, b, segs, *_ in grp:
+                            self._launch_site(p, b, [s[:2] for s in segs])
+                done = {id(it) for it in grp}
+                items = [it for it in items if id(it) not in done]
+        for p, b, segs, *_ in items:
+            self._run(p, b, segs, side=side)
+
+    def end_backward(self):
+        """Launch the sites that completed their segments in this backward, grouped."""
+        items, self.ready = self.ready, []
+        for it in items:
+            self.held_bytes -= it[3]
+        self._run_group(items, side=True)
 
     def offer(self, p, dz, x2, bias, gw, gb):
         """True when the weight gradient was deferred or run here (grads preallocated)."""
@@ -388,6 +471,11 @@ class _WgradDeferral:
             self.held_bytes += nb
             self.stats["deferred"] += 1
             return True
+        if (self.active and self.grouped and len(segs) >= self.depth
+                and self.held_bytes + nb <= self.budget_bytes):  # complete: launched with the others by end_backward()
+            self.ready.append((p, bias, segs, nb))
+            self.held_bytes += nb
+            return True
         self._run(p, bias, segs, side=self.active)
         return True
 
@@ -395,9 +483,9 @@ class _WgradDeferral:
         """Run every held weight gradient (on the side stream when set) and every deferred
         column-sum reduction (on the current stream)."""
         pend, self.pending = self.pending, {}
+        ready, self.ready = self.ready, []
         self.held_bytes = 0
-        for p, bias, segs, _ in pend.values():
-            self._run(p, bias, segs, side=True)
+        self._run_group(ready + list(pend.values()), side=True)
         for e in self.ln_sites.values():
             self._ln_reduce(e)
         for e in self.bias_sites.values():
@@ -418,6 +506,7 @@ class _WgradDeferral:
     def drop(self):
         """Forget held operands (an abandoned backward whose gradients are discarded)."""
         self.pending = {}
+        self.ready = []
         self.held_bytes = 0
         self.active = False
         for e in self.ln_sites.values():

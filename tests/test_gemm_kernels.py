@@ -349,3 +349,49 @@ def test_gemm_wgrad_multi_segment_no_bias(T, N, K, nseg):
     finally:
         _ext().set_wgrad4w(False)
     _close(dW, ref, 1e-3)
+
+
+@pytest.mark.parametrize("with_bias", [False, True])
+def test_gemm_wgrad_grouped(with_bias):
+    """One grouped launch over several Linears' deferred segments (csrc/gemm256.hip
+    wgrad_group_kernel): each dW (and bias column sum) == its fp32 sum of dy_s^T x_s, added onto
+    the existing gradient; sites of different shapes and segment counts in one launch."""
+    torch.manual_seed(3)
+    shapes = [(256, 768, 768, 3), (256, 2304, 768, 1), (512, 768, 3072, 8), (128, 256, 512, 2)]
+    dys, xs, dWs, dbs, refs, refbs = [], [], [], [], [], []
+    for T, N, K, nseg in shapes:
+        d = [torch.randn(T, N, device="cuda").bfloat16() for _ in range(nseg)]
+        x = [torch.randn(T, K, device="cuda").bfloat16() for _ in range(nseg)]
+        dW = torch.randn(N, K, device="cuda")
+        db = torch.randn(N, device="cuda") if with_bias else None
+        ref = dW.clone()
+        refb = db.clone() if with_bias else None
+        for a, b in zip(d, x):
+            ref += a.float().t() @ b.float()
+            if with_bias:
+                refb += a.float().sum(0)
+        dys.append(d); xs.append(x); dWs.append(dW); dbs.append(db); refs.append(ref); refbs.append(refb)
+    assert _ext().gemm_wgrad_grouped(dys, xs, dWs, dbs)
+    for dW, ref, db, refb in zip(dWs, refs, dbs, refbs):
+        _close(dW, ref, 1e-3)
+        if with_bias:
+            _close(db, refb, 1e-3)
+
+
+def test_gemm_wgrad_grouped_declines_untileable_and_is_deterministic():
+    """A site with a 128-wide side declines the whole group (nothing launched); a valid group
+    gives the same bits twice (one writer per element)."""
+    torch.manual_seed(4)
+    d = [torch.randn(256, 128, device="cuda").bfloat16()]
+    x = [torch.randn(256, 768, device="cuda").bfloat16()]
+    dW = torch.zeros(128, 768, device="cuda")
+    assert not _ext().gemm_wgrad_grouped([d], [x], [dW], [None])
+    assert dW.abs().max().item() == 0
+    d = [torch.randn(1024, 768, device="cuda").bfloat16() for _ in range(4)]
+    x = [torch.randn(1024, 3072, device="cuda").bfloat16() for _ in range(4)]
+    outs = []
+    for _ in range(2):
+        dW = torch.zeros(768, 3072, device="cuda")
+        assert _ext().gemm_wgrad_grouped([d], [x], [dW], [None])
+        outs.append(dW)
+    assert torch.equal(outs[0], outs[1])

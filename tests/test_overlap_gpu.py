@@ -114,3 +114,24 @@ def test_overlapped_schedule_half_tile_modes(mode, monkeypatch):
     scale = g0.abs().max().item()
     err = (g0 - g1).abs().max().item()
     assert err <= max(4 * noise, 1e-6 * scale), (err, noise, scale)
+
+
+@pytest.mark.parametrize("overlap", [True, False])
+def test_grouped_flush_matches_sequential(overlap, monkeypatch):
+    """Grouped deferral flushes (ops/nn.py _WgradDeferral.grouped, csrc/gemm256.hip
+    wgrad_group_kernel): every site that completes its segments in a backward runs in ONE launch
+    (one workgroup per 256 x 256 tile over all its segments, no token split).  The tiny model has
+    too few tiles to group by default, so the threshold is lowered; the gradients must match the
+    sequential loop's within fp32 rounding and the grouped launch must have run."""
+    from distributed_pipeline_amd.ops.nn import WGRAD_DEFER
+    monkeypatch.setattr(type(WGRAD_DEFER), "group_min_tiles", 1)
+    g0, _, _ = _loop(False, steps=1)
+    before = dict(WGRAD_DEFER.stats)
+    g1, _, _ = _loop(overlap, defer=2, steps=1)
+    assert WGRAD_DEFER.stats["group_launches"] > before["group_launches"]
+    assert WGRAD_DEFER.stats["group_sites"] - before["group_sites"] >= 2 * (WGRAD_DEFER.stats["group_launches"]
+                                                                        - before["group_launches"])
+    assert not WGRAD_DEFER.pending and not WGRAD_DEFER.ready
+    scale = g0.abs().max().item()
+    err = (g0 - g1).abs().max().item()
+    assert err <= 2e-5 * scale, (err, scale)

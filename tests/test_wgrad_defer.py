@@ -53,6 +53,8 @@ def test_deferral_pairs_flushes_and_matches(monkeypatch):
         else:
             d.active = True
         assert d.offer(w, dz, x2, b, w.grad, b.grad)
+        if d.active:
+            d.end_backward()  # the trainer's call after every deferred backward
     assert fake.calls == [2, 2, 1], fake.calls
     assert not d.pending
     torch.testing.assert_close(w.grad, ref_w)
@@ -106,3 +108,20 @@ def test_deferral_respects_the_memory_budget(monkeypatch):
     # w1's second segment would need twice the budget: both run now as one launch
     assert d.offer(w1, torch.ones(16, 8).bfloat16(), torch.ones(16, 4).bfloat16(), None, w1.grad, None)
     assert fake.calls == [1, 2] and d.held_bytes == 0 and not d.pending
+
+
+def test_grouped_flush_collects_complete_sites_once_per_weight(monkeypatch):
+    """Sites that complete their segments wait in ``ready`` until end_backward(); a weight that
+    completed twice before it (no end_backward between) is never put in one grouped launch twice."""
+    fake = _FakeExt()
+    monkeypatch.setattr(nn_ops, "get_ext", lambda *a, **k: fake)
+    d = nn_ops._WgradDeferral()
+    d.depth = 2
+    w = _param((8, 4))
+    d.active = True
+    for _ in range(4):
+        assert d.offer(w, torch.ones(16, 8).bfloat16(), torch.ones(16, 4).bfloat16(), None, w.grad, None)
+    assert fake.calls == [] and len(d.ready) == 2 and not d.pending
+    d.end_backward()  # CPU tensors: not groupable, one multi-segment call per entry
+    assert fake.calls == [2, 2] and not d.ready and d.held_bytes == 0
+    torch.testing.assert_close(w.grad, torch.full((8, 4), 64.0))

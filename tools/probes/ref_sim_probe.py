@@ -111,6 +111,8 @@ def main():
     print(f"sim={a.sim} comm={a.comm}: {(time.perf_counter() - t) / a.steps * 1e3:.2f} ms/step (host enqueue "
           f"{host / a.steps * 1e3:.2f} ms/step); engine host ms/step: "
           + ", ".join(f"{k} {v / a.steps * 1e3:.2f}" for k, v in sorted(acc.items())), flush=True)
+    from distributed_pipeline_amd.ops.nn import WGRAD_DEFER
+    print("weight-gradient deferral:", WGRAD_DEFER.stats, flush=True)
 
 
 if __name__ == "__main__":

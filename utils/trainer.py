@@ -759,6 +759,8 @@ class TrainLoop:
                         defer.flush()
                 with self._range("backward"), self._inplace_grads():
                     self.backward_from_losses(losses)
+                if defer is not None and defer.active:
+                    defer.end_backward()
                 if join is not None:
                     # a side-stream term (the logged nll) overlaps the backward: log after it
                     join()
@@ -934,6 +936,8 @@ class TrainLoop:
                     t0 = time.perf_counter()
                     with self._range("backward"), self._inplace_grads():
                         self.backward_from_losses(losses)
+                    if defer.active:
+                        defer.end_backward()  # this backward's complete sites, one grouped launch
                     self.host_time["bwd"] += time.perf_counter() - t0
                     done = torch.cuda.Event()
                     done.record(st)
