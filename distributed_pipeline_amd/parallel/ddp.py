@@ -787,7 +787,13 @@ class DDPEngine(nn.Module):
         for b in self.buckets:
             b.launched = False
         self._next_launch = 0
-        self.finalize()
+        # no hook fired here by design: this is not the first-backward check of unused
+        # parameters / bucket order (which would flag every parameter and then be spent)
+        track, self._track_unused = self._track_unused, False
+        try:
+            self.finalize()
+        finally:
+            self._track_unused = track
 
     def average_gradients(self):
         if self.world_size > 1:
