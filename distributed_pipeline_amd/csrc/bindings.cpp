@@ -155,8 +155,9 @@ static void emb_grad(const at::Tensor& ids, const at::Tensor& dy, at::Tensor& dW
 // here as dW[t] -= g x_t, db[t] -= g over the valid targets, by the sorted segment-sum scatter
 // of the embedding backward - a compare, subtract and select less per logit in the kernel
 // dw_acc / db_acc: fp32 buffers of W's / b's shape (the parameters' flat .grad views) the kernel
-// accumulates into directly (its split-token partials are fp32 atomics anyway); the matching
-// results are then undefined - no zero-filled scratch and no autograd-side add per call
+// accumulates into directly (its token splits' partials go through a scratch summed in split
+// order); the matching results are then undefined - no zero-filled [V, E] result and no
+// autograd-side add per call
 static std::vector<at::Tensor> lxent_bwd(const at::Tensor& dloss, const at::Tensor& x,
                                          const at::Tensor& W, c10::optional<at::Tensor> b,
                                          const at::Tensor& tgt, const at::Tensor& lse, bool need_dx,
@@ -187,11 +188,14 @@ static std::vector<at::Tensor> lxent_bwd(const at::Tensor& dloss, const at::Tens
     dW = ext_w ? *dw_acc : at::zeros({V, E}, f32);
     if (need_db) db = ext_b ? *db_acc : at::zeros({V}, f32);
     const bool scatter = onehot_scatter && need_dw && (E == 128 || E == 256);
-    if (N > 0)
+    if (N > 0) {
+      const int64_t wsn = dpa::lxent_dw_ws_floats(N, V, E);
+      at::Tensor ws = wsn > 0 ? at::empty({wsn}, f32) : at::Tensor();
       dpa::launch_lxent_dw(bf_ptr(x), bf_ptr(W), opt_bf_ptr(b), tgt.data_ptr<int64_t>(),
                            lse.data_ptr<float>(), dloss.data_ptr<float>(), N, V, E,
                            dW.data_ptr<float>(), need_db ? db.data_ptr<float>() : nullptr,
-                           cur_stream(), !scatter);
+                           cur_stream(), !scatter, wsn > 0 ? ws.data_ptr<float>() : nullptr);
+    }
     if (scatter && N > 0) {
       const at::Tensor valid = tgt.ge(0).logical_and(tgt.lt(V));
       const at::Tensor ng = at::where(valid, dloss.neg(), at::zeros({}, dloss.options()));

@@ -33,7 +33,7 @@ void launch_comm_sim_stats(const unsigned long long* tl, int nb, const unsigned 
 // ---- wgrad4w.hip: one-wave-per-SIMD weight gradient (both operands token-major) ----
 bool launch_wgrad4w(const uint16_t* const* as, const uint16_t* const* bs, int nseg, int T, int M, int N, int splits,
                     int kps, float* dW, float* ws, hipStream_t s);
-void set_wgrad4w(bool on);  // gemm256.hip: route db-free weight gradients to wgrad4w (default on)
+void set_wgrad4w(bool on);  // gemm256.hip: route db-free weight gradients to wgrad4w (default off: measured no faster)
 
 // ---- optim.hip -------------------------------------------------------------
 void launch_sqnorm(const void* g, bool g_bf16, int64_t n, float* partial, int nparts, float scale,
@@ -71,9 +71,12 @@ void launch_lxent_fwd(const uint16_t* x, const uint16_t* W, const uint16_t* b, c
 void launch_lxent_dx(const uint16_t* x, const uint16_t* W, const uint16_t* b, const int64_t* tgt,
                      const float* lse, const float* dloss, int N, int V, int E, uint16_t* dx,
                      float* dx_acc, hipStream_t s);
+// dW (+ db) += the head gradient; ws: lxent_dw_ws_floats(N, V, E) floats of scratch when that is
+// > 0 (the token splits' partials, summed in split order: deterministic)
+int64_t lxent_dw_ws_floats(int N, int V, int E);
 void launch_lxent_dw(const uint16_t* x, const uint16_t* W, const uint16_t* b, const int64_t* tgt,
                      const float* lse, const float* dloss, int N, int V, int E, float* dW, float* db,
-                     hipStream_t s, bool onehot = true);
+                     hipStream_t s, bool onehot, float* ws);
 
 // ---- norm.hip (fused dropout + residual + LayerNorm) ---------------------------
 bool launch_add_ln_fwd(const uint16_t* y, const uint16_t* res, const uint16_t* g, const uint16_t* b,

@@ -495,7 +495,7 @@ template <int E, bool ONEHOT = true>
 __global__ void __launch_bounds__(512) lxent_dw_kernel(
     const bf16_t* __restrict__ x, const bf16_t* __restrict__ W, const bf16_t* __restrict__ bias,
     const int64_t* __restrict__ target, const float* __restrict__ lse, const float* __restrict__ dloss,
-    int N, int V, int t_per_split, float* __restrict__ dW, float* __restrict__ db) {
+    int N, int V, int t_per_split, float* __restrict__ dW, float* __restrict__ db, float* __restrict__ ws) {
   constexpr int KS = E / 16, ROWB = E * 2, KT = E / 32, CH = E / 8;
   __shared__ __attribute__((aligned(16))) char smem[64 * ROWB + 3 * 64 * 4];
   char* xt = smem;
@@ -597,16 +597,37 @@ __global__ void __launch_bounds__(512) lxent_dw_kernel(
     __syncthreads();
   }
   dbs += __shfl_xor(dbs, 32, 64);
-  if (h == 0 && v_ok && db) atomicAdd(db + v, dbs);
+  // ws: this token split's partials, plain stores into slab blockIdx.y ([V][E] then [V] for the
+  // bias), summed in split order by xent_split_reduce_kernel - deterministic.  Without ws (one
+  // token split) the block is the only adder of its rows.
+  float* const pw = ws ? ws + (int64_t)blockIdx.y * V * (E + 1) : nullptr;
+  if (h == 0 && v_ok && db) {
+    if (pw) pw[(int64_t)V * E + v] = dbs;
+    else db[v] += dbs;
+  }
   // dacc[kt] reg i: row = vocab vw + acc_row(i,h), col = k
 #pragma unroll
   for (int kt = 0; kt < KT; ++kt) {
 #pragma unroll
     for (int i = 0; i < 16; ++i) {
       const int vv = vw + acc_row(i, h);
-      if (vv < V) atomicAdd(dW + (int64_t)vv * E + kt * 32 + (lane & 31), dacc[kt][i]);
+      if (vv < V) {
+        const int64_t o = (int64_t)vv * E + kt * 32 + (lane & 31);
+        if (pw) pw[o] = dacc[kt][i];
+        else dW[o] += dacc[kt][i];
+      }
     }
   }
+}
+
+// dst[i] += sum_s slab_s[i] in split order (slabs of `stride` floats; i < n)
+__global__ void __launch_bounds__(256) xent_split_reduce_kernel(const float* __restrict__ ws, int64_t stride,
+                                                                int splits, int64_t n, float* __restrict__ dst) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  float a = dst[i];
+  for (int sp = 0; sp < splits; ++sp) a += ws[(int64_t)sp * stride + i];
+  dst[i] = a;
 }
 
 __global__ void __launch_bounds__(256) f32_to_bf16_kernel(const float* __restrict__ a,
@@ -754,23 +775,46 @@ void launch_lxent_dx(const uint16_t* x, const uint16_t* W, const uint16_t* b, co
   else dx_impl<256>(x, W, b, tgt, lse, dloss, N, V, dx, dx_acc, s);
 }
 
-void launch_lxent_dw(const uint16_t* x, const uint16_t* W, const uint16_t* b, const int64_t* tgt,
-                     const float* lse, const float* dloss, int N, int V, int E, float* dW, float* db,
-                     hipStream_t s, bool onehot) {
-  const int vb = (V + 255) / 256;
+// token splits of the weight-gradient kernel (enough workgroups to fill the chip)
+static void lxent_dw_plan(int N, int V, int& vb, int& tps, int& TSx) {
+  vb = (V + 255) / 256;
   const int tchunks = (N + 63) / 64;
   const int TS = pick_splits(vb, tchunks, 960);
-  const int tps = ((tchunks + TS - 1) / TS) * 64;
-  const int TSx = (N + tps - 1) / tps;
+  tps = ((tchunks + TS - 1) / TS) * 64;
+  TSx = (N + tps - 1) / tps;
+}
+
+int64_t lxent_dw_ws_floats(int N, int V, int E) {
+  int vb, tps, TSx;
+  lxent_dw_plan(N, V, vb, tps, TSx);
+  return TSx > 1 ? (int64_t)TSx * V * (E + 1) : 0;
+}
+
+// ws: lxent_dw_ws_floats of scratch (the token splits' partials, reduced in order: the tied
+// embedding's head gradient is bitwise reproducible); required when that is > 0
+void launch_lxent_dw(const uint16_t* x, const uint16_t* W, const uint16_t* b, const int64_t* tgt,
+                     const float* lse, const float* dloss, int N, int V, int E, float* dW, float* db,
+                     hipStream_t s, bool onehot, float* ws) {
+  int vb, tps, TSx;
+  lxent_dw_plan(N, V, vb, tps, TSx);
+  float* wsp = TSx > 1 ? ws : nullptr;
 #define DPA_LXDW(EE, OH)                                                                                \
   hipLaunchKernelGGL((lxent_dw_kernel<EE, OH>), dim3(vb, TSx), dim3(512), 0, s, (const bf16_t*)x,        \
-                     (const bf16_t*)W, (const bf16_t*)b, tgt, lse, dloss, N, V, tps, dW, db)
+                     (const bf16_t*)W, (const bf16_t*)b, tgt, lse, dloss, N, V, tps, dW, db, wsp)
   if (E == 128) {
     if (onehot) DPA_LXDW(128, true); else DPA_LXDW(128, false);
   } else {
     if (onehot) DPA_LXDW(256, true); else DPA_LXDW(256, false);
   }
 #undef DPA_LXDW
+  if (wsp) {
+    const int64_t stride = (int64_t)V * (E + 1), nw = (int64_t)V * E;
+    hipLaunchKernelGGL(xent_split_reduce_kernel, dim3((unsigned)((nw + 255) / 256)), dim3(256), 0, s,
+                       (const float*)wsp, stride, TSx, nw, dW);
+    if (db)
+      hipLaunchKernelGGL(xent_split_reduce_kernel, dim3((unsigned)((V + 255) / 256)), dim3(256), 0, s,
+                         (const float*)(wsp + nw), stride, TSx, (int64_t)V, db);
+  }
 }
 
 }  // namespace dpa

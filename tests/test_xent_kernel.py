@@ -108,3 +108,32 @@ def test_chunked_linear_cross_entropy_wide_E(N, V, E, with_bias, chunk_mb, keep,
     torch.testing.assert_close(W.grad, Wr.grad, rtol=3e-2, atol=2e-2 * Wr.grad.abs().max().item())
     if with_bias:
         torch.testing.assert_close(b.grad, br.grad, rtol=3e-2, atol=2e-2 * br.grad.abs().max().item())
+
+
+def test_lxent_weight_gradient_bitwise_reproducible():
+    """The head weight / bias gradient of the tied embedding is split over tokens; the splits'
+    partials are summed in split order (no fp32 atomics), so two runs - accumulated onto a
+    non-zero gradient, as into the flat .grad - give the same bits."""
+    torch.manual_seed(4)
+    dev = "cuda"
+    N, V, E = 65536, 30522, 128
+    x = (torch.randn(N, E, device=dev) * 0.5).bfloat16()
+    W = (torch.randn(V, E, device=dev) * 0.5).bfloat16()
+    b = (torch.randn(V, device=dev) * 0.1).bfloat16()
+    tgt = torch.randint(0, V, (N,), device=dev)
+    tgt[torch.rand(N, device=dev) < 0.4] = 0  # a padding-like hot target
+    from distributed_pipeline_amd.ops._ext import get_ext
+    ext = get_ext(required=True)
+    _, lse = ext.lxent_fwd(x, W, b, tgt)
+    g = torch.randn(N, device=dev)
+    base_w, base_b = torch.randn(V, E, device=dev), torch.randn(V, device=dev)
+    outs = []
+    for _ in range(2):
+        gw, gb = base_w.clone(), base_b.clone()
+        ext.lxent_bwd(g, x, W, b, tgt, lse, False, True, True, dw_acc=gw, db_acc=gb)
+        outs.append((gw, gb))
+    assert torch.equal(outs[0][0], outs[1][0]) and torch.equal(outs[0][1], outs[1][1])
+    ref_loss, _, Wr, br = _ref(x, W, b, tgt)
+    ref_loss.backward(g)
+    torch.testing.assert_close(outs[0][0] - base_w, Wr.grad, rtol=2e-2, atol=1e-2 * Wr.grad.abs().max().item())
+    torch.testing.assert_close(outs[0][1] - base_b, br.grad, rtol=2e-2, atol=1e-2 * br.grad.abs().max().item())
