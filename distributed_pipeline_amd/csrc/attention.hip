@@ -1004,10 +1004,10 @@ int64_t attn_colpart_rows(int B, int L, int H, int D, bool causal) {
 }
 
 // db[part * H * D + h * D + d] += sum_r colpart[(r * H + h) * 3 D + part * D + d] over the R row
-// groups: grid (3 * H * D / 64, chunks of R), 4 row lanes x 64 columns per block, one atomic
-// per column and chunk
-__global__ void __launch_bounds__(256) colpart_reduce_d_kernel(const float* __restrict__ colpart,
-                                                               float* __restrict__ db, int R, int H, int D,
+// groups in two fixed-order passes (no fp32 atomics: deterministic).  Pass 1, grid
+// (3 * H * D / 64, chunks of R), 4 row lanes x 64 columns per block: the chunk's sum is stored in
+// place over the chunk's first row (read by no other block); pass 2 adds the chunk sums in order.
+__global__ void __launch_bounds__(256) colpart_reduce_d_kernel(float* __restrict__ colpart, int R, int H, int D,
                                                                int rchunk) {
   __shared__ float red[4][64];
   const int c64 = D / 64, x = blockIdx.x;
@@ -1018,15 +1018,28 @@ __global__ void __launch_bounds__(256) colpart_reduce_d_kernel(const float* __re
   for (int r = r0 + rl; r < r1; r += 4) t += colpart[((int64_t)r * H + h) * 3 * D + part * D + d];
   red[rl][threadIdx.x & 63] = t;
   __syncthreads();
-  if (rl == 0) {
+  if (rl == 0 && r0 < r1) {
     const int i = threadIdx.x;
-    atomicAdd(db + part * H * D + h * D + d, red[0][i] + red[1][i] + red[2][i] + red[3][i]);
+    colpart[((int64_t)r0 * H + h) * 3 * D + part * D + d] = (red[0][i] + red[1][i]) + (red[2][i] + red[3][i]);
   }
 }
 
-void launch_colpart_reduce(const float* colpart, float* db, int R, int H, int D, hipStream_t s) {
+// grid (3 * H * D / 64), 64 threads
+__global__ void __launch_bounds__(64) colpart_final_d_kernel(const float* __restrict__ colpart, float* __restrict__ db,
+                                                             int R, int H, int D, int rchunk) {
+  const int c64 = D / 64, x = blockIdx.x;
+  const int part = x / (H * c64), h = (x / c64) % H, cc = x % c64;
+  const int d = cc * 64 + threadIdx.x;
+  float t = 0.f;
+  for (int r0 = 0; r0 < R; r0 += rchunk) t += colpart[((int64_t)r0 * H + h) * 3 * D + part * D + d];
+  db[part * H * D + h * D + d] += t;
+}
+
+void launch_colpart_reduce(float* colpart, float* db, int R, int H, int D, hipStream_t s) {
   const int rchunk = 64, nch = (R + rchunk - 1) / rchunk;
-  hipLaunchKernelGGL(colpart_reduce_d_kernel, dim3(3 * H * (D / 64), nch), dim3(256), 0, s, colpart, db, R, H,
+  hipLaunchKernelGGL(colpart_reduce_d_kernel, dim3(3 * H * (D / 64), nch), dim3(256), 0, s, colpart, R, H, D,
+                     rchunk);
+  hipLaunchKernelGGL(colpart_final_d_kernel, dim3(3 * H * (D / 64)), dim3(64), 0, s, (const float*)colpart, db, R, H,
                      D, rchunk);
 }
 

@@ -1247,10 +1247,10 @@ __global__ void __launch_bounds__(256, 1) attn128_bwd_kv_d128_kernel(
   }
 }
 
-// db[q*H*64 + h*64 + d] += sum_b colpart[(b*H + h)*192 + q*64 + d]: grid (H*3, chunks of B)
-__global__ void __launch_bounds__(256) colpart_reduce_kernel(const float* __restrict__ colpart,
-                                                             float* __restrict__ db, int B, int H,
-                                                             int bchunk) {
+// db[q*H*64 + h*64 + d] += sum_b colpart[(b*H + h)*192 + q*64 + d] in two fixed-order passes (no
+// fp32 atomics): grid (H*3, chunks of B) stores each chunk's sum over its first row in place,
+// then colpart_final_kernel adds the chunk sums in order
+__global__ void __launch_bounds__(256) colpart_reduce_kernel(float* __restrict__ colpart, int B, int H, int bchunk) {
   __shared__ float red[4][64];
   const int hq = blockIdx.x, h = hq / 3, q = hq - 3 * h;
   const int d = threadIdx.x & 63, r = threadIdx.x >> 6;
@@ -1259,7 +1259,16 @@ __global__ void __launch_bounds__(256) colpart_reduce_kernel(const float* __rest
   for (int b = b0 + r; b < b1; b += 4) t += colpart[((int64_t)b * H + h) * 192 + q * 64 + d];
   red[r][d] = t;
   __syncthreads();
-  if (r == 0) atomicAdd(db + q * H * HD + h * HD + d, red[0][d] + red[1][d] + red[2][d] + red[3][d]);
+  if (r == 0 && b0 < b1)
+    colpart[((int64_t)b0 * H + h) * 192 + q * 64 + d] = (red[0][d] + red[1][d]) + (red[2][d] + red[3][d]);
+}
+
+__global__ void __launch_bounds__(64) colpart_final_kernel(const float* __restrict__ colpart, float* __restrict__ db,
+                                                           int B, int H, int bchunk) {
+  const int hq = blockIdx.x, h = hq / 3, q = hq - 3 * h, d = threadIdx.x;
+  float t = 0.f;
+  for (int b0 = 0; b0 < B; b0 += bchunk) t += colpart[((int64_t)b0 * H + h) * 192 + q * 64 + d];
+  db[q * H * HD + h * HD + d] += t;
 }
 
 static bool enabled() { return true; }
@@ -1340,8 +1349,9 @@ bool launch_attn128_bwd(const uint16_t* qkv, const uint16_t* out, const uint16_t
   if (dbias && !defer_reduce) {  // deferred: the caller reduces several calls' partials at once
     const int bchunk = 64, nch = (B + bchunk - 1) / bchunk;
     if (!db_accumulate) (void)hipMemsetAsync(dbias, 0, sizeof(float) * 3 * H * a128::HD, s);
-    hipLaunchKernelGGL(a128::colpart_reduce_kernel, dim3(3 * H, nch), dim3(256), 0, s, colpart,
-                       dbias, B, H, bchunk);
+    hipLaunchKernelGGL(a128::colpart_reduce_kernel, dim3(3 * H, nch), dim3(256), 0, s, colpart, B, H, bchunk);
+    hipLaunchKernelGGL(a128::colpart_final_kernel, dim3(3 * H), dim3(64), 0, s, (const float*)colpart, dbias, B, H,
+                       bchunk);
   }
   return true;
 }

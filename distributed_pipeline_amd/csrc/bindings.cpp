@@ -1095,7 +1095,7 @@ static std::vector<at::Tensor> diff_loss_bwd(const at::Tensor& xs, const at::Ten
                                              const at::Tensor& ids, const at::Tensor& t,
                                              const at::Tensor& W, c10::optional<at::Tensor> dmse,
                                              c10::optional<at::Tensor> dtT, double sa_last, bool need_dout,
-                                             bool need_dxs, c10::optional<at::Tensor> dW) {
+                                             bool need_dxs, c10::optional<at::Tensor> dW, bool fold_t0) {
   check_loss_inputs(xs, out, ids, t, W);
   const int64_t B = xs.size(0), L = xs.size(1), E = xs.size(2);
   const float* pm = nullptr;
@@ -1122,7 +1122,7 @@ static std::vector<at::Tensor> diff_loss_bwd(const at::Tensor& xs, const at::Ten
                               ids.data_ptr<int64_t>(), t.data_ptr<int64_t>(), W.data_ptr<float>(), pm, pt,
                               (int)B, (int)L, (int)E, (int)W.size(0), (float)sa_last,
                               need_dout ? d_out.data_ptr() : nullptr,
-                              need_dxs ? d_xs.data_ptr<float>() : nullptr, pw, cur_stream());
+                              need_dxs ? d_xs.data_ptr<float>() : nullptr, pw, cur_stream(), fold_t0 && need_dxs);
   return {d_out, d_xs};
 }
 
@@ -1250,7 +1250,9 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         "DiffuSeq embedding gather + x_start noise + masked q_sample -> (x_start, x_start bf16, x_t bf16)");
   m.def("emb_qsample_bwd", &emb_qsample_bwd, "scatter-add of the q_sample gradients into dW (fp32)");
   m.def("diff_loss_fwd", &diff_loss_fwd, "DiffuSeq per-sample (mse, tT) losses");
-  m.def("diff_loss_bwd", &diff_loss_bwd, "backward of diff_loss_fwd -> (d_out, d_x_start)");
+  m.def("diff_loss_bwd", &diff_loss_bwd, "backward of diff_loss_fwd -> (d_out, d_x_start)", py::arg("xs"),
+        py::arg("out"), py::arg("ids"), py::arg("t"), py::arg("W"), py::arg("dmse"), py::arg("dtT"),
+        py::arg("sa_last"), py::arg("need_dout"), py::arg("need_dxs"), py::arg("dW"), py::arg("fold_t0") = false);
   m.def("rng_base_add", &rng_base_add, "advance the device-side Philox offset base (graph replays)");
   m.def("timestep_emb", &timestep_emb, "sinusoidal timestep embedding [cos | sin] -> bf16");
 }

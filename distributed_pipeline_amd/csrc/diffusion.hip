@@ -8,11 +8,14 @@
 //                     eps0 / eps are generated in-kernel (counter-based Philox + Box-Muller), so
 //                     the noise tensors never exist in memory.
 //   emb_qsample_bwd : dW[ids] += d_xstart + d_xstart16 + (mask ? sqrt(abar_t) : 1) d_x_t
-//                     (fp32 atomics straight into the tied embedding's gradient; the tied
-//                     rounding head's dW comes from the fused linear-CE kernel)
+//                     (a deterministic segment sum over the stably sorted ids straight into the
+//                     tied embedding's gradient; the tied rounding head's dW comes from the fused
+//                     linear-CE kernel, also without atomics)
 //   diff_loss_fwd   : per sample  mse = mean((target - out)^2), target = t==0 ? x0_mean : x_start
 //                                 tT  = mean((sqrt(abar_{T-1}) x_start)^2)
-//   diff_loss_bwd   : d_out, d_xstart (fp32) and, for t==0 samples, dW[ids] += d x0_mean
+//   diff_loss_bwd   : d_out, d_xstart (fp32) and, for t==0 samples, d x0_mean: folded into
+//                     d_xstart (fold_t0: x_start = x0_mean + noise, so it reaches dW through
+//                     emb_qsample_bwd) or added into dW[ids] with fp32 atomics
 //   timestep_emb    : [cos(t f_j) | sin(t f_j)], f_j = 10000^(-j/half) -> bf16
 //
 // Forward layout: a token row of E fp32 values is owned by E/4 consecutive lanes
@@ -411,7 +414,7 @@ __global__ void __launch_bounds__(256) diff_loss_bwd_kernel(
     const float* __restrict__ x_start, const void* __restrict__ out_, const int64_t* __restrict__ ids,
     const int64_t* __restrict__ t, const float* __restrict__ W, const float* __restrict__ dmse,
     const float* __restrict__ dtT, int B, int L, int E, int V, float sa_last,
-    void* __restrict__ d_out_, float* __restrict__ d_xs, float* __restrict__ dW) {
+    void* __restrict__ d_out_, float* __restrict__ d_xs, float* __restrict__ dW, bool fold_t0) {
   const int vpr = E >> 2;
   const int64_t n = (int64_t)B * L * vpr;
   const float inv = 1.f / (float)(L * E);
@@ -433,18 +436,22 @@ __global__ void __launch_bounds__(256) diff_loss_bwd_kernel(
     const bool id_ok = id >= 0 && id < V;
     if (t0) tg = id_ok ? *reinterpret_cast<const f32x4*>(W + id * E + c) : f32x4{0.f, 0.f, 0.f, 0.f};
     f32x4 dy, dx;
+    // fold_t0: x_start = W[id] + noise (emb_qsample), so the t == 0 branch's gradient into the
+    // embedding row, -dy, rides on d_xs and reaches dW through the sorted, deterministic
+    // emb_qsample backward instead of fp32 atomics here
+    const bool sub = !t0 || (fold_t0 && id_ok);
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
       const float r = y[k] - tg[k];
       dy[k] = gm * r;
-      dx[k] = gt * xs[k] - (t0 ? 0.f : gm * r);
+      dx[k] = gt * xs[k] - (sub ? gm * r : 0.f);
     }
     if (d_out_) {
       if (OUT_BF16) store4_bf(reinterpret_cast<bf16_t*>(d_out_) + o, dy);
       else *reinterpret_cast<f32x4*>(reinterpret_cast<float*>(d_out_) + o) = dy;
     }
     if (d_xs) *reinterpret_cast<f32x4*>(d_xs + o) = dx;
-    if (t0 && dW && id_ok) {  // d x0_mean of the t == 0 branch -> tied embedding rows (rare)
+    if (t0 && dW && id_ok && !fold_t0) {  // d x0_mean of the t == 0 branch -> tied embedding rows
 #pragma unroll
       for (int k = 0; k < 4; ++k) atomicAdd(dW + id * E + c + k, -dy[k]);
     }
@@ -547,15 +554,15 @@ bool launch_diff_loss_fwd(const float* x_start, const void* out, bool out_bf16, 
 bool launch_diff_loss_bwd(const float* x_start, const void* out, bool out_bf16, const int64_t* ids,
                           const int64_t* t, const float* W, const float* dmse, const float* dtT, int B,
                           int L, int E, int V, float sa_last, void* d_out, float* d_xs, float* dW,
-                          hipStream_t s) {
-  if (E % 4 != 0 || B <= 0) return false;
+                          hipStream_t s, bool fold_t0) {
+  if (E % 4 != 0 || B <= 0 || (fold_t0 && d_xs == nullptr)) return false;
   const unsigned g = grid_cap((int64_t)B * L * (E / 4), 256 * 16);
   if (out_bf16)
     hipLaunchKernelGGL(diff_loss_bwd_kernel<true>, dim3(g), dim3(256), 0, s, x_start, out, ids, t, W,
-                       dmse, dtT, B, L, E, V, sa_last, d_out, d_xs, dW);
+                       dmse, dtT, B, L, E, V, sa_last, d_out, d_xs, dW, fold_t0);
   else
     hipLaunchKernelGGL(diff_loss_bwd_kernel<false>, dim3(g), dim3(256), 0, s, x_start, out, ids, t, W,
-                       dmse, dtT, B, L, E, V, sa_last, d_out, d_xs, dW);
+                       dmse, dtT, B, L, E, V, sa_last, d_out, d_xs, dW, fold_t0);
   return true;
 }
 

@@ -417,7 +417,12 @@ __global__ void __launch_bounds__(512) gemm256_kernel(
       const int t = tid & 255;
       red[(t >> 7) * 256 + grp * 128 + (t & 127)] = cs;
       __syncthreads();
-      if (tid < 256) atomicAdd(colsum + m0 + tid, red[tid] + red[256 + tid]);
+      // split-K: this slab's bias partial into the workspace's [slabs][M] tail (summed in slab
+      // order by the launcher's reduce, no atomics); one slab: the only adder of these rows
+      if (tid < 256) {
+        if (wsp) wsp[(int64_t)splits * nseg * M * N + (int64_t)z * M + m0 + tid] = red[tid] + red[256 + tid];
+        else colsum[m0 + tid] += red[tid] + red[256 + tid];
+      }
     }
     // Stage each 128-row half of the fp32 tile in LDS ([128][256], 16-float blocks
     // XOR-swizzled by row & 3), then add it with fully coalesced atomics (a wave
@@ -1570,7 +1575,7 @@ int64_t gemm256_wgrad_workspace_floats(int T, int N, int K, int nseg) {
   if (!g256_enabled() || N % 256 || K % 256 || T % 128 || T < 128 || nseg < 1 || nseg > g256::WG_MAXSEG)
     return 0;
   const WgradPlan p = wgrad_plan(T, N, K, nseg);
-  return p.ws ? (int64_t)p.splits * nseg * N * K : 0;
+  return p.ws ? (int64_t)p.splits * nseg * ((int64_t)N * K + N) : 0;  // [slabs][N][K] + bias partials [slabs][N]
 }
 
 __global__ void __launch_bounds__(256) wgrad_reduce_kernel(const float* __restrict__ ws, float* __restrict__ dW,
@@ -1580,6 +1585,16 @@ __global__ void __launch_bounds__(256) wgrad_reduce_kernel(const float* __restri
   f32x4 acc = reinterpret_cast<const f32x4*>(dW)[i];
   for (int s = 0; s < splits; ++s) acc += reinterpret_cast<const f32x4*>(ws)[s * n4 + i];
   reinterpret_cast<f32x4*>(dW)[i] = acc;
+}
+
+// db[m] += sum over slabs (in order) of the split-K bias partials [slabs][N]
+__global__ void __launch_bounds__(256) wgrad_colsum_reduce_kernel(const float* __restrict__ part, float* __restrict__ db,
+                                                                  int n, int slabs) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  float a = db[i];
+  for (int s = 0; s < slabs; ++s) a += part[(int64_t)s * n + i];
+  db[i] = a;
 }
 
 // The one-wave-per-SIMD TR x TR kernel (csrc/wgrad4w.hip) takes every weight gradient whose bias
@@ -1618,6 +1633,9 @@ bool launch_gemm256_wgrad(const uint16_t* dy, const uint16_t* x, float* dW, floa
     const int64_t n4 = (int64_t)N * K / 4;
     hipLaunchKernelGGL(wgrad_reduce_kernel, dim3((unsigned)((n4 + 255) / 256)), dim3(256), 0, s, wsp, dW, n4,
                        p.splits);
+    if (db)
+      hipLaunchKernelGGL(wgrad_colsum_reduce_kernel, dim3((unsigned)((N + 255) / 256)), dim3(256), 0, s,
+                         wsp + (int64_t)p.splits * N * K, db, N, p.splits);
   }
   return true;
 }
@@ -1648,6 +1666,9 @@ bool launch_gemm256_wgrad_multi(const uint16_t* const* dys, const uint16_t* cons
     const int64_t n4 = (int64_t)N * K / 4;
     hipLaunchKernelGGL(wgrad_reduce_kernel, dim3((unsigned)((n4 + 255) / 256)), dim3(256), 0, s, wsp, dW, n4,
                        p.splits * nseg);
+    if (db)
+      hipLaunchKernelGGL(wgrad_colsum_reduce_kernel, dim3((unsigned)((N + 255) / 256)), dim3(256), 0, s,
+                         wsp + (int64_t)p.splits * nseg * N * K, db, N, p.splits * nseg);
   }
   return true;
 }

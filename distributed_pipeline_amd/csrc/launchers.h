@@ -94,14 +94,16 @@ bool launch_add_ln_bwd(const uint16_t* dout, const uint16_t* hsave, const float*
                        const uint16_t* beta = nullptr,    // beta: `hsave` is the LN output ...
                        const uint16_t* hcopy = nullptr,   // ... and hcopy the guarded h copy
                        bool pair_hash = false);           // dy's dropout bits: common.h pair_hash
-// the deferred second stage of part_mode 1/2 (R = the rows of each summed micro-batch)
-bool launch_ln_colreduce(const float* part, int64_t R, int D, float* dg, float* db, float* dyb, hipStream_t s);
+// the deferred second stage of part_mode 1/2 (R = the rows of each summed micro-batch); consumes
+// the partials (ordered two-pass sums, no atomics)
+bool launch_ln_colreduce(float* part, int64_t R, int D, float* dg, float* db, float* dyb, hipStream_t s);
 // dpos[L][H] (zeroed; += sum over b) and dtemb[B][H] (= sum over l) of a [B][L][H] bf16 gradient in
 // one read; part: seq_pos_groups(B) * L * H floats of workspace.  L in {64, 128, 256}, H % 64 == 0.
 int seq_pos_groups(int B);
 bool launch_seq_pos_sums(const uint16_t* d, int B, int L, int H, float* dpos, float* dtemb, float* part,
                          hipStream_t s);
-bool launch_colsum_acc(const float* part, int rows, int cols, float* dst, hipStream_t s);
+// dst[c] += sum_r part[r][c] in a fixed order (deterministic); consumes part
+bool launch_colsum_acc(float* part, int rows, int cols, float* dst, hipStream_t s);
 // fp32 workspace (floats) the small-R two-stage column sums of launch_add_ln_bwd use (0: none)
 int64_t ln_bwd_ws_floats(int64_t R, int D);
 
@@ -125,7 +127,7 @@ bool launch_attn128_bwd_d128(const uint16_t* qkv, const uint16_t* out, const uin
 // attention backward bias-gradient partials: rows of the colpart scratch ([rows][3 D] fp32) and
 // the reduce pass db[3 H D] += column sums
 int64_t attn_colpart_rows(int B, int L, int H, int D, bool causal);
-void launch_colpart_reduce(const float* colpart, float* db, int R, int H, int D, hipStream_t s);
+void launch_colpart_reduce(float* colpart, float* db, int R, int H, int D, hipStream_t s);  // consumes colpart
 bool launch_attn128_fwd_d128(const uint16_t* qkv, uint16_t* out, float* lse, int B, int L, int H,
                              float p, bool causal, uint32_t seed, uint32_t offset, hipStream_t s);
 bool launch_attn128_fwd(const uint16_t* qkv, uint16_t* out, float* lse, int B, int L, int H,
@@ -177,7 +179,7 @@ bool launch_diff_loss_fwd(const float* x_start, const void* out, bool out_bf16, 
 bool launch_diff_loss_bwd(const float* x_start, const void* out, bool out_bf16, const int64_t* ids,
                           const int64_t* t, const float* W, const float* dmse, const float* dtT, int B,
                           int L, int E, int V, float sa_last, void* d_out, float* d_xs, float* dW,
-                          hipStream_t s);
+                          hipStream_t s, bool fold_t0 = false);  // fold_t0: the t == 0 W term into d_xs
 void launch_timestep_emb(const float* ts, int B, int dim, float max_period, uint16_t* out,
                          hipStream_t s);
 

@@ -568,12 +568,13 @@ __global__ void __launch_bounds__(256) add_ln_bwd_rowblk_kernel(
   }
 }
 
-// Second stage of the small-R column sums: grid (D / 64, #accumulators, NSEG); a block sums
-// column chunk x of accumulator y over its segment of the nb block partials (64 columns x 4
-// row lanes, 16-byte-free coalesced 256-B rows) and adds one atomic per column.
-__global__ void __launch_bounds__(256) ln_colreduce_kernel(const float* __restrict__ part, int nb, int D,
-                                                          float* __restrict__ d0, float* __restrict__ d1,
-                                                          float* __restrict__ d2, int astride) {
+// Second stage of the two-stage column sums, in two fixed-order passes (no fp32 atomics: the
+// LayerNorm / bias gradients are bitwise reproducible).  Pass 1, grid (D / 64, #accumulators,
+// NSEG): a block sums column chunk x of accumulator y over its segment of the nb block partials
+// (64 columns x 4 row lanes, coalesced 256-B rows) and stores the segment sum IN PLACE, over its
+// segment's first partial row (a row no other block reads).  Pass 2 (ln_colfinal_kernel) adds the
+// NSEG segment sums in segment order onto the destination.
+__global__ void __launch_bounds__(256) ln_colreduce_kernel(float* __restrict__ part, int nb, int D, int astride) {
   __shared__ float red[4][64];
   const int c = blockIdx.x * 64 + (threadIdx.x & 63), rl = threadIdx.x >> 6, a = blockIdx.y;
   const int per = (nb + gridDim.z - 1) / gridDim.z;
@@ -582,10 +583,29 @@ __global__ void __launch_bounds__(256) ln_colreduce_kernel(const float* __restri
   for (int r = r0 + rl; r < r1; r += 4) t += part[((int64_t)r * astride + a) * D + c];
   red[rl][threadIdx.x & 63] = t;
   __syncthreads();
-  if (rl == 0) {
-    float* dst = a == 0 ? d0 : a == 1 ? d1 : d2;
-    atomicAdd(dst + c, red[0][threadIdx.x] + red[1][threadIdx.x] + red[2][threadIdx.x] + red[3][threadIdx.x]);
-  }
+  if (rl == 0 && r0 < r1)
+    part[((int64_t)r0 * astride + a) * D + c] =
+        (red[0][threadIdx.x] + red[1][threadIdx.x]) + (red[2][threadIdx.x] + red[3][threadIdx.x]);
+}
+
+// grid (D / 64, #accumulators), 64 threads: dst_a[c] += sum over segments (in order) of pass 1's sums
+__global__ void __launch_bounds__(64) ln_colfinal_kernel(const float* __restrict__ part, int nb, int D, int astride,
+                                                        int nseg, float* __restrict__ d0, float* __restrict__ d1,
+                                                        float* __restrict__ d2) {
+  const int c = blockIdx.x * 64 + threadIdx.x, a = blockIdx.y;
+  const int per = (nb + nseg - 1) / nseg;
+  float t = 0.f;
+  for (int sg = 0; sg < nseg && sg * per < nb; ++sg) t += part[((int64_t)sg * per * astride + a) * D + c];
+  float* dst = a == 0 ? d0 : a == 1 ? d1 : d2;
+  dst[c] += t;
+}
+
+static void colsum_two_pass(float* part, int nb, int D, int astride, int nacc, float* d0, float* d1, float* d2,
+                            hipStream_t s) {
+  const int nseg = nb >= 256 ? 16 : nb >= 32 ? 4 : 1;
+  hipLaunchKernelGGL(ln_colreduce_kernel, dim3(D / 64, nacc, nseg), dim3(256), 0, s, part, nb, D, astride);
+  hipLaunchKernelGGL(ln_colfinal_kernel, dim3(D / 64, nacc), dim3(64), 0, s, (const float*)part, nb, D, astride,
+                     nseg, d0, d1, d2);
 }
 
 #define DPA_LN_DISPATCH(D, FN, ...)                      \
@@ -661,6 +681,9 @@ constexpr int LN_WIDE_D = 1536;
 // per wave and stores 2.4 MB of partials instead of 18.9 MB, 8192 rows 4 per wave.  Interleaved
 // A/Bs (profiles/ln_bwd_blocks_r5.txt): seq512 8 x 64 -1.1% at 1024 blocks and -0.2% more at
 // 256; the 32 x 64 schedule -0.75% at 256 vs 1024 (= the old 512 at 8192 rows), +0.3% at 128.
+// Large R (> LN_SMALL_R): the 4-wave grid of ln_bwd_blocks, its block partials summed in two
+// ordered passes too (4.7 MB at 512 blocks x 3 x 768) instead of one fp32 atomic per column per
+// block - the reduction is deterministic at every R.
 static int64_t ln_bwd_two_stage_blocks(int64_t R, int D) {
   if (D >= LN_WIDE_D) return R < 1024 ? R : 1024;  // add_ln_bwd_rowblk_kernel: one row per block at a time
   const int64_t cap = device_cu_count();
@@ -668,16 +691,14 @@ static int64_t ln_bwd_two_stage_blocks(int64_t R, int D) {
     const int64_t nb = (R + LN_SMALL_ROWS - 1) / LN_SMALL_ROWS;
     return cap > 0 && nb > cap ? cap : nb;
   }
-  return 0;
+  return ln_bwd_blocks(R);
 }
 int64_t ln_bwd_ws_floats(int64_t R, int D) { return ln_bwd_two_stage_blocks(R, D) * 3 * D; }
 
-// Second stage of the two-stage column sums: part[nb][3][D] -> dg, db (, dyb) (+=)
-static void ln_colreduce_launch(const float* part, int nb, int D, float* dg, float* db, float* dyb,
-                                hipStream_t s) {
-  const int nseg = nb >= 256 ? 16 : nb >= 32 ? 4 : 1;
-  hipLaunchKernelGGL(ln_colreduce_kernel, dim3(D / 64, dyb ? 3 : 2, nseg), dim3(256), 0, s, part, nb, D, dg, db,
-                     dyb, 3);
+// Second stage of the two-stage column sums: part[nb][3][D] -> dg, db (, dyb) (+=); the partials
+// are consumed (pass 1 stores its segment sums over them)
+static void ln_colreduce_launch(float* part, int nb, int D, float* dg, float* db, float* dyb, hipStream_t s) {
+  colsum_two_pass(part, nb, D, 3, dyb ? 3 : 2, dg, db, dyb, s);
 }
 
 // part_mode (two-stage shapes only, ws = a caller-owned partial buffer of ln_bwd_ws_floats):
@@ -736,7 +757,7 @@ static void ln_bwd_impl(const uint16_t* dout, const uint16_t* hsave, const float
 #define DPA_LN_BWD(P, X, H)                             \
   do {                                                  \
     if constexpr (D < LN_WIDE_D) {                      \
-      if (two_stage) {                                  \
+      if (two_stage && R <= LN_SMALL_R) {               \
         DPA_LN_BWD_NW(P, X, H, LN_SMALL_NW);            \
         break;                                          \
       }                                                 \
@@ -752,7 +773,7 @@ static void ln_bwd_impl(const uint16_t* dout, const uint16_t* hsave, const float
   if (two_stage && reduce) ln_colreduce_launch(part, nb, D, dg, db, dyb_k, s);
 }
 
-bool launch_ln_colreduce(const float* part, int64_t R, int D, float* dg, float* db, float* dyb, hipStream_t s) {
+bool launch_ln_colreduce(float* part, int64_t R, int D, float* dg, float* db, float* dyb, hipStream_t s) {
   const int64_t nb = ln_bwd_two_stage_blocks(R, D);
   if (nb <= 0 || D % 64) return false;
   ln_colreduce_launch(part, (int)nb, D, dg, db, dyb, s);
@@ -762,11 +783,9 @@ bool launch_ln_colreduce(const float* part, int64_t R, int D, float* dg, float* 
 // dst[c] += sum_r part[r][c] (fp32 [rows][cols] partials, cols % 64 == 0): the bias
 // gradient of a fused epilogue's per-tile column sums, accumulated straight onto the
 // parameter's fp32 .grad (no ATen reduce + autograd add per micro-batch)
-bool launch_colsum_acc(const float* part, int rows, int cols, float* dst, hipStream_t s) {
+bool launch_colsum_acc(float* part, int rows, int cols, float* dst, hipStream_t s) {
   if (cols % 64 || rows <= 0) return false;
-  const int nseg = rows >= 256 ? 16 : rows >= 32 ? 4 : 1;
-  hipLaunchKernelGGL(ln_colreduce_kernel, dim3(cols / 64, 1, nseg), dim3(256), 0, s, part, rows, cols, dst,
-                     (float*)nullptr, (float*)nullptr, 1);
+  colsum_two_pass(part, rows, cols, 1, 1, dst, nullptr, nullptr, s);
   return true;
 }
 

@@ -191,7 +191,7 @@ class GaussianDiffusion:
             float(self.sqrt_one_minus_alphas_cumprod[0]))
         model_out = model(x_t, self.scale_timesteps(t))                       # x0_hat (bf16)
         sa_last = float(self.sqrt_alphas_cumprod[self.num_timesteps - 1])
-        mse, tT_loss = dops.diffusion_mse(x_start, model_out, input_ids, t, W, sa_last)
+        mse, tT_loss = dops.diffusion_mse(x_start, model_out, input_ids, t, W, sa_last, t0_via_x_start=True)
         terms = {"mse": mse}
         decoder_nll = self.token_discrete_loss(x_start16, net, input_ids)
         if compute_nll:

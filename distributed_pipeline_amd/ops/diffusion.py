@@ -73,26 +73,30 @@ class _EmbQSampleFn(torch.autograd.Function):
 
 class _DiffLossFn(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x_start, out, ids, t, W, sa_last):
+    def forward(ctx, x_start, out, ids, t, W, sa_last, t0_via_x_start):
         ctx.set_materialize_grads(False)
         mse, tT = get_ext().diff_loss_fwd(x_start, out, ids, t, W.detach(), float(sa_last))
         ctx.save_for_backward(x_start, out, ids, t)
-        ctx.W, ctx.sa_last = W, float(sa_last)
+        ctx.W, ctx.sa_last, ctx.fold = W, float(sa_last), bool(t0_via_x_start)
         return mse, tT
 
     @staticmethod
     def backward(ctx, dmse, dtT):
         x_start, out, ids, t = ctx.saved_tensors
         if dmse is None and dtT is None:
-            return (None,) * 6
+            return (None,) * 7
         buf = ret = None
-        if ctx.needs_input_grad[4] and dmse is not None:
-            buf, ret = _grad_buffer(ctx.W)  # t == 0 samples: d x0_mean into the embedding rows
+        # t == 0 samples: d x0_mean into the embedding rows.  When x_start = W[ids] + noise
+        # (emb_qsample) and both get gradients, that term rides on d_xs into the sorted,
+        # deterministic embedding backward; otherwise fp32 atomics into W's gradient here.
+        fold = ctx.fold and ctx.needs_input_grad[0] and ctx.needs_input_grad[4]
+        if ctx.needs_input_grad[4] and dmse is not None and not fold:
+            buf, ret = _grad_buffer(ctx.W)
         d_out, d_xs = get_ext().diff_loss_bwd(x_start, out, ids, t, ctx.W.detach(), _f(dmse), _f(dtT),
                                               ctx.sa_last, ctx.needs_input_grad[1],
-                                              ctx.needs_input_grad[0], buf)
+                                              ctx.needs_input_grad[0], buf, fold_t0=fold)
         return (d_xs if ctx.needs_input_grad[0] else None,
-                d_out if ctx.needs_input_grad[1] else None, None, None, ret, None)
+                d_out if ctx.needs_input_grad[1] else None, None, None, ret, None, None)
 
 
 def emb_qsample(W, ids, mask, t, sqrt_alphas_cumprod, sqrt_one_minus_alphas_cumprod, std0):
@@ -103,10 +107,12 @@ def emb_qsample(W, ids, mask, t, sqrt_alphas_cumprod, sqrt_one_minus_alphas_cump
                                sqrt_one_minus_alphas_cumprod, float(std0), seed, off)
 
 
-def diffusion_mse(x_start, out, ids, t, W, sqrt_alpha_bar_last):
-    """-> (mse [B], tT [B]) fp32 (DiffuSeq ``training_losses_seq2seq`` terms)."""
+def diffusion_mse(x_start, out, ids, t, W, sqrt_alpha_bar_last, t0_via_x_start=False):
+    """-> (mse [B], tT [B]) fp32 (DiffuSeq ``training_losses_seq2seq`` terms).
+    ``t0_via_x_start``: x_start is :func:`emb_qsample`'s (W[ids] + noise), so the t == 0 samples'
+    embedding gradient may be routed through d x_start (deterministic)."""
     return _DiffLossFn.apply(x_start, out.contiguous(), ids.contiguous(), t.to(torch.long).contiguous(),
-                             W, float(sqrt_alpha_bar_last))
+                             W, float(sqrt_alpha_bar_last), bool(t0_via_x_start))
 
 
 def timestep_embedding(timesteps, dim, max_period=10000):
