@@ -413,9 +413,12 @@ static std::vector<at::Tensor> bias_act_bwd(const at::Tensor& dy, const at::Tens
   if (want_db) db = at::zeros({N}, dy.options().dtype(at::kFloat));
   if (act != 0 || want_db) {
     CHECK_CONTIG(zy);
+    at::Tensor ws = want_db ? at::empty({dpa::bias_act_bwd_ws_floats(R, N)}, dy.options().dtype(at::kFloat))
+                            : at::Tensor();
     dpa::launch_bias_act_bwd(bf_ptr(dy), bf_ptr(zy),
                              act == 0 ? nullptr : reinterpret_cast<uint16_t*>(dz.data_ptr()),
-                             want_db ? db.data_ptr<float>() : nullptr, R, N, (int)act, cur_stream());
+                             want_db ? db.data_ptr<float>() : nullptr, R, N, (int)act, cur_stream(),
+                             want_db ? ws.data_ptr<float>() : nullptr);
   }
   return {dz, db};
 }
@@ -531,8 +534,10 @@ static std::vector<at::Tensor> attn_bwd(const at::Tensor& dout, const at::Tensor
     // no fused column sums on this path (L != 128): one column-sum pass over the bf16 dqkv,
     // accumulated onto db (zeroed unless it is the parameter's .grad)
     if (!acc) db.zero_();
-    dpa::launch_bias_act_bwd(bf_ptr(dqkv), nullptr, nullptr, db.data_ptr<float>(), (int64_t)B * L,
-                             (int)(3LL * H * D), 0, cur_stream());
+    const int Nq = (int)(3LL * H * D);
+    at::Tensor ws = at::empty({dpa::bias_act_bwd_ws_floats((int64_t)B * L, Nq)}, db.options());
+    dpa::launch_bias_act_bwd(bf_ptr(dqkv), nullptr, nullptr, db.data_ptr<float>(), (int64_t)B * L, Nq, 0,
+                             cur_stream(), ws.data_ptr<float>());
     got = true;
   }
   // contract: with a usable db_acc the bias gradient is always accumulated (result undefined)

@@ -78,7 +78,7 @@ __global__ void __launch_bounds__(256) bias_act_fwd_kernel(bf16_t* __restrict__ 
 __global__ void __launch_bounds__(256) bias_act_bwd_kernel(const bf16_t* __restrict__ dy,
                                                           const bf16_t* __restrict__ zy,
                                                           bf16_t* __restrict__ dz,
-                                                          float* __restrict__ db, int64_t R, int N,
+                                                          float* __restrict__ part, int64_t R, int N,
                                                           int act) {
   __shared__ float red[4][64 * 8 + 4];
   const int c8 = (blockIdx.x * 64 + threadIdx.x) * 8;
@@ -116,15 +116,17 @@ __global__ void __launch_bounds__(256) bias_act_bwd_kernel(const bf16_t* __restr
       }
     }
   }
-  if (!db) return;
+  if (!part) return;
 #pragma unroll
   for (int k = 0; k < 8; ++k) red[threadIdx.y][threadIdx.x * 8 + k] = acc[k];
   __syncthreads();
+  // this row block's column sums, a plain store into part[row block][N]; launch_colsum_acc adds the
+  // row blocks in order (deterministic, no fp32 atomics)
   if (threadIdx.y == 0 && c8 < N) {
 #pragma unroll
     for (int k = 0; k < 8; ++k) {
       const int cc = threadIdx.x * 8 + k;
-      atomicAdd(db + c8 + k, red[0][cc] + red[1][cc] + red[2][cc] + red[3][cc]);
+      part[(int64_t)blockIdx.y * N + c8 + k] = (red[0][cc] + red[1][cc]) + (red[2][cc] + red[3][cc]);
     }
   }
 }
@@ -143,11 +145,20 @@ void launch_bias_act_fwd(uint16_t* z, const uint16_t* bias, uint16_t* y, int64_t
                      (bf16_t*)z, (const bf16_t*)bias, (bf16_t*)y, R, N, act);
 }
 
-void launch_bias_act_bwd(const uint16_t* dy, const uint16_t* zy, uint16_t* dz, float* db, int64_t R,
-                         int N, int act, hipStream_t s) {
+int64_t bias_act_bwd_ws_floats(int64_t R, int N) {
   const int cb = (N / 8 + 63) / 64;
-  hipLaunchKernelGGL(bias_act_bwd_kernel, dim3(cb, row_blocks(R, cb)), dim3(64, 4), 0, s,
-                     (const bf16_t*)dy, (const bf16_t*)zy, (bf16_t*)dz, db, R, N, act);
+  return (int64_t)row_blocks(R, cb) * N;
+}
+
+// db (nullable) += column sums of dz; ws: bias_act_bwd_ws_floats(R, N) floats when db is given
+void launch_bias_act_bwd(const uint16_t* dy, const uint16_t* zy, uint16_t* dz, float* db, int64_t R,
+                         int N, int act, hipStream_t s, float* ws) {
+  const int cb = (N / 8 + 63) / 64;
+  const unsigned rb = row_blocks(R, cb);
+  float* part = db ? ws : nullptr;
+  hipLaunchKernelGGL(bias_act_bwd_kernel, dim3(cb, rb), dim3(64, 4), 0, s,
+                     (const bf16_t*)dy, (const bf16_t*)zy, (bf16_t*)dz, part, R, N, act);
+  if (part) launch_colsum_acc(part, (int)rb, N, db, s);
 }
 
 }  // namespace dpa

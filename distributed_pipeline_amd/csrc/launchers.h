@@ -110,8 +110,11 @@ int64_t ln_bwd_ws_floats(int64_t R, int D);
 // ---- elementwise.hip (bias + activation epilogues) -------------------------------
 void launch_bias_act_fwd(uint16_t* z, const uint16_t* bias, uint16_t* y, int64_t R, int N, int act,
                          hipStream_t s);
+// db (nullable) += column sums of dz, through ws = bias_act_bwd_ws_floats(R, N) floats of scratch
+// (row-block partials summed in order: deterministic); ws is required when db is given
+int64_t bias_act_bwd_ws_floats(int64_t R, int N);
 void launch_bias_act_bwd(const uint16_t* dy, const uint16_t* zy, uint16_t* dz, float* db, int64_t R,
-                         int N, int act, hipStream_t s);
+                         int N, int act, hipStream_t s, float* ws);
 
 // ---- attention.hip (head_dim 64 or 128, dropout, causal) ---------------------------------
 // head_major: qkv is [B, 3H, L, D] (QKV GEMM head-major store; L == 128, D == 64, bidirectional only)

@@ -580,10 +580,11 @@ __global__ void __launch_bounds__(256) ln_colreduce_kernel(float* __restrict__ p
   const int per = (nb + gridDim.z - 1) / gridDim.z;
   const int r0 = blockIdx.z * per, r1 = min(nb, r0 + per);
   float t = 0.f;
-  for (int r = r0 + rl; r < r1; r += 4) t += part[((int64_t)r * astride + a) * D + c];
+  if (c < D)
+    for (int r = r0 + rl; r < r1; r += 4) t += part[((int64_t)r * astride + a) * D + c];
   red[rl][threadIdx.x & 63] = t;
   __syncthreads();
-  if (rl == 0 && r0 < r1)
+  if (rl == 0 && r0 < r1 && c < D)
     part[((int64_t)r0 * astride + a) * D + c] =
         (red[0][threadIdx.x] + red[1][threadIdx.x]) + (red[2][threadIdx.x] + red[3][threadIdx.x]);
 }
@@ -593,6 +594,7 @@ __global__ void __launch_bounds__(64) ln_colfinal_kernel(const float* __restrict
                                                         int nseg, float* __restrict__ d0, float* __restrict__ d1,
                                                         float* __restrict__ d2) {
   const int c = blockIdx.x * 64 + threadIdx.x, a = blockIdx.y;
+  if (c >= D) return;
   const int per = (nb + nseg - 1) / nseg;
   float t = 0.f;
   for (int sg = 0; sg < nseg && sg * per < nb; ++sg) t += part[((int64_t)sg * per * astride + a) * D + c];
@@ -603,8 +605,9 @@ __global__ void __launch_bounds__(64) ln_colfinal_kernel(const float* __restrict
 static void colsum_two_pass(float* part, int nb, int D, int astride, int nacc, float* d0, float* d1, float* d2,
                             hipStream_t s) {
   const int nseg = nb >= 256 ? 16 : nb >= 32 ? 4 : 1;
-  hipLaunchKernelGGL(ln_colreduce_kernel, dim3(D / 64, nacc, nseg), dim3(256), 0, s, part, nb, D, astride);
-  hipLaunchKernelGGL(ln_colfinal_kernel, dim3(D / 64, nacc), dim3(64), 0, s, (const float*)part, nb, D, astride,
+  const unsigned cb = (unsigned)((D + 63) / 64);
+  hipLaunchKernelGGL(ln_colreduce_kernel, dim3(cb, nacc, nseg), dim3(256), 0, s, part, nb, D, astride);
+  hipLaunchKernelGGL(ln_colfinal_kernel, dim3(cb, nacc), dim3(64), 0, s, (const float*)part, nb, D, astride,
                      nseg, d0, d1, d2);
 }
 
@@ -784,7 +787,7 @@ bool launch_ln_colreduce(float* part, int64_t R, int D, float* dg, float* db, fl
 // gradient of a fused epilogue's per-tile column sums, accumulated straight onto the
 // parameter's fp32 .grad (no ATen reduce + autograd add per micro-batch)
 bool launch_colsum_acc(float* part, int rows, int cols, float* dst, hipStream_t s) {
-  if (cols % 64 || rows <= 0) return false;
+  if (cols <= 0 || rows <= 0) return false;
   colsum_two_pass(part, rows, cols, 1, 1, dst, nullptr, nullptr, s);
   return true;
 }

@@ -67,3 +67,42 @@ def test_training_steps_bitwise_reproducible(exec_microbatch, overlap, defer):
     assert torch.equal(g0, g1), _first_diff(sp, g0, g1)
     assert torch.equal(p0, p1), _first_diff(sp, p0, p1)
     assert l0 == l1
+
+
+def _run_gpt2(steps=2):
+    from basic_utils import logger
+    from distributed_pipeline_amd.ops.nn import RNG
+    from utils.initialization import create_model_from_config, seed_all
+    from utils.trainer import LMTrainLoop
+
+    logger.configure(dir="/tmp/dpa_determinism_gpt2", format_strs=[])
+    seed_all(0)
+    RNG.counter = 0
+    model = create_model_from_config(model="gpt2", precision="bf16", config_name="tiny", hidden_size=256,
+                                     num_layers=2, num_heads=4, vocab_size=50257, seq_len=256,
+                                     dropout=0.1).cuda()
+    g = torch.Generator().manual_seed(2)
+    ids = torch.randint(0, 50257, (16, 256), generator=g)
+    batch = {"input_ids": ids, "labels": ids.clone()}
+    loop = LMTrainLoop(model=model, data=iter([batch] * (steps + 1)), batch_size=16, microbatch=8, lr=1e-4,
+                       ema_rate="0.9999", log_interval=1, save_interval=10 ** 9, resume_checkpoint="",
+                       learning_steps=steps, checkpoint_path="/tmp/dpa_determinism_gpt2", ddp_engine="native",
+                       precision="bf16", exec_microbatch=0, device_prefetch=False)
+    torch.manual_seed(7)
+    losses = []
+    for _ in range(steps):
+        loop.run_step(batch)
+        losses.append(logger.dumpkvs()["loss"])
+    torch.cuda.synchronize()
+    sp = loop.ddp_model.space
+    return sp.grad_flat.clone(), sp.param_flat.clone(), losses, sp
+
+
+def test_gpt2_training_steps_bitwise_reproducible():
+    """The causal-LM path too: general attention kernels (ordered qkv-bias sums), tied wte/LM head
+    (sorted embedding gradient, split-K head weight gradient with an ordered merge)."""
+    g0, p0, l0, sp = _run_gpt2()
+    g1, p1, l1, _ = _run_gpt2()
+    assert torch.equal(g0, g1), _first_diff(sp, g0, g1)
+    assert torch.equal(p0, p1), _first_diff(sp, p0, p1)
+    assert l0 == l1
