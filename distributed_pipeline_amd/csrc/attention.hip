@@ -342,6 +342,9 @@ __global__ void __launch_bounds__(256, D == 64 ? 2 : 1) attn_fwd_online_kernel(c
   }
   const DropCfg dc = make_drop(p, seed, offset, (uint32_t)(b * H + hd));
   const uint32_t qterm = (uint32_t)q * DROP_CQ;
+  const uint32_t thr_h = min(dc.thr16, 65535u) ^ 0x8000u;  // p < 1 - 2^-17
+  const uint32_t ts2 = thr_h | (thr_h << 16), c15 = 0x000F000Fu, c8000 = 0x80008000u;
+  const uint32_t sq = dc.seedmix ^ qterm;
   const int kv_end = CAUSAL ? min(L, it.t * 128 + 128) : L;
   // source lane (in this half's numbering) of the query that register i of O belongs to
   int src[16];
@@ -372,7 +375,7 @@ __global__ void __launch_bounds__(256, D == 64 ? 2 : 1) attn_fwd_online_kernel(c
       constexpr bool MASKED = decltype(mtag)::value;
       const int nsub = MASKED && CAUSAL ? min(2, max(0, (qbase + 31 - kv0) / 32 + 1)) : 2;
       f32x16 acc[2];
-      float tmax = -1e30f;
+      float tm[2] = {-1e30f, -1e30f};  // two independent max chains, one per subtile
 #pragma unroll
       for (int t = 0; t < 2; ++t) {
         acc[t] = zero16();
@@ -388,12 +391,13 @@ __global__ void __launch_bounds__(256, D == 64 ? 2 : 1) attn_fwd_online_kernel(c
           }
         }
 #pragma unroll
-        for (int i = 0; i < 16; ++i) tmax = fmaxf(tmax, acc[t][i]);
+        for (int i = 0; i < 16; ++i) tm[t] = fmaxf(tm[t], acc[t][i]);
       }
       if (nsub > 0) {
         // running max in the scaled (exp2) domain; O and l are rescaled only when some
         // query's max grew by more than 2^8 (lazy rescale: p <= 256 otherwise, exact
         // in fp32 and bf16), which after the first tiles is almost never
+        float tmax = fmaxf(tm[0], tm[1]);
         tmax = fmaxf(tmax, __shfl_xor(tmax, 32, 64)) * att_c<D>();
         if (__any(tmax > m + 8.f)) {
           const float mn = fmaxf(m, tmax);
@@ -408,6 +412,7 @@ __global__ void __launch_bounds__(256, D == 64 ? 2 : 1) attn_fwd_online_kernel(c
           }
         }
         float add = 0.f;
+        bf16x8 pf[2][2];  // P (dropped) as the A fragments of O += P^T V
 #pragma unroll
         for (int t = 0; t < 2; ++t) {
           if (t >= nsub) continue;
@@ -419,13 +424,19 @@ __global__ void __launch_bounds__(256, D == 64 ? 2 : 1) attn_fwd_online_kernel(c
             add += pr;
             acc[t][i] = pr;
           }
-          if constexpr (DROP) {  // hashes as an independent batch after the exps (ILP), then the keep selects
-            uint32_t hh[8];
+          // registers 2j, 2j + 1 are keys 2k, 2k + 1 of one query: one packed dword per pair,
+          // dropped as a pair from its hash (drop_pair)
+          uint32_t pk[8];
 #pragma unroll
-            for (int j = 0; j < 8; ++j) hh[j] = drop_hash_t(dc, qterm, kt0 + (uint32_t)(acc_off(2 * j) >> 1) * DROP_CK);
+          for (int j = 0; j < 8; ++j) pk[j] = pack_bf2(acc[t][2 * j], acc[t][2 * j + 1]);
+          if constexpr (DROP) {
 #pragma unroll
-            for (int i = 0; i < 16; ++i) acc[t][i] = keep_from(dc, hh[i >> 1], i & 1) ? acc[t][i] * dc.scale : 0.f;
+            for (int j = 0; j < 8; ++j)
+              pk[j] = drop_pair(pk[j], drop_hash_s(sq, kt0 + (uint32_t)(acc_off(2 * j) >> 1) * DROP_CK, c8000), ts2, c15);
           }
+#pragma unroll
+          for (int s = 0; s < 2; ++s)
+            pf[t][s] = __builtin_bit_cast(bf16x8, (u32x4){pk[4 * s], pk[4 * s + 1], pk[4 * s + 2], pk[4 * s + 3]});
         }
         l += add;
 #pragma unroll
@@ -433,7 +444,7 @@ __global__ void __launch_bounds__(256, D == 64 ? 2 : 1) attn_fwd_online_kernel(c
           if (t >= nsub) continue;
 #pragma unroll
           for (int s = 0; s < 2; ++s) {
-            const bf16x8 af = acc_to_frag(acc[t], s);
+            const bf16x8 af = pf[t][s];
 #pragma unroll
             for (int dt = 0; dt < D / 32; ++dt)
               o[dt] = mfma32(af, lds_tr_frag<2 * D>(vt_lds, t * 32 + 16 * s, dt * 32, lane), o[dt]);
@@ -447,7 +458,7 @@ __global__ void __launch_bounds__(256, D == 64 ? 2 : 1) attn_fwd_online_kernel(c
   }
   l += __shfl_xor(l, 32, 64);
   if (hf == 0 && q_ok) lse[((int64_t)b * H + hd) * L + q] = (m + log2f(l)) * LN2f;
-  const float inv_l = 1.f / l;
+  const float inv_l = (DROP ? dc.scale : 1.f) / l;  // the kept probabilities' 1 / (1 - p)
   bf16_t* ob = out + (int64_t)b * L * H * D + (int64_t)hd * D;
 #pragma unroll
   for (int i = 0; i < 16; ++i) {

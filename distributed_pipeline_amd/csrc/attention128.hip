@@ -270,6 +270,7 @@ __global__ void __launch_bounds__(256, 2) attn128_fwd_kernel(const bf16_t* __res
   const int G = gridDim.x;
   int item = blockIdx.x;
   if (item < nitems) issue(item, 0);
+#pragma unroll 1
   for (int k = 0; item < nitems; ++k, item += G) {
     const int cur = k & 1;
     // This item's K/V DMA and Q loads landed; only the previous item's 5 stores
@@ -339,12 +340,32 @@ __global__ void __launch_bounds__(256, 2) attn128_fwd_kernel(const bf16_t* __res
     f32x16 o[2];
     o[0] = zero16();
     o[1] = zero16();
+    // 1 / l and the kept probabilities' 1 / (1 - p) scale the scores here (queries on the lane;
+    // the output's rows sit on registers and would need a cross-lane fetch per row)
     const float fk = DROP ? inv_l * dc.scale : inv_l;
     // key pair of register 2j of tile t: t * 16 + (j & 1) + 4 (j >> 1) + 2 hf
     const uint32_t hq = (uint32_t)q * 0x9E3779B1u, hk0 = (uint32_t)(2 * hf) * 0x85EBCA77u;
+    const uint32_t sq = dc.seedmix ^ hq, c8000 = 0x80008000u, c15 = 0x000F000Fu;
+    const uint32_t thr_h = min(dc.thr16, 65535u) ^ 0x8000u, ts2 = thr_h | (thr_h << 16);
+    bf16x8 pfr[4][2];  // P (dropped) as A fragments: registers 2j, 2j + 1 = one key pair, one dword
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+      uint32_t pk[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) pk[j] = pack_bf2(acc[t][2 * j] * fk, acc[t][2 * j + 1] * fk);
+      if constexpr (DROP) {
+#pragma unroll
+        for (int j = 0; j < 8; ++j)  // drop_hash(dc, q, t * 32 + acc_row(2 j, hf)), per-lane terms hoisted
+          pk[j] = drop_pair(pk[j], drop_hash_s(sq, hk0 + (uint32_t)(t * 16 + (j & 1) + 4 * (j >> 1)) * 0x85EBCA77u, c8000),
+                            ts2, c15);
+      }
+#pragma unroll
+      for (int s = 0; s < 2; ++s)
+        pfr[t][s] = __builtin_bit_cast(bf16x8, (u32x4){pk[4 * s], pk[4 * s + 1], pk[4 * s + 2], pk[4 * s + 3]});
+    }
 #define DPA_FWD_PV(T, S)                                                                            \
   {                                                                                                \
-    const bf16x8 af = acc_to_frag(acc[T], S);                                                      \
+    const bf16x8 af = pfr[T][S];                                                                   \
     constexpr int R0 = (T * 32 + 16 * S) * 128;                                                    \
     const bf16x8 v0 = cat44(rdtro<IMG + R0>(ki + tp), rdtro<IMG + R0 + 1024 + 64>(ki + tp));       \
     const bf16x8 v1 = cat44(rdtro<IMG + R0 + 64>(ki + tp), rdtro<IMG + R0 + 1024>(ki + tp));       \
@@ -352,21 +373,6 @@ __global__ void __launch_bounds__(256, 2) attn128_fwd_kernel(const bf16_t* __res
     o[0] = mfma32(af, v0, o[0]);                                                                   \
     o[1] = mfma32(af, v1, o[1]);                                                                   \
   }
-#pragma unroll
-    for (int t = 0; t < 4; ++t) {
-      if constexpr (DROP) {
-        // one hash per key pair (registers 2j, 2j + 1 are keys 2m, 2m + 1), as one batch
-        uint32_t hh[8];
-#pragma unroll
-        for (int j = 0; j < 8; ++j)  // drop_hash(dc, q, t * 32 + acc_row(2 j, hf)), per-lane terms hoisted
-          hh[j] = mix32(dc.seedmix ^ hq ^ (hk0 + (uint32_t)(t * 16 + (j & 1) + 4 * (j >> 1)) * 0x85EBCA77u));
-#pragma unroll
-        for (int i = 0; i < 16; ++i) acc[t][i] = keep_from(dc, hh[i >> 1], i & 1) ? acc[t][i] * fk : 0.f;
-      } else {
-#pragma unroll
-        for (int i = 0; i < 16; ++i) acc[t][i] *= fk;
-      }
-    }
     DPA_FWD_PV(0, 0) DPA_FWD_PV(0, 1) DPA_FWD_PV(1, 0) DPA_FWD_PV(1, 1)
     DPA_FWD_PV(2, 0) DPA_FWD_PV(2, 1) DPA_FWD_PV(3, 0) DPA_FWD_PV(3, 1)
 #undef DPA_FWD_PV

@@ -139,6 +139,33 @@ __device__ __forceinline__ bool pair_keep(uint32_t h, uint32_t col, uint32_t thr
 }
 __host__ __device__ __forceinline__ uint32_t pair_thr16(float p) { return (uint32_t)(p * 65536.f + 0.5f); }
 
+// Attention dropout on a packed bf16 key pair (keys 2k, 2k + 1 of one query = the low and high
+// halves of the pair's hash; a half is kept when half >= thr16, unsigned).  With both sides
+// offset by 0x8000 the keep test is a signed 16-bit compare, done for both halves at once by a
+// saturating packed subtract whose sign, spread by a packed shift, masks the dropped half
+// (exact for every thr16).  Three VALU ops per PAIR (the 0x8000 offset rides the hash's last
+// xor) replace a compare, a select and a scale multiply per element, and the caller moves the
+// 1 / (1 - p) scale to its output normalisation.  The equivalent vector C compiles to per-half
+// compares and selects, hence the asm.
+typedef __attribute__((ext_vector_type(4))) uint32_t u32x4;
+// drop_hash_t(dc, qt, kt) ^ 0x80008000 from sq = seedmix ^ qt: mix32 with its last two xors
+// as one three-input xor
+__device__ __forceinline__ uint32_t drop_hash_s(uint32_t sq, uint32_t kt, uint32_t c8000) {
+  uint32_t x = sq ^ kt;
+  x ^= x >> 16;
+  x *= 0x7feb352du;
+  uint32_t r;
+  asm("v_bitop3_b32 %0, %1, %2, %3 bitop3:0x96" : "=v"(r) : "v"(x), "v"(x >> 15), "v"(c8000));
+  return r;
+}
+__device__ __forceinline__ uint32_t drop_pair(uint32_t pk, uint32_t hs, uint32_t ts2, uint32_t c15) {
+  // hs = hash ^ 0x80008000, ts2 = (thr16 ^ 0x8000) in both halves, c15 = 15 in both halves
+  uint32_t d, msk;
+  asm("v_pk_sub_i16 %0, %1, %2 clamp" : "=v"(d) : "v"(hs), "v"(ts2));
+  asm("v_pk_ashrrev_i16 %0, %1, %2" : "=v"(msk) : "v"(c15), "v"(d));
+  return pk & ~msk;
+}
+
 __device__ __forceinline__ float u32_to_unit(uint32_t x) {  // [0,1)
   return (float)(x >> 8) * (1.0f / 16777216.0f);
 }

@@ -87,6 +87,43 @@ def test_attention_dropout_consistent_with_mask(D):
     torch.testing.assert_close(dqkv.float(), x.grad, rtol=5e-2, atol=5e-2 * x.grad.abs().max().item())
 
 
+@pytest.mark.parametrize("B,L,H,causal,D", [(1, 1024, 2, True, 64),   # GPT-2 length
+                                              (4, 384, 2, True, 64),    # B*H % 8 == 0 item order
+                                              (2, 320, 4, False, 64),
+                                              (1, 256, 2, True, 128)])
+def test_attention_online_dropout_vs_fp32(B, L, H, causal, D):
+    """The single-pass forward (L > 128; packed-pair dropout, 1/(1-p) in the output scale) and
+    both backward kernels with dropout, against an fp32 reference built on the keep mask the
+    forward used (read back with V = one-hot probes; dropped entries are exact zeros)."""
+    torch.manual_seed(3)
+    p = 0.1
+    qkv = (torch.randn(B, L, 3 * H * D, device="cuda") * 0.5).bfloat16()
+    out, lse = _ext().attn_fwd(qkv, H, p, causal, 13, 2)
+    keep = torch.zeros(B, H, L, L, device="cuda")
+    idx = torch.arange(D, device="cuda")
+    for blk in range(L // D):
+        probe = qkv.clone().view(B, L, 3, H, D)
+        probe[:, :, 2] = 0
+        probe[:, blk * D + idx, 2, :, idx] = 1.0
+        o, _ = _ext().attn_fwd(probe.view(B, L, -1).contiguous(), H, p, causal, 13, 2)
+        keep[..., blk * D:(blk + 1) * D] = (o.view(B, L, H, D).permute(0, 2, 1, 3).float() != 0).float()
+    allowed = torch.tril(torch.ones(L, L, device="cuda")) if causal else torch.ones(L, L, device="cuda")
+    frac = (keep * allowed).sum().item() / (allowed.sum().item() * B * H)
+    assert abs(frac - (1 - p)) < 0.01
+    x = qkv.float().requires_grad_(True)
+    ref_o, ref_lse = _ref(x, H, causal, keep, p)
+    torch.testing.assert_close(lse, ref_lse, rtol=1e-3, atol=1e-2)
+    torch.testing.assert_close(out.float(), ref_o, rtol=3e-2, atol=3e-2)
+    dout = torch.randn_like(ref_o)
+    ref_o.backward(dout)
+    dqkv, _ = _ext().attn_bwd(dout.bfloat16(), qkv, out, lse, H, p, causal, 13, 2)
+    g = x.grad
+    for i, name in enumerate("qkv"):
+        a = dqkv.view(B, L, 3, H * D)[:, :, i].float()
+        r = g.view(B, L, 3, H * D)[:, :, i]
+        torch.testing.assert_close(a, r, rtol=5e-2, atol=5e-2 * r.abs().max().item(), msg=name)
+
+
 @pytest.mark.parametrize("B,L,H,causal", [(2, 128, 4, False), (2, 256, 2, False), (2, 192, 2, True),
                                             (4, 256, 2, True),
                                             (1, 512, 2, True),
