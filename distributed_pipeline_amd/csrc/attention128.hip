@@ -877,25 +877,26 @@ __global__ void __launch_bounds__(256, 1) attn128_fwd_d128_kernel(const bf16_t* 
     const float fk = dc.on ? inv_l * dc.scale : inv_l;
     // key pair of register 2j of tile t: t * 16 + (j & 1) + 4 (j >> 1) + 2 hf
     const uint32_t hq = (uint32_t)q * 0x9E3779B1u, hk0 = (uint32_t)(2 * hf) * 0x85EBCA77u;
+    const uint32_t sq = dc.seedmix ^ hq, c8000 = 0x80008000u, c15 = 0x000F000Fu;
+    const uint32_t thr_h = min(dc.thr16, 65535u) ^ 0x8000u, ts2 = thr_h | (thr_h << 16);
     f32x16 o[4];
 #pragma unroll
     for (int dt = 0; dt < 4; ++dt) o[dt] = zero16();
 #pragma unroll
     for (int t = 0; t < 4; ++t) {
+      // registers 2j, 2j + 1 = one key pair = one packed dword, dropped as a pair (drop_pair)
+      uint32_t pk[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) pk[j] = pack_bf2(acc[t][2 * j] * fk, acc[t][2 * j + 1] * fk);
       if (dc.on) {
-        uint32_t hh[8];  // one hash per key pair, as a batch
 #pragma unroll
         for (int j = 0; j < 8; ++j)  // drop_hash(dc, q, t * 32 + acc_row(2 j, hf)), per-lane terms hoisted
-          hh[j] = mix32(dc.seedmix ^ hq ^ (hk0 + (uint32_t)(t * 16 + (j & 1) + 4 * (j >> 1)) * 0x85EBCA77u));
-#pragma unroll
-        for (int i = 0; i < 16; ++i) acc[t][i] = keep_from(dc, hh[i >> 1], i & 1) ? acc[t][i] * fk : 0.f;
-      } else {
-#pragma unroll
-        for (int i = 0; i < 16; ++i) acc[t][i] *= fk;
+          pk[j] = drop_pair(pk[j], drop_hash_s(sq, hk0 + (uint32_t)(t * 16 + (j & 1) + 4 * (j >> 1)) * 0x85EBCA77u, c8000),
+                            ts2, c15);
       }
 #pragma unroll
       for (int s = 0; s < 2; ++s) {
-        const bf16x8 af = acc_to_frag(acc[t], s);
+        const bf16x8 af = __builtin_bit_cast(bf16x8, (u32x4){pk[4 * s], pk[4 * s + 1], pk[4 * s + 2], pk[4 * s + 3]});
         bf16x8 vf[4];
 #pragma unroll
         for (int dt = 0; dt < 4; ++dt) vf[dt] = frag_tp2(vi, t * 32 + 16 * s, dt * 32, lane);
