@@ -22,6 +22,8 @@
 // Out-of-range targets (< 0 or >= V) are ignored (loss 0, no gradient).
 #include <cstdlib>
 
+#include <type_traits>
+
 #include "common.h"
 #include "launchers.h"
 #include "mfma.h"
@@ -504,6 +506,10 @@ __global__ void __launch_bounds__(512) lxent_dw_kernel(
   int* s_tg = reinterpret_cast<int*>(s_g + 64);
 
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, h = lane >> 5;
+  // waves w and w + 4 share a SIMD and run the same MFMA -> VALU -> MFMA chain between the same
+  // barriers; a static priority for the first lets it run ahead, so the second's VALU work
+  // fills the first's MFMA phases instead of colliding with its own
+  if (w < 4) __builtin_amdgcn_s_setprio(1);
   const int vw = blockIdx.x * 256 + w * 32;       // this wave's 32 vocabulary rows
   const int v = vw + (lane & 31);                 // this lane's column (vocab)
   const bool v_ok = v < V;
@@ -569,23 +575,39 @@ __global__ void __launch_bounds__(512) lxent_dw_kernel(
 #pragma unroll
       for (int s = 0; s < KS; ++s)
         acc = mfma32(lds_frag<ROWB, true>(xt, tt * 32 + (lane & 31), 2 * s + h), wf[s], acc);
+      // the one-hot term lands on (token, vocab row) pairs whose target is one of this wave's 32
+      // rows: ~32 x 32 / V of the subtiles (3% at V = 30522).  One wave-uniform test per subtile
+      // (lane l checks token l) lets the others skip the per-logit compare and select.
+      auto softmax_grad = [&](auto oh) {
+        constexpr bool OH = decltype(oh)::value;
 #pragma unroll
-      for (int g4 = 0; g4 < 4; ++g4) {
-        // per-token scalars of rows tt*32 + 8 g4 + 4 h + r, one 16-byte read each
-        const int rb = tt * 32 + 8 * g4 + 4 * h;
-        const f32x4 l4 = *reinterpret_cast<const f32x4*>(s_lse + rb);
-        const f32x4 g4v = *reinterpret_cast<const f32x4*>(s_g + rb);
-        const int4 t4 = *reinterpret_cast<const int4*>(s_tg + rb);
-        const int tgs[4] = {t4.x, t4.y, t4.z, t4.w};
+        for (int g4 = 0; g4 < 4; ++g4) {
+          // per-token scalars of rows tt*32 + 8 g4 + 4 h + r, one 16-byte read each
+          const int rb = tt * 32 + 8 * g4 + 4 * h;
+          const f32x4 l4 = *reinterpret_cast<const f32x4*>(s_lse + rb);
+          const f32x4 g4v = *reinterpret_cast<const f32x4*>(s_g + rb);
+          int tgs[4] = {-1, -1, -1, -1};
+          if constexpr (OH) {
+            const int4 t4 = *reinterpret_cast<const int4*>(s_tg + rb);
+            tgs[0] = t4.x; tgs[1] = t4.y; tgs[2] = t4.z; tgs[3] = t4.w;
+          }
 #pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const int i = 4 * g4 + r;
-          const float gp = g4v[r] * fexp2(fmaf(acc[i], LOG2E, -l4[r]));
-          const float d = (ONEHOT && tgs[r] == v) ? gp - g4v[r] : gp;
-          acc[i] = d;
-          dbs += d;
+          for (int r = 0; r < 4; ++r) {
+            const int i = 4 * g4 + r;
+            const float gp = g4v[r] * fexp2(fmaf(acc[i], LOG2E, -l4[r]));
+            const float d = (OH && tgs[r] == v) ? gp - g4v[r] : gp;
+            acc[i] = d;
+            dbs += d;
+          }
         }
+      };
+      bool hit = false;
+      if constexpr (ONEHOT) {
+        const int tgl = s_tg[tt * 32 + (lane & 31)];
+        hit = __any(tgl >= vw && tgl < vw + 32);
       }
+      if (hit) softmax_grad(std::true_type{});
+      else softmax_grad(std::false_type{});
 #pragma unroll
       for (int s = 0; s < 2; ++s) {
         const bf16x8 af = acc_to_frag(acc, s);
