@@ -179,3 +179,42 @@ def test_fused_sublayers_res_gemm_match_composed_no_dropout(monkeypatch):
     for n in g_c:
         scale = g_c[n].abs().max().item() + 1e-6
         assert (g_f[n] - g_c[n]).abs().max().item() / scale < 3e-2, n
+
+
+def test_q8_mlp_backward_survives_a_gemm256_toggle(monkeypatch):
+    """a forward that stored u8 act' codes ("deriv8") and a backward whose fused dact
+    GEMM declines (here: the persistent kernels switched off between the two, as the A/B tools
+    do) must decode the codes and take the plain dgrad + activation-backward path, not fail."""
+    from distributed_pipeline_amd.models.layers import Linear
+    torch.manual_seed(0)
+    fc1 = Linear(256, 1024, act="gelu").cuda()
+    fc2 = Linear(1024, 256).cuda()
+    x = torch.randn(512, 256, device="cuda").bfloat16()
+    dy = torch.randn(512, 256, device="cuda").bfloat16()
+    params = (*fc1.parameters(), *fc2.parameters())
+    decodes = []
+    real_decode = opsnn.act_q8_decode
+    monkeypatch.setattr(opsnn, "act_q8_decode", lambda *a: decodes.append(1) or real_decode(*a))
+
+    def run(toggle):
+        for q in params:
+            q.grad = None
+        xi = x.clone().requires_grad_(True)
+        y = opsnn.mlp(xi, fc1, fc2)
+        if toggle:
+            get_ext().set_gemm256(False)
+        try:
+            y.backward(dy)
+        finally:
+            get_ext().set_gemm256(True)
+        return y.float(), xi.grad.float(), [q.grad.float().clone() for q in params]
+
+    assert opsnn._ACT_Q8
+    y0, dx0, g0 = run(False)
+    assert not decodes  # the fused dact GEMM consumed the codes
+    y1, dx1, g1 = run(True)
+    assert decodes  # the fallback decoded them
+    assert torch.equal(y0, y1)
+    torch.testing.assert_close(dx1, dx0, rtol=3e-2, atol=3e-2 * dx0.abs().max().item())
+    for a, b in zip(g1, g0):
+        assert (a - b).abs().max().item() <= 3e-2 * (b.abs().max().item() + 1e-6)
