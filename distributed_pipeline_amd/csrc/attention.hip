@@ -319,9 +319,9 @@ __global__ void __launch_bounds__(256, D == 64 ? 2 : 1) attn_fwd_online_kernel(c
                                                              bf16_t* __restrict__ out,
                                                              float* __restrict__ lse, int L, int H,
                                                              float p, uint32_t seed, uint32_t offset) {
-  __shared__ __attribute__((aligned(16))) char smem[2 * 64 * 2 * D];
-  char* kt_lds = smem;
-  char* vt_lds = smem + 64 * 2 * D;
+  // two K/V stages: tile i+1 is stored into the other stage while tile i is read, so one
+  // barrier per tile (it both publishes stage i+1 and retires stage i)
+  __shared__ __attribute__((aligned(16))) char smem[2 * 2 * 64 * 2 * D];
   const AttnItem it0 = attn_item(L, H, CAUSAL);
   for (int pass = 0; pass < it0.npass; ++pass) {  // 2 row tiles per block when causal
   const AttnItem it = attn_pass(it0, pass, L);
@@ -357,11 +357,14 @@ __global__ void __launch_bounds__(256, D == 64 ? 2 : 1) attn_fwd_online_kernel(c
   TileRegs<D> kr, vr;
   tile_load<D>(kr, kb, ld, 0, L, tid);
   tile_load<D>(vr, vb, ld, 0, L, tid);
-  for (int kv0 = 0; kv0 < kv_end; kv0 += 64) {
-    tile_store<D>(kt_lds, kr, tid);
-    tile_store<D>(vt_lds, vr, tid);
-    __syncthreads();
-    if (kv0 + 64 < kv_end) {  // next tile's loads overlap this tile's matrix-core work
+  tile_store<D>(smem, kr, tid);
+  tile_store<D>(smem + 64 * 2 * D, vr, tid);
+  __syncthreads();
+  for (int kv0 = 0, stg = 0; kv0 < kv_end; kv0 += 64, stg ^= 1) {
+    char* kt_lds = smem + stg * (2 * 64 * 2 * D);
+    char* vt_lds = kt_lds + 64 * 2 * D;
+    const bool more = kv0 + 64 < kv_end;
+    if (more) {  // next tile's loads overlap this tile's matrix-core work
       tile_load<D>(kr, kb, ld, kv0 + 64, L, tid);
       tile_load<D>(vr, vb, ld, kv0 + 64, L, tid);
     }
@@ -454,6 +457,11 @@ __global__ void __launch_bounds__(256, D == 64 ? 2 : 1) attn_fwd_online_kernel(c
     };
     if (tile_masked) tile(std::true_type{});
     else tile(std::false_type{});
+    if (more) {  // the other stage: every wave left it at the previous barrier
+      char* nk = smem + (stg ^ 1) * (2 * 64 * 2 * D);
+      tile_store<D>(nk, kr, tid);
+      tile_store<D>(nk + 64 * 2 * D, vr, tid);
+    }
     __syncthreads();
   }
   l += __shfl_xor(l, 32, 64);
